@@ -1,0 +1,183 @@
+#!/usr/bin/env python3
+"""CRC-32C throughput on device-resident batched records (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2], the north-star roofline run): per GPU,
+65,536 chunks x 64 KiB = 4 GiB of random bytes resident in HBM; one step = one
+batched CRC-32C pass over all chunks (libzscrc team kernel, 64-lane teams).
+With N > 1 GPUs (one process per GPU, torchrun) every rank owns its own 4 GiB
+shard (weak scaling, no data crosses xGMI) and the per-chunk digests are
+all-gathered over RCCL inside the timed step.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+Rank 0 prints ONE JSON line.  `value` = bytes checksummed by all ranks / max
+over ranks of the timed wall time, in GiB/s.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from zeroskip_amd import device as zd  # noqa: E402
+from zeroskip_amd._lib import check, lib  # noqa: E402
+
+METRIC = "CRC32C GiB/s device-resident batched records, 1/2/4/8 MI355X; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+CHUNK = 64 * 1024
+NCHUNK = 65536
+GIB = float(1 << 30)
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(seconds: float = 12.0) -> dict:
+    """The CPU oracle (SSE4.2 restatement of src/crc32c.c:370-453) on a bounded
+    sample of the same workload: 2,048 x 64 KiB chunks (128 MiB), one core."""
+    from oracle import oracle
+    sample_n = 2048
+    data = np.random.default_rng(1).integers(0, 256, sample_n * CHUNK, dtype=np.uint8)
+    res = {}
+    for impl, budget in (("hw", seconds * 0.6), ("sw", seconds * 0.4)):
+        done, t0 = 0, oracle.now()
+        while True:
+            oracle.batch(data, n=sample_n, stride=CHUNK, fixed_len=CHUNK, impl=impl, threads=1)
+            done += 1
+            el = oracle.now() - t0
+            if el >= budget:
+                break
+        res[impl] = done * sample_n * CHUNK / el / GIB
+    return {
+        "value": round(res["hw"], 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+        "sample": (f"{sample_n} x 64 KiB chunks (128 MiB) repeated ~{seconds:.0f} s on 1 core of "
+                   f"{cpu_model()} ({os.cpu_count()} threads visible); value = SSE4.2 crc32q "
+                   f"3-way path (crc32c_hw class); slice-by-4 crc32c_sw class = "
+                   f"{res['sw']:.3f} GiB/s"),
+        "sw_value": round(res["sw"], 3),
+    }
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world != 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    if lib().zscrc_device_count() < 1:
+        raise SystemExit("libzscrc: no gfx950 device")
+
+    # --- device-resident synthetic input: 4 GiB per rank ----------------------
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x9E3779B9 + rank)
+    data = torch.randint(0, 256, (NCHUNK * CHUNK,), dtype=torch.uint8, device=dev, generator=g)
+    out = torch.empty(NCHUNK, dtype=torch.int32, device=dev)
+    gathered = torch.empty(NCHUNK * world, dtype=torch.int32, device=dev) if world > 1 else None
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        check(lib().zscrc_device_fixed(data.data_ptr(), CHUNK, CHUNK, 0, out.data_ptr(), NCHUNK,
+                                       0, stream.cuda_stream), "zscrc_device_fixed")
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, out)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # --- timed region -----------------------------------------------------------
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        check(lib().zscrc_device_fixed(data.data_ptr(), CHUNK, CHUNK, 0, out.data_ptr(), NCHUNK,
+                                       0, stream.cuda_stream), "zscrc_device_fixed")
+        ev[i][1].record(stream)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, out)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    bytes_per_launch = NCHUNK * CHUNK + NCHUNK * 4       # algorithmic: input + u32 digests
+    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9  # GB/s
+    total_bytes = NCHUNK * CHUNK * world * args.steps
+    value = total_bytes / elapsed / GIB
+
+    if rank == 0:
+        traffic = None
+        tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(tpath):
+            try:
+                traffic = json.load(open(tpath)).get("config3_bytes_per_launch")
+            except Exception:
+                traffic = None
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (torch.randint bytes, device-resident)",
+            "config": {"workload": "config3: 65536 x 64 KiB chunks per GPU (4 GiB), batched CRC-32C",
+                       "records_per_gpu": NCHUNK, "record_bytes": CHUNK,
+                       "parallelism": f"shard{world}" + ("+rccl_allgather_digests" if world > 1 else "")},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "kernel": "zs::team_kernel<64>",
+                         "kernel_ms": round(kern_ms, 4)},
+        }
+        if world == 1 and not args.no_cpu:
+            line["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

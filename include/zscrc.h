@@ -1,0 +1,122 @@
+/*
+ * zscrc.h -- C ABI of libzscrc, the MI355X-native CRC-32C engine for zeroskip.
+ *
+ * Part 1 is a drop-in for the reference's checksum API: same names, same
+ * signatures, same results, so zeroskip's src/ files link unchanged once
+ * src/crc32c.c is dropped from libzeroskip_la_SOURCES (src/Makefile.am:47).
+ * Part 2 is the new batched / device-resident API (status-returning).
+ *
+ * No HIP or torch types appear here: device pointers are plain pointers,
+ * a stream is an opaque `void *` (a hipStream_t, NULL = default stream).
+ */
+#ifndef ZSCRC_H
+#define ZSCRC_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <sys/uio.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* zeroskip's string type (reference include/libzeroskip/cstring.h:23-29). */
+#ifndef _CSTRING_H_
+struct _cstring {
+    size_t len;
+    size_t alloc;
+    char *buf;
+};
+typedef struct _cstring cstring;
+#endif
+
+/* ======================================================================
+ * Part 1 -- reference API (include/libzeroskip/crc32c.h:15-24,
+ * exported by src/libzeroskip.symbols:113-120).  crc = 0 starts a new CRC;
+ * a previous result chains: crc32c(crc32c(0,A),B) == crc32c(0,A||B).
+ * These never fail (the reference has no error channel).
+ * ====================================================================== */
+
+/* replaces src/crc32c.c:668-673 (CPU feature probe; also warms the GPU context
+ * when ZSCRC_GPU_MIN enables offload) */
+void crc32c_init(void);
+/* replaces src/crc32c.c:613-645 (portable table path) */
+uint32_t crc32c_sw(uint32_t crc, const void *buf, size_t len);
+/* replaces src/crc32c.c:370-453; called directly by mfile.c:538,
+ * zeroskip-file.c:283-318, zeroskip-record.c:212-259, zeroskip-header.c:45-161,
+ * zeroskip-packed.c:298-327, zeroskip-dotzsdb.c:106-525 */
+uint32_t crc32c_hw(uint32_t crc, const void *buf, size_t len);
+/* replaces src/crc32c.c:675-684 */
+uint32_t crc32c(uint32_t crc, const void *buf, size_t len);
+/* replaces src/crc32c.c:686-689 */
+uint32_t crc32c_map(const char *base, unsigned len);
+/* replaces src/crc32c.c:703-706 */
+uint32_t crc32c_cstring(const cstring *buf);
+/* replaces src/crc32c.c:708-711 */
+uint32_t crc32c_buf(const char *buf);
+/* replaces src/crc32c.c:691-701 */
+uint32_t crc32c_iovec(struct iovec *iov, int iovcnt);
+
+/* ======================================================================
+ * Part 2 -- new API.
+ * ====================================================================== */
+
+enum zscrc_status {
+    ZSCRC_OK = 0,
+    ZSCRC_EINVAL = -1,   /* bad argument                     */
+    ZSCRC_ENODEV = -2,   /* no usable gfx950 device          */
+    ZSCRC_EHIP = -3,     /* HIP runtime error (see zscrc_last_error) */
+    ZSCRC_ENOMEM = -4,   /* device or pinned allocation failed */
+};
+
+/* flags */
+#define ZSCRC_RAW 1u /* seeds/outputs are raw registers: no pre/post inversion */
+
+/* crc(A||B) from crc(A), crc(B) and |B|.  Generalises crc32c_shift
+ * (src/crc32c.c:363-367) to any length. */
+uint32_t crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
+/* raw register after `nbytes` zero bytes (x^(8n) mod P multiply) */
+uint32_t zscrc_shift(uint32_t reg, uint64_t nbytes);
+
+/* Device-resident batch.  Every pointer is a device pointer on the current
+ * HIP device.  Record i is d_base[d_off[i] .. d_off[i]+d_len[i]); d_seed may
+ * be NULL (seed 0).  d_out[i] = crc32c(seed_i, record_i).  Asynchronous on
+ * `stream`; returns after launch. */
+int zscrc_device_batch(const void *d_base, const uint64_t *d_off, const uint64_t *d_len,
+                       const uint32_t *d_seed, uint32_t *d_out, size_t n,
+                       unsigned flags, void *stream);
+
+/* Device-resident fixed-stride batch: record i = d_base[i*stride .. +len). */
+int zscrc_device_fixed(const void *d_base, uint64_t stride, uint64_t len, uint32_t seed,
+                       uint32_t *d_out, size_t n, unsigned flags, void *stream);
+
+/* One long device-resident span, split over every CU and folded on the GPU.
+ * d_out (device, 1 word) receives crc32c(seed, span).  `scratch` may be NULL
+ * (library-owned) or a device buffer of zscrc_span_scratch_bytes(len). */
+size_t zscrc_span_scratch_bytes(uint64_t len);
+int zscrc_device_span(const void *d_buf, uint64_t len, uint32_t seed, uint32_t *d_out,
+                      void *scratch, unsigned flags, void *stream);
+
+/* Host-resident batch: copies [min off, max off+len) to the device, runs the
+ * batch, copies results back.  Synchronous.  The PCIe-bound path. */
+int zscrc_host_batch(const void *base, const uint64_t *off, const uint64_t *len,
+                     const uint32_t *seed, uint32_t *out, size_t n);
+
+/* Diagnostics. */
+const char *zscrc_last_error(void);
+/* counters: [0] scalar calls on CPU, [1] scalar calls offloaded,
+ * [2] kernel launches, [3] bytes checksummed on the GPU */
+void zscrc_stats(uint64_t out[4]);
+/* scalar calls of at least `min_bytes` go to the GPU (0 = never; default from
+ * env ZSCRC_GPU_MIN, else never). */
+void zscrc_set_gpu_min(uint64_t min_bytes);
+/* team size tuning: records <= g1_max bytes use one lane each, <= g16_max a
+ * 16-lane team, larger a 64-lane (whole wavefront) team. */
+void zscrc_set_teams(uint64_t g1_max, uint64_t g16_max);
+/* Number of gfx950 devices visible (0 if none / no HIP runtime). */
+int zscrc_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZSCRC_H */

@@ -1,0 +1,141 @@
+"""ctypes view of the CPU checker (TEST INFRASTRUCTURE ONLY).
+
+Only tests/, ``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg
+may import this module.  It restates /root/reference/src/crc32c.c (see
+oracle/zs_oracle.c for the file:line map) and is never used by the product
+package ``zeroskip_amd``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "build", "libzsoracle.so")
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    if force or not os.path.exists(_SO):
+        subprocess.check_call(["make", "-s", "-C", _HERE])
+    return _SO
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(_SO)
+        u32, u64, vp, sz = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_size_t
+        for name in ("oracle_crc32c_sw", "oracle_crc32c_hw", "oracle_crc32c",
+                     "oracle_crc32c_bitwise"):
+            f = getattr(L, name)
+            f.argtypes = [u32, vp, sz]
+            f.restype = u32
+        L.oracle_crc32c_init.argtypes = []
+        L.oracle_crc32c_init.restype = None
+        L.oracle_have_sse42.restype = ctypes.c_int
+        L.oracle_shift.argtypes = [u32, u64]
+        L.oracle_shift.restype = u32
+        L.oracle_combine.argtypes = [u32, u32, u64]
+        L.oracle_combine.restype = u32
+        L.oracle_batch.argtypes = [vp, vp, vp, vp, vp, u64, u64, u64, ctypes.c_int, ctypes.c_int]
+        L.oracle_batch.restype = ctypes.c_int
+        L.oracle_now.restype = ctypes.c_double
+        L.oracle_commit_crc.argtypes = [u32, u64, ctypes.c_int]
+        L.oracle_commit_crc.restype = u32
+        L.oracle_header_crc.argtypes = [u64, u32, ctypes.c_char_p, u32, u32]
+        L.oracle_header_crc.restype = u32
+        L.oracle_dotzsdb_crc.argtypes = [u64, u64, ctypes.c_char_p, u32]
+        L.oracle_dotzsdb_crc.restype = u32
+        L.oracle_get_sb4.argtypes = [vp]
+        _lib = L
+    return _lib
+
+
+def _buf(data):
+    if isinstance(data, np.ndarray):
+        a = np.ascontiguousarray(data).view(np.uint8)
+        return a, a.ctypes.data, a.nbytes
+    b = bytes(data)
+    cb = ctypes.create_string_buffer(b, len(b))
+    return cb, ctypes.addressof(cb), len(b)
+
+
+def crc32c_sw(crc: int, data) -> int:
+    keep, ptr, n = _buf(data)
+    return lib().oracle_crc32c_sw(crc, ptr, n)
+
+
+def crc32c_hw(crc: int, data) -> int:
+    keep, ptr, n = _buf(data)
+    return lib().oracle_crc32c_hw(crc, ptr, n)
+
+
+def crc32c_bitwise(crc: int, data) -> int:
+    keep, ptr, n = _buf(data)
+    return lib().oracle_crc32c_bitwise(crc, ptr, n)
+
+
+def shift(reg: int, nbytes: int) -> int:
+    return lib().oracle_shift(reg, nbytes)
+
+
+def combine(crc_a: int, crc_b: int, len_b: int) -> int:
+    return lib().oracle_combine(crc_a, crc_b, len_b)
+
+
+def batch(base: np.ndarray, offs=None, lens=None, seeds=None, *, n=None, stride=0,
+          fixed_len=0, impl: str = "hw", threads: int = 1) -> np.ndarray:
+    """CRC32C of records inside ``base`` (uint8 array)."""
+    base = np.ascontiguousarray(base).view(np.uint8)
+    if n is None:
+        n = len(offs) if offs is not None else len(lens)
+    out = np.zeros(n, dtype=np.uint32)
+    o = None if offs is None else np.ascontiguousarray(offs, dtype=np.uint64)
+    ln = None if lens is None else np.ascontiguousarray(lens, dtype=np.uint64)
+    s = None if seeds is None else np.ascontiguousarray(seeds, dtype=np.uint32)
+    rc = lib().oracle_batch(base.ctypes.data,
+                            None if o is None else o.ctypes.data,
+                            None if ln is None else ln.ctypes.data,
+                            None if s is None else s.ctypes.data,
+                            out.ctypes.data, n, stride, fixed_len,
+                            {"sw": 0, "hw": 1, "bitwise": 2}[impl], threads)
+    assert rc == 0
+    return out
+
+
+def now() -> float:
+    return lib().oracle_now()
+
+
+def commit_crc(span_crc: int, span_len: int, final: bool = False) -> int:
+    return lib().oracle_commit_crc(span_crc, span_len, int(final))
+
+
+def header_crc(signature: int, version: int, uuid: bytes, startidx: int, endidx: int) -> int:
+    return lib().oracle_header_crc(signature, version, uuid, startidx, endidx)
+
+
+def dotzsdb_crc(signature: int, offset: int, uuidstr: bytes, curidx: int) -> int:
+    assert len(uuidstr) == 37
+    return lib().oracle_dotzsdb_crc(signature, offset, uuidstr, curidx)
+
+
+def slice4_tables() -> np.ndarray:
+    t = np.zeros((4, 256), dtype=np.uint32)
+    lib().oracle_get_sb4(t.ctypes.data)
+    return t
+
+
+def crc32c_py(crc: int, data: bytes) -> int:
+    """Independent pure-Python bit-at-a-time CRC-32C (small inputs only)."""
+    r = crc ^ 0xFFFFFFFF
+    for b in bytes(data):
+        r ^= b
+        for _ in range(8):
+            r = (r >> 1) ^ (0x82F63B78 if r & 1 else 0)
+    return r ^ 0xFFFFFFFF

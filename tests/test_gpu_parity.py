@@ -1,0 +1,183 @@
+"""Parity of the gfx950 kernels (through the C ABI) with the CPU oracle.
+
+Bit-exact equality on every record; the oracle (oracle/zs_oracle.c) is the
+checker, the golden fixtures pin it to the reference's known answers."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle
+from tests.golden.datagen import xorshift64_bytes
+from zeroskip_amd import device as zd
+from zeroskip_amd import crc32c as zc
+from zeroskip_amd._lib import lib, stats
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "crc32c_golden.json")))
+M32 = 0xFFFFFFFF
+
+
+def to_dev(a: np.ndarray, dev) -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def u32(t: torch.Tensor) -> np.ndarray:
+    torch.cuda.synchronize()
+    return t.cpu().numpy().view(np.uint32)
+
+
+def rand_bytes(n, seed):
+    return np.random.default_rng(seed).integers(0, 256, n, dtype=np.uint8)
+
+
+@pytest.fixture(params=[(1024, 16384), (0, 0), (1 << 40, 1 << 40), (0, 1 << 40)],
+                ids=["default", "all-g64", "all-g1", "all-g16"])
+def teams(request, gpu):
+    lib().zscrc_set_teams(*request.param)
+    yield request.param
+    lib().zscrc_set_teams(1024, 16384)
+
+
+def test_golden_cases_variable_batch(gpu, teams):
+    data = xorshift64_bytes(GOLDEN["data"]["bytes"])
+    rows = np.array(GOLDEN["cases"], dtype=np.uint64)
+    d = to_dev(data, gpu)
+    offs = to_dev(rows[:, 0].astype(np.int64), gpu)
+    lens = to_dev(rows[:, 1].astype(np.int64), gpu)
+    seeds = to_dev(rows[:, 2].astype(np.uint32).view(np.int32), gpu)
+    out = u32(zd.crc_batch(d, offs, lens, seeds))
+    assert np.array_equal(out, rows[:, 3].astype(np.uint32))
+
+
+def test_kats_on_device(gpu):
+    for k in GOLDEN["kats"] + [dict(hex=GOLDEN["crc32bench"]["text"].encode().hex(), seed=0,
+                                    crc=GOLDEN["crc32bench"]["crc"])]:
+        raw = np.frombuffer(bytes.fromhex(k["hex"]), dtype=np.uint8)
+        buf = to_dev(np.concatenate([raw, np.zeros(8, np.uint8)]), gpu)
+        offs = torch.zeros(1, dtype=torch.int64, device=gpu)
+        lens = torch.full((1,), len(raw), dtype=torch.int64, device=gpu)
+        seeds = torch.tensor([np.uint32(k["seed"]).view(np.int32)], device=gpu)
+        assert u32(zd.crc_batch(buf, offs, lens, seeds))[0] == k["crc"]
+
+
+@pytest.mark.parametrize("stride,length,n", [
+    (64, 64, 1 << 20),          # BASELINE config 2, full size: 1M x 64 B
+    (320, 312, 20000),          # zsbench BATCHED span (key 40 B + value 272 B)
+    (65536, 65536, 512),        # config 3 shape (64 KiB chunks), 32 MiB
+    (4096, 4000, 3000),
+    (1040, 1037, 5000),         # unaligned starts, ragged tails
+    (100000, 99999, 300),
+    (8, 8, 100000),
+    (5, 5, 1000),               # < 8 bytes: serial path
+])
+def test_fixed_stride(gpu, stride, length, n):
+    data = rand_bytes(stride * (n - 1) + length, stride + length)
+    out = u32(zd.crc_fixed(to_dev(data, gpu), stride, length, n, seed=0x1234))
+    ref = _oracle_seeded(data, stride, length, n, 0x1234)
+    bad = np.nonzero(out != ref)[0]
+    assert bad.size == 0, bad[:10]
+
+
+def _oracle_seeded(data, stride, length, n, seed):
+    offs = np.arange(n, dtype=np.uint64) * stride
+    lens = np.full(n, length, dtype=np.uint64)
+    seeds = np.full(n, seed, dtype=np.uint32)
+    return oracle.batch(data, offs, lens, seeds, impl="hw", threads=8)
+
+
+def test_variable_random_batch(gpu, teams):
+    rng = np.random.default_rng(42)
+    n = 4000
+    lens = np.exp(rng.uniform(0, np.log(300000), n)).astype(np.int64)
+    lens[rng.integers(0, n, 200)] = rng.integers(0, 9, 200)  # tiny records
+    total = int(lens.sum()) + 64 * n
+    data = rand_bytes(total, 99)
+    gaps = rng.integers(0, 64, n)
+    offs = np.cumsum(np.concatenate([[0], lens[:-1] + gaps[:-1]])).astype(np.int64)
+    seeds = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    out = u32(zd.crc_batch(to_dev(data, gpu), to_dev(offs, gpu), to_dev(lens, gpu),
+                           to_dev(seeds.view(np.int32), gpu)))
+    ref = oracle.batch(data, offs.astype(np.uint64), lens.astype(np.uint64), seeds, impl="hw",
+                       threads=8)
+    bad = np.nonzero(out != ref)[0]
+    assert bad.size == 0, [(int(i), int(offs[i]), int(lens[i])) for i in bad[:10]]
+
+
+def test_raw_registers(gpu):
+    data = rand_bytes(64 * 4096, 5)
+    reg_in = 0x0BADF00D
+    out = u32(zd.crc_fixed(to_dev(data, gpu), 4096, 4096, 64, seed=reg_in, raw=True))
+    for i in range(64):
+        want = (~oracle.crc32c_hw(~reg_in & M32, data[i * 4096:(i + 1) * 4096])) & M32
+        assert out[i] == want
+
+
+@pytest.mark.parametrize("length,offset", [
+    (0, 0), (5, 3), (1000, 1), ((1 << 20) - 1, 0), (1 << 20, 0), ((3 << 20) + 7, 5),
+    ((64 << 20) + 13, 2), (256 << 20, 0),
+])
+def test_span(gpu, length, offset):
+    data = rand_bytes(length + offset + 16, length)
+    out = u32(zd.crc_span(to_dev(data, gpu), seed=0xC0FFEE, length=length, offset=offset))
+    assert out[0] == oracle.crc32c_hw(0xC0FFEE, data[offset:offset + length])
+
+
+def test_span_equals_fold_of_records(gpu):
+    # size-independent property at BASELINE config-3 record size: one span CRC
+    # over N chunks == combine-chain of the N per-chunk CRCs
+    n, L = 2048, 65536
+    d = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=gpu)
+    per = u32(zd.crc_fixed(d, L, L, n))
+    whole = u32(zd.crc_span(d))[0]
+    acc = 0
+    for c in per:
+        acc = zc.crc32c_combine(acc, int(c), L)
+    assert acc == whole
+    # and a sample of chunks against the oracle
+    host = d.cpu().numpy()
+    for i in (0, 1, 777, n - 1):
+        assert per[i] == oracle.crc32c_hw(0, host[i * L:(i + 1) * L])
+
+
+def test_host_batch(gpu):
+    import ctypes
+    rng = np.random.default_rng(8)
+    n = 500
+    lens = rng.integers(0, 50000, n).astype(np.uint64)
+    offs = np.cumsum(np.concatenate([[0], lens[:-1] + 3])).astype(np.uint64)
+    data = rand_bytes(int(offs[-1] + lens[-1]) + 8, 1)
+    seeds = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    out = np.zeros(n, dtype=np.uint32)
+    rc = lib().zscrc_host_batch(data.ctypes.data, offs.ctypes.data, lens.ctypes.data,
+                                seeds.ctypes.data, out.ctypes.data, n)
+    assert rc == 0, lib().zscrc_last_error()
+    assert np.array_equal(out, oracle.batch(data, offs, lens, seeds, impl="hw", threads=8))
+
+
+def test_scalar_offload(gpu):
+    before = stats()
+    lib().zscrc_set_gpu_min(1 << 20)
+    try:
+        d = rand_bytes((5 << 20) + 3, 77)
+        assert zc.crc32c_hw(0x42, d) == oracle.crc32c_hw(0x42, d)
+        assert zc.crc32c(0, d[1:]) == oracle.crc32c_hw(0, d[1:])
+        small = d[:37]
+        assert zc.crc32c_hw(0, small) == oracle.crc32c_hw(0, small)
+    finally:
+        lib().zscrc_set_gpu_min(0)
+    after = stats()
+    assert after[1] - before[1] == 2   # both large calls ran on the GPU
+    assert after[0] - before[0] == 1   # the 37-byte call stayed on the CPU
+
+
+def test_config2_full_size_vs_oracle(gpu):
+    # BASELINE config 2 at full size: 1,048,576 x 64 B records, every CRC checked
+    n = 1 << 20
+    d = torch.randint(0, 256, (n * 64,), dtype=torch.uint8, device=gpu)
+    out = u32(zd.crc_fixed(d, 64, 64, n))
+    ref = oracle.batch(d.cpu().numpy(), n=n, stride=64, fixed_len=64, impl="hw", threads=8)
+    assert np.array_equal(out, ref)

@@ -1,0 +1,57 @@
+"""Kernel-variant sweep on one GPU (tuning aid; prints one JSON line per case)."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from zeroskip_amd import device as zd  # noqa: E402
+from zeroskip_amd._lib import lib  # noqa: E402
+
+
+def timeit(fn, reps=10, warm=3):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b))
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def main():
+    dev = torch.device("cuda:0")
+    big = torch.randint(0, 256, (4 << 30,), dtype=torch.uint8, device=dev)
+    out = torch.empty(1 << 24, dtype=torch.int32, device=dev)
+    cases = [
+        ("cfg3 64KiB g64", 65536, 65536, 65536, (0, 0)),
+        ("cfg3 64KiB g16", 65536, 65536, 65536, (0, 1 << 40)),
+        ("cfg3 64KiB g1", 65536, 65536, 65536, (1 << 40, 1 << 40)),
+        ("cfg2 64B g1", 64, 64, 1 << 20, (1024, 16384)),
+        ("cfg2 64B g1 x16 (1 GiB)", 64, 64, 1 << 24, (1024, 16384)),
+        ("zsbench 312B g1", 320, 312, 10_000_000, (1024, 16384)),
+        ("zsbench 312B g16", 320, 312, 10_000_000, (0, 1 << 40)),
+        ("4KiB g1", 4096, 4096, 1 << 20, (1 << 40, 1 << 40)),
+        ("4KiB g16", 4096, 4096, 1 << 20, (0, 1 << 40)),
+        ("4KiB g64", 4096, 4096, 1 << 20, (0, 0)),
+    ]
+    for name, stride, length, n, teams in cases:
+        lib().zscrc_set_teams(*teams)
+        ms = timeit(lambda: zd.crc_fixed(big, stride, length, n, out=out[:n]))
+        byt = n * length
+        print(json.dumps({"case": name, "ms": round(ms, 4), "GBs": round(byt / ms / 1e6, 1),
+                          "GiBs": round(byt / ms / 1e6 * 1e9 / (1 << 30), 1)}), flush=True)
+    lib().zscrc_set_teams(1024, 16384)
+    ms = timeit(lambda: zd.crc_span(big))
+    print(json.dumps({"case": "span 4 GiB", "ms": round(ms, 4), "GBs": round((4 << 30) / ms / 1e6, 1)}))
+
+
+if __name__ == "__main__":
+    main()

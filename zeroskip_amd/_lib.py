@@ -1,0 +1,79 @@
+"""ctypes binding of libzscrc.so (the C ABI of include/zscrc.h)."""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libzscrc.so")
+
+_u32, _u64, _vp, _sz, _int = (ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p,
+                              ctypes.c_size_t, ctypes.c_int)
+
+# name -> (restype, argtypes); mirrors include/zscrc.h
+SIGNATURES = {
+    "crc32c_init": (None, []),
+    "crc32c_sw": (_u32, [_u32, _vp, _sz]),
+    "crc32c_hw": (_u32, [_u32, _vp, _sz]),
+    "crc32c": (_u32, [_u32, _vp, _sz]),
+    "crc32c_map": (_u32, [ctypes.c_char_p, ctypes.c_uint]),
+    "crc32c_cstring": (_u32, [_vp]),
+    "crc32c_buf": (_u32, [ctypes.c_char_p]),
+    "crc32c_iovec": (_u32, [_vp, _int]),
+    "crc32c_combine": (_u32, [_u32, _u32, _u64]),
+    "zscrc_shift": (_u32, [_u32, _u64]),
+    "zscrc_device_batch": (_int, [_vp, _vp, _vp, _vp, _vp, _sz, ctypes.c_uint, _vp]),
+    "zscrc_device_fixed": (_int, [_vp, _u64, _u64, _u32, _vp, _sz, ctypes.c_uint, _vp]),
+    "zscrc_span_scratch_bytes": (_sz, [_u64]),
+    "zscrc_device_span": (_int, [_vp, _u64, _u32, _vp, _vp, ctypes.c_uint, _vp]),
+    "zscrc_host_batch": (_int, [_vp, _vp, _vp, _vp, _vp, _sz]),
+    "zscrc_last_error": (ctypes.c_char_p, []),
+    "zscrc_stats": (None, [_vp]),
+    "zscrc_set_gpu_min": (None, [_u64]),
+    "zscrc_set_teams": (None, [_u64, _u64]),
+    "zscrc_device_count": (_int, []),
+}
+
+ZSCRC_RAW = 1
+
+_lib = None
+
+
+class ZscrcError(RuntimeError):
+    pass
+
+
+def build_library(force: bool = False) -> str:
+    """Compile libzscrc.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    args = ["make", "-s", "-C", _HERE] + (["-B"] if force else [])
+    subprocess.check_call(args)
+    return LIB_PATH
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with `make -C {_HERE}` "
+                "(there is no CPU fallback for the GPU engine)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = "libzscrc") -> None:
+    if rc != 0:
+        msg = lib().zscrc_last_error()
+        raise ZscrcError(f"{what} failed with status {rc}: {msg.decode() if msg else ''}")
+
+
+def stats() -> list[int]:
+    a = (ctypes.c_uint64 * 4)()
+    lib().zscrc_stats(a)
+    return list(a)

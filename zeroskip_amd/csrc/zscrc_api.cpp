@@ -1,0 +1,528 @@
+/*
+ * zscrc_api.cpp -- the C ABI of libzscrc (declared in include/zscrc.h).
+ *
+ * Part 1 re-exports the reference's checksum symbols (crc32c_hw et al.,
+ * /root/reference/include/libzeroskip/crc32c.h:15-24) with identical
+ * semantics.  Part 2 drives the gfx950 kernels in zscrc_kernels.hip.
+ *
+ * Per HIP device the library keeps one context: the 36 KiB operator-table
+ * block (zscrc_internal.h GT_*), the CU count that sizes the persistent grid,
+ * and growable scratch for spans and host-staged batches.
+ */
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+
+#include "../../include/zscrc.h"
+#include "zscrc_gf2.h"
+#include "zscrc_internal.h"
+
+extern "C" {
+uint32_t zscrc_cpu_table(uint32_t crc, const void *buf, size_t len);
+uint32_t zscrc_cpu_hw(uint32_t crc, const void *buf, size_t len);
+int zscrc_cpu_have_sse42(void);
+void zscrc_cpu_init(void);
+int zs_launch_team(int g, const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
+int zs_launch_span_fold(const zs::SpanFold *f, hipStream_t stream);
+}
+
+namespace {
+
+constexpr int MAX_DEV = 64;
+constexpr uint64_t SPAN_SPLIT_MIN = 1u << 20; /* below: one wavefront team */
+constexpr uint64_t SEG_MIN = 64u << 10;
+
+thread_local char t_err[256];
+std::atomic<uint64_t> g_stat[4];
+std::atomic<uint64_t> g_gpu_min{0};
+std::atomic<uint64_t> g_g1_max{1024};
+std::atomic<uint64_t> g_g16_max{16384};
+int g_strict = 0;
+
+struct DevCtx {
+    std::mutex mu;
+    bool ready = false;
+    int ncu = 0;
+    uint32_t *gtab = nullptr;
+    void *scratch = nullptr;   /* span partials */
+    size_t scratch_bytes = 0;
+    void *stage = nullptr;     /* host-batch staging */
+    size_t stage_bytes = 0;
+};
+DevCtx g_ctx[MAX_DEV];
+std::once_flag g_env_once;
+
+void set_err(const char *what, hipError_t e)
+{
+    snprintf(t_err, sizeof t_err, "%s: %s", what, e == hipSuccess ? "ok" : hipGetErrorString(e));
+}
+
+void env_init()
+{
+    const char *s = getenv("ZSCRC_GPU_MIN");
+    if (s)
+        g_gpu_min = strtoull(s, nullptr, 0);
+    s = getenv("ZSCRC_STRICT");
+    g_strict = s && *s && *s != '0';
+    s = getenv("ZSCRC_G1_MAX");
+    if (s)
+        g_g1_max = strtoull(s, nullptr, 0);
+    s = getenv("ZSCRC_G16_MAX");
+    if (s)
+        g_g16_max = strtoull(s, nullptr, 0);
+}
+
+bool is_gfx950(int dev)
+{
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, dev) != hipSuccess)
+        return false;
+    return strncmp(p.gcnArchName, "gfx950", 6) == 0;
+}
+
+void build_gtab(uint32_t *t)
+{
+    zs_gf2_shift_table(t + GT_S4, 4);
+    zs_gf2_shift_table(t + GT_U16, 4 + 15 * 64);
+    zs_gf2_shift_table(t + GT_U64, 4 + 63 * 64);
+    for (int k = 0; k < 6; ++k)
+        zs_gf2_shift_table(t + GT_Z + 1024 * k, 64ull << k);
+}
+
+/* Context of the current device, initialised on first use. */
+int get_ctx(DevCtx **out)
+{
+    std::call_once(g_env_once, env_init);
+    int dev = -1;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess || dev < 0 || dev >= MAX_DEV) {
+        set_err("hipGetDevice", e);
+        return ZSCRC_ENODEV;
+    }
+    DevCtx &c = g_ctx[dev];
+    std::lock_guard<std::mutex> lk(c.mu);
+    if (c.ready) {
+        *out = &c;
+        return ZSCRC_OK;
+    }
+    if (!is_gfx950(dev)) {
+        snprintf(t_err, sizeof t_err, "device %d is not gfx950 (MI355X)", dev);
+        return ZSCRC_ENODEV;
+    }
+    int ncu = 0;
+    e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess || ncu <= 0) {
+        set_err("hipDeviceGetAttribute(CU count)", e);
+        return ZSCRC_EHIP;
+    }
+    static uint32_t host_tab[GT_WORDS];
+    static std::once_flag tab_once;
+    std::call_once(tab_once, [] { build_gtab(host_tab); });
+    e = hipMalloc(&c.gtab, sizeof host_tab);
+    if (e != hipSuccess) {
+        set_err("hipMalloc(tables)", e);
+        return ZSCRC_ENOMEM;
+    }
+    e = hipMemcpy(c.gtab, host_tab, sizeof host_tab, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        set_err("hipMemcpy(tables)", e);
+        return ZSCRC_EHIP;
+    }
+    c.ncu = ncu;
+    c.ready = true;
+    *out = &c;
+    return ZSCRC_OK;
+}
+
+int grow(void **p, size_t *have, size_t need)
+{
+    if (*have >= need)
+        return ZSCRC_OK;
+    if (*p)
+        (void)hipFree(*p);
+    *p = nullptr;
+    *have = 0;
+    size_t n = need + need / 4;
+    hipError_t e = hipMalloc(p, n);
+    if (e != hipSuccess) {
+        set_err("hipMalloc(scratch)", e);
+        return ZSCRC_ENOMEM;
+    }
+    *have = n;
+    return ZSCRC_OK;
+}
+
+int team_for_len(uint64_t len)
+{
+    if (len <= g_g1_max)
+        return 1;
+    if (len <= g_g16_max)
+        return 16;
+    return 64;
+}
+
+zs::BatchDesc make_desc()
+{
+    zs::BatchDesc d;
+    memset(&d, 0, sizeof d);
+    d.last_len = ~0ull;
+    d.len_lo = 0;
+    d.len_hi = ~0ull;
+    return d;
+}
+
+int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s)
+{
+    int rc = zs_launch_team(g, &d, c->gtab, c->ncu, s);
+    if (rc) {
+        set_err("team kernel launch", hipGetLastError());
+        return ZSCRC_EHIP;
+    }
+    g_stat[2]++;
+    return ZSCRC_OK;
+}
+
+/* Span over [d_buf, d_buf+len): split across the chip, fold on the GPU. */
+int span_impl(DevCtx *c, const void *d_buf, uint64_t len, uint32_t seed, uint32_t *d_out,
+              void *scratch, unsigned flags, hipStream_t s)
+{
+    const uint32_t xio = (flags & ZSCRC_RAW) ? 0u : 0xffffffffu;
+    zs::BatchDesc d = make_desc();
+    if (len < SPAN_SPLIT_MIN) {
+        d.base = static_cast<const uint8_t *>(d_buf);
+        d.n = 1;
+        d.fixed_len = len;
+        d.fixed_seed = seed;
+        d.xor_io = xio;
+        d.out = d_out;
+        return launch(c, len <= g_g1_max ? 1 : 64, d, s);
+    }
+    const uint64_t nwaves = (uint64_t)c->ncu * 16;
+    uint64_t seg = (len + 2 * nwaves - 1) / (2 * nwaves);
+    seg = (seg + 4095) & ~4095ull;
+    if (seg < SEG_MIN)
+        seg = SEG_MIN;
+    const uint64_t w = (len + seg - 1) / seg;
+    uint32_t *part = static_cast<uint32_t *>(scratch);
+    if (!part) {
+        int rc = grow(&c->scratch, &c->scratch_bytes, w * 4);
+        if (rc)
+            return rc;
+        part = static_cast<uint32_t *>(c->scratch);
+    }
+    d.base = static_cast<const uint8_t *>(d_buf);
+    d.n = w;
+    d.stride = seg;
+    d.fixed_len = seg;
+    d.last_len = len - (w - 1) * seg;
+    d.fixed_seed = 0;
+    d.xor_io = 0;
+    d.out = part;
+    int rc = launch(c, 64, d, s);
+    if (rc)
+        return rc;
+    zs::SpanFold f;
+    memset(&f, 0, sizeof f);
+    f.part = part;
+    f.out = d_out;
+    f.w = (uint32_t)w;
+    f.k = zs_gf2_xpow8n(seg);
+    f.kp2[0] = f.k;
+    for (int b = 1; b < 32; ++b)
+        f.kp2[b] = zs_gf2_mul(f.kp2[b - 1], f.kp2[b - 1]);
+    f.x_last = zs_gf2_xpow8n(d.last_len);
+    f.x_total = zs_gf2_xpow8n(len);
+    f.r0 = seed ^ xio;
+    f.xor_out = xio;
+    if (zs_launch_span_fold(&f, s)) {
+        set_err("span fold launch", hipGetLastError());
+        return ZSCRC_EHIP;
+    }
+    g_stat[2]++;
+    return ZSCRC_OK;
+}
+
+/* Scalar call offloaded to the GPU; returns false to fall back to the CPU. */
+bool gpu_scalar(uint32_t crc, const void *buf, size_t len, uint32_t *res)
+{
+    DevCtx *c = nullptr;
+    if (get_ctx(&c))
+        return false;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (grow(&c->stage, &c->stage_bytes, len + 64))
+        return false;
+    uint8_t *dbuf = static_cast<uint8_t *>(c->stage);
+    uint32_t *dout = reinterpret_cast<uint32_t *>(dbuf + ((len + 15) & ~size_t(15)));
+    hipError_t e = hipMemcpy(dbuf, buf, len, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        set_err("hipMemcpy H2D", e);
+        return false;
+    }
+    if (span_impl(c, dbuf, len, crc, dout, nullptr, 0, nullptr))
+        return false;
+    e = hipMemcpy(res, dout, 4, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+        set_err("hipMemcpy D2H", e);
+        return false;
+    }
+    g_stat[3] += len;
+    return true;
+}
+
+} /* namespace */
+
+/* ====================================================== Part 1: reference API */
+extern "C" {
+
+void crc32c_init(void)
+{
+    std::call_once(g_env_once, env_init);
+    zscrc_cpu_init();
+}
+
+uint32_t crc32c_sw(uint32_t crc, const void *buf, size_t len)
+{
+    g_stat[0]++;
+    return zscrc_cpu_table(crc, buf, len);
+}
+
+uint32_t crc32c_hw(uint32_t crc, const void *buf, size_t len)
+{
+    std::call_once(g_env_once, env_init);
+    const uint64_t gmin = g_gpu_min;
+    if (gmin && len >= gmin && buf) {
+        uint32_t r;
+        if (gpu_scalar(crc, buf, len, &r)) {
+            g_stat[1]++;
+            return r;
+        }
+        if (g_strict) {
+            fprintf(stderr, "libzscrc: GPU offload failed (%s) and ZSCRC_STRICT is set\n", t_err);
+            abort();
+        }
+    }
+    g_stat[0]++;
+    return zscrc_cpu_hw(crc, buf, len);
+}
+
+uint32_t crc32c(uint32_t crc, const void *buf, size_t len) { return crc32c_hw(crc, buf, len); }
+
+uint32_t crc32c_map(const char *base, unsigned len) { return crc32c(0, base, (size_t)len); }
+
+uint32_t crc32c_cstring(const cstring *buf) { return crc32c_map(buf->buf, (unsigned)buf->len); }
+
+uint32_t crc32c_buf(const char *buf) { return crc32c_map(buf, (unsigned)strlen(buf)); }
+
+uint32_t crc32c_iovec(struct iovec *iov, int iovcnt)
+{
+    uint32_t crc = 0;
+    for (int i = 0; i < iovcnt; ++i)
+        if (iov[i].iov_len)
+            crc = crc32c(crc, iov[i].iov_base, iov[i].iov_len);
+    return crc;
+}
+
+/* ============================================================ Part 2: new API */
+uint32_t crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b)
+{
+    return zs_gf2_shift(crc_a, len_b) ^ crc_b;
+}
+
+uint32_t zscrc_shift(uint32_t reg, uint64_t nbytes) { return zs_gf2_shift(reg, nbytes); }
+
+int zscrc_device_batch(const void *d_base, const uint64_t *d_off, const uint64_t *d_len,
+                       const uint32_t *d_seed, uint32_t *d_out, size_t n, unsigned flags,
+                       void *stream)
+{
+    if (n == 0)
+        return ZSCRC_OK;
+    if (!d_base || !d_off || !d_len || !d_out)
+        return ZSCRC_EINVAL;
+    DevCtx *c;
+    int rc = get_ctx(&c);
+    if (rc)
+        return rc;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    zs::BatchDesc d = make_desc();
+    d.base = static_cast<const uint8_t *>(d_base);
+    d.off = d_off;
+    d.len = d_len;
+    d.seed = d_seed;
+    d.out = d_out;
+    d.n = n;
+    d.xor_io = (flags & ZSCRC_RAW) ? 0u : 0xffffffffu;
+    const uint64_t g1 = g_g1_max, g16 = g_g16_max;
+    /* three length classes, each a persistent launch that skips the others */
+    d.len_lo = 0;
+    d.len_hi = g1;
+    if ((rc = launch(c, 1, d, s)))
+        return rc;
+    if (g16 > g1) {
+        d.len_lo = g1 + 1;
+        d.len_hi = g16;
+        if ((rc = launch(c, 16, d, s)))
+            return rc;
+    }
+    d.len_lo = (g16 > g1 ? g16 : g1) + 1;
+    d.len_hi = ~0ull;
+    return launch(c, 64, d, s);
+}
+
+int zscrc_device_fixed(const void *d_base, uint64_t stride, uint64_t len, uint32_t seed,
+                       uint32_t *d_out, size_t n, unsigned flags, void *stream)
+{
+    if (n == 0)
+        return ZSCRC_OK;
+    if (!d_base || !d_out)
+        return ZSCRC_EINVAL;
+    DevCtx *c;
+    int rc = get_ctx(&c);
+    if (rc)
+        return rc;
+    zs::BatchDesc d = make_desc();
+    d.base = static_cast<const uint8_t *>(d_base);
+    d.stride = stride;
+    d.fixed_len = len;
+    d.fixed_seed = seed;
+    d.out = d_out;
+    d.n = n;
+    d.xor_io = (flags & ZSCRC_RAW) ? 0u : 0xffffffffu;
+    return launch(c, team_for_len(len), d, static_cast<hipStream_t>(stream));
+}
+
+size_t zscrc_span_scratch_bytes(uint64_t len)
+{
+    (void)len;
+    return 4u * (2u * 256u * 16u + 16u); /* <= 2 segments per wave on 256 CUs */
+}
+
+int zscrc_device_span(const void *d_buf, uint64_t len, uint32_t seed, uint32_t *d_out,
+                      void *scratch, unsigned flags, void *stream)
+{
+    if (!d_out || (!d_buf && len))
+        return ZSCRC_EINVAL;
+    DevCtx *c;
+    int rc = get_ctx(&c);
+    if (rc)
+        return rc;
+    std::lock_guard<std::mutex> lk(c->mu);
+    return span_impl(c, d_buf, len, seed, d_out, scratch, flags, static_cast<hipStream_t>(stream));
+}
+
+int zscrc_host_batch(const void *base, const uint64_t *off, const uint64_t *len,
+                     const uint32_t *seed, uint32_t *out, size_t n)
+{
+    if (n == 0)
+        return ZSCRC_OK;
+    if (!base || !off || !len || !out)
+        return ZSCRC_EINVAL;
+    DevCtx *c;
+    int rc = get_ctx(&c);
+    if (rc)
+        return rc;
+    uint64_t lo = ~0ull, hi = 0;
+    for (size_t i = 0; i < n; ++i) {
+        if (off[i] < lo)
+            lo = off[i];
+        if (off[i] + len[i] > hi)
+            hi = off[i] + len[i];
+    }
+    if (hi < lo)
+        hi = lo;
+    const uint64_t data = (hi - lo + 15) & ~15ull;
+    const uint64_t need = data + n * (8 + 8 + 4 + 4) + 64;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if ((rc = grow(&c->stage, &c->stage_bytes, need)))
+        return rc;
+    uint8_t *dbase = static_cast<uint8_t *>(c->stage);
+    uint64_t *doff = reinterpret_cast<uint64_t *>(dbase + data);
+    uint64_t *dlen = doff + n;
+    uint32_t *dseed = reinterpret_cast<uint32_t *>(dlen + n);
+    uint32_t *dout = dseed + n;
+    uint64_t *hoff = static_cast<uint64_t *>(malloc(n * 8));
+    if (!hoff)
+        return ZSCRC_ENOMEM;
+    for (size_t i = 0; i < n; ++i)
+        hoff[i] = off[i] - lo;
+    hipError_t e = hipMemcpy(dbase, static_cast<const uint8_t *>(base) + lo, hi - lo,
+                             hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMemcpy(doff, hoff, n * 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMemcpy(dlen, len, n * 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess && seed)
+        e = hipMemcpy(dseed, seed, n * 4, hipMemcpyHostToDevice);
+    free(hoff);
+    if (e != hipSuccess) {
+        set_err("hipMemcpy H2D", e);
+        return ZSCRC_EHIP;
+    }
+    zs::BatchDesc d = make_desc();
+    d.base = dbase;
+    d.off = doff;
+    d.len = dlen;
+    d.seed = seed ? dseed : nullptr;
+    d.out = dout;
+    d.n = n;
+    d.xor_io = 0xffffffffu;
+    const uint64_t g1 = g_g1_max, g16 = g_g16_max;
+    d.len_hi = g1;
+    if ((rc = launch(c, 1, d, nullptr)))
+        return rc;
+    if (g16 > g1) {
+        d.len_lo = g1 + 1;
+        d.len_hi = g16;
+        if ((rc = launch(c, 16, d, nullptr)))
+            return rc;
+    }
+    d.len_lo = (g16 > g1 ? g16 : g1) + 1;
+    d.len_hi = ~0ull;
+    if ((rc = launch(c, 64, d, nullptr)))
+        return rc;
+    e = hipMemcpy(out, dout, n * 4, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+        set_err("hipMemcpy D2H", e);
+        return ZSCRC_EHIP;
+    }
+    for (size_t i = 0; i < n; ++i)
+        g_stat[3] += len[i];
+    return ZSCRC_OK;
+}
+
+const char *zscrc_last_error(void) { return t_err; }
+
+void zscrc_stats(uint64_t out[4])
+{
+    for (int i = 0; i < 4; ++i)
+        out[i] = g_stat[i];
+}
+
+void zscrc_set_gpu_min(uint64_t min_bytes)
+{
+    std::call_once(g_env_once, env_init);
+    g_gpu_min = min_bytes;
+}
+
+void zscrc_set_teams(uint64_t g1_max, uint64_t g16_max)
+{
+    std::call_once(g_env_once, env_init);
+    g_g1_max = g1_max;
+    g_g16_max = g16_max;
+}
+
+int zscrc_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess)
+        return 0;
+    int k = 0;
+    for (int i = 0; i < n; ++i)
+        k += is_gfx950(i);
+    return k;
+}
+
+} /* extern "C" */

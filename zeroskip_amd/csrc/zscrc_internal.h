@@ -1,0 +1,48 @@
+/* zscrc_internal.h -- structures shared by the kernels and the host API. */
+#ifndef ZSCRC_INTERNAL_H
+#define ZSCRC_INTERNAL_H
+
+#include <stdint.h>
+
+/* Global operator-table block (uint32 words), built on the host per device. */
+enum {
+    GT_S4 = 0,       /* shift(b<<8j, 4): slice-by-4 tables, j = byte position */
+    GT_U16 = 1024,   /* shift(b<<8j, 4 + 15*64): word then skip, 16-lane team */
+    GT_U64 = 2048,   /* shift(b<<8j, 4 + 63*64): word then skip, 64-lane team */
+    GT_Z = 3072,     /* GT_Z + k*1024: shift(b<<8j, 64<<k), k = 0..5          */
+    GT_WORDS = 3072 + 6 * 1024,
+};
+
+namespace zs {
+
+struct BatchDesc {
+    const uint8_t *base;
+    const uint64_t *off;  /* NULL -> rec * stride        */
+    const uint64_t *len;  /* NULL -> fixed_len           */
+    const uint32_t *seed; /* NULL -> fixed_seed          */
+    uint32_t *out;
+    uint64_t n;
+    uint64_t stride;
+    uint64_t fixed_len;
+    uint64_t last_len;    /* ~0 = none; else length of record n-1 */
+    uint64_t len_lo;      /* process records with len_lo <= len <= len_hi */
+    uint64_t len_hi;
+    uint32_t fixed_seed;
+    uint32_t xor_io;      /* 0xFFFFFFFF standard CRC, 0 raw registers */
+};
+
+struct SpanFold {
+    const uint32_t *part; /* W raw segment registers */
+    uint32_t *out;
+    uint32_t w;
+    uint32_t k;           /* x^(8*SEG) */
+    uint32_t kp2[32];     /* k^(2^b)   */
+    uint32_t x_last;      /* x^(8*len of last segment) */
+    uint32_t x_total;     /* x^(8*span len) */
+    uint32_t r0;          /* initial register */
+    uint32_t xor_out;
+};
+
+} /* namespace zs */
+
+#endif

@@ -1,0 +1,348 @@
+/*
+ * zscrc_kernels.hip -- CDNA4 (gfx950) CRC-32C kernels.
+ *
+ * Replaces the byte loop of the reference's crc32c_hw / crc32c_sw
+ * (/root/reference/src/crc32c.c:370-453, :613-645) for batches of
+ * device-resident records.  Integer/bit work only: no MFMA.
+ *
+ * Work decomposition ("team of G lanes per record", G in {1, 16, 64}):
+ *   A record's bytes are cut into 64-byte pieces.  Team lane j owns the
+ *   pieces j, j+G, j+2G, ... of the record (a "step" is G*64 bytes), so one
+ *   wave-wide load step reads 64 lanes x 64 B of contiguous memory per team.
+ *   Each lane runs slice-by-4 over its piece; the last word of every piece
+ *   uses the fused operator "word then skip (G-1)*64 zero bytes" (U tables),
+ *   which jumps the lane's register over the other lanes' pieces.  At the end
+ *   the G lane registers are folded with log2(G) "shift by 64<<k bytes"
+ *   operators (Z tables) -- the reference's crc32c_shift (crc32c.c:363-367)
+ *   generalised to a tree.
+ *
+ *   The record is aligned to the step grid at its END: the grid starts
+ *   S*G*64 bytes before the (4-aligned) end, and bytes before the record
+ *   start are zero.  Leading zeros do not change a register that starts at
+ *   0, and the initial register (~seed) is XORed into the first four record
+ *   bytes, so the result is exact.  0-3 tail bytes past the last 4-aligned
+ *   address are folded byte-wise by the last lane.
+ *
+ * LDS (one 1024-thread workgroup per CU, persistent over records):
+ *   [0, 128K)    slice-by-4 tables, 32 bank-private replicas (conflict-free:
+ *                lane l always reads bank l%32).  Table j (byte position j of
+ *                the word) lives at ((j>>1)<<16) + ((j&1)<<7); entry e at
+ *                +e*256; replica r at +4r.  One v_perm_b32 builds an address.
+ *   [128K, 132K) U: "word then skip" operator for this G (4 x 256 dwords)
+ *   [132K, 156K) Z_k, k = 0..5: shift by 64<<k bytes (4 x 256 dwords each)
+ */
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "zscrc_internal.h"
+
+namespace zs {
+
+constexpr int WG = 1024;
+constexpr int WAVES = WG / 64;
+constexpr uint32_t LDS_BYTES = 163840;
+constexpr uint32_t OFF_U = 131072;
+constexpr uint32_t OFF_Z = 135168;
+
+/* Global-address-space views: flat pointers would tie every load to the LDS
+ * counter (lgkmcnt) and serialise them against the table lookups. */
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u32x4 *g4p;
+typedef const __attribute__((address_space(1))) uint32_t *g32p;
+typedef const __attribute__((address_space(1))) uint8_t *g8p;
+
+__device__ __forceinline__ uint64_t uni64(uint64_t v)
+{
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint32_t lds32(const char *L, uint32_t addr)
+{
+    return *reinterpret_cast<const uint32_t *>(L + addr);
+}
+
+/* register x -> register after 4 zero bytes (= one slice-by-4 step on x). */
+__device__ __forceinline__ uint32_t m4(const char *L, uint32_t x, uint32_t c_lo, uint32_t c_hi)
+{
+    const uint32_t a0 = __builtin_amdgcn_perm(x, c_lo, 0x0C020400u);
+    const uint32_t a1 = __builtin_amdgcn_perm(x, c_lo, 0x0C020500u);
+    const uint32_t a2 = __builtin_amdgcn_perm(x, c_hi, 0x0C020600u);
+    const uint32_t a3 = __builtin_amdgcn_perm(x, c_hi, 0x0C020700u);
+    return lds32(L, a0) ^ lds32(L, a1 + 128) ^ lds32(L, a2) ^ lds32(L, a3 + 128);
+}
+
+/* 4-lookup operator from a compact (non-replicated) 4 KiB table at `base`. */
+__device__ __forceinline__ uint32_t op4(const char *L, uint32_t base, uint32_t x)
+{
+    return lds32(L, base + ((x << 2) & 0x3fcu)) ^ lds32(L, base + 1024 + ((x >> 6) & 0x3fcu)) ^
+           lds32(L, base + 2048 + ((x >> 14) & 0x3fcu)) ^ lds32(L, base + 3072 + ((x >> 22) & 0x3fcu));
+}
+
+/* One byte (Sarwate): table j=3 is shift(b<<24, 4) = shift(b, 1). */
+__device__ __forceinline__ uint32_t byte_step(const char *L, uint32_t r, uint32_t b, uint32_t c_hi)
+{
+    const uint32_t x = r ^ b;
+    return lds32(L, __builtin_amdgcn_perm(x, c_hi, 0x0C020400u) + 128) ^ (r >> 8);
+}
+
+/* 16 words of one piece; the last one optionally fused with the skip. */
+template <bool SKIP>
+__device__ __forceinline__ uint32_t piece(const char *L, uint32_t acc, const uint32_t (&w)[16],
+                                          uint32_t c_lo, uint32_t c_hi)
+{
+#pragma unroll
+    for (int k = 0; k < 15; ++k)
+        acc = m4(L, acc ^ w[k], c_lo, c_hi);
+    if (SKIP)
+        return op4(L, OFF_U, acc ^ w[15]);
+    return m4(L, acc ^ w[15], c_lo, c_hi);
+}
+
+__device__ __forceinline__ void load_piece(uintptr_t p, bool al16, uint32_t (&w)[16])
+{
+    if (al16) {
+        const g4p q = (g4p)p;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const u32x4 v = q[i];
+            w[4 * i + 0] = v.x;
+            w[4 * i + 1] = v.y;
+            w[4 * i + 2] = v.z;
+            w[4 * i + 3] = v.w;
+        }
+    } else {
+        const g32p q = (g32p)p;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            w[i] = q[i];
+    }
+}
+
+/*
+ * Register after processing [a, a+len) starting from register R0, computed
+ * by a team of G lanes (team lane j).  The result is valid in lane j == G-1.
+ */
+template <int G>
+__device__ uint32_t team_register(const uint8_t *a, uint64_t len, uint32_t R0, int j, int lane,
+                                  const char *L, uint32_t c_lo, uint32_t c_hi)
+{
+    if (len < 8) {
+        uint32_t r = R0;
+        if (j == G - 1)
+            for (uint64_t i = 0; i < len; ++i)
+                r = byte_step(L, r, ((g8p)a)[i], c_hi);
+        return r;
+    }
+    constexpr uint64_t STEP = (uint64_t)G * 64;
+    const uintptr_t A = reinterpret_cast<uintptr_t>(a);
+    const uintptr_t E = (A + len) & ~uintptr_t(3);
+    const uint64_t nb = E - A;                       /* >= 5 */
+    const uint64_t S = (nb + STEP - 1) / STEP;       /* steps */
+    const uintptr_t V0 = E - S * STEP;               /* grid start (<= A) */
+    const bool al16 = (V0 & 15) == 0;
+
+    uint32_t acc = 0;
+    uint32_t w[16];
+    /* ---- step 0: may start before the record, and carries R0 ---- */
+    {
+        const uintptr_t p = V0 + 64 * (uintptr_t)j;
+        if (V0 == A) {
+            load_piece(p, al16, w);
+            if (j == 0)
+                w[0] ^= R0;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const uintptr_t q = p + 4 * k;
+                uint32_t v = 0;
+                if (q + 4 > A) {
+                    v = *(g32p)q;
+                    if (q < A)
+                        v &= 0xffffffffu << (8 * (uint32_t)(A - q));
+                }
+                const int64_t d = (int64_t)(A - q);
+                if (d >= 0 && d < 4)
+                    v ^= R0 << (8 * (uint32_t)d);
+                else if (d < 0 && d > -4)
+                    v ^= R0 >> (8 * (uint32_t)(-d));
+                w[k] = v;
+            }
+        }
+    }
+    if (S == 1) {
+        acc = piece<false>(L, acc, w, c_lo, c_hi);
+    } else {
+        uint32_t nx[16];
+        load_piece(V0 + STEP + 64 * (uintptr_t)j, al16, nx);
+        acc = piece<G != 1>(L, acc, w, c_lo, c_hi);
+        for (uint64_t s = 1; s < S; ++s) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                w[k] = nx[k];
+            if (s + 1 < S) {
+                load_piece(V0 + (s + 1) * STEP + 64 * (uintptr_t)j, al16, nx);
+                acc = piece<G != 1>(L, acc, w, c_lo, c_hi);
+            } else {
+                acc = piece<false>(L, acc, w, c_lo, c_hi);
+            }
+        }
+    }
+    /* ---- fold the team: lane j's register is relative to E - (G-1-j)*64 ---- */
+#pragma unroll
+    for (int k = 0; (1 << k) < G; ++k) {
+        const uint32_t sh = op4(L, OFF_Z + 4096u * k, acc);
+        const uint32_t other = __shfl(sh, lane - (1 << k));
+        if (j & (1 << k))
+            acc ^= other;
+    }
+    /* ---- 0..3 tail bytes ---- */
+    if (j == G - 1) {
+        const g8p t = (g8p)E;
+        const uint32_t tail = (uint32_t)((A + len) - E);
+        for (uint32_t i = 0; i < tail; ++i)
+            acc = byte_step(L, acc, t[i], c_hi);
+    }
+    return acc;
+}
+
+template <int G>
+__device__ void fill_lds(char *L, const uint32_t *__restrict__ gtab)
+{
+    /* slice tables, 32 replicas, written 4 replicas per 16-byte store */
+    uint4 *L4 = reinterpret_cast<uint4 *>(L);
+    for (int i = threadIdx.x; i < 8192; i += WG) {
+        const int d = i * 4;                 /* dword index */
+        const int half = d >> 14;
+        const int e = (d >> 6) & 255;
+        const int tj = half * 2 + ((d >> 5) & 1);
+        const uint32_t v = gtab[GT_S4 + tj * 256 + e];
+        L4[i] = make_uint4(v, v, v, v);
+    }
+    if (G > 1) {
+        uint32_t *U = reinterpret_cast<uint32_t *>(L + OFF_U);
+        const int src = G == 16 ? GT_U16 : GT_U64;
+        for (int i = threadIdx.x; i < 1024; i += WG)
+            U[i] = gtab[src + i];
+        uint32_t *Z = reinterpret_cast<uint32_t *>(L + OFF_Z);
+        constexpr int NZ = G == 16 ? 4 : 6;
+        for (int i = threadIdx.x; i < NZ * 1024; i += WG)
+            Z[i] = gtab[GT_Z + i];
+    }
+}
+
+template <int G>
+__global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
+{
+    __shared__ __attribute__((aligned(16))) char L[LDS_BYTES];
+    fill_lds<G>(L, gtab);
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const int j = lane % G;
+    const uint32_t c_lo = (uint32_t)(lane & 31) << 2;
+    const uint32_t c_hi = c_lo | 0x10000u;
+    uint64_t team = ((uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6)) * (64 / G) + lane / G;
+    if (G == 64)
+        team = uni64(team); /* whole-wave team: keep record state in SGPRs */
+    const uint64_t nteams = (uint64_t)gridDim.x * WAVES * (64 / G);
+
+    for (uint64_t rec = team; rec < d.n; rec += nteams) {
+        uint64_t len = d.len ? ((const __attribute__((address_space(1))) uint64_t *)d.len)[rec] : d.fixed_len;
+        if (d.last_len != ~0ull && rec + 1 == d.n)
+            len = d.last_len;
+        if (len < d.len_lo || len > d.len_hi)
+            continue;
+        const uint8_t *a =
+            d.base + (d.off ? ((const __attribute__((address_space(1))) uint64_t *)d.off)[rec] : rec * d.stride);
+        const uint32_t seed = d.seed ? ((g32p)d.seed)[rec] : d.fixed_seed;
+        const uint32_t r = team_register<G>(a, len, seed ^ d.xor_io, j, lane, L, c_lo, c_hi);
+        if (j == G - 1)
+            d.out[rec] = r ^ d.xor_io;
+    }
+}
+
+/* ------------------------------------------------------------ span fold */
+__device__ __forceinline__ uint32_t gmul(uint32_t a, uint32_t b)
+{
+    uint32_t acc = 0;
+#pragma unroll 4
+    for (int i = 0; i < 32; ++i) {
+        acc ^= (a & 0x80000000u) ? b : 0u;
+        a <<= 1;
+        b = (b >> 1) ^ ((b & 1u) ? 0x82F63B78u : 0u);
+    }
+    return acc;
+}
+
+/* K^m from the table K^(2^b). */
+__device__ __forceinline__ uint32_t kpow(const uint32_t *kp2, uint32_t m)
+{
+    uint32_t r = 0x80000000u;
+    for (int b = 0; m; ++b, m >>= 1)
+        if (m & 1)
+            r = gmul(r, kp2[b]);
+    return r;
+}
+
+/*
+ * Fold W raw segment registers P_0..P_{W-1} of a span whose segments are all
+ * SEG bytes long except the last:
+ *   H = Horner_{i<W-1}(P_i, K = x^(8 SEG));  reg = H * x^(8 lastlen) ^ P_{W-1}
+ *   reg ^= R0 * x^(8 L)                       (initial register)
+ */
+__global__ __launch_bounds__(1024) void span_fold_kernel(SpanFold f)
+{
+    __shared__ uint32_t red[1024];
+    const uint32_t W = f.w;
+    const uint32_t nh = W - 1; /* Horner terms */
+    const uint32_t per = (nh + 1023) / 1024;
+    const uint32_t s = threadIdx.x * per;
+    const uint32_t e = s + per < nh ? s + per : nh;
+    uint32_t h = 0;
+    for (uint32_t i = s; i < e; ++i)
+        h = gmul(h, f.k) ^ f.part[i];
+    if (s < e)
+        h = gmul(h, kpow(f.kp2, nh - e));
+    red[threadIdx.x] = h;
+    __syncthreads();
+    for (int o = 512; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o)
+            red[threadIdx.x] ^= red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        uint32_t reg = gmul(red[0], f.x_last) ^ f.part[W - 1];
+        reg ^= gmul(f.r0, f.x_total);
+        *f.out = reg ^ f.xor_out;
+    }
+}
+
+} // namespace zs
+
+/* ------------------------------------------------------------ launchers */
+extern "C" int zs_launch_team(int g, const zs::BatchDesc *d, const uint32_t *gtab, int grid,
+                              hipStream_t stream)
+{
+    switch (g) {
+    case 1:
+        hipLaunchKernelGGL(zs::team_kernel<1>, dim3(grid), dim3(zs::WG), 0, stream, *d, gtab);
+        break;
+    case 16:
+        hipLaunchKernelGGL(zs::team_kernel<16>, dim3(grid), dim3(zs::WG), 0, stream, *d, gtab);
+        break;
+    case 64:
+        hipLaunchKernelGGL(zs::team_kernel<64>, dim3(grid), dim3(zs::WG), 0, stream, *d, gtab);
+        break;
+    default:
+        return -1;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int zs_launch_span_fold(const zs::SpanFold *f, hipStream_t stream)
+{
+    hipLaunchKernelGGL(zs::span_fold_kernel, dim3(1), dim3(1024), 0, stream, *f);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
