@@ -176,6 +176,9 @@ __device__ uint32_t team_register(const uint8_t *a, uint64_t len, uint32_t R0, i
     } else {
         uint32_t nx[16];
         load_piece(V0 + STEP + 64 * (uintptr_t)j, al16, nx);
+        /* R0's bytes [A, A+4) can spill past step 0 into lane 0's first word */
+        if (j == 0 && A + 4 > V0 + STEP)
+            nx[0] ^= R0 >> (8 * (uint32_t)(V0 + STEP - A));
         acc = piece<G != 1>(L, acc, w, c_lo, c_hi);
         for (uint64_t s = 1; s < S; ++s) {
 #pragma unroll
