@@ -34,12 +34,12 @@ def rand_bytes(n, seed):
     return np.random.default_rng(seed).integers(0, 256, n, dtype=np.uint8)
 
 
-@pytest.fixture(params=[(1024, 16384), (0, 0), (1 << 40, 1 << 40), (0, 1 << 40)],
+@pytest.fixture(params=[(1024, 1 << 20), (0, 0), (1 << 40, 1 << 40), (0, 1 << 40)],
                 ids=["default", "all-g64", "all-g1", "all-g16"])
 def teams(request, gpu):
     lib().zscrc_set_teams(*request.param)
     yield request.param
-    lib().zscrc_set_teams(1024, 16384)
+    lib().zscrc_set_teams(1024, 1 << 20)
 
 
 def test_golden_cases_variable_batch(gpu, teams):

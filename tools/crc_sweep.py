@@ -34,13 +34,19 @@ def main():
         ("cfg3 64KiB g64", 65536, 65536, 65536, (0, 0)),
         ("cfg3 64KiB g16", 65536, 65536, 65536, (0, 1 << 40)),
         ("cfg3 64KiB g1", 65536, 65536, 65536, (1 << 40, 1 << 40)),
-        ("cfg2 64B g1", 64, 64, 1 << 20, (1024, 16384)),
-        ("cfg2 64B g1 x16 (1 GiB)", 64, 64, 1 << 24, (1024, 16384)),
-        ("zsbench 312B g1", 320, 312, 10_000_000, (1024, 16384)),
+        ("cfg2 64B g1", 64, 64, 1 << 20, (1024, 1 << 20)),
+        ("cfg2 64B g1 x16 (1 GiB)", 64, 64, 1 << 24, (1024, 1 << 20)),
+        ("zsbench 312B g1", 320, 312, 10_000_000, (1024, 1 << 20)),
         ("zsbench 312B g16", 320, 312, 10_000_000, (0, 1 << 40)),
         ("4KiB g1", 4096, 4096, 1 << 20, (1 << 40, 1 << 40)),
         ("4KiB g16", 4096, 4096, 1 << 20, (0, 1 << 40)),
         ("4KiB g64", 4096, 4096, 1 << 20, (0, 0)),
+        ("zsbench 312B default", 320, 312, 10_000_000, (1024, 1 << 20)),
+        ("1KiB g1", 1024, 1024, 1 << 22, (1 << 40, 1 << 40)),
+        ("1KiB g16", 1024, 1024, 1 << 22, (0, 1 << 40)),
+        ("256KiB g16", 262144, 262144, 16384, (0, 1 << 40)),
+        ("256KiB g64", 262144, 262144, 16384, (0, 0)),
+        ("1MiB g64 (4096 recs)", 1 << 20, 1 << 20, 4096, (0, 0)),
     ]
     for name, stride, length, n, teams in cases:
         lib().zscrc_set_teams(*teams)
@@ -48,7 +54,7 @@ def main():
         byt = n * length
         print(json.dumps({"case": name, "ms": round(ms, 4), "GBs": round(byt / ms / 1e6, 1),
                           "GiBs": round(byt / ms / 1e6 * 1e9 / (1 << 30), 1)}), flush=True)
-    lib().zscrc_set_teams(1024, 16384)
+    lib().zscrc_set_teams(1024, 1 << 20)
     ms = timeit(lambda: zd.crc_span(big))
     print(json.dumps({"case": "span 4 GiB", "ms": round(ms, 4), "GBs": round((4 << 30) / ms / 1e6, 1)}))
 

@@ -40,7 +40,7 @@ thread_local char t_err[256];
 std::atomic<uint64_t> g_stat[4];
 std::atomic<uint64_t> g_gpu_min{0};
 std::atomic<uint64_t> g_g1_max{1024};
-std::atomic<uint64_t> g_g16_max{16384};
+std::atomic<uint64_t> g_g16_max{1u << 20};
 int g_strict = 0;
 
 struct DevCtx {
@@ -156,11 +156,14 @@ int grow(void **p, size_t *have, size_t need)
     return ZSCRC_OK;
 }
 
-int team_for_len(uint64_t len)
+/* Team size for n records of `len` bytes: 16-lane teams keep four records
+ * per wave in flight (best on >= 1 KiB records, profiles/r01/sweep), but only
+ * when there are enough records to give every team one. */
+int team_for(uint64_t len, uint64_t n, int ncu)
 {
     if (len <= g_g1_max)
         return 1;
-    if (len <= g_g16_max)
+    if (len <= g_g16_max && n >= (uint64_t)ncu * 16 * 4)
         return 16;
     return 64;
 }
@@ -391,7 +394,7 @@ int zscrc_device_fixed(const void *d_base, uint64_t stride, uint64_t len, uint32
     d.out = d_out;
     d.n = n;
     d.xor_io = (flags & ZSCRC_RAW) ? 0u : 0xffffffffu;
-    return launch(c, team_for_len(len), d, static_cast<hipStream_t>(stream));
+    return launch(c, team_for(len, n, c->ncu), d, static_cast<hipStream_t>(stream));
 }
 
 size_t zscrc_span_scratch_bytes(uint64_t len)

@@ -100,9 +100,61 @@ __device__ __forceinline__ uint32_t piece(const char *L, uint32_t acc, const uin
     return m4(L, acc ^ w[15], c_lo, c_hi);
 }
 
-__device__ __forceinline__ void load_piece(uintptr_t p, bool al16, uint32_t (&w)[16])
+/* One record as seen by its team (every field team-uniform). */
+struct Item {
+    uintptr_t A;      /* first byte                       */
+    uintptr_t E;      /* last 4-aligned address <= A+len  */
+    uintptr_t V0;     /* step-grid start (<= A)           */
+    uint64_t S;       /* steps of G*64 bytes; 0 = short record (< 8 bytes) */
+    uint64_t len;
+    uint64_t rec;
+    uint32_t R0;      /* initial register */
+};
+
+/* Next record for this team at or after `rec` that passes the length filter. */
+template <int G>
+__device__ __forceinline__ bool fetch_record(const BatchDesc &d, uint64_t rec, uint64_t nteams, Item &it)
 {
-    if (al16) {
+    constexpr uint64_t STEP = (uint64_t)G * 64;
+    for (; rec < d.n; rec += nteams) {
+        uint64_t len = d.len ? ((const __attribute__((address_space(1))) uint64_t *)d.len)[rec] : d.fixed_len;
+        if (d.last_len != ~0ull && rec + 1 == d.n)
+            len = d.last_len;
+        if (len < d.len_lo || len > d.len_hi)
+            continue;
+        const uint64_t off =
+            d.off ? ((const __attribute__((address_space(1))) uint64_t *)d.off)[rec] : rec * d.stride;
+        const uint32_t seed = d.seed ? ((g32p)d.seed)[rec] : d.fixed_seed;
+        const uintptr_t A = reinterpret_cast<uintptr_t>(d.base) + off;
+        const uintptr_t E = len < 8 ? A : ((A + len) & ~uintptr_t(3));
+        const uint64_t S = len < 8 ? 0 : (E - A + STEP - 1) / STEP;
+        it.A = A;
+        it.E = E;
+        it.V0 = E - S * STEP;
+        it.S = S;
+        it.len = len;
+        it.rec = rec;
+        it.R0 = seed ^ d.xor_io;
+        return true;
+    }
+    return false;
+}
+
+/* Issue the loads of lane j's piece of step s.  Step 0 of a front-padded grid
+ * loads only the dwords that reach the record (the rest is zero); nothing
+ * before the record's first aligned dword is ever touched. */
+template <int G>
+__device__ __forceinline__ void issue(const Item &it, uint64_t s, int j, uint32_t (&w)[16])
+{
+    constexpr uint64_t STEP = (uint64_t)G * 64;
+    const uintptr_t p = it.V0 + s * STEP + 64 * (uintptr_t)j;
+    if (s == 0 && it.V0 != it.A) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uintptr_t q = p + 4 * k;
+            w[k] = (q + 4 > it.A) ? *(g32p)q : 0u;
+        }
+    } else if ((it.V0 & 15) == 0) {
         const g4p q = (g4p)p;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -112,6 +164,15 @@ __device__ __forceinline__ void load_piece(uintptr_t p, bool al16, uint32_t (&w)
             w[4 * i + 2] = v.z;
             w[4 * i + 3] = v.w;
         }
+    } else if ((it.V0 & 7) == 0) {
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+        const __attribute__((address_space(1))) u32x2 *q = (const __attribute__((address_space(1))) u32x2 *)p;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const u32x2 v = q[i];
+            w[2 * i + 0] = v.x;
+            w[2 * i + 1] = v.y;
+        }
     } else {
         const g32p q = (g32p)p;
 #pragma unroll
@@ -120,79 +181,42 @@ __device__ __forceinline__ void load_piece(uintptr_t p, bool al16, uint32_t (&w)
     }
 }
 
-/*
- * Register after processing [a, a+len) starting from register R0, computed
- * by a team of G lanes (team lane j).  The result is valid in lane j == G-1.
- */
+/* Data fix-ups that need the record start: zero bytes before A in the word
+ * that straddles it, and XOR the initial register into bytes [A, A+4). */
 template <int G>
-__device__ uint32_t team_register(const uint8_t *a, uint64_t len, uint32_t R0, int j, int lane,
-                                  const char *L, uint32_t c_lo, uint32_t c_hi)
+__device__ __forceinline__ void fixup(const Item &it, uint64_t s, int j, uint32_t (&w)[16])
 {
-    if (len < 8) {
-        uint32_t r = R0;
-        if (j == G - 1)
-            for (uint64_t i = 0; i < len; ++i)
-                r = byte_step(L, r, ((g8p)a)[i], c_hi);
-        return r;
-    }
     constexpr uint64_t STEP = (uint64_t)G * 64;
-    const uintptr_t A = reinterpret_cast<uintptr_t>(a);
-    const uintptr_t E = (A + len) & ~uintptr_t(3);
-    const uint64_t nb = E - A;                       /* >= 5 */
-    const uint64_t S = (nb + STEP - 1) / STEP;       /* steps */
-    const uintptr_t V0 = E - S * STEP;               /* grid start (<= A) */
-    const bool al16 = (V0 & 15) == 0;
-
-    uint32_t acc = 0;
-    uint32_t w[16];
-    /* ---- step 0: may start before the record, and carries R0 ---- */
-    {
-        const uintptr_t p = V0 + 64 * (uintptr_t)j;
-        if (V0 == A) {
-            load_piece(p, al16, w);
-            if (j == 0)
-                w[0] ^= R0;
-        } else {
+    if (s == 0) {
+        if (it.V0 != it.A) {
+            const uintptr_t p = it.V0 + 64 * (uintptr_t)j;
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
-                const uintptr_t q = p + 4 * k;
-                uint32_t v = 0;
-                if (q + 4 > A) {
-                    v = *(g32p)q;
-                    if (q < A)
-                        v &= 0xffffffffu << (8 * (uint32_t)(A - q));
-                }
-                const int64_t d = (int64_t)(A - q);
+                const int64_t d = (int64_t)(it.A - (p + 4 * k));
+                uint32_t v = w[k];
+                if (d > 0 && d < 4)
+                    v &= 0xffffffffu << (8 * (uint32_t)d);
                 if (d >= 0 && d < 4)
-                    v ^= R0 << (8 * (uint32_t)d);
+                    v ^= it.R0 << (8 * (uint32_t)d);
                 else if (d < 0 && d > -4)
-                    v ^= R0 >> (8 * (uint32_t)(-d));
+                    v ^= it.R0 >> (8 * (uint32_t)(-d));
                 w[k] = v;
             }
+        } else if (j == 0) {
+            w[0] ^= it.R0;
         }
+    } else if (s == 1 && j == 0 && it.A + 4 > it.V0 + STEP) {
+        /* R0's bytes can spill past step 0 into lane 0's first word */
+        w[0] ^= it.R0 >> (8 * (uint32_t)(it.V0 + STEP - it.A));
     }
-    if (S == 1) {
-        acc = piece<false>(L, acc, w, c_lo, c_hi);
-    } else {
-        uint32_t nx[16];
-        load_piece(V0 + STEP + 64 * (uintptr_t)j, al16, nx);
-        /* R0's bytes [A, A+4) can spill past step 0 into lane 0's first word */
-        if (j == 0 && A + 4 > V0 + STEP)
-            nx[0] ^= R0 >> (8 * (uint32_t)(V0 + STEP - A));
-        acc = piece<G != 1>(L, acc, w, c_lo, c_hi);
-        for (uint64_t s = 1; s < S; ++s) {
-#pragma unroll
-            for (int k = 0; k < 16; ++k)
-                w[k] = nx[k];
-            if (s + 1 < S) {
-                load_piece(V0 + (s + 1) * STEP + 64 * (uintptr_t)j, al16, nx);
-                acc = piece<G != 1>(L, acc, w, c_lo, c_hi);
-            } else {
-                acc = piece<false>(L, acc, w, c_lo, c_hi);
-            }
-        }
-    }
-    /* ---- fold the team: lane j's register is relative to E - (G-1-j)*64 ---- */
+}
+
+/* Fold the team (lane j's register sits (G-1-j)*64 bytes before E), then the
+ * 0..3 tail bytes.  Result valid in lane G-1. */
+template <int G>
+__device__ __forceinline__ uint32_t finish(const Item &it, uint32_t acc, int j, int lane, const char *L,
+                                           uint32_t c_hi)
+{
 #pragma unroll
     for (int k = 0; (1 << k) < G; ++k) {
         const uint32_t sh = op4(L, OFF_Z + 4096u * k, acc);
@@ -200,10 +224,9 @@ __device__ uint32_t team_register(const uint8_t *a, uint64_t len, uint32_t R0, i
         if (j & (1 << k))
             acc ^= other;
     }
-    /* ---- 0..3 tail bytes ---- */
     if (j == G - 1) {
-        const g8p t = (g8p)E;
-        const uint32_t tail = (uint32_t)((A + len) - E);
+        const g8p t = (g8p)it.E;
+        const uint32_t tail = (uint32_t)((it.A + it.len) - it.E);
         for (uint32_t i = 0; i < tail; ++i)
             acc = byte_step(L, acc, t[i], c_hi);
     }
@@ -251,18 +274,51 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
         team = uni64(team); /* whole-wave team: keep record state in SGPRs */
     const uint64_t nteams = (uint64_t)gridDim.x * WAVES * (64 / G);
 
-    for (uint64_t rec = team; rec < d.n; rec += nteams) {
-        uint64_t len = d.len ? ((const __attribute__((address_space(1))) uint64_t *)d.len)[rec] : d.fixed_len;
-        if (d.last_len != ~0ull && rec + 1 == d.n)
-            len = d.last_len;
-        if (len < d.len_lo || len > d.len_hi)
+    /* Flattened (record, step) walk with the next item's loads in flight
+     * while the current item is computed -- also across record boundaries. */
+    Item nxt;
+    uint64_t ns = 0;
+    bool have = fetch_record<G>(d, team, nteams, nxt);
+    uint32_t nx[16];
+    if (have && nxt.S)
+        issue<G>(nxt, 0, j, nx);
+    uint32_t acc = 0;
+    while (have) {
+        const Item cur = nxt;
+        const uint64_t cs = ns;
+        uint32_t w[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            w[k] = nx[k];
+        if (cur.S && cs + 1 < cur.S) {
+            ns = cs + 1;
+        } else {
+            have = fetch_record<G>(d, cur.rec + nteams, nteams, nxt);
+            ns = 0;
+        }
+        if (have && nxt.S)
+            issue<G>(nxt, ns, j, nx);
+
+        if (cur.S == 0) { /* < 8 bytes: byte-serial on one lane */
+            if (j == G - 1) {
+                uint32_t r = cur.R0;
+                for (uint64_t i = 0; i < cur.len; ++i)
+                    r = byte_step(L, r, ((g8p)cur.A)[i], c_hi);
+                d.out[cur.rec] = r ^ d.xor_io;
+            }
             continue;
-        const uint8_t *a =
-            d.base + (d.off ? ((const __attribute__((address_space(1))) uint64_t *)d.off)[rec] : rec * d.stride);
-        const uint32_t seed = d.seed ? ((g32p)d.seed)[rec] : d.fixed_seed;
-        const uint32_t r = team_register<G>(a, len, seed ^ d.xor_io, j, lane, L, c_lo, c_hi);
-        if (j == G - 1)
-            d.out[rec] = r ^ d.xor_io;
+        }
+        fixup<G>(cur, cs, j, w);
+        if (G > 1 && cs + 1 < cur.S)
+            acc = piece<true>(L, acc, w, c_lo, c_hi);
+        else
+            acc = piece<false>(L, acc, w, c_lo, c_hi);
+        if (cs + 1 == cur.S) {
+            const uint32_t r = finish<G>(cur, acc, j, lane, L, c_hi);
+            if (j == G - 1)
+                d.out[cur.rec] = r ^ d.xor_io;
+            acc = 0;
+        }
     }
 }
 
