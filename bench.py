@@ -169,7 +169,7 @@ def main() -> None:
                        "parallelism": f"shard{world}" + ("+rccl_allgather_digests" if world > 1 else "")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "kernel": "zs::team_kernel<64>",
+                         "traffic": traffic, "kernel": f"zs::team_kernel<{lib().zscrc_team_for(CHUNK, NCHUNK)}>",
                          "kernel_ms": round(kern_ms, 4)},
         }
         if world == 1 and not args.no_cpu:

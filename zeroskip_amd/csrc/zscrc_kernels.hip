@@ -143,7 +143,7 @@ __device__ __forceinline__ bool fetch_record(const BatchDesc &d, uint64_t rec, u
 /* Issue the loads of lane j's piece of step s.  Step 0 of a front-padded grid
  * loads only the dwords that reach the record (the rest is zero); nothing
  * before the record's first aligned dword is ever touched. */
-template <int G>
+template <int G, bool NT>
 __device__ __forceinline__ void issue(const Item &it, uint64_t s, int j, uint32_t (&w)[16])
 {
     constexpr uint64_t STEP = (uint64_t)G * 64;
@@ -158,7 +158,7 @@ __device__ __forceinline__ void issue(const Item &it, uint64_t s, int j, uint32_
         const g4p q = (g4p)p;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const u32x4 v = q[i];
+            const u32x4 v = NT ? __builtin_nontemporal_load(q + i) : q[i];
             w[4 * i + 0] = v.x;
             w[4 * i + 1] = v.y;
             w[4 * i + 2] = v.z;
@@ -169,7 +169,7 @@ __device__ __forceinline__ void issue(const Item &it, uint64_t s, int j, uint32_
         const __attribute__((address_space(1))) u32x2 *q = (const __attribute__((address_space(1))) u32x2 *)p;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            const u32x2 v = q[i];
+            const u32x2 v = NT ? __builtin_nontemporal_load(q + i) : q[i];
             w[2 * i + 0] = v.x;
             w[2 * i + 1] = v.y;
         }
@@ -258,7 +258,59 @@ __device__ void fill_lds(char *L, const uint32_t *__restrict__ gtab)
     }
 }
 
+/* A (record, step) work item of one team. */
+struct Cursor {
+    Item it;
+    uint64_t s;
+    bool ok;
+};
+
 template <int G>
+__device__ __forceinline__ Cursor next_cursor(const BatchDesc &d, const Cursor &c, uint64_t nteams)
+{
+    Cursor n = c;
+    if (!c.ok)
+        return n;
+    if (c.it.S && c.s + 1 < c.it.S) {
+        n.s = c.s + 1;
+        return n;
+    }
+    n.s = 0;
+    n.ok = fetch_record<G>(d, c.it.rec + nteams, nteams, n.it);
+    return n;
+}
+
+/* Compute one item whose words are in w; emits the record's CRC after its
+ * last step. */
+template <int G>
+__device__ __forceinline__ void compute(const BatchDesc &d, const Cursor &c, uint32_t (&w)[16],
+                                        uint32_t &acc, int j, int lane, const char *L, uint32_t c_lo,
+                                        uint32_t c_hi)
+{
+    const Item &it = c.it;
+    if (it.S == 0) { /* < 8 bytes: byte-serial on one lane */
+        if (j == G - 1) {
+            uint32_t r = it.R0;
+            for (uint64_t i = 0; i < it.len; ++i)
+                r = byte_step(L, r, ((g8p)it.A)[i], c_hi);
+            d.out[it.rec] = r ^ d.xor_io;
+        }
+        return;
+    }
+    fixup<G>(it, c.s, j, w);
+    if (G > 1 && c.s + 1 < it.S)
+        acc = piece<true>(L, acc, w, c_lo, c_hi);
+    else
+        acc = piece<false>(L, acc, w, c_lo, c_hi);
+    if (c.s + 1 == it.S) {
+        const uint32_t r = finish<G>(it, acc, j, lane, L, c_hi);
+        if (j == G - 1)
+            d.out[it.rec] = r ^ d.xor_io;
+        acc = 0;
+    }
+}
+
+template <int G, bool NT>
 __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
 {
     __shared__ __attribute__((aligned(16))) char L[LDS_BYTES];
@@ -274,50 +326,49 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
         team = uni64(team); /* whole-wave team: keep record state in SGPRs */
     const uint64_t nteams = (uint64_t)gridDim.x * WAVES * (64 / G);
 
-    /* Flattened (record, step) walk with the next item's loads in flight
-     * while the current item is computed -- also across record boundaries. */
-    Item nxt;
-    uint64_t ns = 0;
-    bool have = fetch_record<G>(d, team, nteams, nxt);
-    uint32_t nx[16];
-    if (have && nxt.S)
-        issue<G>(nxt, 0, j, nx);
+    /* Flattened (record, step) walk.  Two items' loads stay in flight while
+     * a third is computed (a ring of two 64-byte register buffers per lane),
+     * also across record boundaries. */
+    Cursor c0;
+    c0.s = 0;
+    c0.ok = fetch_record<G>(d, team, nteams, c0.it);
+    Cursor c1 = next_cursor<G>(d, c0, nteams);
+    uint32_t ba[16], bb[16];
+    if (c0.ok && c0.it.S)
+        issue<G, NT>(c0.it, c0.s, j, ba);
+    if (c1.ok && c1.it.S)
+        issue<G, NT>(c1.it, c1.s, j, bb);
     uint32_t acc = 0;
-    while (have) {
-        const Item cur = nxt;
-        const uint64_t cs = ns;
-        uint32_t w[16];
+    for (;;) {
+        if (!c0.ok)
+            break;
+        {
+            uint32_t w[16];
 #pragma unroll
-        for (int k = 0; k < 16; ++k)
-            w[k] = nx[k];
-        if (cur.S && cs + 1 < cur.S) {
-            ns = cs + 1;
-        } else {
-            have = fetch_record<G>(d, cur.rec + nteams, nteams, nxt);
-            ns = 0;
+            for (int k = 0; k < 16; ++k)
+                w[k] = ba[k];
+            const Cursor cur = c0;
+            const Cursor c2 = next_cursor<G>(d, c1, nteams);
+            if (c2.ok && c2.it.S)
+                issue<G, NT>(c2.it, c2.s, j, ba);
+            c0 = c1;
+            c1 = c2;
+            compute<G>(d, cur, w, acc, j, lane, L, c_lo, c_hi);
         }
-        if (have && nxt.S)
-            issue<G>(nxt, ns, j, nx);
-
-        if (cur.S == 0) { /* < 8 bytes: byte-serial on one lane */
-            if (j == G - 1) {
-                uint32_t r = cur.R0;
-                for (uint64_t i = 0; i < cur.len; ++i)
-                    r = byte_step(L, r, ((g8p)cur.A)[i], c_hi);
-                d.out[cur.rec] = r ^ d.xor_io;
-            }
-            continue;
-        }
-        fixup<G>(cur, cs, j, w);
-        if (G > 1 && cs + 1 < cur.S)
-            acc = piece<true>(L, acc, w, c_lo, c_hi);
-        else
-            acc = piece<false>(L, acc, w, c_lo, c_hi);
-        if (cs + 1 == cur.S) {
-            const uint32_t r = finish<G>(cur, acc, j, lane, L, c_hi);
-            if (j == G - 1)
-                d.out[cur.rec] = r ^ d.xor_io;
-            acc = 0;
+        if (!c0.ok)
+            break;
+        {
+            uint32_t w[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                w[k] = bb[k];
+            const Cursor cur = c0;
+            const Cursor c2 = next_cursor<G>(d, c1, nteams);
+            if (c2.ok && c2.it.S)
+                issue<G, NT>(c2.it, c2.s, j, bb);
+            c0 = c1;
+            c1 = c2;
+            compute<G>(d, cur, w, acc, j, lane, L, c_lo, c_hi);
         }
     }
 }
@@ -381,22 +432,22 @@ __global__ __launch_bounds__(1024) void span_fold_kernel(SpanFold f)
 } // namespace zs
 
 /* ------------------------------------------------------------ launchers */
-extern "C" int zs_launch_team(int g, const zs::BatchDesc *d, const uint32_t *gtab, int grid,
+extern "C" int zs_launch_team(int g, int nt, const zs::BatchDesc *d, const uint32_t *gtab, int grid,
                               hipStream_t stream)
 {
-    switch (g) {
-    case 1:
-        hipLaunchKernelGGL(zs::team_kernel<1>, dim3(grid), dim3(zs::WG), 0, stream, *d, gtab);
-        break;
-    case 16:
-        hipLaunchKernelGGL(zs::team_kernel<16>, dim3(grid), dim3(zs::WG), 0, stream, *d, gtab);
-        break;
-    case 64:
-        hipLaunchKernelGGL(zs::team_kernel<64>, dim3(grid), dim3(zs::WG), 0, stream, *d, gtab);
-        break;
+#define ZS_LAUNCH(G, NT) \
+    hipLaunchKernelGGL((zs::team_kernel<G, NT>), dim3(grid), dim3(zs::WG), 0, stream, *d, gtab)
+    switch (g * 2 + (nt ? 1 : 0)) {
+    case 2: ZS_LAUNCH(1, false); break;
+    case 3: ZS_LAUNCH(1, true); break;
+    case 32: ZS_LAUNCH(16, false); break;
+    case 33: ZS_LAUNCH(16, true); break;
+    case 128: ZS_LAUNCH(64, false); break;
+    case 129: ZS_LAUNCH(64, true); break;
     default:
         return -1;
     }
+#undef ZS_LAUNCH
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
