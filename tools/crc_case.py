@@ -1,0 +1,21 @@
+"""Run one fixed-stride batch case repeatedly (profiling target).
+usage: python tools/crc_case.py STRIDE LEN N [G1_MAX G16_MAX] [REPS]"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from zeroskip_amd import device as zd  # noqa: E402
+from zeroskip_amd._lib import lib  # noqa: E402
+
+stride, length, n = (int(x) for x in sys.argv[1:4])
+if len(sys.argv) > 5:
+    lib().zscrc_set_teams(int(sys.argv[4]), int(sys.argv[5]))
+reps = int(sys.argv[6]) if len(sys.argv) > 6 else 5
+d = torch.randint(0, 256, (stride * (n - 1) + length,), dtype=torch.uint8, device="cuda")
+out = torch.empty(n, dtype=torch.int32, device="cuda")
+for _ in range(reps):
+    zd.crc_fixed(d, stride, length, n, out=out)
+torch.cuda.synchronize()
+print("done", stride, length, n)
