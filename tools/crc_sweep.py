@@ -50,14 +50,12 @@ def main():
     ]
     for name, stride, length, n, teams in cases:
         lib().zscrc_set_teams(*teams)
-        for nt in (0, 1):
-            lib().zscrc_set_nt(nt)
+        for nt in (0,):
             ms = timeit(lambda: zd.crc_fixed(big, stride, length, n, out=out[:n]))
             byt = n * length
             print(json.dumps({"case": name, "nt": nt, "ms": round(ms, 4),
                               "GBs": round(byt / ms / 1e6, 1),
                               "GiBs": round(byt / ms / 1e6 * 1e9 / (1 << 30), 1)}), flush=True)
-    lib().zscrc_set_nt(0)
     lib().zscrc_set_teams(1024, 1 << 20)
     ms = timeit(lambda: zd.crc_span(big))
     print(json.dumps({"case": "span 4 GiB", "ms": round(ms, 4), "GBs": round((4 << 30) / ms / 1e6, 1)}))

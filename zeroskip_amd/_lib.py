@@ -32,7 +32,6 @@ SIGNATURES = {
     "zscrc_stats": (None, [_vp]),
     "zscrc_set_gpu_min": (None, [_u64]),
     "zscrc_set_teams": (None, [_u64, _u64]),
-    "zscrc_set_nt": (None, [_int]),
     "zscrc_team_for": (_int, [_u64, _u64]),
     "zscrc_device_count": (_int, []),
 }

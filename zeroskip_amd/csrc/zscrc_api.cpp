@@ -26,7 +26,7 @@ uint32_t zscrc_cpu_table(uint32_t crc, const void *buf, size_t len);
 uint32_t zscrc_cpu_hw(uint32_t crc, const void *buf, size_t len);
 int zscrc_cpu_have_sse42(void);
 void zscrc_cpu_init(void);
-int zs_launch_team(int g, int nt, const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
+int zs_launch_team(int g, int fixed, const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
 int zs_launch_span_fold(const zs::SpanFold *f, hipStream_t stream);
 }
 
@@ -42,7 +42,6 @@ std::atomic<uint64_t> g_gpu_min{0};
 std::atomic<uint64_t> g_g1_max{1024};
 std::atomic<uint64_t> g_g16_max{1u << 20};
 int g_strict = 0;
-std::atomic<int> g_nt{0}; /* non-temporal data loads (env ZSCRC_NT) */
 
 struct DevCtx {
     std::mutex mu;
@@ -69,9 +68,6 @@ void env_init()
         g_gpu_min = strtoull(s, nullptr, 0);
     s = getenv("ZSCRC_STRICT");
     g_strict = s && *s && *s != '0';
-    s = getenv("ZSCRC_NT");
-    if (s)
-        g_nt = atoi(s);
     s = getenv("ZSCRC_G1_MAX");
     if (s)
         g_g1_max = strtoull(s, nullptr, 0);
@@ -184,7 +180,9 @@ zs::BatchDesc make_desc()
 
 int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s)
 {
-    int rc = zs_launch_team(g, g_nt, &d, c->gtab, c->ncu, s);
+    /* fixed-stride form when no per-record arrays are involved */
+    const int fixed = !d.off && !d.len && !d.seed && d.len_lo == 0 && d.len_hi == ~0ull;
+    int rc = zs_launch_team(g, fixed, &d, c->gtab, c->ncu, s);
     if (rc) {
         set_err("team kernel launch", hipGetLastError());
         return ZSCRC_EHIP;
@@ -512,12 +510,6 @@ void zscrc_set_gpu_min(uint64_t min_bytes)
 {
     std::call_once(g_env_once, env_init);
     g_gpu_min = min_bytes;
-}
-
-void zscrc_set_nt(int on)
-{
-    std::call_once(g_env_once, env_init);
-    g_nt = on ? 1 : 0;
 }
 
 int zscrc_team_for(uint64_t len, uint64_t n)

@@ -111,20 +111,35 @@ struct Item {
     uint32_t R0;      /* initial register */
 };
 
+/* A (record, step) work item of one team. */
+struct Cursor {
+    Item it;
+    uint64_t s;
+    bool ok;
+};
+
 /* Next record for this team at or after `rec` that passes the length filter. */
-template <int G>
+/* FIXED: record i = base + i*stride, fixed_len bytes (last_len for the last
+ * one when set), fixed_seed -- no per-record metadata loads, so nothing here
+ * waits on the vector-memory counter and the data prefetch ring survives. */
+template <int G, bool FIXED>
 __device__ __forceinline__ bool fetch_record(const BatchDesc &d, uint64_t rec, uint64_t nteams, Item &it)
 {
     constexpr uint64_t STEP = (uint64_t)G * 64;
     for (; rec < d.n; rec += nteams) {
-        uint64_t len = d.len ? ((const __attribute__((address_space(1))) uint64_t *)d.len)[rec] : d.fixed_len;
-        if (d.last_len != ~0ull && rec + 1 == d.n)
-            len = d.last_len;
-        if (len < d.len_lo || len > d.len_hi)
-            continue;
-        const uint64_t off =
-            d.off ? ((const __attribute__((address_space(1))) uint64_t *)d.off)[rec] : rec * d.stride;
-        const uint32_t seed = d.seed ? ((g32p)d.seed)[rec] : d.fixed_seed;
+        uint64_t len, off;
+        uint32_t seed;
+        if (FIXED) {
+            len = (d.last_len != ~0ull && rec + 1 == d.n) ? d.last_len : d.fixed_len;
+            off = rec * d.stride;
+            seed = d.fixed_seed;
+        } else {
+            len = d.len ? ((const __attribute__((address_space(1))) uint64_t *)d.len)[rec] : d.fixed_len;
+            if (len < d.len_lo || len > d.len_hi)
+                continue;
+            off = d.off ? ((const __attribute__((address_space(1))) uint64_t *)d.off)[rec] : rec * d.stride;
+            seed = d.seed ? ((g32p)d.seed)[rec] : d.fixed_seed;
+        }
         const uintptr_t A = reinterpret_cast<uintptr_t>(d.base) + off;
         const uintptr_t E = len < 8 ? A : ((A + len) & ~uintptr_t(3));
         const uint64_t S = len < 8 ? 0 : (E - A + STEP - 1) / STEP;
@@ -140,49 +155,34 @@ __device__ __forceinline__ bool fetch_record(const BatchDesc &d, uint64_t rec, u
     return false;
 }
 
-/* Issue the loads of lane j's piece of step s.  Step 0 of a front-padded grid
- * loads only the dwords that reach the record (the rest is zero); nothing
- * before the record's first aligned dword is ever touched. */
-template <int G, bool NT>
-__device__ __forceinline__ void issue(const Item &it, uint64_t s, int j, uint32_t (&w)[16])
+/* Issue the loads of lane j's piece of step s: always exactly four 16-byte
+ * loads (gfx950 serves 4-byte-aligned dwordx4 loads; tools/unaligned_probe),
+ * so the compiler can count the prefetch ring with partial vmcnt waits.  In
+ * a front-padded step 0 each block address is clamped up to the record's
+ * first aligned dword, so nothing before the record is ever touched (fixup
+ * re-aligns the clamped block).  Items without loads read a dummy address. */
+template <int G>
+__device__ __forceinline__ void issue(const Cursor &c, int j, uintptr_t dummy, uint32_t (&w)[16])
 {
     constexpr uint64_t STEP = (uint64_t)G * 64;
-    const uintptr_t p = it.V0 + s * STEP + 64 * (uintptr_t)j;
-    if (s == 0 && it.V0 != it.A) {
+    const bool live = c.ok && c.it.S;
+    const uintptr_t p = c.it.V0 + c.s * STEP + 64 * (uintptr_t)j;
+    const uintptr_t lo = c.it.A & ~uintptr_t(3);
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const uintptr_t q = p + 4 * k;
-            w[k] = (q + 4 > it.A) ? *(g32p)q : 0u;
-        }
-    } else if ((it.V0 & 15) == 0) {
-        const g4p q = (g4p)p;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const u32x4 v = NT ? __builtin_nontemporal_load(q + i) : q[i];
-            w[4 * i + 0] = v.x;
-            w[4 * i + 1] = v.y;
-            w[4 * i + 2] = v.z;
-            w[4 * i + 3] = v.w;
-        }
-    } else if ((it.V0 & 7) == 0) {
-        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-        const __attribute__((address_space(1))) u32x2 *q = (const __attribute__((address_space(1))) u32x2 *)p;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const u32x2 v = NT ? __builtin_nontemporal_load(q + i) : q[i];
-            w[2 * i + 0] = v.x;
-            w[2 * i + 1] = v.y;
-        }
-    } else {
-        const g32p q = (g32p)p;
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-            w[i] = q[i];
+    for (int i = 0; i < 4; ++i) {
+        uintptr_t q = p + 16 * i;
+        q = q < lo ? lo : q;
+        const u32x4 v = *(g4p)(live ? q : dummy);
+        w[4 * i + 0] = v.x;
+        w[4 * i + 1] = v.y;
+        w[4 * i + 2] = v.z;
+        w[4 * i + 3] = v.w;
     }
 }
 
-/* Data fix-ups that need the record start: zero bytes before A in the word
- * that straddles it, and XOR the initial register into bytes [A, A+4). */
+/* Data fix-ups that need the record start (step 0 of a front-padded grid):
+ * undo the clamp of issue(), zero every byte before A, and XOR the initial
+ * register into bytes [A, A+4) -- which can spill into step 1. */
 template <int G>
 __device__ __forceinline__ void fixup(const Item &it, uint64_t s, int j, uint32_t (&w)[16])
 {
@@ -190,11 +190,24 @@ __device__ __forceinline__ void fixup(const Item &it, uint64_t s, int j, uint32_
     if (s == 0) {
         if (it.V0 != it.A) {
             const uintptr_t p = it.V0 + 64 * (uintptr_t)j;
+            const uintptr_t lo = it.A & ~uintptr_t(3);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uintptr_t q = p + 16 * i;
+                /* the block was loaded from max(q, lo): shift it up by m words */
+                const uint64_t m = q < lo ? (lo - q) >> 2 : 0;
+                const uint32_t b0 = w[4 * i], b1 = w[4 * i + 1], b2 = w[4 * i + 2];
+                w[4 * i + 3] = m == 0 ? w[4 * i + 3] : m == 1 ? b2 : m == 2 ? b1 : b0;
+                w[4 * i + 2] = m == 0 ? b2 : m == 1 ? b1 : b0;
+                w[4 * i + 1] = m == 0 ? b1 : b0;
+            }
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
                 const int64_t d = (int64_t)(it.A - (p + 4 * k));
                 uint32_t v = w[k];
-                if (d > 0 && d < 4)
+                if (d >= 4)
+                    v = 0;
+                else if (d > 0)
                     v &= 0xffffffffu << (8 * (uint32_t)d);
                 if (d >= 0 && d < 4)
                     v ^= it.R0 << (8 * (uint32_t)d);
@@ -206,7 +219,6 @@ __device__ __forceinline__ void fixup(const Item &it, uint64_t s, int j, uint32_
             w[0] ^= it.R0;
         }
     } else if (s == 1 && j == 0 && it.A + 4 > it.V0 + STEP) {
-        /* R0's bytes can spill past step 0 into lane 0's first word */
         w[0] ^= it.R0 >> (8 * (uint32_t)(it.V0 + STEP - it.A));
     }
 }
@@ -258,14 +270,7 @@ __device__ void fill_lds(char *L, const uint32_t *__restrict__ gtab)
     }
 }
 
-/* A (record, step) work item of one team. */
-struct Cursor {
-    Item it;
-    uint64_t s;
-    bool ok;
-};
-
-template <int G>
+template <int G, bool FIXED>
 __device__ __forceinline__ Cursor next_cursor(const BatchDesc &d, const Cursor &c, uint64_t nteams)
 {
     Cursor n = c;
@@ -276,7 +281,7 @@ __device__ __forceinline__ Cursor next_cursor(const BatchDesc &d, const Cursor &
         return n;
     }
     n.s = 0;
-    n.ok = fetch_record<G>(d, c.it.rec + nteams, nteams, n.it);
+    n.ok = fetch_record<G, FIXED>(d, c.it.rec + nteams, nteams, n.it);
     return n;
 }
 
@@ -310,7 +315,7 @@ __device__ __forceinline__ void compute(const BatchDesc &d, const Cursor &c, uin
     }
 }
 
-template <int G, bool NT>
+template <int G, bool FIXED>
 __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
 {
     __shared__ __attribute__((aligned(16))) char L[LDS_BYTES];
@@ -326,26 +331,62 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
         team = uni64(team); /* whole-wave team: keep record state in SGPRs */
     const uint64_t nteams = (uint64_t)gridDim.x * WAVES * (64 / G);
 
-    /* Flattened (record, step) walk: the next item's loads are in flight
-     * while the current one is computed, also across record boundaries.
-     * (A two-deep register ring measured 4 % slower on config 3.) */
-    Cursor nxt;
-    nxt.s = 0;
-    nxt.ok = fetch_record<G>(d, team, nteams, nxt.it);
-    uint32_t nx[16];
-    if (nxt.ok && nxt.it.S)
-        issue<G, NT>(nxt.it, 0, j, nx);
+    /* Flattened (record, step) walk, loads running ahead of compute also
+     * across record boundaries.  Fixed-stride batches keep two items in flight
+     * (ring of two 64-byte register buffers); variable batches one, because
+     * their per-record metadata loads wait on the same vmcnt counter. */
+    Cursor c0;
+    c0.s = 0;
+    c0.ok = fetch_record<G, FIXED>(d, team, nteams, c0.it);
     uint32_t acc = 0;
-    while (nxt.ok) {
-        const Cursor cur = nxt;
-        uint32_t w[16];
+    const uintptr_t dummy = reinterpret_cast<uintptr_t>(gtab);
+    uint32_t ba[16];
+    issue<G>(c0, j, dummy, ba);
+    if (FIXED) {
+        Cursor c1 = next_cursor<G, FIXED>(d, c0, nteams);
+        uint32_t bb[16];
+        issue<G>(c1, j, dummy, bb);
+        for (;;) {
+            if (!c0.ok)
+                break;
+            {
+                uint32_t w[16];
 #pragma unroll
-        for (int k = 0; k < 16; ++k)
-            w[k] = nx[k];
-        nxt = next_cursor<G>(d, cur, nteams);
-        if (nxt.ok && nxt.it.S)
-            issue<G, NT>(nxt.it, nxt.s, j, nx);
-        compute<G>(d, cur, w, acc, j, lane, L, c_lo, c_hi);
+                for (int k = 0; k < 16; ++k)
+                    w[k] = ba[k];
+                const Cursor cur = c0;
+                const Cursor c2 = next_cursor<G, FIXED>(d, c1, nteams);
+                issue<G>(c2, j, dummy, ba);
+                c0 = c1;
+                c1 = c2;
+                compute<G>(d, cur, w, acc, j, lane, L, c_lo, c_hi);
+            }
+            if (!c0.ok)
+                break;
+            {
+                uint32_t w[16];
+#pragma unroll
+                for (int k = 0; k < 16; ++k)
+                    w[k] = bb[k];
+                const Cursor cur = c0;
+                const Cursor c2 = next_cursor<G, FIXED>(d, c1, nteams);
+                issue<G>(c2, j, dummy, bb);
+                c0 = c1;
+                c1 = c2;
+                compute<G>(d, cur, w, acc, j, lane, L, c_lo, c_hi);
+            }
+        }
+    } else {
+        while (c0.ok) {
+            const Cursor cur = c0;
+            uint32_t w[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                w[k] = ba[k];
+            c0 = next_cursor<G, FIXED>(d, cur, nteams);
+            issue<G>(c0, j, dummy, ba);
+            compute<G>(d, cur, w, acc, j, lane, L, c_lo, c_hi);
+        }
     }
 }
 
@@ -408,12 +449,12 @@ __global__ __launch_bounds__(1024) void span_fold_kernel(SpanFold f)
 } // namespace zs
 
 /* ------------------------------------------------------------ launchers */
-extern "C" int zs_launch_team(int g, int nt, const zs::BatchDesc *d, const uint32_t *gtab, int grid,
+extern "C" int zs_launch_team(int g, int fixed, const zs::BatchDesc *d, const uint32_t *gtab, int grid,
                               hipStream_t stream)
 {
-#define ZS_LAUNCH(G, NT) \
-    hipLaunchKernelGGL((zs::team_kernel<G, NT>), dim3(grid), dim3(zs::WG), 0, stream, *d, gtab)
-    switch (g * 2 + (nt ? 1 : 0)) {
+#define ZS_LAUNCH(G, FIXED) \
+    hipLaunchKernelGGL((zs::team_kernel<G, FIXED>), dim3(grid), dim3(zs::WG), 0, stream, *d, gtab)
+    switch (g * 2 + (fixed ? 1 : 0)) {
     case 2: ZS_LAUNCH(1, false); break;
     case 3: ZS_LAUNCH(1, true); break;
     case 32: ZS_LAUNCH(16, false); break;
