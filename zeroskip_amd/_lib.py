@@ -33,6 +33,7 @@ SIGNATURES = {
     "zscrc_set_gpu_min": (None, [_u64]),
     "zscrc_set_teams": (None, [_u64, _u64]),
     "zscrc_team_for": (_int, [_u64, _u64]),
+    "zscrc_set_prefetch": (None, [_int, _int]),
     "zscrc_device_count": (_int, []),
 }
 

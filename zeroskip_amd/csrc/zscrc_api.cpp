@@ -26,7 +26,8 @@ uint32_t zscrc_cpu_table(uint32_t crc, const void *buf, size_t len);
 uint32_t zscrc_cpu_hw(uint32_t crc, const void *buf, size_t len);
 int zscrc_cpu_have_sse42(void);
 void zscrc_cpu_init(void);
-int zs_launch_team(int g, int fixed, const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
+int zs_launch_team(int g, int fixed, int depth, const zs::BatchDesc *d, const uint32_t *gtab, int grid,
+                   hipStream_t stream);
 int zs_launch_span_fold(const zs::SpanFold *f, hipStream_t stream);
 }
 
@@ -42,6 +43,8 @@ std::atomic<uint64_t> g_gpu_min{0};
 std::atomic<uint64_t> g_g1_max{1024};
 std::atomic<uint64_t> g_g16_max{1u << 20};
 int g_strict = 0;
+/* prefetch depth of fixed-stride launches per team size (1 or 2), index 0/1/2 = G 1/16/64 */
+std::atomic<int> g_depth[3] = {{2}, {1}, {1}};
 
 struct DevCtx {
     std::mutex mu;
@@ -182,7 +185,8 @@ int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s)
 {
     /* fixed-stride form when no per-record arrays are involved */
     const int fixed = !d.off && !d.len && !d.seed && d.len_lo == 0 && d.len_hi == ~0ull;
-    int rc = zs_launch_team(g, fixed, &d, c->gtab, c->ncu, s);
+    const int depth = g_depth[g == 1 ? 0 : g == 16 ? 1 : 2];
+    int rc = zs_launch_team(g, fixed, depth, &d, c->gtab, c->ncu, s);
     if (rc) {
         set_err("team kernel launch", hipGetLastError());
         return ZSCRC_EHIP;
@@ -510,6 +514,18 @@ void zscrc_set_gpu_min(uint64_t min_bytes)
 {
     std::call_once(g_env_once, env_init);
     g_gpu_min = min_bytes;
+}
+
+void zscrc_set_prefetch(int g, int depth)
+{
+    if (depth < 1 || depth > 2)
+        return;
+    if (g == 1)
+        g_depth[0] = depth;
+    else if (g == 16)
+        g_depth[1] = depth;
+    else if (g == 64)
+        g_depth[2] = depth;
 }
 
 int zscrc_team_for(uint64_t len, uint64_t n)

@@ -165,14 +165,25 @@ template <int G>
 __device__ __forceinline__ void issue(const Cursor &c, int j, uintptr_t dummy, uint32_t (&w)[16])
 {
     constexpr uint64_t STEP = (uint64_t)G * 64;
-    const bool live = c.ok && c.it.S;
     const uintptr_t p = c.it.V0 + c.s * STEP + 64 * (uintptr_t)j;
-    const uintptr_t lo = c.it.A & ~uintptr_t(3);
+    uintptr_t q[4];
+    if (!(c.ok && c.it.S)) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            q[i] = dummy;
+    } else if (c.s == 0 && c.it.V0 != c.it.A) {
+        const uintptr_t lo = c.it.A & ~uintptr_t(3);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            q[i] = p + 16 * i < lo ? lo : p + 16 * i;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            q[i] = p + 16 * i;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        uintptr_t q = p + 16 * i;
-        q = q < lo ? lo : q;
-        const u32x4 v = *(g4p)(live ? q : dummy);
+        const u32x4 v = *(g4p)q[i];
         w[4 * i + 0] = v.x;
         w[4 * i + 1] = v.y;
         w[4 * i + 2] = v.z;
@@ -315,7 +326,7 @@ __device__ __forceinline__ void compute(const BatchDesc &d, const Cursor &c, uin
     }
 }
 
-template <int G, bool FIXED>
+template <int G, bool FIXED, int DEPTH>
 __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
 {
     __shared__ __attribute__((aligned(16))) char L[LDS_BYTES];
@@ -342,7 +353,7 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(gtab);
     uint32_t ba[16];
     issue<G>(c0, j, dummy, ba);
-    if (FIXED) {
+    if (FIXED && DEPTH == 2) {
         Cursor c1 = next_cursor<G, FIXED>(d, c0, nteams);
         uint32_t bb[16];
         issue<G>(c1, j, dummy, bb);
@@ -449,18 +460,22 @@ __global__ __launch_bounds__(1024) void span_fold_kernel(SpanFold f)
 } // namespace zs
 
 /* ------------------------------------------------------------ launchers */
-extern "C" int zs_launch_team(int g, int fixed, const zs::BatchDesc *d, const uint32_t *gtab, int grid,
-                              hipStream_t stream)
+extern "C" int zs_launch_team(int g, int fixed, int depth, const zs::BatchDesc *d, const uint32_t *gtab,
+                              int grid, hipStream_t stream)
 {
-#define ZS_LAUNCH(G, FIXED) \
-    hipLaunchKernelGGL((zs::team_kernel<G, FIXED>), dim3(grid), dim3(zs::WG), 0, stream, *d, gtab)
-    switch (g * 2 + (fixed ? 1 : 0)) {
-    case 2: ZS_LAUNCH(1, false); break;
-    case 3: ZS_LAUNCH(1, true); break;
-    case 32: ZS_LAUNCH(16, false); break;
-    case 33: ZS_LAUNCH(16, true); break;
-    case 128: ZS_LAUNCH(64, false); break;
-    case 129: ZS_LAUNCH(64, true); break;
+#define ZS_LAUNCH(G, FIXED, DEPTH) \
+    hipLaunchKernelGGL((zs::team_kernel<G, FIXED, DEPTH>), dim3(grid), dim3(zs::WG), 0, stream, *d, gtab)
+    const int key = g * 4 + (fixed ? 2 : 0) + (fixed && depth == 2 ? 1 : 0);
+    switch (key) {
+    case 4: ZS_LAUNCH(1, false, 1); break;
+    case 6: ZS_LAUNCH(1, true, 1); break;
+    case 7: ZS_LAUNCH(1, true, 2); break;
+    case 64: ZS_LAUNCH(16, false, 1); break;
+    case 66: ZS_LAUNCH(16, true, 1); break;
+    case 67: ZS_LAUNCH(16, true, 2); break;
+    case 256: ZS_LAUNCH(64, false, 1); break;
+    case 258: ZS_LAUNCH(64, true, 1); break;
+    case 259: ZS_LAUNCH(64, true, 2); break;
     default:
         return -1;
     }
