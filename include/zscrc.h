@@ -113,12 +113,16 @@ void zscrc_set_gpu_min(uint64_t min_bytes);
 /* team size tuning: records <= g1_max bytes use one lane each, <= g16_max a
  * 16-lane team, larger a 64-lane (whole wavefront) team. */
 void zscrc_set_teams(uint64_t g1_max, uint64_t g16_max);
-/* tuning: register-prefetch depth (1 or 2 items) of fixed-stride launches
- * for team size g (1, 16 or 64) */
+/* tuning: record walk for team size g (1, 16 or 64): 0 = two-level loop,
+ * 1 / 2 = flattened (record, step) loop with a 1- / 2-item register ring */
 void zscrc_set_prefetch(int g, int depth);
 /* team size the fixed-stride path picks for n records of len bytes (1/16/64;
  * 0 if no device) */
 int zscrc_team_for(uint64_t len, uint64_t n);
+/* Diagnostic: plain streaming read of len bytes (multiple of 4096) -- the
+ * measured HBM read ceiling on this GPU.  d_scratch4: 4 writable device bytes. */
+int zscrc_diag_stream_read(const void *d_buf, uint64_t len, void *d_scratch4, int grid_mult,
+                           void *stream);
 /* Number of gfx950 devices visible (0 if none / no HIP runtime). */
 int zscrc_device_count(void);
 

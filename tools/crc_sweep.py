@@ -48,10 +48,16 @@ def main():
         ("256KiB g64", 262144, 262144, 16384, (0, 0)),
         ("1MiB g64 (4096 recs)", 1 << 20, 1 << 20, 4096, (0, 0)),
     ]
+    scratch = torch.zeros(4, dtype=torch.int32, device=dev)
+    for mult in (1, 2, 4):
+        ms = timeit(lambda: lib().zscrc_diag_stream_read(big.data_ptr(), 4 << 30, scratch.data_ptr(),
+                                                          mult, torch.cuda.current_stream().cuda_stream))
+        print(json.dumps({"case": f"stream_read grid x{mult}", "ms": round(ms, 4),
+                          "GBs": round((4 << 30) / ms / 1e6, 1)}), flush=True)
     for name, stride, length, n, teams in cases:
         lib().zscrc_set_teams(*teams)
         g = 1 if teams[0] >= length else (16 if teams[1] >= length else 64)
-        for depth in (1, 2, 1, 2):
+        for depth in (0, 1, 2, 0, 1, 2):
             lib().zscrc_set_prefetch(g, depth)
             ms = timeit(lambda: zd.crc_fixed(big, stride, length, n, out=out[:n]))
             byt = n * length

@@ -29,6 +29,7 @@ void zscrc_cpu_init(void);
 int zs_launch_team(int g, int fixed, int depth, const zs::BatchDesc *d, const uint32_t *gtab, int grid,
                    hipStream_t stream);
 int zs_launch_span_fold(const zs::SpanFold *f, hipStream_t stream);
+int zs_launch_stream_read(const void *buf, uint64_t n, uint32_t *out, int grid, hipStream_t stream);
 }
 
 namespace {
@@ -43,7 +44,8 @@ std::atomic<uint64_t> g_gpu_min{0};
 std::atomic<uint64_t> g_g1_max{1024};
 std::atomic<uint64_t> g_g16_max{1u << 20};
 int g_strict = 0;
-/* prefetch depth of fixed-stride launches per team size (1 or 2), index 0/1/2 = G 1/16/64 */
+/* walk of fixed-stride launches per team size: 0 two-level, 1/2 flattened with a
+ * 1/2-item ring; index 0/1/2 = G 1/16/64 (variable batches: 0 or 1) */
 std::atomic<int> g_depth[3] = {{2}, {1}, {1}};
 
 struct DevCtx {
@@ -502,6 +504,22 @@ int zscrc_host_batch(const void *base, const uint64_t *off, const uint64_t *len,
     return ZSCRC_OK;
 }
 
+int zscrc_diag_stream_read(const void *d_buf, uint64_t len, void *d_scratch4, int grid_mult, void *stream)
+{
+    DevCtx *c;
+    int rc = get_ctx(&c);
+    if (rc)
+        return rc;
+    if (grid_mult < 1)
+        grid_mult = 1;
+    if (zs_launch_stream_read(d_buf, len, static_cast<uint32_t *>(d_scratch4), c->ncu * grid_mult,
+                              static_cast<hipStream_t>(stream))) {
+        set_err("stream read launch", hipGetLastError());
+        return ZSCRC_EHIP;
+    }
+    return ZSCRC_OK;
+}
+
 const char *zscrc_last_error(void) { return t_err; }
 
 void zscrc_stats(uint64_t out[4])
@@ -518,7 +536,7 @@ void zscrc_set_gpu_min(uint64_t min_bytes)
 
 void zscrc_set_prefetch(int g, int depth)
 {
-    if (depth < 1 || depth > 2)
+    if (depth < 0 || depth > 2)
         return;
     if (g == 1)
         g_depth[0] = depth;

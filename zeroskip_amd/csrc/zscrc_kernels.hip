@@ -191,6 +191,19 @@ __device__ __forceinline__ void issue(const Cursor &c, int j, uintptr_t dummy, u
     }
 }
 
+/* Four plain 16-byte loads of the piece at p (interior steps). */
+__device__ __forceinline__ void issue_plain(uintptr_t p, uint32_t (&w)[16])
+{
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const u32x4 v = *(g4p)(p + 16 * i);
+        w[4 * i + 0] = v.x;
+        w[4 * i + 1] = v.y;
+        w[4 * i + 2] = v.z;
+        w[4 * i + 3] = v.w;
+    }
+}
+
 /* Data fix-ups that need the record start (step 0 of a front-padded grid):
  * undo the clamp of issue(), zero every byte before A, and XOR the initial
  * register into bytes [A, A+4) -- which can spill into step 1. */
@@ -353,7 +366,75 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(gtab);
     uint32_t ba[16];
     issue<G>(c0, j, dummy, ba);
-    if (FIXED && DEPTH == 2) {
+    if (DEPTH == 0) {
+        /* Two-level walk: a lean interior step loop per record (plain loads
+         * one step ahead), the record's first/last steps peeled so the next
+         * record's first piece is loaded while the last piece is computed. */
+        constexpr uint64_t STEP = (uint64_t)G * 64;
+        Item cur = c0.it;
+        bool ok = c0.ok;
+        while (ok) {
+            Item nxt;
+            const bool ok2 = fetch_record<G, FIXED>(d, cur.rec + nteams, nteams, nxt);
+            Cursor cn;
+            cn.it = nxt;
+            cn.s = 0;
+            cn.ok = ok2;
+            uint32_t w[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                w[k] = ba[k];
+            if (cur.S == 0) {
+                issue<G>(cn, j, dummy, ba);
+                if (j == G - 1) {
+                    uint32_t r = cur.R0;
+                    for (uint64_t i = 0; i < cur.len; ++i)
+                        r = byte_step(L, r, ((g8p)cur.A)[i], c_hi);
+                    d.out[cur.rec] = r ^ d.xor_io;
+                }
+                cur = nxt;
+                ok = ok2;
+                continue;
+            }
+            uintptr_t p = cur.V0 + STEP + 64 * (uintptr_t)j;
+            if (cur.S > 1)
+                issue_plain(p, ba);
+            else
+                issue<G>(cn, j, dummy, ba);
+            fixup<G>(cur, 0, j, w);
+            if (G > 1 && cur.S > 1)
+                acc = piece<true>(L, acc, w, c_lo, c_hi);
+            else
+                acc = piece<false>(L, acc, w, c_lo, c_hi);
+            const bool spill = j == 0 && cur.A + 4 > cur.V0 + STEP;
+            const uint32_t spill_v = cur.R0 >> (8 * (uint32_t)((cur.V0 + STEP - cur.A) & 3));
+            for (uint64_t s = 1; s + 1 < cur.S; ++s) {
+#pragma unroll
+                for (int k = 0; k < 16; ++k)
+                    w[k] = ba[k];
+                issue_plain(p + STEP, ba);
+                if (s == 1 && spill)
+                    w[0] ^= spill_v;
+                acc = piece<G != 1>(L, acc, w, c_lo, c_hi);
+                p += STEP;
+            }
+            if (cur.S > 1) {
+#pragma unroll
+                for (int k = 0; k < 16; ++k)
+                    w[k] = ba[k];
+                issue<G>(cn, j, dummy, ba);
+                if (cur.S == 2 && spill)
+                    w[0] ^= spill_v;
+                acc = piece<false>(L, acc, w, c_lo, c_hi);
+            }
+            const uint32_t r = finish<G>(cur, acc, j, lane, L, c_hi);
+            if (j == G - 1)
+                d.out[cur.rec] = r ^ d.xor_io;
+            acc = 0;
+            cur = nxt;
+            ok = ok2;
+        }
+    } else if (FIXED && DEPTH == 2) {
         Cursor c1 = next_cursor<G, FIXED>(d, c0, nteams);
         uint32_t bb[16];
         issue<G>(c1, j, dummy, bb);
@@ -457,28 +538,64 @@ __global__ __launch_bounds__(1024) void span_fold_kernel(SpanFold f)
     }
 }
 
+/* ------------------------------------------------------ diagnostics */
+/* Plain coalesced streaming read (16 B per lane, 1 KiB per wave-instruction,
+ * 4 instructions in flight per wave) XOR-reduced into one word: the measured
+ * HBM read ceiling that the CRC kernels are judged against on the same GPU. */
+__global__ __launch_bounds__(1024) void stream_read_kernel(const uint8_t *buf, uint64_t n, uint32_t *out)
+{
+    const uint64_t wave = (uint64_t)blockIdx.x * 16 + (threadIdx.x >> 6);
+    const uint64_t nw = (uint64_t)gridDim.x * 16;
+    const int lane = threadIdx.x & 63;
+    uint32_t acc = 0;
+    for (uint64_t s = wave; (s + 1) * 4096 <= n; s += nw) {
+        const g4p q = (g4p)(buf + s * 4096 + 16 * (uint64_t)lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const u32x4 v = q[64 * i];
+            acc ^= v.x ^ v.y ^ v.z ^ v.w;
+        }
+    }
+    if (acc == 0x9E3779B9u)
+        out[0] = acc; /* keeps the loads live; practically never taken */
+}
+
 } // namespace zs
 
 /* ------------------------------------------------------------ launchers */
+extern "C" int zs_launch_stream_read(const void *buf, uint64_t n, uint32_t *out, int grid, hipStream_t stream)
+{
+    hipLaunchKernelGGL(zs::stream_read_kernel, dim3(grid), dim3(1024), 0, stream,
+                       static_cast<const uint8_t *>(buf), n, out);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
 extern "C" int zs_launch_team(int g, int fixed, int depth, const zs::BatchDesc *d, const uint32_t *gtab,
                               int grid, hipStream_t stream)
 {
 #define ZS_LAUNCH(G, FIXED, DEPTH) \
     hipLaunchKernelGGL((zs::team_kernel<G, FIXED, DEPTH>), dim3(grid), dim3(zs::WG), 0, stream, *d, gtab)
-    const int key = g * 4 + (fixed ? 2 : 0) + (fixed && depth == 2 ? 1 : 0);
-    switch (key) {
-    case 4: ZS_LAUNCH(1, false, 1); break;
-    case 6: ZS_LAUNCH(1, true, 1); break;
-    case 7: ZS_LAUNCH(1, true, 2); break;
-    case 64: ZS_LAUNCH(16, false, 1); break;
-    case 66: ZS_LAUNCH(16, true, 1); break;
-    case 67: ZS_LAUNCH(16, true, 2); break;
-    case 256: ZS_LAUNCH(64, false, 1); break;
-    case 258: ZS_LAUNCH(64, true, 1); break;
-    case 259: ZS_LAUNCH(64, true, 2); break;
+#define ZS_CASES(G)                                   \
+    if (!fixed) {                                     \
+        if (depth == 0)                               \
+            ZS_LAUNCH(G, false, 0);                   \
+        else                                          \
+            ZS_LAUNCH(G, false, 1);                   \
+    } else if (depth == 0) {                          \
+        ZS_LAUNCH(G, true, 0);                        \
+    } else if (depth == 1) {                          \
+        ZS_LAUNCH(G, true, 1);                        \
+    } else {                                          \
+        ZS_LAUNCH(G, true, 2);                        \
+    }
+    switch (g) {
+    case 1: ZS_CASES(1); break;
+    case 16: ZS_CASES(16); break;
+    case 64: ZS_CASES(64); break;
     default:
         return -1;
     }
+#undef ZS_CASES
 #undef ZS_LAUNCH
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
