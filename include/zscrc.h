@@ -113,8 +113,9 @@ void zscrc_set_gpu_min(uint64_t min_bytes);
 /* team size tuning: records <= g1_max bytes use one lane each, <= g16_max a
  * 16-lane team, larger a 64-lane (whole wavefront) team. */
 void zscrc_set_teams(uint64_t g1_max, uint64_t g16_max);
-/* tuning: record walk for team size g (1, 16 or 64): 0 = two-level loop,
- * 1 / 2 = flattened (record, step) loop with a 1- / 2-item register ring */
+/* tuning: record walk for team size g (1, 16 or 64): -1 = automatic (default),
+ * 0 = two-level loop, 1 / 2 = flattened (record, step) loop with a 1- / 2-item
+ * register ring */
 void zscrc_set_prefetch(int g, int depth);
 /* team size the fixed-stride path picks for n records of len bytes (1/16/64;
  * 0 if no device) */

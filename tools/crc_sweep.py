@@ -57,13 +57,15 @@ def main():
     for name, stride, length, n, teams in cases:
         lib().zscrc_set_teams(*teams)
         g = 1 if teams[0] >= length else (16 if teams[1] >= length else 64)
-        for depth in (0, 1, 2, 0, 1, 2):
+        for depth in (-1, 0, 1, 2, -1):
             lib().zscrc_set_prefetch(g, depth)
             ms = timeit(lambda: zd.crc_fixed(big, stride, length, n, out=out[:n]))
             byt = n * length
             print(json.dumps({"case": name, "depth": depth, "ms": round(ms, 4),
                               "GBs": round(byt / ms / 1e6, 1),
                               "GiBs": round(byt / ms / 1e6 * 1e9 / (1 << 30), 1)}), flush=True)
+    for g in (1, 16, 64):
+        lib().zscrc_set_prefetch(g, -1)
     lib().zscrc_set_teams(1024, 1 << 20)
     ms = timeit(lambda: zd.crc_span(big))
     print(json.dumps({"case": "span 4 GiB", "ms": round(ms, 4), "GBs": round((4 << 30) / ms / 1e6, 1)}))

@@ -44,9 +44,9 @@ std::atomic<uint64_t> g_gpu_min{0};
 std::atomic<uint64_t> g_g1_max{1024};
 std::atomic<uint64_t> g_g16_max{1u << 20};
 int g_strict = 0;
-/* walk of fixed-stride launches per team size: 0 two-level, 1/2 flattened with a
- * 1/2-item ring; index 0/1/2 = G 1/16/64 (variable batches: 0 or 1) */
-std::atomic<int> g_depth[3] = {{2}, {1}, {1}};
+/* record-walk override per team size (index 0/1/2 = G 1/16/64): -1 = automatic
+ * (walk_for), 0 = two-level loop, 1/2 = flattened loop with a 1/2-item ring */
+std::atomic<int> g_depth[3] = {{-1}, {-1}, {-1}};
 
 struct DevCtx {
     std::mutex mu;
@@ -183,17 +183,66 @@ zs::BatchDesc make_desc()
     return d;
 }
 
+/* Record walk by record length (profiles/r01/sweep_walks.jsonl, same-GPU A/B):
+ * records >= 8 KiB: the two-level loop (G16 on 64 KiB chunks reads at the
+ * streaming-read ceiling); shorter records: the flattened (record, step) loop,
+ * whose register ring keeps loads in flight across record boundaries -- two
+ * items deep where the batch is fixed-stride, except 4-8 KiB G16 records. */
+int walk_for(int g, int fixed, uint64_t len)
+{
+    if (len >= 8192)
+        return 0;
+    if (!fixed)
+        return 1;
+    return (g == 16 && len > 2048) ? 1 : 2;
+}
+
 int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s)
 {
     /* fixed-stride form when no per-record arrays are involved */
     const int fixed = !d.off && !d.len && !d.seed && d.len_lo == 0 && d.len_hi == ~0ull;
-    const int depth = g_depth[g == 1 ? 0 : g == 16 ? 1 : 2];
+    const uint64_t typical = fixed ? d.fixed_len : (d.len_lo > 0 ? d.len_lo : 1);
+    int depth = g_depth[g == 1 ? 0 : g == 16 ? 1 : 2];
+    if (depth < 0)
+        depth = walk_for(g, fixed, typical);
+    if (!fixed && depth == 2)
+        depth = 1;
     int rc = zs_launch_team(g, fixed, depth, &d, c->gtab, c->ncu, s);
     if (rc) {
         set_err("team kernel launch", hipGetLastError());
         return ZSCRC_EHIP;
     }
     g_stat[2]++;
+    return ZSCRC_OK;
+}
+
+/* A variable-length batch as persistent launches over length classes, each
+ * skipping the records of the others: <= g1_max one lane per record; up to
+ * 8 KiB 16-lane teams on the flattened walk; up to g16_max 16-lane teams on
+ * the two-level walk; longer records whole-wave teams. */
+int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s)
+{
+    const uint64_t g1 = g_g1_max, g16 = g_g16_max;
+    struct Class {
+        int g;
+        uint64_t lo, hi;
+    } cls[4] = {
+        {1, 0, g1},
+        {16, g1 + 1, g16 < 8191 ? g16 : 8191},
+        {16, g1 + 1 > 8192 ? g1 + 1 : 8192, g16},
+        {64, (g16 > g1 ? g16 : g1) + 1, ~0ull},
+    };
+    if (g1 == ~0ull)
+        cls[1].lo = cls[2].lo = cls[3].lo = ~0ull;
+    for (const Class &k : cls) {
+        if (k.lo > k.hi)
+            continue;
+        d.len_lo = k.lo;
+        d.len_hi = k.hi;
+        int rc = launch(c, k.g, d, s);
+        if (rc)
+            return rc;
+    }
     return ZSCRC_OK;
 }
 
@@ -366,21 +415,7 @@ int zscrc_device_batch(const void *d_base, const uint64_t *d_off, const uint64_t
     d.out = d_out;
     d.n = n;
     d.xor_io = (flags & ZSCRC_RAW) ? 0u : 0xffffffffu;
-    const uint64_t g1 = g_g1_max, g16 = g_g16_max;
-    /* three length classes, each a persistent launch that skips the others */
-    d.len_lo = 0;
-    d.len_hi = g1;
-    if ((rc = launch(c, 1, d, s)))
-        return rc;
-    if (g16 > g1) {
-        d.len_lo = g1 + 1;
-        d.len_hi = g16;
-        if ((rc = launch(c, 16, d, s)))
-            return rc;
-    }
-    d.len_lo = (g16 > g1 ? g16 : g1) + 1;
-    d.len_hi = ~0ull;
-    return launch(c, 64, d, s);
+    return launch_classes(c, d, s);
 }
 
 int zscrc_device_fixed(const void *d_base, uint64_t stride, uint64_t len, uint32_t seed,
@@ -480,19 +515,7 @@ int zscrc_host_batch(const void *base, const uint64_t *off, const uint64_t *len,
     d.out = dout;
     d.n = n;
     d.xor_io = 0xffffffffu;
-    const uint64_t g1 = g_g1_max, g16 = g_g16_max;
-    d.len_hi = g1;
-    if ((rc = launch(c, 1, d, nullptr)))
-        return rc;
-    if (g16 > g1) {
-        d.len_lo = g1 + 1;
-        d.len_hi = g16;
-        if ((rc = launch(c, 16, d, nullptr)))
-            return rc;
-    }
-    d.len_lo = (g16 > g1 ? g16 : g1) + 1;
-    d.len_hi = ~0ull;
-    if ((rc = launch(c, 64, d, nullptr)))
+    if ((rc = launch_classes(c, d, nullptr)))
         return rc;
     e = hipMemcpy(out, dout, n * 4, hipMemcpyDeviceToHost);
     if (e != hipSuccess) {
@@ -536,7 +559,7 @@ void zscrc_set_gpu_min(uint64_t min_bytes)
 
 void zscrc_set_prefetch(int g, int depth)
 {
-    if (depth < 0 || depth > 2)
+    if (depth < -1 || depth > 2)
         return;
     if (g == 1)
         g_depth[0] = depth;
