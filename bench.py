@@ -138,6 +138,21 @@ def main() -> None:
         elapsed = t.item()
 
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    # same-GPU measured read ceiling: a plain coalesced streaming read of the
+    # same 4 GiB buffer (libzscrc diagnostic kernel), median of 10
+    scratch = torch.zeros(4, dtype=torch.int32, device=dev)
+    rd = []
+    for i in range(13):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        check(lib().zscrc_diag_stream_read(data.data_ptr(), NCHUNK * CHUNK, scratch.data_ptr(), 2,
+                                           stream.cuda_stream), "stream read")
+        b.record(stream)
+        torch.cuda.synchronize()
+        if i >= 3:
+            rd.append(a.elapsed_time(b))
+    read_peak = NCHUNK * CHUNK / (sorted(rd)[len(rd) // 2] * 1e-3) / 1e9
     bytes_per_launch = NCHUNK * CHUNK + NCHUNK * 4       # algorithmic: input + u32 digests
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9  # GB/s
     total_bytes = NCHUNK * CHUNK * world * args.steps
@@ -170,7 +185,9 @@ def main() -> None:
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "kernel": f"zs::team_kernel<{lib().zscrc_team_for(CHUNK, NCHUNK)}>",
-                         "kernel_ms": round(kern_ms, 4)},
+                         "kernel_ms": round(kern_ms, 4),
+                         "measured_read_peak": round(read_peak, 1),
+                         "frac_of_measured_read_peak": round(achieved / read_peak, 4)},
         }
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline()
