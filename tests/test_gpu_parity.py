@@ -181,3 +181,40 @@ def test_config2_full_size_vs_oracle(gpu):
     out = u32(zd.crc_fixed(d, 64, 64, n))
     ref = oracle.batch(d.cpu().numpy(), n=n, stride=64, fixed_len=64, impl="hw", threads=8)
     assert np.array_equal(out, ref)
+
+
+def _sharded_worker(rank, world, port, total, q):
+    import os
+    import torch.distributed as dist
+    from zeroskip_amd import shard
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    data = np.random.default_rng(321).integers(0, 256, total, dtype=np.uint8)
+    lo, hi = shard.shard_ranges(total, world)[rank]
+    local = torch.from_numpy(data[lo:hi].copy()).to("cuda:0")
+    q.put((rank, shard.sharded_crc(local, seed=0x77)))   # GPU raw partials, gloo exchange
+    dist.destroy_process_group()
+
+
+def test_sharded_span_gpu_partials(gpu):
+    # two ranks on the one GPU of this box (gloo for the digest exchange; the
+    # 8-GPU run uses RCCL): per-rank libzscrc raw partials folded == oracle
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    total, world = (24 << 20) + 12345, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = oracle.crc32c_hw(0x77, np.random.default_rng(321).integers(0, 256, total, dtype=np.uint8))
+    assert all(c == want for _, c in res)
