@@ -127,6 +127,57 @@ int zscrc_diag_stream_read(const void *d_buf, uint64_t len, void *d_scratch4, in
 /* Number of gfx950 devices visible (0 if none / no HIP runtime). */
 int zscrc_device_count(void);
 
+/* ======================================================================
+ * Part 3 -- zeroskip file images (verify-on-open / `consistent` / repack).
+ * A commit's CRC covers its span (the bytes since crc32_begin, ending where
+ * the commit record starts) followed by the commit record's host-order
+ * trailer words (src/zeroskip-file.c:253-350).
+ * ====================================================================== */
+
+/* walk / parse results (>= 0) */
+#define ZSCRC_ZS_END 0        /* walked to the end of the image            */
+#define ZSCRC_ZS_STOPPED 1    /* stopped at a record type the reference walk
+                               * does not advance over (record.c:314-325)  */
+#define ZSCRC_ZS_TRUNCATED 2  /* a record runs past the end of the image   */
+#define ZSCRC_ZS_OVERFLOW 3   /* more commits than `cap`; *n_commits = all  */
+#define ZSCRC_ZS_BADSIG 4     /* header signature is not "ZEROSKIP"         */
+
+/* file kinds */
+#define ZSCRC_ZS_ACTIVE 0
+#define ZSCRC_ZS_FINALISED 1
+#define ZSCRC_ZS_PACKED 2
+
+/* Walk an active or finalised file image from its 40-byte header
+ * (zeroskip-record.c:283-331) and list every commit's span [off, off+len);
+ * the commit record starts at off+len. */
+int zscrc_zs_walk(const void *image, uint64_t size, uint64_t *span_off, uint64_t *span_len, size_t cap,
+                  size_t *n_commits, uint64_t *end_off);
+/* Packed file: [0] = records-region commit span, [1] = pointer-section span
+ * (zeroskip-packed.c:70-131, :278-339). */
+int zscrc_zs_packed_spans(const void *image, uint64_t size, uint64_t span_off[2], uint64_t span_len[2]);
+/* 40-byte header CRC over host-order fields (zeroskip-header.c:105-170). */
+int zscrc_zs_header_crc(const void *image, uint64_t size, uint32_t *stored, uint32_t *computed);
+/* 61-byte .zsdb CRC over host-order fields (zeroskip-dotzsdb.c:160-235). */
+int zscrc_zs_dotzsdb_crc(const void *image, uint64_t size, uint32_t *stored, uint32_t *computed);
+/* Device: verify n commits of a device-resident image.  d_crc[i] = computed
+ * commit CRC, d_status[i] = 1 match / 0 mismatch / 2 no commit record. */
+int zscrc_device_verify_commits(const void *d_image, const uint64_t *d_span_off, const uint64_t *d_span_len,
+                                size_t n, uint32_t *d_crc, uint32_t *d_status, void *stream);
+
+typedef struct zscrc_zs_report {
+    int header_rc;            /* zscrc_zs_header_crc result */
+    uint32_t header_stored, header_computed;
+    int walk_rc;              /* zscrc_zs_walk / packed_spans result */
+    uint64_t end_off;         /* where the walk ended */
+    uint64_t n_commits;       /* commits checked on the GPU */
+    uint64_t n_bad;           /* commits whose CRC does not match */
+    uint64_t first_bad;       /* index of the first bad commit */
+} zscrc_zs_report;
+
+/* Host convenience: header check on the CPU, walk, copy the image to the
+ * current device, verify every commit there.  Synchronous. */
+int zscrc_zs_verify_image(const void *image, uint64_t size, int kind, zscrc_zs_report *rep);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,75 @@
+"""GPU verification of zeroskip file images against the format oracle:
+every commit CRC (span + host-order trailer) recomputed on the device."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import zs_format as zf
+from tests.test_format_oracle import UUID, build_active
+from zeroskip_amd import zsfile
+
+pytestmark = pytest.mark.gpu
+
+
+def test_active_image_all_commits_ok(gpu):
+    img = build_active(200, seed=11)
+    rep = zsfile.verify_image(img)
+    assert rep["header_rc"] == 0 and rep["header_stored"] == rep["header_computed"]
+    assert rep["walk_rc"] == zsfile.END and rep["n_commits"] == 200 and rep["n_bad"] == 0
+
+
+def test_corruption_located(gpu):
+    img = bytearray(build_active(200, seed=12))
+    commits, _, _ = zf.walk(bytes(img))
+    img[commits[137]["span_off"] + 5] ^= 0x01
+    rep = zsfile.verify_image(bytes(img))
+    assert rep["n_bad"] == 1 and rep["first_bad"] == 137
+    img2 = bytearray(build_active(50, seed=13))
+    c = zf.walk(bytes(img2))[0][20]
+    img2[c["commit_off"] + 7] ^= 0x80            # stored CRC byte
+    rep = zsfile.verify_image(bytes(img2))
+    assert rep["n_bad"] == 1 and rep["first_bad"] == 20
+
+
+def test_long_commit_and_packed(gpu):
+    w = zf.FileWriter(UUID)
+    w.add(b"k" * 100, np.random.default_rng(3).integers(0, 256, (17 << 20) + 5, dtype=np.uint8).tobytes())
+    w.commit()
+    w.add(b"small", b"v")
+    w.commit()
+    rep = zsfile.verify_image(w.image())
+    assert rep["n_commits"] == 2 and rep["n_bad"] == 0
+    recs = sorted((b"%016d" % i, None if i % 11 == 0 else b"y" * (i % 300)) for i in range(5000))
+    rep = zsfile.verify_image(zf.packed_file(recs, UUID, 2, 9), zsfile.PACKED)
+    assert rep["walk_rc"] == 0 and rep["n_commits"] == 2 and rep["n_bad"] == 0
+
+
+def test_device_commits_match_oracle_crcs(gpu):
+    # several files concatenated in one device image; commit spans of all
+    # sizes (empty txn commits, deletes restarting the span, multi-record txns)
+    imgs, offs, lens, want = [], [], [], []
+    base = 0
+    for s in range(6):
+        rng = np.random.default_rng(100 + s)
+        w = zf.FileWriter(UUID, idx=s)
+        for t in range(300):
+            for _ in range(int(rng.integers(0, 5))):
+                w.add(b"%016d" % int(rng.integers(0, 10**9)),
+                      rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8).tobytes())
+            if t % 13 == 5:
+                w.remove(b"%016d" % t)
+            w.commit()
+        img = w.image()
+        commits, _, _ = zf.walk(img)
+        for c in commits:
+            offs.append(base + c["span_off"])
+            lens.append(c["span_len"])
+            want.append(c["computed"])
+        imgs.append(img)
+        base += len(img)
+    d = torch.from_numpy(np.frombuffer(b"".join(imgs), dtype=np.uint8).copy()).cuda()
+    crc, st = zsfile.verify_commits(d, torch.tensor(offs, dtype=torch.int64, device="cuda"),
+                                    torch.tensor(lens, dtype=torch.int64, device="cuda"))
+    torch.cuda.synchronize()
+    assert (st.cpu().numpy() == 1).all()
+    assert (crc.cpu().numpy().view(np.uint32) == np.array(want, dtype=np.uint32)).all()

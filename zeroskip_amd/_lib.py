@@ -36,6 +36,12 @@ SIGNATURES = {
     "zscrc_set_prefetch": (None, [_int, _int]),
     "zscrc_diag_stream_read": (_int, [_vp, _u64, _vp, _int, _vp]),
     "zscrc_device_count": (_int, []),
+    "zscrc_zs_walk": (_int, [_vp, _u64, _vp, _vp, _sz, _vp, _vp]),
+    "zscrc_zs_packed_spans": (_int, [_vp, _u64, _vp, _vp]),
+    "zscrc_zs_header_crc": (_int, [_vp, _u64, _vp, _vp]),
+    "zscrc_zs_dotzsdb_crc": (_int, [_vp, _u64, _vp, _vp]),
+    "zscrc_device_verify_commits": (_int, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
+    "zscrc_zs_verify_image": (_int, [_vp, _u64, _int, _vp]),
 }
 
 ZSCRC_RAW = 1

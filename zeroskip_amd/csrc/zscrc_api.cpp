@@ -200,7 +200,7 @@ int walk_for(int g, int fixed, uint64_t len)
 int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s)
 {
     /* fixed-stride form when no per-record arrays are involved */
-    const int fixed = !d.off && !d.len && !d.seed && d.len_lo == 0 && d.len_hi == ~0ull;
+    const int fixed = !d.off && !d.len && !d.seed && !d.status && d.len_lo == 0 && d.len_hi == ~0ull;
     const uint64_t typical = fixed ? d.fixed_len : (d.len_lo > 0 ? d.len_lo : 1);
     int depth = g_depth[g == 1 ? 0 : g == 16 ? 1 : 2];
     if (depth < 0)
@@ -541,6 +541,28 @@ int zscrc_diag_stream_read(const void *d_buf, uint64_t len, void *d_scratch4, in
         return ZSCRC_EHIP;
     }
     return ZSCRC_OK;
+}
+
+int zscrc_internal_verify_commits(const void *d_image, const uint64_t *d_off, const uint64_t *d_len,
+                                  uint32_t *d_crc, uint32_t *d_status, size_t n, void *stream)
+{
+    if (n == 0)
+        return ZSCRC_OK;
+    if (!d_image || !d_off || !d_len || !d_crc || !d_status)
+        return ZSCRC_EINVAL;
+    DevCtx *c;
+    int rc = get_ctx(&c);
+    if (rc)
+        return rc;
+    zs::BatchDesc d = make_desc();
+    d.base = static_cast<const uint8_t *>(d_image);
+    d.off = d_off;
+    d.len = d_len;
+    d.out = d_crc;
+    d.status = d_status;
+    d.n = n;
+    d.xor_io = 0xffffffffu;
+    return launch_classes(c, d, static_cast<hipStream_t>(stream));
 }
 
 const char *zscrc_last_error(void) { return t_err; }

@@ -29,6 +29,11 @@ struct BatchDesc {
     uint64_t len_hi;
     uint32_t fixed_seed;
     uint32_t xor_io;      /* 0xFFFFFFFF standard CRC, 0 raw registers */
+    /* zeroskip commit verification: when non-NULL, record i is the span of a
+     * commit record that starts right after it; out[i] receives the commit
+     * CRC (span + host-order trailer words) and status[i] 1 = matches the
+     * stored CRC, 0 = mismatch, 2 = no commit record there. */
+    uint32_t *status;
 };
 
 struct SpanFold {

@@ -204,6 +204,55 @@ __device__ __forceinline__ void issue_plain(uintptr_t p, uint32_t (&w)[16])
     }
 }
 
+/* Read the big-endian 64-bit word at a (8-aligned in a zeroskip file). */
+__device__ __forceinline__ uint64_t load_be64(uintptr_t a)
+{
+    const uint32_t hi = ((g32p)a)[0], lo = ((g32p)a)[1];
+    return ((uint64_t)__builtin_bswap32(hi) << 32) | __builtin_bswap32(lo);
+}
+
+/* Register r through one host-order (little-endian) 64-bit word. */
+__device__ __forceinline__ uint32_t feed64(const char *L, uint32_t r, uint64_t v, uint32_t c_lo, uint32_t c_hi)
+{
+    r = m4(L, r ^ (uint32_t)v, c_lo, c_hi);
+    return m4(L, r ^ (uint32_t)(v >> 32), c_lo, c_hi);
+}
+
+enum { REC_COMMIT = 4, REC_2ND_HALF = 8, REC_FINAL = 16, REC_LONG_COMMIT = 36, REC_LONG_FINAL = 48 };
+
+/* Store record `rec`'s result from its final register r.  In commit mode the
+ * CRC continues over the commit record's trailer words exactly as the writer
+ * hashes them (src/zeroskip-file.c:266-328): short -> LE(type<<56|len<<32);
+ * long -> LE(type1<<56), LE(len), LE(2ND_HALF<<56); then compared with the CRC
+ * stored in the record's low 32 bits. */
+__device__ __forceinline__ void emit(const BatchDesc &d, uint64_t rec, uintptr_t end, uint32_t r,
+                                     const char *L, uint32_t c_lo, uint32_t c_hi)
+{
+    if (!d.status) {
+        d.out[rec] = r ^ d.xor_io;
+        return;
+    }
+    const uint64_t w0 = load_be64(end);
+    const uint32_t t = (uint32_t)(w0 >> 56);
+    uint32_t stored, st = 0;
+    if (t == REC_COMMIT || t == REC_FINAL) {
+        r = feed64(L, r, w0 & 0xFFFFFFFF00000000ull, c_lo, c_hi);
+        stored = (uint32_t)w0;
+    } else if (t == REC_LONG_COMMIT || t == REC_LONG_FINAL) {
+        const uint64_t w1 = load_be64(end + 8), w2 = load_be64(end + 16);
+        r = feed64(L, r, w0, c_lo, c_hi);
+        r = feed64(L, r, w1, c_lo, c_hi);
+        r = feed64(L, r, w2 & 0xFF00000000000000ull, c_lo, c_hi);
+        stored = (uint32_t)w2;
+    } else {
+        stored = ~(r ^ 0xffffffffu);
+        st = 2;
+    }
+    const uint32_t crc = r ^ 0xffffffffu;
+    d.out[rec] = crc;
+    d.status[rec] = st == 2 ? 2u : (crc == stored ? 1u : 0u);
+}
+
 /* Data fix-ups that need the record start (step 0 of a front-padded grid):
  * undo the clamp of issue(), zero every byte before A, and XOR the initial
  * register into bytes [A, A+4) -- which can spill into step 1. */
@@ -322,7 +371,7 @@ __device__ __forceinline__ void compute(const BatchDesc &d, const Cursor &c, uin
             uint32_t r = it.R0;
             for (uint64_t i = 0; i < it.len; ++i)
                 r = byte_step(L, r, ((g8p)it.A)[i], c_hi);
-            d.out[it.rec] = r ^ d.xor_io;
+            emit(d, it.rec, it.A + it.len, r, L, c_lo, c_hi);
         }
         return;
     }
@@ -334,7 +383,7 @@ __device__ __forceinline__ void compute(const BatchDesc &d, const Cursor &c, uin
     if (c.s + 1 == it.S) {
         const uint32_t r = finish<G>(it, acc, j, lane, L, c_hi);
         if (j == G - 1)
-            d.out[it.rec] = r ^ d.xor_io;
+            emit(d, it.rec, it.A + it.len, r, L, c_lo, c_hi);
         acc = 0;
     }
 }
@@ -374,12 +423,9 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
         Item cur = c0.it;
         bool ok = c0.ok;
         while (ok) {
-            Item nxt;
-            const bool ok2 = fetch_record<G, FIXED>(d, cur.rec + nteams, nteams, nxt);
             Cursor cn;
-            cn.it = nxt;
             cn.s = 0;
-            cn.ok = ok2;
+            cn.ok = fetch_record<G, FIXED>(d, cur.rec + nteams, nteams, cn.it);
             uint32_t w[16];
 #pragma unroll
             for (int k = 0; k < 16; ++k)
@@ -390,10 +436,10 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
                     uint32_t r = cur.R0;
                     for (uint64_t i = 0; i < cur.len; ++i)
                         r = byte_step(L, r, ((g8p)cur.A)[i], c_hi);
-                    d.out[cur.rec] = r ^ d.xor_io;
+                    emit(d, cur.rec, cur.A + cur.len, r, L, c_lo, c_hi);
                 }
-                cur = nxt;
-                ok = ok2;
+                cur = cn.it;
+                ok = cn.ok;
                 continue;
             }
             uintptr_t p = cur.V0 + STEP + 64 * (uintptr_t)j;
@@ -429,10 +475,10 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
             }
             const uint32_t r = finish<G>(cur, acc, j, lane, L, c_hi);
             if (j == G - 1)
-                d.out[cur.rec] = r ^ d.xor_io;
+                emit(d, cur.rec, cur.A + cur.len, r, L, c_lo, c_hi);
             acc = 0;
-            cur = nxt;
-            ok = ok2;
+            cur = cn.it;
+            ok = cn.ok;
         }
     } else if (FIXED && DEPTH == 2) {
         Cursor c1 = next_cursor<G, FIXED>(d, c0, nteams);

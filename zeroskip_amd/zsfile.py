@@ -1,0 +1,93 @@
+"""zeroskip file images: walk, span descriptors and GPU commit verification.
+
+Python view of include/zscrc.h Part 3 (zeroskip_amd/csrc/zscrc_zs.cpp).  The
+walk follows the reference (src/zeroskip-record.c:283-331); each commit's CRC
+(span + host-order trailer words, src/zeroskip-file.c:253-350) is recomputed
+and compared on the GPU.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from ._lib import check, lib
+
+END, STOPPED, TRUNCATED, OVERFLOW, BADSIG = 0, 1, 2, 3, 4
+ACTIVE, FINALISED, PACKED = 0, 1, 2
+
+
+class Report(ctypes.Structure):
+    _fields_ = [("header_rc", ctypes.c_int), ("header_stored", ctypes.c_uint32),
+                ("header_computed", ctypes.c_uint32), ("walk_rc", ctypes.c_int),
+                ("end_off", ctypes.c_uint64), ("n_commits", ctypes.c_uint64),
+                ("n_bad", ctypes.c_uint64), ("first_bad", ctypes.c_uint64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+def _host(image):
+    a = np.ascontiguousarray(np.frombuffer(image, dtype=np.uint8) if isinstance(image, (bytes, bytearray, memoryview)) else image)
+    return a, a.ctypes.data, a.nbytes
+
+
+def walk(image):
+    """(span_off, span_len, rc, end_off) of every commit of an active or
+    finalised file image."""
+    a, p, n = _host(image)
+    cap = n // 8 + 1
+    off = np.empty(cap, np.uint64)
+    ln = np.empty(cap, np.uint64)
+    nc = ctypes.c_size_t()
+    end = ctypes.c_uint64()
+    rc = lib().zscrc_zs_walk(p, n, off.ctypes.data, ln.ctypes.data, cap, ctypes.byref(nc),
+                             ctypes.byref(end))
+    if rc < 0:
+        check(rc, "zscrc_zs_walk")
+    return off[:nc.value], ln[:nc.value], rc, end.value
+
+
+def packed_spans(image):
+    a, p, n = _host(image)
+    off = np.empty(2, np.uint64)
+    ln = np.empty(2, np.uint64)
+    rc = lib().zscrc_zs_packed_spans(p, n, off.ctypes.data, ln.ctypes.data)
+    return off, ln, rc
+
+
+def header_crc(image):
+    a, p, n = _host(image)
+    st, cp = ctypes.c_uint32(), ctypes.c_uint32()
+    rc = lib().zscrc_zs_header_crc(p, n, ctypes.byref(st), ctypes.byref(cp))
+    return rc, st.value, cp.value
+
+
+def dotzsdb_crc(image):
+    a, p, n = _host(image)
+    st, cp = ctypes.c_uint32(), ctypes.c_uint32()
+    rc = lib().zscrc_zs_dotzsdb_crc(p, n, ctypes.byref(st), ctypes.byref(cp))
+    return rc, st.value, cp.value
+
+
+def verify_image(image, kind: int = ACTIVE) -> dict:
+    """Header on the CPU, every commit on the current GPU (synchronous)."""
+    a, p, n = _host(image)
+    rep = Report()
+    check(lib().zscrc_zs_verify_image(p, n, kind, ctypes.byref(rep)), "zscrc_zs_verify_image")
+    return rep.as_dict()
+
+
+def verify_commits(d_image: torch.Tensor, span_off: torch.Tensor, span_len: torch.Tensor):
+    """Device-resident commit verification: (crc, status) int32 tensors;
+    status 1 = stored CRC matches, 0 = mismatch, 2 = no commit record."""
+    n = span_off.numel()
+    crc = torch.empty(n, dtype=torch.int32, device=d_image.device)
+    st = torch.empty(n, dtype=torch.int32, device=d_image.device)
+    with torch.cuda.device(d_image.device):
+        check(lib().zscrc_device_verify_commits(
+            d_image.data_ptr(), span_off.data_ptr(), span_len.data_ptr(), n, crc.data_ptr(),
+            st.data_ptr(), torch.cuda.current_stream(d_image.device).cuda_stream),
+            "zscrc_device_verify_commits")
+    return crc, st
