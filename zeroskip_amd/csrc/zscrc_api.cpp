@@ -30,6 +30,8 @@ int zs_launch_team(int g, int fixed, int depth, const zs::BatchDesc *d, const ui
                    hipStream_t stream);
 int zs_launch_span_fold(const zs::SpanFold *f, hipStream_t stream);
 int zs_launch_stream_read(const void *buf, uint64_t n, uint32_t *out, int grid, hipStream_t stream);
+int zs_launch_classify(const zs::Classify *c, hipStream_t stream);
+int zs_launch_part_fold(const zs::BatchDesc *d, const uint32_t *gtab, hipStream_t stream);
 }
 
 namespace {
@@ -57,6 +59,10 @@ struct DevCtx {
     size_t scratch_bytes = 0;
     void *stage = nullptr;     /* host-batch staging */
     size_t stage_bytes = 0;
+    void *classes = nullptr;   /* class lists + counters of variable batches */
+    size_t classes_bytes = 0;
+    void *parts = nullptr;     /* part registers of split long records */
+    size_t parts_bytes = 0;
 };
 DevCtx g_ctx[MAX_DEV];
 std::once_flag g_env_once;
@@ -96,6 +102,8 @@ void build_gtab(uint32_t *t)
     zs_gf2_shift_table(t + GT_U64, 4 + 63 * 64);
     for (int k = 0; k < 6; ++k)
         zs_gf2_shift_table(t + GT_Z + 1024 * k, 64ull << k);
+    for (int k = 0; k < 64; ++k)
+        t[GT_POW2 + k] = zs_gf2_xpow8n(1ull << k);
 }
 
 /* Context of the current device, initialised on first use. */
@@ -197,14 +205,14 @@ int walk_for(int g, int fixed, uint64_t len)
     return (g == 16 && len > 2048) ? 1 : 2;
 }
 
-int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s)
+int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s, int depth_hint = -1)
 {
     /* fixed-stride form when no per-record arrays are involved */
     const int fixed = !d.off && !d.len && !d.seed && !d.status && d.len_lo == 0 && d.len_hi == ~0ull;
     const uint64_t typical = fixed ? d.fixed_len : (d.len_lo > 0 ? d.len_lo : 1);
     int depth = g_depth[g == 1 ? 0 : g == 16 ? 1 : 2];
     if (depth < 0)
-        depth = walk_for(g, fixed, typical);
+        depth = depth_hint >= 0 ? depth_hint : walk_for(g, fixed, typical);
     if (!fixed && depth == 2)
         depth = 1;
     int rc = zs_launch_team(g, fixed, depth, &d, c->gtab, c->ncu, s);
@@ -216,32 +224,82 @@ int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s)
     return ZSCRC_OK;
 }
 
-/* A variable-length batch as persistent launches over length classes, each
- * skipping the records of the others: <= g1_max one lane per record; up to
- * 8 KiB 16-lane teams on the flattened walk; up to g16_max 16-lane teams on
- * the two-level walk; longer records whole-wave teams. */
+/* A variable-length batch: a device-side classify kernel sorts the records
+ * into four length classes (lists + counts stay on the device: no host
+ * round trip), then one persistent launch per class walks its list:
+ *   <= g1_max          one lane per record, flattened walk
+ *   <= 8 KiB           16-lane teams, flattened walk
+ *   <= g16_max         16-lane teams, two-level walk
+ *   longer             whole-wave teams on 2^k equal parts per record (k from
+ *                      the class count, >= 8192 parts in all), then a fold
+ *                      kernel combines each record's part registers. */
 int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s)
 {
     const uint64_t g1 = g_g1_max, g16 = g_g16_max;
-    struct Class {
-        int g;
-        uint64_t lo, hi;
-    } cls[4] = {
-        {1, 0, g1},
-        {16, g1 + 1, g16 < 8191 ? g16 : 8191},
-        {16, g1 + 1 > 8192 ? g1 + 1 : 8192, g16},
-        {64, (g16 > g1 ? g16 : g1) + 1, ~0ull},
-    };
-    if (g1 == ~0ull)
-        cls[1].lo = cls[2].lo = cls[3].lo = ~0ull;
-    for (const Class &k : cls) {
-        if (k.lo > k.hi)
-            continue;
-        d.len_lo = k.lo;
-        d.len_hi = k.hi;
-        int rc = launch(c, k.g, d, s);
+    const uint64_t n = d.n;
+    uint64_t b1 = g16 < 8191 ? g16 : 8191;
+    if (b1 < g1)
+        b1 = g1;
+    const uint64_t b2 = g16 > b1 ? g16 : b1;
+    const size_t list_bytes = 4 * n * sizeof(uint32_t) + 64;
+    const size_t part_bytes = (n * 16 + 16384) * sizeof(uint32_t);
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        int rc = grow(&c->classes, &c->classes_bytes, list_bytes);
+        if (!rc)
+            rc = grow(&c->parts, &c->parts_bytes, part_bytes);
         if (rc)
             return rc;
+    }
+    uint32_t *cnt = static_cast<uint32_t *>(c->classes);
+    uint32_t *lists = cnt + 16;
+    hipError_t e = hipMemsetAsync(cnt, 0, 64, s);
+    if (e != hipSuccess) {
+        set_err("hipMemsetAsync(class counters)", e);
+        return ZSCRC_EHIP;
+    }
+    zs::Classify cl;
+    memset(&cl, 0, sizeof cl);
+    cl.len = d.len;
+    cl.n = n;
+    cl.bound[0] = g1;
+    cl.bound[1] = b1;
+    cl.bound[2] = b2;
+    for (int k = 0; k < 4; ++k)
+        cl.list[k] = lists + (uint64_t)k * n;
+    cl.count = cnt;
+    if (zs_launch_classify(&cl, s)) {
+        set_err("classify launch", hipGetLastError());
+        return ZSCRC_EHIP;
+    }
+    g_stat[2]++;
+    const int team[4] = {1, 16, 16, 64};
+    const int walk[4] = {1, 1, 0, 0};
+    d.len_lo = 0;
+    d.len_hi = ~0ull;
+    for (int k = 0; k < 4; ++k) {
+        zs::BatchDesc dk = d;
+        dk.list = cl.list[k];
+        dk.list_count = cnt + k;
+        if (k == 3) {
+            dk.split = 1;
+            dk.part_out = static_cast<uint32_t *>(c->parts);
+        }
+        int rc = launch(c, team[k], dk, s, walk[k]);
+        if (rc)
+            return rc;
+        if (k == 3) {
+            zs::BatchDesc df = d;
+            df.list = cl.list[k];
+            df.list_count = cnt + k;
+            df.split = 1;
+            df.part_out = static_cast<uint32_t *>(c->parts);
+            if (zs_launch_part_fold(&df, c->gtab, s)) {
+                set_err("part fold launch", hipGetLastError());
+                return ZSCRC_EHIP;
+            }
+            g_stat[2]++;
+        }
     }
     return ZSCRC_OK;
 }

@@ -10,7 +10,8 @@ enum {
     GT_U16 = 1024,   /* shift(b<<8j, 4 + 15*64): word then skip, 16-lane team */
     GT_U64 = 2048,   /* shift(b<<8j, 4 + 63*64): word then skip, 64-lane team */
     GT_Z = 3072,     /* GT_Z + k*1024: shift(b<<8j, 64<<k), k = 0..5          */
-    GT_WORDS = 3072 + 6 * 1024,
+    GT_POW2 = 3072 + 6 * 1024, /* 64 words: x^(8*2^k) mod P, k = 0..63          */
+    GT_WORDS = 3072 + 6 * 1024 + 64,
 };
 
 namespace zs {
@@ -34,7 +35,33 @@ struct BatchDesc {
      * CRC (span + host-order trailer words) and status[i] 1 = matches the
      * stored CRC, 0 = mismatch, 2 = no commit record there. */
     uint32_t *status;
+    /* record lists built on the device by classify_kernel: when `list` is
+     * non-NULL the launch covers records list[0 .. *list_count) */
+    const uint32_t *list;
+    const uint32_t *list_count;
+    /* split long records into 2^lp equal parts (lp chosen in-kernel from the
+     * record count) whose raw registers go to part_out[idx << lp | part];
+     * part_fold_kernel folds them per record */
+    uint32_t split;
+    uint32_t *part_out;
 };
+
+struct Classify {
+    const uint64_t *len;
+    uint64_t n;
+    uint64_t bound[3];    /* class c holds bound[c-1] < len <= bound[c] */
+    uint32_t *list[4];
+    uint32_t *count;      /* 4 counters, zeroed before the launch */
+};
+
+/* parts per long record for `count` records: >= 16 and >= 8192 items */
+__host__ __device__ inline uint32_t split_log_parts(uint64_t count)
+{
+    uint32_t lp = 4;
+    while ((count << lp) < 8192 && lp < 10)
+        ++lp;
+    return lp;
+}
 
 struct SpanFold {
     const uint32_t *part; /* W raw segment registers */

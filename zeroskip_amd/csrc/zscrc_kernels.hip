@@ -63,6 +63,19 @@ __device__ __forceinline__ uint32_t lds32(const char *L, uint32_t addr)
     return *reinterpret_cast<const uint32_t *>(L + addr);
 }
 
+/* GF(2) product of two reflected residues mod P (bit 31 = x^0). */
+__device__ __forceinline__ uint32_t gmul(uint32_t a, uint32_t b)
+{
+    uint32_t acc = 0;
+#pragma unroll 4
+    for (int i = 0; i < 32; ++i) {
+        acc ^= (a & 0x80000000u) ? b : 0u;
+        a <<= 1;
+        b = (b >> 1) ^ ((b & 1u) ? 0x82F63B78u : 0u);
+    }
+    return acc;
+}
+
 /* register x -> register after 4 zero bytes (= one slice-by-4 step on x). */
 __device__ __forceinline__ uint32_t m4(const char *L, uint32_t x, uint32_t c_lo, uint32_t c_hi)
 {
@@ -107,7 +120,8 @@ struct Item {
     uintptr_t V0;     /* step-grid start (<= A)           */
     uint64_t S;       /* steps of G*64 bytes; 0 = short record (< 8 bytes) */
     uint64_t len;
-    uint64_t rec;
+    uint64_t rec;     /* output index (record, or part slot when splitting) */
+    uint64_t w;       /* work index of this team's walk */
     uint32_t R0;      /* initial register */
 };
 
@@ -123,24 +137,39 @@ struct Cursor {
  * one when set), fixed_seed -- no per-record metadata loads, so nothing here
  * waits on the vector-memory counter and the data prefetch ring survives. */
 template <int G, bool FIXED>
-__device__ __forceinline__ bool fetch_record(const BatchDesc &d, uint64_t rec, uint64_t nteams, Item &it)
+__device__ __forceinline__ bool fetch_record(const BatchDesc &d, uint64_t w, uint64_t nteams, uint64_t nitems,
+                                             uint32_t lp, Item &it)
 {
     constexpr uint64_t STEP = (uint64_t)G * 64;
-    for (; rec < d.n; rec += nteams) {
-        uint64_t len, off;
+    for (; w < nitems; w += nteams) {
+        uint64_t len, off, lo = 0, rec = w;
         uint32_t seed;
         if (FIXED) {
             len = (d.last_len != ~0ull && rec + 1 == d.n) ? d.last_len : d.fixed_len;
             off = rec * d.stride;
             seed = d.fixed_seed;
         } else {
+            rec = w >> lp;
+            if (d.list)
+                rec = ((g32p)d.list)[rec];
             len = d.len ? ((const __attribute__((address_space(1))) uint64_t *)d.len)[rec] : d.fixed_len;
             if (len < d.len_lo || len > d.len_hi)
                 continue;
             off = d.off ? ((const __attribute__((address_space(1))) uint64_t *)d.off)[rec] : rec * d.stride;
             seed = d.seed ? ((g32p)d.seed)[rec] : d.fixed_seed;
+            if (lp) {
+                /* part (w mod 2^lp) of the record: equal 64-byte-multiple parts */
+                const uint64_t P = (((len + (1ull << lp) - 1) >> lp) + 63) & ~63ull;
+                const uint64_t part = w & ((1ull << lp) - 1);
+                lo = part * P < len ? part * P : len;
+                const uint64_t hi = lo + P < len ? lo + P : len;
+                len = hi - lo;
+                if (part)
+                    seed = d.xor_io; /* parts after the first start from a zero register */
+                rec = w;             /* part_out index */
+            }
         }
-        const uintptr_t A = reinterpret_cast<uintptr_t>(d.base) + off;
+        const uintptr_t A = reinterpret_cast<uintptr_t>(d.base) + off + lo;
         const uintptr_t E = len < 8 ? A : ((A + len) & ~uintptr_t(3));
         const uint64_t S = len < 8 ? 0 : (E - A + STEP - 1) / STEP;
         it.A = A;
@@ -149,6 +178,7 @@ __device__ __forceinline__ bool fetch_record(const BatchDesc &d, uint64_t rec, u
         it.S = S;
         it.len = len;
         it.rec = rec;
+        it.w = w;
         it.R0 = seed ^ d.xor_io;
         return true;
     }
@@ -228,6 +258,10 @@ enum { REC_COMMIT = 4, REC_2ND_HALF = 8, REC_FINAL = 16, REC_LONG_COMMIT = 36, R
 __device__ __forceinline__ void emit(const BatchDesc &d, uint64_t rec, uintptr_t end, uint32_t r,
                                      const char *L, uint32_t c_lo, uint32_t c_hi)
 {
+    if (d.part_out) {
+        d.part_out[rec] = r; /* raw register of one part */
+        return;
+    }
     if (!d.status) {
         d.out[rec] = r ^ d.xor_io;
         return;
@@ -344,7 +378,8 @@ __device__ void fill_lds(char *L, const uint32_t *__restrict__ gtab)
 }
 
 template <int G, bool FIXED>
-__device__ __forceinline__ Cursor next_cursor(const BatchDesc &d, const Cursor &c, uint64_t nteams)
+__device__ __forceinline__ Cursor next_cursor(const BatchDesc &d, const Cursor &c, uint64_t nteams,
+                                              uint64_t nitems, uint32_t lp)
 {
     Cursor n = c;
     if (!c.ok)
@@ -354,7 +389,7 @@ __device__ __forceinline__ Cursor next_cursor(const BatchDesc &d, const Cursor &
         return n;
     }
     n.s = 0;
-    n.ok = fetch_record<G, FIXED>(d, c.it.rec + nteams, nteams, n.it);
+    n.ok = fetch_record<G, FIXED>(d, c.it.w + nteams, nteams, nitems, lp, n.it);
     return n;
 }
 
@@ -403,6 +438,11 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
     if (G == 64)
         team = uni64(team); /* whole-wave team: keep record state in SGPRs */
     const uint64_t nteams = (uint64_t)gridDim.x * WAVES * (64 / G);
+    /* work items: records, or records x 2^lp parts; a device-built class list
+     * supplies the record count without a host round trip */
+    const uint64_t count = FIXED ? d.n : (d.list ? (uint64_t)__builtin_amdgcn_readfirstlane(*(g32p)d.list_count) : d.n);
+    const uint32_t lp = (!FIXED && d.split) ? split_log_parts(count) : 0;
+    const uint64_t nitems = count << lp;
 
     /* Flattened (record, step) walk, loads running ahead of compute also
      * across record boundaries.  Fixed-stride batches keep two items in flight
@@ -410,7 +450,7 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
      * their per-record metadata loads wait on the same vmcnt counter. */
     Cursor c0;
     c0.s = 0;
-    c0.ok = fetch_record<G, FIXED>(d, team, nteams, c0.it);
+    c0.ok = fetch_record<G, FIXED>(d, team, nteams, nitems, lp, c0.it);
     uint32_t acc = 0;
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(gtab);
     uint32_t ba[16];
@@ -425,7 +465,7 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
         while (ok) {
             Cursor cn;
             cn.s = 0;
-            cn.ok = fetch_record<G, FIXED>(d, cur.rec + nteams, nteams, cn.it);
+            cn.ok = fetch_record<G, FIXED>(d, cur.w + nteams, nteams, nitems, lp, cn.it);
             uint32_t w[16];
 #pragma unroll
             for (int k = 0; k < 16; ++k)
@@ -481,7 +521,7 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
             ok = cn.ok;
         }
     } else if (FIXED && DEPTH == 2) {
-        Cursor c1 = next_cursor<G, FIXED>(d, c0, nteams);
+        Cursor c1 = next_cursor<G, FIXED>(d, c0, nteams, nitems, lp);
         uint32_t bb[16];
         issue<G>(c1, j, dummy, bb);
         for (;;) {
@@ -493,7 +533,7 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
                 for (int k = 0; k < 16; ++k)
                     w[k] = ba[k];
                 const Cursor cur = c0;
-                const Cursor c2 = next_cursor<G, FIXED>(d, c1, nteams);
+                const Cursor c2 = next_cursor<G, FIXED>(d, c1, nteams, nitems, lp);
                 issue<G>(c2, j, dummy, ba);
                 c0 = c1;
                 c1 = c2;
@@ -507,7 +547,7 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
                 for (int k = 0; k < 16; ++k)
                     w[k] = bb[k];
                 const Cursor cur = c0;
-                const Cursor c2 = next_cursor<G, FIXED>(d, c1, nteams);
+                const Cursor c2 = next_cursor<G, FIXED>(d, c1, nteams, nitems, lp);
                 issue<G>(c2, j, dummy, bb);
                 c0 = c1;
                 c1 = c2;
@@ -521,7 +561,7 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
 #pragma unroll
             for (int k = 0; k < 16; ++k)
                 w[k] = ba[k];
-            c0 = next_cursor<G, FIXED>(d, cur, nteams);
+            c0 = next_cursor<G, FIXED>(d, cur, nteams, nitems, lp);
             issue<G>(c0, j, dummy, ba);
             compute<G>(d, cur, w, acc, j, lane, L, c_lo, c_hi);
         }
@@ -529,18 +569,6 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
 }
 
 /* ------------------------------------------------------------ span fold */
-__device__ __forceinline__ uint32_t gmul(uint32_t a, uint32_t b)
-{
-    uint32_t acc = 0;
-#pragma unroll 4
-    for (int i = 0; i < 32; ++i) {
-        acc ^= (a & 0x80000000u) ? b : 0u;
-        a <<= 1;
-        b = (b >> 1) ^ ((b & 1u) ? 0x82F63B78u : 0u);
-    }
-    return acc;
-}
-
 /* K^m from the table K^(2^b). */
 __device__ __forceinline__ uint32_t kpow(const uint32_t *kp2, uint32_t m)
 {
@@ -584,6 +612,106 @@ __global__ __launch_bounds__(1024) void span_fold_kernel(SpanFold f)
     }
 }
 
+/* ------------------------------------------------- classes and parts */
+
+
+/* Partition a variable batch into length classes on the device: class c gets
+ * the records with bound[c-1] < len <= bound[c], appended to list[c] with one
+ * wave-aggregated atomic per class and wave.  Order inside a list is
+ * irrelevant: every result is written at its record index. */
+__global__ __launch_bounds__(256) void classify_kernel(Classify c)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    const int lane = threadIdx.x & 63;
+    for (uint64_t base = (uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u); base < c.n; base += stride) {
+        const uint64_t rec = base + lane;
+        int cls = -1;
+        if (rec < c.n) {
+            const uint64_t len = ((const __attribute__((address_space(1))) uint64_t *)c.len)[rec];
+            cls = len <= c.bound[0] ? 0 : len <= c.bound[1] ? 1 : len <= c.bound[2] ? 2 : 3;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint64_t m = __ballot(cls == k);
+            if (!m)
+                continue;
+            uint32_t pos = 0;
+            if (lane == __ffsll((unsigned long long)m) - 1)
+                pos = atomicAdd(&c.count[k], (uint32_t)__popcll(m));
+            pos = __shfl(pos, __ffsll((unsigned long long)m) - 1);
+            if (cls == k)
+                c.list[k][pos + __popcll(m & ((1ull << lane) - 1))] = (uint32_t)rec;
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t xpow8(const uint32_t *pow2, uint64_t n)
+{
+    uint32_t r = 0x80000000u;
+    for (int k = 0; n; ++k, n >>= 1)
+        if (n & 1)
+            r = gmul(r, pow2[k]);
+    return r;
+}
+
+/* Fold the 2^lp part registers of every listed record (register after part p
+ * = shift(register before, |part p|) ^ raw_p), then finish like emit(): plain
+ * CRC, or the commit trailer + comparison in commit mode. */
+__global__ __launch_bounds__(256) void part_fold_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
+{
+    const uint32_t *pow2 = gtab + GT_POW2;
+    const uint64_t count = d.list ? (uint64_t)*(g32p)d.list_count : d.n;
+    const uint32_t lp = split_log_parts(count);
+    const uint64_t K = 1ull << lp;
+    const uint32_t X4 = pow2[2]; /* x^32: one slice-by-4 step */
+    for (uint64_t idx = (uint64_t)blockIdx.x * 256 + threadIdx.x; idx < count;
+         idx += (uint64_t)gridDim.x * 256) {
+        const uint64_t rec = d.list ? ((g32p)d.list)[idx] : idx;
+        const uint64_t len = ((const __attribute__((address_space(1))) uint64_t *)d.len)[rec];
+        if (len < d.len_lo || len > d.len_hi)
+            continue;
+        const uint64_t P = (((len + K - 1) >> lp) + 63) & ~63ull;
+        const uint32_t XP = xpow8(pow2, P);
+        const uint32_t *parts = d.part_out + (idx << lp);
+        uint32_t reg = parts[0];
+        for (uint64_t p = 1; p < K; ++p) {
+            const uint64_t lo = p * P;
+            if (lo >= len)
+                break;
+            const uint64_t plen = len - lo < P ? len - lo : P;
+            reg = gmul(reg, plen == P ? XP : xpow8(pow2, plen)) ^ parts[p];
+        }
+        if (!d.status) {
+            d.out[rec] = reg ^ d.xor_io;
+            continue;
+        }
+        const uint64_t off = ((const __attribute__((address_space(1))) uint64_t *)d.off)[rec];
+        const uintptr_t end = reinterpret_cast<uintptr_t>(d.base) + off + len;
+        const uint64_t w0 = load_be64(end);
+        const uint32_t t = (uint32_t)(w0 >> 56);
+        uint64_t tw[3];
+        int nt = 0;
+        uint32_t stored = 0;
+        if (t == REC_COMMIT || t == REC_FINAL) {
+            tw[nt++] = w0 & 0xFFFFFFFF00000000ull;
+            stored = (uint32_t)w0;
+        } else if (t == REC_LONG_COMMIT || t == REC_LONG_FINAL) {
+            const uint64_t w2 = load_be64(end + 16);
+            tw[nt++] = w0;
+            tw[nt++] = load_be64(end + 8);
+            tw[nt++] = w2 & 0xFF00000000000000ull;
+            stored = (uint32_t)w2;
+        }
+        for (int i = 0; i < nt; ++i) {
+            reg = gmul(reg ^ (uint32_t)tw[i], X4);
+            reg = gmul(reg ^ (uint32_t)(tw[i] >> 32), X4);
+        }
+        const uint32_t crc = reg ^ 0xffffffffu;
+        d.out[rec] = crc;
+        d.status[rec] = nt == 0 ? 2u : (crc == stored ? 1u : 0u);
+    }
+}
+
 /* ------------------------------------------------------ diagnostics */
 /* Plain coalesced streaming read (16 B per lane, 1 KiB per wave-instruction,
  * 4 instructions in flight per wave) XOR-reduced into one word: the measured
@@ -609,6 +737,23 @@ __global__ __launch_bounds__(1024) void stream_read_kernel(const uint8_t *buf, u
 } // namespace zs
 
 /* ------------------------------------------------------------ launchers */
+extern "C" int zs_launch_classify(const zs::Classify *c, hipStream_t stream)
+{
+    uint64_t blocks = (c->n + 255) / 256;
+    if (blocks > 4096)
+        blocks = 4096;
+    if (blocks == 0)
+        blocks = 1;
+    hipLaunchKernelGGL(zs::classify_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, *c);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int zs_launch_part_fold(const zs::BatchDesc *d, const uint32_t *gtab, hipStream_t stream)
+{
+    hipLaunchKernelGGL(zs::part_fold_kernel, dim3(1024), dim3(256), 0, stream, *d, gtab);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
 extern "C" int zs_launch_stream_read(const void *buf, uint64_t n, uint32_t *out, int grid, hipStream_t stream)
 {
     hipLaunchKernelGGL(zs::stream_read_kernel, dim3(grid), dim3(1024), 0, stream,
