@@ -51,7 +51,7 @@ int g_strict = 0;
 std::atomic<int> g_depth[3] = {{-1}, {-1}, {-1}};
 
 struct DevCtx {
-    std::mutex mu;
+    std::recursive_mutex mu;
     bool ready = false;
     int ncu = 0;
     uint32_t *gtab = nullptr;
@@ -117,7 +117,7 @@ int get_ctx(DevCtx **out)
         return ZSCRC_ENODEV;
     }
     DevCtx &c = g_ctx[dev];
-    std::lock_guard<std::mutex> lk(c.mu);
+    std::lock_guard<std::recursive_mutex> lk(c.mu);
     if (c.ready) {
         *out = &c;
         return ZSCRC_OK;
@@ -244,7 +244,7 @@ int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s)
     const size_t list_bytes = 4 * n * sizeof(uint32_t) + 64;
     const size_t part_bytes = (n * 16 + 16384) * sizeof(uint32_t);
     {
-        std::lock_guard<std::mutex> lk(c->mu);
+        std::lock_guard<std::recursive_mutex> lk(c->mu);
         int rc = grow(&c->classes, &c->classes_bytes, list_bytes);
         if (!rc)
             rc = grow(&c->parts, &c->parts_bytes, part_bytes);
@@ -370,7 +370,7 @@ bool gpu_scalar(uint32_t crc, const void *buf, size_t len, uint32_t *res)
     DevCtx *c = nullptr;
     if (get_ctx(&c))
         return false;
-    std::lock_guard<std::mutex> lk(c->mu);
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
     if (grow(&c->stage, &c->stage_bytes, len + 64))
         return false;
     uint8_t *dbuf = static_cast<uint8_t *>(c->stage);
@@ -513,7 +513,7 @@ int zscrc_device_span(const void *d_buf, uint64_t len, uint32_t seed, uint32_t *
     int rc = get_ctx(&c);
     if (rc)
         return rc;
-    std::lock_guard<std::mutex> lk(c->mu);
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
     return span_impl(c, d_buf, len, seed, d_out, scratch, flags, static_cast<hipStream_t>(stream));
 }
 
@@ -539,7 +539,7 @@ int zscrc_host_batch(const void *base, const uint64_t *off, const uint64_t *len,
         hi = lo;
     const uint64_t data = (hi - lo + 15) & ~15ull;
     const uint64_t need = data + n * (8 + 8 + 4 + 4) + 64;
-    std::lock_guard<std::mutex> lk(c->mu);
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
     if ((rc = grow(&c->stage, &c->stage_bytes, need)))
         return rc;
     uint8_t *dbase = static_cast<uint8_t *>(c->stage);
