@@ -208,7 +208,7 @@ int walk_for(int g, int fixed, uint64_t len)
 int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s, int depth_hint = -1)
 {
     /* fixed-stride form when no per-record arrays are involved */
-    const int fixed = !d.off && !d.len && !d.seed && !d.status && d.len_lo == 0 && d.len_hi == ~0ull;
+    const int fixed = !d.desc && !d.off && !d.len && !d.seed && !d.status && d.len_lo == 0 && d.len_hi == ~0ull;
     const uint64_t typical = fixed ? d.fixed_len : (d.len_lo > 0 ? d.len_lo : 1);
     int depth = g_depth[g == 1 ? 0 : g == 16 ? 1 : 2];
     if (depth < 0)
@@ -241,7 +241,7 @@ int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s)
     if (b1 < g1)
         b1 = g1;
     const uint64_t b2 = g16 > b1 ? g16 : b1;
-    const size_t list_bytes = 4 * n * sizeof(uint32_t) + 64;
+    const size_t list_bytes = 64 + n * sizeof(zs::RecDesc);
     const size_t part_bytes = (n * 16 + 16384) * sizeof(uint32_t);
     {
         std::lock_guard<std::recursive_mutex> lk(c->mu);
@@ -252,7 +252,7 @@ int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s)
             return rc;
     }
     uint32_t *cnt = static_cast<uint32_t *>(c->classes);
-    uint32_t *lists = cnt + 16;
+    zs::RecDesc *desc = reinterpret_cast<zs::RecDesc *>(static_cast<char *>(c->classes) + 64);
     hipError_t e = hipMemsetAsync(cnt, 0, 64, s);
     if (e != hipSuccess) {
         set_err("hipMemsetAsync(class counters)", e);
@@ -260,27 +260,32 @@ int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s)
     }
     zs::Classify cl;
     memset(&cl, 0, sizeof cl);
+    cl.off = d.off;
     cl.len = d.len;
+    cl.seed = d.seed;
     cl.n = n;
     cl.bound[0] = g1;
     cl.bound[1] = b1;
     cl.bound[2] = b2;
-    for (int k = 0; k < 4; ++k)
-        cl.list[k] = lists + (uint64_t)k * n;
     cl.count = cnt;
-    if (zs_launch_classify(&cl, s)) {
-        set_err("classify launch", hipGetLastError());
-        return ZSCRC_EHIP;
+    cl.desc = desc;
+    for (int pass = 0; pass < 2; ++pass) {
+        cl.pass = pass;
+        if (zs_launch_classify(&cl, s)) {
+            set_err("classify launch", hipGetLastError());
+            return ZSCRC_EHIP;
+        }
+        g_stat[2]++;
     }
-    g_stat[2]++;
     const int team[4] = {1, 16, 16, 64};
     const int walk[4] = {1, 1, 0, 0};
     d.len_lo = 0;
     d.len_hi = ~0ull;
+    d.desc = desc;
+    d.class_count = cnt;
     for (int k = 0; k < 4; ++k) {
         zs::BatchDesc dk = d;
-        dk.list = cl.list[k];
-        dk.list_count = cnt + k;
+        dk.klass = (uint32_t)k;
         if (k == 3) {
             dk.split = 1;
             dk.part_out = static_cast<uint32_t *>(c->parts);
@@ -289,12 +294,7 @@ int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s)
         if (rc)
             return rc;
         if (k == 3) {
-            zs::BatchDesc df = d;
-            df.list = cl.list[k];
-            df.list_count = cnt + k;
-            df.split = 1;
-            df.part_out = static_cast<uint32_t *>(c->parts);
-            if (zs_launch_part_fold(&df, c->gtab, s)) {
+            if (zs_launch_part_fold(&dk, c->gtab, s)) {
                 set_err("part fold launch", hipGetLastError());
                 return ZSCRC_EHIP;
             }

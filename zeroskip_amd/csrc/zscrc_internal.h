@@ -16,6 +16,8 @@ enum {
 
 namespace zs {
 
+struct RecDesc;
+
 struct BatchDesc {
     const uint8_t *base;
     const uint64_t *off;  /* NULL -> rec * stride        */
@@ -35,10 +37,12 @@ struct BatchDesc {
      * CRC (span + host-order trailer words) and status[i] 1 = matches the
      * stored CRC, 0 = mismatch, 2 = no commit record there. */
     uint32_t *status;
-    /* record lists built on the device by classify_kernel: when `list` is
-     * non-NULL the launch covers records list[0 .. *list_count) */
-    const uint32_t *list;
-    const uint32_t *list_count;
+    /* variable batches: class-sorted record descriptors built on the device
+     * by classify_kernel; this launch covers class `klass`, i.e. entries
+     * [sum(class_count[<klass]), +class_count[klass]) */
+    const struct RecDesc *desc;
+    const uint32_t *class_count;
+    uint32_t klass;
     /* split long records into 2^lp equal parts (lp chosen in-kernel from the
      * record count) whose raw registers go to part_out[idx << lp | part];
      * part_fold_kernel folds them per record */
@@ -46,12 +50,22 @@ struct BatchDesc {
     uint32_t *part_out;
 };
 
+struct RecDesc {
+    uint64_t off;
+    uint64_t len;
+    uint32_t seed;
+    uint32_t rec;         /* index in the caller's batch */
+};
+
 struct Classify {
+    const uint64_t *off;
     const uint64_t *len;
+    const uint32_t *seed; /* NULL -> 0 */
     uint64_t n;
     uint64_t bound[3];    /* class c holds bound[c-1] < len <= bound[c] */
-    uint32_t *list[4];
-    uint32_t *count;      /* 4 counters, zeroed before the launch */
+    uint32_t *count;      /* [0..3] class sizes, [4..7] scatter cursors; zeroed */
+    RecDesc *desc;        /* n entries, class-sorted after the scatter pass */
+    int pass;             /* 0 = count, 1 = scatter */
 };
 
 /* parts per long record for `count` records: >= 16 and >= 8192 items */

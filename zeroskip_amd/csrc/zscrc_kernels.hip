@@ -136,53 +136,79 @@ struct Cursor {
 /* FIXED: record i = base + i*stride, fixed_len bytes (last_len for the last
  * one when set), fixed_seed -- no per-record metadata loads, so nothing here
  * waits on the vector-memory counter and the data prefetch ring survives. */
+/* The team's next record descriptor, loaded one record ahead. */
+struct Meta {
+    uint64_t off, len;
+    uint32_t seed, rec;
+    uint64_t idx;
+};
+
+__device__ __forceinline__ void load_meta(const RecDesc *list, uint64_t idx, uint64_t clamp, Meta &m)
+{
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    typedef const __attribute__((address_space(1))) u32x2 *g2p;
+    const g2p p = (g2p)(list + (idx < clamp ? idx : clamp));
+    const u32x2 a = p[0], b = p[1], c = p[2];
+    m.off = ((uint64_t)a.y << 32) | a.x;
+    m.len = ((uint64_t)b.y << 32) | b.x;
+    m.seed = c.x;
+    m.rec = c.y;
+    m.idx = idx;
+}
+
 template <int G, bool FIXED>
-__device__ __forceinline__ bool fetch_record(const BatchDesc &d, uint64_t w, uint64_t nteams, uint64_t nitems,
-                                             uint32_t lp, Item &it)
+__device__ __forceinline__ bool fetch_record(const BatchDesc &d, const RecDesc *list, uint64_t count,
+                                             uint64_t w, uint64_t nteams, uint64_t nitems, uint32_t lp,
+                                             Meta &pre, Item &it)
 {
     constexpr uint64_t STEP = (uint64_t)G * 64;
-    for (; w < nitems; w += nteams) {
-        uint64_t len, off, lo = 0, rec = w;
-        uint32_t seed;
-        if (FIXED) {
-            len = (d.last_len != ~0ull && rec + 1 == d.n) ? d.last_len : d.fixed_len;
-            off = rec * d.stride;
-            seed = d.fixed_seed;
-        } else {
-            rec = w >> lp;
-            if (d.list)
-                rec = ((g32p)d.list)[rec];
-            len = d.len ? ((const __attribute__((address_space(1))) uint64_t *)d.len)[rec] : d.fixed_len;
-            if (len < d.len_lo || len > d.len_hi)
-                continue;
-            off = d.off ? ((const __attribute__((address_space(1))) uint64_t *)d.off)[rec] : rec * d.stride;
-            seed = d.seed ? ((g32p)d.seed)[rec] : d.fixed_seed;
-            if (lp) {
-                /* part (w mod 2^lp) of the record: equal 64-byte-multiple parts */
-                const uint64_t P = (((len + (1ull << lp) - 1) >> lp) + 63) & ~63ull;
-                const uint64_t part = w & ((1ull << lp) - 1);
-                lo = part * P < len ? part * P : len;
-                const uint64_t hi = lo + P < len ? lo + P : len;
-                len = hi - lo;
-                if (part)
-                    seed = d.xor_io; /* parts after the first start from a zero register */
-                rec = w;             /* part_out index */
-            }
+    if (w >= nitems)
+        return false;
+    uint64_t len, off, lo = 0, rec = w;
+    uint32_t seed;
+    if (FIXED) {
+        len = (d.last_len != ~0ull && rec + 1 == d.n) ? d.last_len : d.fixed_len;
+        off = rec * d.stride;
+        seed = d.fixed_seed;
+    } else {
+        const uint64_t idx = w >> lp;
+        Meta m = pre;
+        if (m.idx != idx)
+            load_meta(list, idx, count - 1, m);
+        /* prefetch the descriptor of this team's next work item's record */
+        const uint64_t nidx = (w + nteams) >> lp;
+        if (nidx != idx)
+            load_meta(list, nidx, count - 1, pre);
+        else
+            pre = m;
+        len = m.len;
+        off = m.off;
+        seed = m.seed;
+        rec = m.rec;
+        if (lp) {
+            /* part (w mod 2^lp) of the record: equal 64-byte-multiple parts */
+            const uint64_t P = (((len + (1ull << lp) - 1) >> lp) + 63) & ~63ull;
+            const uint64_t part = w & ((1ull << lp) - 1);
+            lo = part * P < len ? part * P : len;
+            const uint64_t hi = lo + P < len ? lo + P : len;
+            len = hi - lo;
+            if (part)
+                seed = d.xor_io; /* parts after the first start from a zero register */
+            rec = w;             /* part_out index */
         }
-        const uintptr_t A = reinterpret_cast<uintptr_t>(d.base) + off + lo;
-        const uintptr_t E = len < 8 ? A : ((A + len) & ~uintptr_t(3));
-        const uint64_t S = len < 8 ? 0 : (E - A + STEP - 1) / STEP;
-        it.A = A;
-        it.E = E;
-        it.V0 = E - S * STEP;
-        it.S = S;
-        it.len = len;
-        it.rec = rec;
-        it.w = w;
-        it.R0 = seed ^ d.xor_io;
-        return true;
     }
-    return false;
+    const uintptr_t A = reinterpret_cast<uintptr_t>(d.base) + off + lo;
+    const uintptr_t E = len < 8 ? A : ((A + len) & ~uintptr_t(3));
+    const uint64_t S = len < 8 ? 0 : (E - A + STEP - 1) / STEP;
+    it.A = A;
+    it.E = E;
+    it.V0 = E - S * STEP;
+    it.S = S;
+    it.len = len;
+    it.rec = rec;
+    it.w = w;
+    it.R0 = seed ^ d.xor_io;
+    return true;
 }
 
 /* Issue the loads of lane j's piece of step s: always exactly four 16-byte
@@ -378,8 +404,9 @@ __device__ void fill_lds(char *L, const uint32_t *__restrict__ gtab)
 }
 
 template <int G, bool FIXED>
-__device__ __forceinline__ Cursor next_cursor(const BatchDesc &d, const Cursor &c, uint64_t nteams,
-                                              uint64_t nitems, uint32_t lp)
+__device__ __forceinline__ Cursor next_cursor(const BatchDesc &d, const RecDesc *list, uint64_t count,
+                                              const Cursor &c, uint64_t nteams, uint64_t nitems, uint32_t lp,
+                                              Meta &pre)
 {
     Cursor n = c;
     if (!c.ok)
@@ -389,7 +416,7 @@ __device__ __forceinline__ Cursor next_cursor(const BatchDesc &d, const Cursor &
         return n;
     }
     n.s = 0;
-    n.ok = fetch_record<G, FIXED>(d, c.it.w + nteams, nteams, nitems, lp, n.it);
+    n.ok = fetch_record<G, FIXED>(d, list, count, c.it.w + nteams, nteams, nitems, lp, pre, n.it);
     return n;
 }
 
@@ -440,9 +467,19 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
     const uint64_t nteams = (uint64_t)gridDim.x * WAVES * (64 / G);
     /* work items: records, or records x 2^lp parts; a device-built class list
      * supplies the record count without a host round trip */
-    const uint64_t count = FIXED ? d.n : (d.list ? (uint64_t)__builtin_amdgcn_readfirstlane(*(g32p)d.list_count) : d.n);
+    uint64_t count = d.n;
+    const RecDesc *list = nullptr;
+    if (!FIXED) {
+        uint32_t base = 0;
+        for (uint32_t k = 0; k < d.klass; ++k)
+            base += __builtin_amdgcn_readfirstlane(((g32p)d.class_count)[k]);
+        count = __builtin_amdgcn_readfirstlane(((g32p)d.class_count)[d.klass]);
+        list = d.desc + base;
+    }
     const uint32_t lp = (!FIXED && d.split) ? split_log_parts(count) : 0;
     const uint64_t nitems = count << lp;
+    Meta pre;
+    pre.idx = ~0ull;
 
     /* Flattened (record, step) walk, loads running ahead of compute also
      * across record boundaries.  Fixed-stride batches keep two items in flight
@@ -450,7 +487,7 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
      * their per-record metadata loads wait on the same vmcnt counter. */
     Cursor c0;
     c0.s = 0;
-    c0.ok = fetch_record<G, FIXED>(d, team, nteams, nitems, lp, c0.it);
+    c0.ok = fetch_record<G, FIXED>(d, list, count, team, nteams, nitems, lp, pre, c0.it);
     uint32_t acc = 0;
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(gtab);
     uint32_t ba[16];
@@ -465,7 +502,7 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
         while (ok) {
             Cursor cn;
             cn.s = 0;
-            cn.ok = fetch_record<G, FIXED>(d, cur.w + nteams, nteams, nitems, lp, cn.it);
+            cn.ok = fetch_record<G, FIXED>(d, list, count, cur.w + nteams, nteams, nitems, lp, pre, cn.it);
             uint32_t w[16];
 #pragma unroll
             for (int k = 0; k < 16; ++k)
@@ -521,7 +558,7 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
             ok = cn.ok;
         }
     } else if (FIXED && DEPTH == 2) {
-        Cursor c1 = next_cursor<G, FIXED>(d, c0, nteams, nitems, lp);
+        Cursor c1 = next_cursor<G, FIXED>(d, list, count, c0, nteams, nitems, lp, pre);
         uint32_t bb[16];
         issue<G>(c1, j, dummy, bb);
         for (;;) {
@@ -533,7 +570,7 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
                 for (int k = 0; k < 16; ++k)
                     w[k] = ba[k];
                 const Cursor cur = c0;
-                const Cursor c2 = next_cursor<G, FIXED>(d, c1, nteams, nitems, lp);
+                const Cursor c2 = next_cursor<G, FIXED>(d, list, count, c1, nteams, nitems, lp, pre);
                 issue<G>(c2, j, dummy, ba);
                 c0 = c1;
                 c1 = c2;
@@ -547,7 +584,7 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
                 for (int k = 0; k < 16; ++k)
                     w[k] = bb[k];
                 const Cursor cur = c0;
-                const Cursor c2 = next_cursor<G, FIXED>(d, c1, nteams, nitems, lp);
+                const Cursor c2 = next_cursor<G, FIXED>(d, list, count, c1, nteams, nitems, lp, pre);
                 issue<G>(c2, j, dummy, bb);
                 c0 = c1;
                 c1 = c2;
@@ -561,7 +598,7 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
 #pragma unroll
             for (int k = 0; k < 16; ++k)
                 w[k] = ba[k];
-            c0 = next_cursor<G, FIXED>(d, cur, nteams, nitems, lp);
+            c0 = next_cursor<G, FIXED>(d, list, count, cur, nteams, nitems, lp, pre);
             issue<G>(c0, j, dummy, ba);
             compute<G>(d, cur, w, acc, j, lane, L, c_lo, c_hi);
         }
@@ -615,19 +652,27 @@ __global__ __launch_bounds__(1024) void span_fold_kernel(SpanFold f)
 /* ------------------------------------------------- classes and parts */
 
 
-/* Partition a variable batch into length classes on the device: class c gets
- * the records with bound[c-1] < len <= bound[c], appended to list[c] with one
- * wave-aggregated atomic per class and wave.  Order inside a list is
+/* Sort a variable batch into four length classes on the device, as compact
+ * descriptors (off, len, seed, record index): pass 0 counts the classes,
+ * pass 1 scatters each record behind the classes before it, with one
+ * wave-aggregated atomic per class and wave.  Order inside a class is
  * irrelevant: every result is written at its record index. */
 __global__ __launch_bounds__(256) void classify_kernel(Classify c)
 {
     const uint64_t stride = (uint64_t)gridDim.x * 256;
     const int lane = threadIdx.x & 63;
-    for (uint64_t base = (uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u); base < c.n; base += stride) {
-        const uint64_t rec = base + lane;
+    uint32_t base[4] = {0, 0, 0, 0};
+    if (c.pass == 1) {
+        base[1] = c.count[0];
+        base[2] = base[1] + c.count[1];
+        base[3] = base[2] + c.count[2];
+    }
+    for (uint64_t b = (uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u); b < c.n; b += stride) {
+        const uint64_t rec = b + lane;
         int cls = -1;
+        uint64_t len = 0;
         if (rec < c.n) {
-            const uint64_t len = ((const __attribute__((address_space(1))) uint64_t *)c.len)[rec];
+            len = ((const __attribute__((address_space(1))) uint64_t *)c.len)[rec];
             cls = len <= c.bound[0] ? 0 : len <= c.bound[1] ? 1 : len <= c.bound[2] ? 2 : 3;
         }
 #pragma unroll
@@ -635,12 +680,21 @@ __global__ __launch_bounds__(256) void classify_kernel(Classify c)
             const uint64_t m = __ballot(cls == k);
             if (!m)
                 continue;
+            const int leader = __ffsll((unsigned long long)m) - 1;
             uint32_t pos = 0;
-            if (lane == __ffsll((unsigned long long)m) - 1)
-                pos = atomicAdd(&c.count[k], (uint32_t)__popcll(m));
-            pos = __shfl(pos, __ffsll((unsigned long long)m) - 1);
-            if (cls == k)
-                c.list[k][pos + __popcll(m & ((1ull << lane) - 1))] = (uint32_t)rec;
+            if (lane == leader)
+                pos = atomicAdd(&c.count[c.pass == 0 ? k : 4 + k], (uint32_t)__popcll(m));
+            if (c.pass == 0)
+                continue;
+            pos = __shfl(pos, leader);
+            if (cls == k) {
+                RecDesc r;
+                r.off = ((const __attribute__((address_space(1))) uint64_t *)c.off)[rec];
+                r.len = len;
+                r.seed = c.seed ? ((g32p)c.seed)[rec] : 0u;
+                r.rec = (uint32_t)rec;
+                c.desc[base[k] + pos + __popcll(m & ((1ull << lane) - 1))] = r;
+            }
         }
     }
 }
@@ -660,16 +714,18 @@ __device__ __forceinline__ uint32_t xpow8(const uint32_t *pow2, uint64_t n)
 __global__ __launch_bounds__(256) void part_fold_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
 {
     const uint32_t *pow2 = gtab + GT_POW2;
-    const uint64_t count = d.list ? (uint64_t)*(g32p)d.list_count : d.n;
+    uint32_t base = 0;
+    for (uint32_t k = 0; k < d.klass; ++k)
+        base += d.class_count[k];
+    const uint64_t count = d.class_count[d.klass];
+    const RecDesc *list = d.desc + base;
     const uint32_t lp = split_log_parts(count);
     const uint64_t K = 1ull << lp;
     const uint32_t X4 = pow2[2]; /* x^32: one slice-by-4 step */
     for (uint64_t idx = (uint64_t)blockIdx.x * 256 + threadIdx.x; idx < count;
          idx += (uint64_t)gridDim.x * 256) {
-        const uint64_t rec = d.list ? ((g32p)d.list)[idx] : idx;
-        const uint64_t len = ((const __attribute__((address_space(1))) uint64_t *)d.len)[rec];
-        if (len < d.len_lo || len > d.len_hi)
-            continue;
+        const RecDesc r = list[idx];
+        const uint64_t len = r.len;
         const uint64_t P = (((len + K - 1) >> lp) + 63) & ~63ull;
         const uint32_t XP = xpow8(pow2, P);
         const uint32_t *parts = d.part_out + (idx << lp);
@@ -682,11 +738,10 @@ __global__ __launch_bounds__(256) void part_fold_kernel(BatchDesc d, const uint3
             reg = gmul(reg, plen == P ? XP : xpow8(pow2, plen)) ^ parts[p];
         }
         if (!d.status) {
-            d.out[rec] = reg ^ d.xor_io;
+            d.out[r.rec] = reg ^ d.xor_io;
             continue;
         }
-        const uint64_t off = ((const __attribute__((address_space(1))) uint64_t *)d.off)[rec];
-        const uintptr_t end = reinterpret_cast<uintptr_t>(d.base) + off + len;
+        const uintptr_t end = reinterpret_cast<uintptr_t>(d.base) + r.off + len;
         const uint64_t w0 = load_be64(end);
         const uint32_t t = (uint32_t)(w0 >> 56);
         uint64_t tw[3];
@@ -707,8 +762,8 @@ __global__ __launch_bounds__(256) void part_fold_kernel(BatchDesc d, const uint3
             reg = gmul(reg ^ (uint32_t)(tw[i] >> 32), X4);
         }
         const uint32_t crc = reg ^ 0xffffffffu;
-        d.out[rec] = crc;
-        d.status[rec] = nt == 0 ? 2u : (crc == stored ? 1u : 0u);
+        d.out[r.rec] = crc;
+        d.status[r.rec] = nt == 0 ? 2u : (crc == stored ? 1u : 0u);
     }
 }
 
