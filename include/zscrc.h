@@ -164,6 +164,11 @@ int zscrc_zs_dotzsdb_crc(const void *image, uint64_t size, uint32_t *stored, uin
 int zscrc_device_verify_commits(const void *d_image, const uint64_t *d_span_off, const uint64_t *d_span_len,
                                 size_t n, uint32_t *d_crc, uint32_t *d_status, void *stream);
 
+/* Device: compute n commit CRCs (the writer's side, zeroskip-file.c:253-350)
+ * and store each one big-endian into its commit record; d_crc[i] receives it. */
+int zscrc_device_write_commits(void *d_image, const uint64_t *d_span_off, const uint64_t *d_span_len, size_t n,
+                               uint32_t *d_crc, void *stream);
+
 typedef struct zscrc_zs_report {
     int header_rc;            /* zscrc_zs_header_crc result */
     uint32_t header_stored, header_computed;

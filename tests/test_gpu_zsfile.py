@@ -78,3 +78,20 @@ def test_device_commits_match_oracle_crcs(gpu):
     torch.cuda.synchronize()
     assert (st.cpu().numpy() == 1).all()
     assert (crc.cpu().numpy().view(np.uint32) == np.array(want, dtype=np.uint32)).all()
+
+
+def test_write_commits_matches_writer(gpu):
+    # GPU writer side: zero every stored CRC, recompute + store on the device,
+    # compare with the oracle writer's image byte for byte
+    img = build_active(300, seed=21)
+    commits, _, _ = zf.walk(img)
+    blank = bytearray(img)
+    for c in commits:
+        blank[c["commit_off"] + 4:c["commit_off"] + 8] = b"\0\0\0\0"
+    d = torch.from_numpy(np.frombuffer(bytes(blank), dtype=np.uint8).copy()).cuda()
+    offs = torch.tensor([c["span_off"] for c in commits], dtype=torch.int64, device="cuda")
+    lens = torch.tensor([c["span_len"] for c in commits], dtype=torch.int64, device="cuda")
+    crc = zsfile.write_commits(d, offs, lens)
+    torch.cuda.synchronize()
+    assert d.cpu().numpy().tobytes() == img
+    assert (crc.cpu().numpy().view(np.uint32) == np.array([c["stored"] for c in commits], np.uint32)).all()

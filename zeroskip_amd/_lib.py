@@ -42,6 +42,7 @@ SIGNATURES = {
     "zscrc_zs_dotzsdb_crc": (_int, [_vp, _u64, _vp, _vp]),
     "zscrc_device_verify_commits": (_int, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
     "zscrc_zs_verify_image": (_int, [_vp, _u64, _int, _vp]),
+    "zscrc_device_write_commits": (_int, [_vp, _vp, _vp, _sz, _vp, _vp]),
 }
 
 ZSCRC_RAW = 1

@@ -208,7 +208,7 @@ int walk_for(int g, int fixed, uint64_t len)
 int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s, int depth_hint = -1)
 {
     /* fixed-stride form when no per-record arrays are involved */
-    const int fixed = !d.desc && !d.off && !d.len && !d.seed && !d.status && d.len_lo == 0 && d.len_hi == ~0ull;
+    const int fixed = !d.desc && !d.off && !d.len && !d.seed && !d.commit && d.len_lo == 0 && d.len_hi == ~0ull;
     const uint64_t typical = fixed ? d.fixed_len : (d.len_lo > 0 ? d.len_lo : 1);
     int depth = g_depth[g == 1 ? 0 : g == 16 ? 1 : 2];
     if (depth < 0)
@@ -602,11 +602,11 @@ int zscrc_diag_stream_read(const void *d_buf, uint64_t len, void *d_scratch4, in
 }
 
 int zscrc_internal_verify_commits(const void *d_image, const uint64_t *d_off, const uint64_t *d_len,
-                                  uint32_t *d_crc, uint32_t *d_status, size_t n, void *stream)
+                                  uint32_t *d_crc, uint32_t *d_status, size_t n, void *stream, int write)
 {
     if (n == 0)
         return ZSCRC_OK;
-    if (!d_image || !d_off || !d_len || !d_crc || !d_status)
+    if (!d_image || !d_off || !d_len || !d_crc || (!write && !d_status))
         return ZSCRC_EINVAL;
     DevCtx *c;
     int rc = get_ctx(&c);
@@ -618,6 +618,7 @@ int zscrc_internal_verify_commits(const void *d_image, const uint64_t *d_off, co
     d.len = d_len;
     d.out = d_crc;
     d.status = d_status;
+    d.commit = write ? 2u : 1u;
     d.n = n;
     d.xor_io = 0xffffffffu;
     return launch_classes(c, d, static_cast<hipStream_t>(stream));

@@ -32,11 +32,13 @@ struct BatchDesc {
     uint64_t len_hi;
     uint32_t fixed_seed;
     uint32_t xor_io;      /* 0xFFFFFFFF standard CRC, 0 raw registers */
-    /* zeroskip commit verification: when non-NULL, record i is the span of a
-     * commit record that starts right after it; out[i] receives the commit
-     * CRC (span + host-order trailer words) and status[i] 1 = matches the
-     * stored CRC, 0 = mismatch, 2 = no commit record there. */
-    uint32_t *status;
+    /* zeroskip commits: commit = 1 (verify) / 2 (write): record i is the span
+     * of a commit record that starts right after it; out[i] receives the
+     * commit CRC (span + host-order trailer words); verify: status[i] 1 =
+     * matches the stored CRC, 0 = mismatch, 2 = no commit record there;
+     * write: the CRC is stored big-endian into the commit record. */
+    uint32_t commit;
+    uint32_t *status;     /* may be NULL */
     /* variable batches: class-sorted record descriptors built on the device
      * by classify_kernel; this launch covers class `klass`, i.e. entries
      * [sum(class_count[<klass]), +class_count[klass]) */

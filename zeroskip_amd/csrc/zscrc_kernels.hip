@@ -123,6 +123,7 @@ struct Item {
     uint64_t rec;     /* output index (record, or part slot when splitting) */
     uint64_t w;       /* work index of this team's walk */
     uint32_t R0;      /* initial register */
+    uint32_t c0, c1;  /* commit mode: the 8 bytes at the record end (raw) */
 };
 
 /* A (record, step) work item of one team. */
@@ -208,17 +209,24 @@ __device__ __forceinline__ bool fetch_record(const BatchDesc &d, const RecDesc *
     it.rec = rec;
     it.w = w;
     it.R0 = seed ^ d.xor_io;
+    if (!FIXED && d.commit && !lp) {
+        /* the commit record's first word, fetched with the record so the
+         * check at the record end never waits on a late load */
+        it.c0 = ((g32p)(A + len))[0];
+        it.c1 = ((g32p)(A + len))[1];
+    }
     return true;
 }
 
 /* Issue the loads of lane j's piece of step s: always exactly four 16-byte
  * loads (gfx950 serves 4-byte-aligned dwordx4 loads; tools/unaligned_probe),
- * so the compiler can count the prefetch ring with partial vmcnt waits.  In
- * a front-padded step 0 each block address is clamped up to the record's
- * first aligned dword, so nothing before the record is ever touched (fixup
- * re-aligns the clamped block).  Items without loads read a dummy address. */
+ * so the compiler can count the prefetch ring with partial vmcnt waits.  A
+ * front-padded step 0 may read caller bytes before the record (fixup zeroes
+ * them) but never before `lo`, the batch buffer's first aligned dword: block
+ * addresses below it are clamped up (fixup re-aligns such blocks).  Items
+ * without loads read a dummy address. */
 template <int G>
-__device__ __forceinline__ void issue(const Cursor &c, int j, uintptr_t dummy, uint32_t (&w)[16])
+__device__ __forceinline__ void issue(const Cursor &c, int j, uintptr_t dummy, uintptr_t lo, uint32_t (&w)[16])
 {
     constexpr uint64_t STEP = (uint64_t)G * 64;
     const uintptr_t p = c.it.V0 + c.s * STEP + 64 * (uintptr_t)j;
@@ -227,8 +235,7 @@ __device__ __forceinline__ void issue(const Cursor &c, int j, uintptr_t dummy, u
 #pragma unroll
         for (int i = 0; i < 4; ++i)
             q[i] = dummy;
-    } else if (c.s == 0 && c.it.V0 != c.it.A) {
-        const uintptr_t lo = c.it.A & ~uintptr_t(3);
+    } else if (c.s == 0 && p < lo) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
             q[i] = p + 16 * i < lo ? lo : p + 16 * i;
@@ -279,74 +286,92 @@ enum { REC_COMMIT = 4, REC_2ND_HALF = 8, REC_FINAL = 16, REC_LONG_COMMIT = 36, R
 /* Store record `rec`'s result from its final register r.  In commit mode the
  * CRC continues over the commit record's trailer words exactly as the writer
  * hashes them (src/zeroskip-file.c:266-328): short -> LE(type<<56|len<<32);
- * long -> LE(type1<<56), LE(len), LE(2ND_HALF<<56); then compared with the CRC
- * stored in the record's low 32 bits. */
-__device__ __forceinline__ void emit(const BatchDesc &d, uint64_t rec, uintptr_t end, uint32_t r,
-                                     const char *L, uint32_t c_lo, uint32_t c_hi)
+ * long -> LE(type1<<56), LE(len), LE(2ND_HALF<<56); then it is compared with
+ * the CRC stored in the record's low 32 bits, or written there. */
+__device__ __forceinline__ void emit(const BatchDesc &d, const Item &it, uint32_t r, const char *L,
+                                     uint32_t c_lo, uint32_t c_hi)
 {
+    const uint64_t rec = it.rec;
     if (d.part_out) {
         d.part_out[rec] = r; /* raw register of one part */
         return;
     }
-    if (!d.status) {
+    if (!d.commit) {
         d.out[rec] = r ^ d.xor_io;
         return;
     }
-    const uint64_t w0 = load_be64(end);
+    const uintptr_t end = it.A + it.len;
+    const uint64_t w0 = ((uint64_t)__builtin_bswap32(it.c0) << 32) | __builtin_bswap32(it.c1);
     const uint32_t t = (uint32_t)(w0 >> 56);
-    uint32_t stored, st = 0;
+    uint32_t stored = 0, st = 2;
+    uintptr_t crc_at = 0;
     if (t == REC_COMMIT || t == REC_FINAL) {
         r = feed64(L, r, w0 & 0xFFFFFFFF00000000ull, c_lo, c_hi);
         stored = (uint32_t)w0;
+        crc_at = end + 4;
+        st = 0;
     } else if (t == REC_LONG_COMMIT || t == REC_LONG_FINAL) {
         const uint64_t w1 = load_be64(end + 8), w2 = load_be64(end + 16);
         r = feed64(L, r, w0, c_lo, c_hi);
         r = feed64(L, r, w1, c_lo, c_hi);
         r = feed64(L, r, w2 & 0xFF00000000000000ull, c_lo, c_hi);
         stored = (uint32_t)w2;
-    } else {
-        stored = ~(r ^ 0xffffffffu);
-        st = 2;
+        crc_at = end + 20;
+        st = 0;
     }
     const uint32_t crc = r ^ 0xffffffffu;
     d.out[rec] = crc;
-    d.status[rec] = st == 2 ? 2u : (crc == stored ? 1u : 0u);
+    if (d.commit == 2 && st == 0)
+        *(uint32_t *)crc_at = __builtin_bswap32(crc);
+    if (d.status)
+        d.status[rec] = st == 2 ? 2u : (d.commit == 2 || crc == stored ? 1u : 0u);
 }
 
 /* Data fix-ups that need the record start (step 0 of a front-padded grid):
  * undo the clamp of issue(), zero every byte before A, and XOR the initial
  * register into bytes [A, A+4) -- which can spill into step 1. */
 template <int G>
-__device__ __forceinline__ void fixup(const Item &it, uint64_t s, int j, uint32_t (&w)[16])
+__device__ __forceinline__ void fixup(const Item &it, uint64_t s, int j, uintptr_t lo, uint32_t (&w)[16])
 {
     constexpr uint64_t STEP = (uint64_t)G * 64;
     if (s == 0) {
         if (it.V0 != it.A) {
             const uintptr_t p = it.V0 + 64 * (uintptr_t)j;
-            const uintptr_t lo = it.A & ~uintptr_t(3);
+            if (p < lo) { /* only records within 64 B of the buffer start */
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const uintptr_t q = p + 16 * i;
-                /* the block was loaded from max(q, lo): shift it up by m words */
-                const uint64_t m = q < lo ? (lo - q) >> 2 : 0;
-                const uint32_t b0 = w[4 * i], b1 = w[4 * i + 1], b2 = w[4 * i + 2];
-                w[4 * i + 3] = m == 0 ? w[4 * i + 3] : m == 1 ? b2 : m == 2 ? b1 : b0;
-                w[4 * i + 2] = m == 0 ? b2 : m == 1 ? b1 : b0;
-                w[4 * i + 1] = m == 0 ? b1 : b0;
+                for (int i = 0; i < 4; ++i) {
+                    const uintptr_t q = p + 16 * i;
+                    /* the block was loaded from max(q, lo): shift it up by m words */
+                    const uint64_t m = q < lo ? (lo - q) >> 2 : 0;
+                    const uint32_t b0 = w[4 * i], b1 = w[4 * i + 1], b2 = w[4 * i + 2];
+                    w[4 * i + 3] = m == 0 ? w[4 * i + 3] : m == 1 ? b2 : m == 2 ? b1 : b0;
+                    w[4 * i + 2] = m == 0 ? b2 : m == 1 ? b1 : b0;
+                    w[4 * i + 1] = m == 0 ? b1 : b0;
+                }
             }
+            const int32_t d0 = (int32_t)(it.A - p); /* < 64*G */
+            if ((it.A & 3) == 0) {
+                /* aligned record (every zeroskip span): whole words only */
 #pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const int64_t d = (int64_t)(it.A - (p + 4 * k));
-                uint32_t v = w[k];
-                if (d >= 4)
-                    v = 0;
-                else if (d > 0)
-                    v &= 0xffffffffu << (8 * (uint32_t)d);
-                if (d >= 0 && d < 4)
-                    v ^= it.R0 << (8 * (uint32_t)d);
-                else if (d < 0 && d > -4)
-                    v ^= it.R0 >> (8 * (uint32_t)(-d));
-                w[k] = v;
+                for (int k = 0; k < 16; ++k) {
+                    const int32_t dk = d0 - 4 * k;
+                    w[k] = dk > 0 ? 0u : (dk == 0 ? w[k] ^ it.R0 : w[k]);
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    const int32_t dk = d0 - 4 * k;
+                    uint32_t v = w[k];
+                    if (dk >= 4)
+                        v = 0;
+                    else if (dk > 0)
+                        v &= 0xffffffffu << (8 * dk);
+                    if (dk >= 0 && dk < 4)
+                        v ^= it.R0 << (8 * dk);
+                    else if (dk < 0 && dk > -4)
+                        v ^= it.R0 >> (8 * -dk);
+                    w[k] = v;
+                }
             }
         } else if (j == 0) {
             w[0] ^= it.R0;
@@ -425,7 +450,7 @@ __device__ __forceinline__ Cursor next_cursor(const BatchDesc &d, const RecDesc 
 template <int G>
 __device__ __forceinline__ void compute(const BatchDesc &d, const Cursor &c, uint32_t (&w)[16],
                                         uint32_t &acc, int j, int lane, const char *L, uint32_t c_lo,
-                                        uint32_t c_hi)
+                                        uint32_t c_hi, uintptr_t lo)
 {
     const Item &it = c.it;
     if (it.S == 0) { /* < 8 bytes: byte-serial on one lane */
@@ -433,11 +458,11 @@ __device__ __forceinline__ void compute(const BatchDesc &d, const Cursor &c, uin
             uint32_t r = it.R0;
             for (uint64_t i = 0; i < it.len; ++i)
                 r = byte_step(L, r, ((g8p)it.A)[i], c_hi);
-            emit(d, it.rec, it.A + it.len, r, L, c_lo, c_hi);
+            emit(d, it, r, L, c_lo, c_hi);
         }
         return;
     }
-    fixup<G>(it, c.s, j, w);
+    fixup<G>(it, c.s, j, lo, w);
     if (G > 1 && c.s + 1 < it.S)
         acc = piece<true>(L, acc, w, c_lo, c_hi);
     else
@@ -445,7 +470,7 @@ __device__ __forceinline__ void compute(const BatchDesc &d, const Cursor &c, uin
     if (c.s + 1 == it.S) {
         const uint32_t r = finish<G>(it, acc, j, lane, L, c_hi);
         if (j == G - 1)
-            emit(d, it.rec, it.A + it.len, r, L, c_lo, c_hi);
+            emit(d, it, r, L, c_lo, c_hi);
         acc = 0;
     }
 }
@@ -490,8 +515,9 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
     c0.ok = fetch_record<G, FIXED>(d, list, count, team, nteams, nitems, lp, pre, c0.it);
     uint32_t acc = 0;
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(gtab);
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(d.base) & ~uintptr_t(3);
     uint32_t ba[16];
-    issue<G>(c0, j, dummy, ba);
+    issue<G>(c0, j, dummy, lo, ba);
     if (DEPTH == 0) {
         /* Two-level walk: a lean interior step loop per record (plain loads
          * one step ahead), the record's first/last steps peeled so the next
@@ -508,12 +534,12 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
             for (int k = 0; k < 16; ++k)
                 w[k] = ba[k];
             if (cur.S == 0) {
-                issue<G>(cn, j, dummy, ba);
+                issue<G>(cn, j, dummy, lo, ba);
                 if (j == G - 1) {
                     uint32_t r = cur.R0;
                     for (uint64_t i = 0; i < cur.len; ++i)
                         r = byte_step(L, r, ((g8p)cur.A)[i], c_hi);
-                    emit(d, cur.rec, cur.A + cur.len, r, L, c_lo, c_hi);
+                    emit(d, cur, r, L, c_lo, c_hi);
                 }
                 cur = cn.it;
                 ok = cn.ok;
@@ -523,8 +549,8 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
             if (cur.S > 1)
                 issue_plain(p, ba);
             else
-                issue<G>(cn, j, dummy, ba);
-            fixup<G>(cur, 0, j, w);
+                issue<G>(cn, j, dummy, lo, ba);
+            fixup<G>(cur, 0, j, lo, w);
             if (G > 1 && cur.S > 1)
                 acc = piece<true>(L, acc, w, c_lo, c_hi);
             else
@@ -545,14 +571,14 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
 #pragma unroll
                 for (int k = 0; k < 16; ++k)
                     w[k] = ba[k];
-                issue<G>(cn, j, dummy, ba);
+                issue<G>(cn, j, dummy, lo, ba);
                 if (cur.S == 2 && spill)
                     w[0] ^= spill_v;
                 acc = piece<false>(L, acc, w, c_lo, c_hi);
             }
             const uint32_t r = finish<G>(cur, acc, j, lane, L, c_hi);
             if (j == G - 1)
-                emit(d, cur.rec, cur.A + cur.len, r, L, c_lo, c_hi);
+                emit(d, cur, r, L, c_lo, c_hi);
             acc = 0;
             cur = cn.it;
             ok = cn.ok;
@@ -560,7 +586,7 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
     } else if (FIXED && DEPTH == 2) {
         Cursor c1 = next_cursor<G, FIXED>(d, list, count, c0, nteams, nitems, lp, pre);
         uint32_t bb[16];
-        issue<G>(c1, j, dummy, bb);
+        issue<G>(c1, j, dummy, lo, bb);
         for (;;) {
             if (!c0.ok)
                 break;
@@ -571,10 +597,10 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
                     w[k] = ba[k];
                 const Cursor cur = c0;
                 const Cursor c2 = next_cursor<G, FIXED>(d, list, count, c1, nteams, nitems, lp, pre);
-                issue<G>(c2, j, dummy, ba);
+                issue<G>(c2, j, dummy, lo, ba);
                 c0 = c1;
                 c1 = c2;
-                compute<G>(d, cur, w, acc, j, lane, L, c_lo, c_hi);
+                compute<G>(d, cur, w, acc, j, lane, L, c_lo, c_hi, lo);
             }
             if (!c0.ok)
                 break;
@@ -585,10 +611,10 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
                     w[k] = bb[k];
                 const Cursor cur = c0;
                 const Cursor c2 = next_cursor<G, FIXED>(d, list, count, c1, nteams, nitems, lp, pre);
-                issue<G>(c2, j, dummy, bb);
+                issue<G>(c2, j, dummy, lo, bb);
                 c0 = c1;
                 c1 = c2;
-                compute<G>(d, cur, w, acc, j, lane, L, c_lo, c_hi);
+                compute<G>(d, cur, w, acc, j, lane, L, c_lo, c_hi, lo);
             }
         }
     } else {
@@ -599,8 +625,8 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
             for (int k = 0; k < 16; ++k)
                 w[k] = ba[k];
             c0 = next_cursor<G, FIXED>(d, list, count, cur, nteams, nitems, lp, pre);
-            issue<G>(c0, j, dummy, ba);
-            compute<G>(d, cur, w, acc, j, lane, L, c_lo, c_hi);
+            issue<G>(c0, j, dummy, lo, ba);
+            compute<G>(d, cur, w, acc, j, lane, L, c_lo, c_hi, lo);
         }
     }
 }
@@ -769,7 +795,7 @@ __global__ __launch_bounds__(256) void part_fold_kernel(BatchDesc d, const uint3
             const uint64_t plen = len - lo < P ? len - lo : P;
             reg = gmul(reg, plen == P ? XP : xpow8(pow2, plen)) ^ parts[p];
         }
-        if (!d.status) {
+        if (!d.commit) {
             d.out[r.rec] = reg ^ d.xor_io;
             continue;
         }
@@ -779,15 +805,18 @@ __global__ __launch_bounds__(256) void part_fold_kernel(BatchDesc d, const uint3
         uint64_t tw[3];
         int nt = 0;
         uint32_t stored = 0;
+        uintptr_t crc_at = 0;
         if (t == REC_COMMIT || t == REC_FINAL) {
             tw[nt++] = w0 & 0xFFFFFFFF00000000ull;
             stored = (uint32_t)w0;
+            crc_at = end + 4;
         } else if (t == REC_LONG_COMMIT || t == REC_LONG_FINAL) {
             const uint64_t w2 = load_be64(end + 16);
             tw[nt++] = w0;
             tw[nt++] = load_be64(end + 8);
             tw[nt++] = w2 & 0xFF00000000000000ull;
             stored = (uint32_t)w2;
+            crc_at = end + 20;
         }
         for (int i = 0; i < nt; ++i) {
             reg = gmul(reg ^ (uint32_t)tw[i], X4);
@@ -795,7 +824,10 @@ __global__ __launch_bounds__(256) void part_fold_kernel(BatchDesc d, const uint3
         }
         const uint32_t crc = reg ^ 0xffffffffu;
         d.out[r.rec] = crc;
-        d.status[r.rec] = nt == 0 ? 2u : (crc == stored ? 1u : 0u);
+        if (d.commit == 2 && nt)
+            *(uint32_t *)crc_at = __builtin_bswap32(crc);
+        if (d.status)
+            d.status[r.rec] = nt == 0 ? 2u : (d.commit == 2 || crc == stored ? 1u : 0u);
     }
 }
 

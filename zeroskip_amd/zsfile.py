@@ -91,3 +91,15 @@ def verify_commits(d_image: torch.Tensor, span_off: torch.Tensor, span_len: torc
             st.data_ptr(), torch.cuda.current_stream(d_image.device).cuda_stream),
             "zscrc_device_verify_commits")
     return crc, st
+
+
+def write_commits(d_image: torch.Tensor, span_off: torch.Tensor, span_len: torch.Tensor) -> torch.Tensor:
+    """Writer side on the GPU: compute every commit CRC and store it
+    big-endian into its commit record in `d_image` (in place)."""
+    n = span_off.numel()
+    crc = torch.empty(n, dtype=torch.int32, device=d_image.device)
+    with torch.cuda.device(d_image.device):
+        check(lib().zscrc_device_write_commits(
+            d_image.data_ptr(), span_off.data_ptr(), span_len.data_ptr(), n, crc.data_ptr(),
+            torch.cuda.current_stream(d_image.device).cuda_stream), "zscrc_device_write_commits")
+    return crc
