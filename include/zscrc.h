@@ -120,7 +120,7 @@ void zscrc_set_prefetch(int g, int depth);
 /* team size the fixed-stride path picks for n records of len bytes (1/16/64;
  * 0 if no device) */
 int zscrc_team_for(uint64_t len, uint64_t n);
-/* Diagnostic: plain streaming read of len bytes (multiple of 4096) -- the
+/* Diagnostic: plain streaming read of len bytes (multiple of 8192) -- the
  * measured HBM read ceiling on this GPU.  d_scratch4: 4 writable device bytes. */
 int zscrc_diag_stream_read(const void *d_buf, uint64_t len, void *d_scratch4, int grid_mult,
                            void *stream);
