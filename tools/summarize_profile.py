@@ -15,10 +15,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def rows(d, pat):
-    out = []
-    for f in glob.glob(os.path.join(d, "**", pat), recursive=True):
-        out += list(csv.DictReader(open(f)))
-    return out
+    """Rows of the newest matching CSV (gpurun_out accumulates older runs)."""
+    files = glob.glob(os.path.join(d, "**", pat), recursive=True)
+    return list(csv.DictReader(open(max(files, key=os.path.getmtime)))) if files else []
 
 
 def main():
@@ -26,8 +25,9 @@ def main():
     kname = sys.argv[5] if len(sys.argv) > 5 else "team_kernel"
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
-    for f in glob.glob(os.path.join(trace, "**", "*_kernel_stats.csv"), recursive=True):
-        shutil.copy(f, os.path.join(dst, "kernel_stats.csv"))
+    newest = max(glob.glob(os.path.join(trace, "**", "*_kernel_stats.csv"), recursive=True),
+                 key=os.path.getmtime)
+    shutil.copy(newest, os.path.join(dst, "kernel_stats.csv"))
     stats = [r for r in rows(trace, "*_kernel_stats.csv") if kname in r["Name"]]
     fetch_kb = [float(r["Counter_Value"]) for r in rows(fetch, "*_counter_collection.csv")
                 if kname in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE"]
