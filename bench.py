@@ -1,14 +1,26 @@
 #!/usr/bin/env python3
 """CRC-32C throughput on device-resident batched records (BASELINE.json metric).
 
-Workload (BASELINE.json configs[2], the north-star roofline run): per GPU,
-65,536 chunks x 64 KiB = 4 GiB of random bytes resident in HBM; one step = one
-batched CRC-32C pass over all chunks (libzscrc team kernel, 64-lane teams).
-With N > 1 GPUs (one process per GPU, torchrun) every rank owns its own 4 GiB
-shard (weak scaling, no data crosses xGMI) and the per-chunk digests are
-all-gathered over RCCL inside the timed step.
+Default workload (BASELINE.json configs[2], the north-star roofline run): per
+GPU, 65,536 chunks x 64 KiB = 4 GiB of random bytes resident in HBM; one step =
+one batched CRC-32C pass over all chunks (libzscrc team kernel).  With N > 1
+GPUs (one process per GPU, torchrun) every rank owns its own 4 GiB shard (weak
+scaling, no data crosses xGMI) and the per-chunk digests are all-gathered over
+RCCL inside the timed step.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload config3]
+
+Other BASELINE configs (parity/measurement runs, same JSON shape):
+  config2  1,048,576 x 64 B records (64 MiB): `value` is the cold rate (32
+           rotating 64 MiB batches = 2 GiB, beyond the 256 MB L3); warm rate
+           (one batch, L3-resident) alongside.
+  config4  zsbench replay: 10 M pairs as byte-exact zeroskip log files
+           (1,526 files, 10 M commits of 312 B spans); one step = GPU verify of
+           every commit; GPU write, NOTBATCHED and end-to-end rates alongside.
+  config5  `consistent` full-DB re-checksum of an ~8 GiB DB (2 packed files of
+           3 GiB with long commits, 1,024 finalised files, active file,
+           .zsdb); strong scaling: the DB is split across ranks, digests
+           all-gathered, split regions folded.
 
 Rank 0 prints ONE JSON line.  `value` = bytes checksummed by all ranks / max
 over ranks of the timed wall time, in GiB/s.
@@ -29,7 +41,8 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from zeroskip_amd import device as zd  # noqa: E402
+from zeroskip_amd import device as zd  # noqa: E402,F401
+from zeroskip_amd import zsfile  # noqa: E402
 from zeroskip_amd._lib import check, lib  # noqa: E402
 
 METRIC = "CRC32C GiB/s device-resident batched records, 1/2/4/8 MI355X; % HBM roofline"
@@ -49,6 +62,17 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
+def _repeat(fn, budget: float) -> tuple[int, float]:
+    from oracle import oracle
+    done, t0 = 0, oracle.now()
+    while True:
+        fn()
+        done += 1
+        el = oracle.now() - t0
+        if el >= budget:
+            return done, el
+
+
 def cpu_baseline(seconds: float = 12.0) -> dict:
     """The CPU oracle (SSE4.2 restatement of src/crc32c.c:370-453) on a bounded
     sample of the same workload: 2,048 x 64 KiB chunks (128 MiB), one core."""
@@ -57,13 +81,8 @@ def cpu_baseline(seconds: float = 12.0) -> dict:
     data = np.random.default_rng(1).integers(0, 256, sample_n * CHUNK, dtype=np.uint8)
     res = {}
     for impl, budget in (("hw", seconds * 0.6), ("sw", seconds * 0.4)):
-        done, t0 = 0, oracle.now()
-        while True:
-            oracle.batch(data, n=sample_n, stride=CHUNK, fixed_len=CHUNK, impl=impl, threads=1)
-            done += 1
-            el = oracle.now() - t0
-            if el >= budget:
-                break
+        done, el = _repeat(lambda: oracle.batch(data, n=sample_n, stride=CHUNK, fixed_len=CHUNK,
+                                                impl=impl, threads=1), budget)
         res[impl] = done * sample_n * CHUNK / el / GIB
     return {
         "value": round(res["hw"], 3), "unit": "GiB/s", "cores": 1, "kind": "port",
@@ -75,12 +94,374 @@ def cpu_baseline(seconds: float = 12.0) -> dict:
     }
 
 
+def cpu_baseline_spans(host: np.ndarray, offs: np.ndarray, lens: np.ndarray, what: str,
+                       seconds: float = 10.0) -> dict:
+    """The CPU oracle's crc32c_hw class over a sample of the workload's spans
+    (commit trailers excluded: they are 8 bytes per span), one core."""
+    from oracle import oracle
+    nbytes = int(lens.sum())
+    o, ln = offs.astype(np.uint64), lens.astype(np.uint64)
+    done, el = _repeat(lambda: oracle.batch(host, o, ln, impl="hw", threads=1), seconds)
+    return {"value": round(done * nbytes / el / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{what}: {len(offs)} spans, {nbytes} bytes, repeated ~{seconds:.0f} s on 1 core "
+                      f"of {cpu_model()} (oracle SSE4.2 crc32c_hw class)"}
+
+
+def traffic_for(key: str):
+    tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        return json.load(open(tpath)).get(key)
+    except Exception:
+        return None
+
+
+def read_ceiling(buf: torch.Tensor, nbytes: int, stream) -> float:
+    """Same-GPU measured read ceiling: a plain coalesced streaming read
+    (libzscrc diagnostic kernel), median of 10, GB/s."""
+    nbytes -= nbytes % 8192
+    scratch = torch.zeros(4, dtype=torch.int32, device=buf.device)
+    rd = []
+    for i in range(13):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        check(lib().zscrc_diag_stream_read(buf.data_ptr(), nbytes, scratch.data_ptr(), 2,
+                                           stream.cuda_stream), "stream read")
+        b.record(stream)
+        torch.cuda.synchronize()
+        if i >= 3:
+            rd.append(a.elapsed_time(b))
+    return nbytes / (sorted(rd)[len(rd) // 2] * 1e-3) / 1e9
+
+
+class Timer:
+    """K timed steps bracketed by barrier + synchronize; max over ranks."""
+
+    def __init__(self, world: int, dev):
+        self.world, self.dev = world, dev
+
+    def run(self, step, steps: int, warmup: int) -> float:
+        for _ in range(warmup):
+            step(None)
+        torch.cuda.synchronize()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(steps)]
+        if self.world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            step(ev[i])
+        torch.cuda.synchronize()
+        if self.world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        if self.world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=self.dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = t.item()
+        self.kern_ms = [a.elapsed_time(b) for a, b in ev]
+        return elapsed
+
+
+def line(args, world, elapsed, total_bytes, config, roofline, scaling="weak", data=None, **extra):
+    d = {
+        "metric": METRIC,
+        "value": round(total_bytes / elapsed / GIB, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": scaling,
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": data or "synthetic (torch.randint bytes, device-resident)",
+        "config": config,
+        "roofline": roofline,
+    }
+    d.update(extra)
+    return d
+
+
+def roof(nbytes: int, kern_ms: float, kernel: str, traffic, read_peak: float | None):
+    achieved = nbytes / (kern_ms * 1e-3) / 1e9
+    r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kernel,
+         "kernel_ms": round(kern_ms, 4), "algorithmic_bytes": nbytes}
+    if read_peak:
+        r["measured_read_peak"] = round(read_peak, 1)
+        r["frac_of_measured_read_peak"] = round(achieved / read_peak, 4)
+    return r
+
+
+# ------------------------------------------------------------------ config 3
+def run_config3(args, world, rank, dev, stream):
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x9E3779B9 + rank)
+    data = torch.randint(0, 256, (NCHUNK * CHUNK,), dtype=torch.uint8, device=dev, generator=g)
+    out = torch.empty(NCHUNK, dtype=torch.int32, device=dev)
+    gathered = torch.empty(NCHUNK * world, dtype=torch.int32, device=dev) if world > 1 else None
+
+    def step(ev):
+        if ev:
+            ev[0].record(stream)
+        check(lib().zscrc_device_fixed(data.data_ptr(), CHUNK, CHUNK, 0, out.data_ptr(), NCHUNK,
+                                       0, stream.cuda_stream), "zscrc_device_fixed")
+        if ev:
+            ev[1].record(stream)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, out)
+
+    tm = Timer(world, dev)
+    elapsed = tm.run(step, args.steps, args.warmup)
+    kern_ms = float(np.mean(tm.kern_ms))
+    read_peak = read_ceiling(data, NCHUNK * CHUNK, stream)
+    r = roof(NCHUNK * CHUNK + NCHUNK * 4, kern_ms, f"zs::team_kernel<{lib().zscrc_team_for(CHUNK, NCHUNK)}>",
+             traffic_for("config3_bytes_per_launch"), read_peak)
+    out_line = line(args, world, elapsed, NCHUNK * CHUNK * world * args.steps,
+                    {"workload": "config3: 65536 x 64 KiB chunks per GPU (4 GiB), batched CRC-32C",
+                     "records_per_gpu": NCHUNK, "record_bytes": CHUNK,
+                     "parallelism": f"shard{world}" + ("+rccl_allgather_digests" if world > 1 else "")}, r)
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out_line["cpu_baseline"] = cpu_baseline()
+    return out_line
+
+
+# ------------------------------------------------------------------ config 2
+def run_config2(args, world, rank, dev, stream):
+    n, rl, rot = 1 << 20, 64, 32
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x64 + rank)
+    bufs = torch.randint(0, 256, (rot, n * rl), dtype=torch.uint8, device=dev, generator=g)
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    it = [0]
+
+    def launch(b):
+        check(lib().zscrc_device_fixed(b.data_ptr(), rl, rl, 0, out.data_ptr(), n, 0, stream.cuda_stream),
+              "zscrc_device_fixed")
+
+    def step_cold(ev):
+        b = bufs[it[0] % rot]
+        it[0] += 1
+        if ev:
+            ev[0].record(stream)
+        launch(b)
+        if ev:
+            ev[1].record(stream)
+
+    def step_warm(ev):
+        if ev:
+            ev[0].record(stream)
+        launch(bufs[0])
+        if ev:
+            ev[1].record(stream)
+
+    tm = Timer(world, dev)
+    steps = max(args.steps, 100)
+    a2 = argparse.Namespace(**{**vars(args), "steps": steps})
+    warm_el = tm.run(step_warm, steps, args.warmup)
+    warm_ms = float(np.median(tm.kern_ms))
+    elapsed = tm.run(step_cold, steps, args.warmup)
+    cold_ms = float(np.median(tm.kern_ms))
+    nbytes = n * rl + n * 4
+    r = roof(nbytes, cold_ms, f"zs::team_kernel<{lib().zscrc_team_for(rl, n)}>",
+             traffic_for("config2_bytes_per_launch"), None)
+    out_line = line(a2, world, elapsed, n * rl * world * steps,
+                    {"workload": "config2: 1,048,576 x 64 B records per GPU (64 MiB), cold: 32 rotating "
+                                 "batches (2 GiB)", "records_per_gpu": n, "record_bytes": rl,
+                     "parallelism": f"shard{world}"}, r,
+                    warm={"value": round(n * rl * world * steps / warm_el / GIB, 2), "kernel_ms": round(warm_ms, 4),
+                          "achieved_GBs": round(nbytes / (warm_ms * 1e-3) / 1e9, 1),
+                          "note": "one batch re-read every step: L3 (Infinity Cache) resident"})
+    if rank == 0 and world == 1 and not args.no_cpu:
+        h = bufs[0, :n * rl // 8].cpu().numpy()
+        from oracle import oracle
+        m = len(h) // rl
+        done, el = _repeat(lambda: oracle.batch(h, n=m, stride=rl, fixed_len=rl, impl="hw", threads=1), 10.0)
+        out_line["cpu_baseline"] = {"value": round(done * m * rl / el / GIB, 3), "unit": "GiB/s", "cores": 1,
+                                    "kind": "port",
+                                    "sample": f"{m} x 64 B records repeated ~10 s on 1 core of {cpu_model()}"}
+    return out_line
+
+
+# ------------------------------------------------------------------ config 4
+def run_config4(args, world, rank, dev, stream):
+    from tools import zsdb_gen as zg
+    pairs_total = args.pairs
+    ppf = zg.pairs_per_file(True)
+    nfiles = -(-pairs_total // ppf)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(0x5EED + rank)
+    uuid = bytes(range(16))
+    t0 = time.perf_counter()
+    img = zg.log_files(uuid, 0, nfiles, ppf, 0, True, gen, dev)
+    torch.cuda.synchronize()
+    t_gen = time.perf_counter() - t0
+    offs, lens = zg.log_spans(nfiles, ppf, True, True, dev)
+    flat = img.view(-1)
+    ncommit = offs.numel()
+    span_bytes = int(lens.sum().item())
+    res = {}
+
+    def step(ev):
+        if ev:
+            ev[0].record(stream)
+        res["crc"], res["st"] = zsfile.verify_commits(flat, offs, lens)
+        if ev:
+            ev[1].record(stream)
+
+    tm = Timer(world, dev)
+    elapsed = tm.run(step, args.steps, args.warmup)
+    kern_ms = float(np.mean(tm.kern_ms))
+    st = res["st"]
+    n_ok = int((st == 1).sum().item())
+    n_stale = int(((st == 0) & (lens == 0)).sum().item())
+    assert n_ok + n_stale == ncommit and n_stale == nfiles, (n_ok, n_stale, ncommit)
+
+    # writer side: recompute + store every commit CRC (the image is unchanged;
+    # the stale finalise commits are not rewritten)
+    offs_w, lens_w = offs[lens > 0].contiguous(), lens[lens > 0].contiguous()
+    ws = []
+    for i in range(6):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        zsfile.write_commits(flat, offs_w, lens_w)
+        b.record(stream)
+        torch.cuda.synchronize()
+        if i:
+            ws.append(a.elapsed_time(b))
+    write_ms = float(np.median(ws))
+
+    # NOTBATCHED (zsbench writeseq): one commit per ~2 MiB file
+    ppf_nb = zg.pairs_per_file(False)
+    nf_nb = -(-pairs_total // ppf_nb)
+    img_nb = zg.log_files(uuid, 0, nf_nb, ppf_nb, 0, False, gen, dev, batched=False)
+    o_nb, l_nb = zg.log_spans(nf_nb, ppf_nb, False, False, dev)
+    nb = []
+    for i in range(6):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        _, st_nb = zsfile.verify_commits(img_nb.view(-1), o_nb, l_nb)
+        b.record(stream)
+        torch.cuda.synchronize()
+        if i:
+            nb.append(a.elapsed_time(b))
+    assert bool((st_nb == 1).all())
+    nb_ms = float(np.median(nb))
+    nb_bytes = int(l_nb.sum().item()) + 8 * nf_nb
+    del img_nb
+
+    # end to end: host image -> H2D (pinned / pageable) -> host walk (threads) -> verify
+    e2e = {}
+    if rank == 0 and not args.no_e2e:
+        host = img.cpu()
+        pinned = torch.empty(host.shape, dtype=torch.uint8, pin_memory=True)
+        pinned.copy_(host)
+        for kind, src in (("pageable", host), ("pinned", pinned)):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            img.copy_(src, non_blocking=True)
+            torch.cuda.synchronize()
+            e2e[f"h2d_{kind}_GBs"] = round(img.numel() / (time.perf_counter() - t0) / 1e9, 2)
+        hn = pinned.numpy()
+        from concurrent.futures import ThreadPoolExecutor
+        for threads in (1, 16):
+            t0 = time.perf_counter()
+            with ThreadPoolExecutor(threads) as ex:
+                walked = sum(len(w[0]) for w in ex.map(zsfile.walk, list(hn)))
+            e2e[f"host_walk_{threads}t_s"] = round(time.perf_counter() - t0, 4)
+        assert walked == ncommit
+        total_s = img.numel() / (e2e["h2d_pinned_GBs"] * 1e9) + e2e["host_walk_16t_s"] + kern_ms * 1e-3
+        e2e["e2e_verify_pinned_walk16_GBs"] = round(img.numel() / total_s / 1e9, 2)
+        e2e["note"] = "the walk and the H2D copy can overlap per file; summed here"
+
+    nbytes = span_bytes + 8 * ncommit + 16 * ncommit + 8 * ncommit   # spans + trailers + descriptors + crc/status
+    r = roof(nbytes, kern_ms, "verify_commits: classify + zs::team_kernel<1> (312 B spans)",
+             traffic_for("config4_bytes_per_launch"), None)
+    out_line = line(args, world, elapsed, span_bytes * world * args.steps,
+                    {"workload": f"config4: zsbench writeseqtxn replay, {pairs_total} pairs per GPU, "
+                                 f"{nfiles} log files, {ncommit} commits (312 B spans + stale finalise "
+                                 "commits), GPU verify of every commit", "pairs": pairs_total,
+                     "files": nfiles, "commits": ncommit, "parallelism": f"replica{world}"},
+                    r, data="synthetic zsbench records (key %016d, 255 charset chars + NUL, fixed seed), "
+                            "byte-exact zeroskip log images in HBM",
+                    write={"ms": round(write_ms, 4), "GBs": round((span_bytes + 8 * ncommit) / (write_ms * 1e-3) / 1e9, 1)},
+                    notbatched={"files": nf_nb, "commits": nf_nb, "verify_ms": round(nb_ms, 4),
+                                "GBs": round(nb_bytes / (nb_ms * 1e-3) / 1e9, 1)},
+                    e2e=e2e, gen_s=round(t_gen, 2))
+    if rank == 0 and world == 1 and not args.no_cpu:
+        k = 200_000
+        h = img[:-(-k // ppf)].cpu().numpy().reshape(-1)
+        o, l_ = offs[:k].cpu().numpy(), lens[:k].cpu().numpy()
+        out_line["cpu_baseline"] = cpu_baseline_spans(h, o, l_, "first 200,000 commit spans of the replay")
+    return out_line
+
+
+# ------------------------------------------------------------------ config 5
+def run_config5(args, world, rank, dev, stream):
+    from tools import zsdb_gen as zg
+    from zeroskip_amd import consistent as cs
+    t0 = time.perf_counter()
+    db = zg.make_db(device=dev, packed=2, packed_region_bytes=args.packed_mib << 20,
+                    finalised=args.finalised)
+    torch.cuda.synchronize()
+    t_gen = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    job = cs.Consistent(cs.open_db(db), rank, world)
+    t_open = time.perf_counter() - t0
+    job.prepare()
+
+    def step(ev):
+        rep = job.run(events=ev)
+        step.rep = rep
+
+    tm = Timer(world, dev)
+    elapsed = tm.run(step, args.steps, args.warmup)
+    rep = step.rep
+    assert rep.ok and len(rep.stale_empty_commits) == args.finalised, rep.as_dict()
+    kern_ms = float(np.mean(tm.kern_ms))
+    ncommit = len(job.c_off)
+    local_bytes = job.local.bytes_checked
+    nbytes = local_bytes + 24 * ncommit + 16 * len(job.pieces)
+    r = roof(nbytes, kern_ms, "verify_commits (classify + team<1> spans + team<64> split long "
+                              "regions + part_fold) + raw pieces, this rank",
+             traffic_for("config5_bytes_per_launch"), None)
+    out_line = line(args, world, elapsed, job.plan.weight * args.steps,
+                    {"workload": f"config5: consistent over a {job.plan.weight / GIB:.2f} GiB DB "
+                                 f"(2 packed x {args.packed_mib} MiB, {args.finalised} finalised, 1 active, "
+                                 f".zsdb), {rep.commits} commits", "db_bytes": job.plan.weight,
+                     "files": rep.files, "commits": rep.commits,
+                     "parallelism": f"split{world}" + ("+allgather_digests" if world > 1 else "")},
+                    r, scaling="strong",
+                    data="synthetic zeroskip DB generated on the GPU (tools/zsdb_gen.py), device-resident",
+                    prepare={k: round(v, 4) if isinstance(v, float) else v for k, v in job.prepare_times.items()},
+                    run_timing={k: round(v, 5) for k, v in rep.timing.items()},
+                    gen_s=round(t_gen, 2), open_s=round(t_open, 2))
+    if rank == 0 and world == 1 and not args.no_cpu:
+        # one finalised file's spans + a 256 MiB slice of a packed records region
+        fin = [f for f in job.db.files if f.kind == zsfile.FINALISED][:16]
+        so = [zsfile.walk(f.image)[:2] for f in fin]
+        host = np.concatenate([f.image for f in fin] + [job.db.files[0].image[40:40 + (256 << 20)]])
+        bases = np.cumsum([0] + [f.size for f in fin])
+        offs = np.concatenate([s[0].astype(np.int64) + b for s, b in zip(so, bases)] + [np.array([bases[-1]])])
+        lens = np.concatenate([s[1].astype(np.int64) for s in so] + [np.array([256 << 20])])
+        out_line["cpu_baseline"] = cpu_baseline_spans(host, offs, lens,
+                                                      "16 finalised files' commits + 256 MiB of a packed region")
+    return out_line
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="config3", choices=["config2", "config3", "config4", "config5"])
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-e2e", action="store_true", help="config4: skip the end-to-end leg")
+    ap.add_argument("--pairs", type=int, default=10_000_000, help="config4 pairs per GPU")
+    ap.add_argument("--packed-mib", type=int, default=3072, help="config5 packed records region size")
+    ap.add_argument("--finalised", type=int, default=1024, help="config5 finalised files")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -92,106 +473,14 @@ def main() -> None:
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
-
     if lib().zscrc_device_count() < 1:
         raise SystemExit("libzscrc: no gfx950 device")
-
-    # --- device-resident synthetic input: 4 GiB per rank ----------------------
-    g = torch.Generator(device=dev)
-    g.manual_seed(0x9E3779B9 + rank)
-    data = torch.randint(0, 256, (NCHUNK * CHUNK,), dtype=torch.uint8, device=dev, generator=g)
-    out = torch.empty(NCHUNK, dtype=torch.int32, device=dev)
-    gathered = torch.empty(NCHUNK * world, dtype=torch.int32, device=dev) if world > 1 else None
     stream = torch.cuda.current_stream(dev)
-
-    def step():
-        check(lib().zscrc_device_fixed(data.data_ptr(), CHUNK, CHUNK, 0, out.data_ptr(), NCHUNK,
-                                       0, stream.cuda_stream), "zscrc_device_fixed")
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, out)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-
-    # --- timed region -----------------------------------------------------------
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        check(lib().zscrc_device_fixed(data.data_ptr(), CHUNK, CHUNK, 0, out.data_ptr(), NCHUNK,
-                                       0, stream.cuda_stream), "zscrc_device_fixed")
-        ev[i][1].record(stream)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, out)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
-
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-
-    # same-GPU measured read ceiling: a plain coalesced streaming read of the
-    # same 4 GiB buffer (libzscrc diagnostic kernel), median of 10
-    scratch = torch.zeros(4, dtype=torch.int32, device=dev)
-    rd = []
-    for i in range(13):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        check(lib().zscrc_diag_stream_read(data.data_ptr(), NCHUNK * CHUNK, scratch.data_ptr(), 2,
-                                           stream.cuda_stream), "stream read")
-        b.record(stream)
-        torch.cuda.synchronize()
-        if i >= 3:
-            rd.append(a.elapsed_time(b))
-    read_peak = NCHUNK * CHUNK / (sorted(rd)[len(rd) // 2] * 1e-3) / 1e9
-    bytes_per_launch = NCHUNK * CHUNK + NCHUNK * 4       # algorithmic: input + u32 digests
-    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9  # GB/s
-    total_bytes = NCHUNK * CHUNK * world * args.steps
-    value = total_bytes / elapsed / GIB
-
+    run = {"config2": run_config2, "config3": run_config3, "config4": run_config4,
+           "config5": run_config5}[args.workload]
+    out = run(args, world, rank, dev, stream)
     if rank == 0:
-        traffic = None
-        tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(tpath):
-            try:
-                traffic = json.load(open(tpath)).get("config3_bytes_per_launch")
-            except Exception:
-                traffic = None
-        line = {
-            "metric": METRIC,
-            "value": round(value, 2),
-            "unit": "GiB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic (torch.randint bytes, device-resident)",
-            "config": {"workload": "config3: 65536 x 64 KiB chunks per GPU (4 GiB), batched CRC-32C",
-                       "records_per_gpu": NCHUNK, "record_bytes": CHUNK,
-                       "parallelism": f"shard{world}" + ("+rccl_allgather_digests" if world > 1 else "")},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "kernel": f"zs::team_kernel<{lib().zscrc_team_for(CHUNK, NCHUNK)}>",
-                         "kernel_ms": round(kern_ms, 4),
-                         "measured_read_peak": round(read_peak, 1),
-                         "frac_of_measured_read_peak": round(achieved / read_peak, 4)},
-        }
-        if world == 1 and not args.no_cpu:
-            line["cpu_baseline"] = cpu_baseline()
-        print(json.dumps(line), flush=True)
+        print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -131,6 +131,7 @@ class FileWriter:
     def __init__(self, uuid: bytes, idx: int = 0):
         self.buf = bytearray(header_bytes(uuid, idx, idx))
         self.begin = None  # crc32_begin offset, None = not computing
+        self.mf_crc32 = 0  # struct mfile.crc32: xcalloc'd (mfile.c:50), then the last span CRC
 
     def add(self, key: bytes, val: bytes):
         if self.begin is None:       # zeroskip.c:930-931
@@ -144,8 +145,22 @@ class FileWriter:
     def commit(self, final: bool = False):
         begin = len(self.buf) if self.begin is None else self.begin
         span = bytes(self.buf[begin:])
-        self.buf += commit_record(oracle.crc32c_hw(0, span), len(span), final)
+        self.mf_crc32 = oracle.crc32c_hw(0, span)
+        self.buf += commit_record(self.mf_crc32, len(span), final)
         self.begin = None
+
+    def finalise(self):
+        """zs_active_file_finalise (zeroskip-active.c:105-144) writes a commit
+        unconditionally.  After an already-committed transaction
+        crc32_data_len is 0 and crc32_end returns the STALE register of the
+        previous span (mfile.c:534-546), so the record is a zero-length commit
+        hashed from the previous span's CRC -- which the reference verifier
+        (zeroskip-record.c:204-232, from 0) rejects unless there was no
+        previous span."""
+        if self.begin is not None:
+            return self.commit()
+        w = REC_COMMIT << 56
+        self.buf += be64(w | oracle.crc32c_hw(self.mf_crc32, le64(w)))
 
     def image(self) -> bytes:
         return bytes(self.buf)

@@ -1,0 +1,239 @@
+"""zsdb_consistent host logic on the CPU: file names, the work split, the
+per-rank passes, the digest exchange + fold (gloo, 2-3 ranks) and the
+verdicts.  The device passes are replaced by an oracle backend (test only);
+the GPU path is tests/test_gpu_consistent.py."""
+from __future__ import annotations
+
+import os
+import struct
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import oracle
+from oracle import zs_format as zf
+from zeroskip_amd import consistent as cs
+from zeroskip_amd import zsfile
+
+UUID = bytes(range(16))
+UUIDSTR = "00010203-0405-0607-0809-0a0b0c0d0e0f"
+M32 = 0xFFFFFFFF
+
+
+class OracleBackend:
+    """Stand-in for the device passes, computed with the CPU oracle."""
+
+    def empty(self, n):
+        return torch.zeros(max(n, 1), dtype=torch.uint8)
+
+    def verify(self, buf, off, ln):
+        img = buf.numpy()
+        crc, st = [], []
+        for o, n in zip(off.tolist(), ln.tolist()):
+            try:
+                _, _, _, stored, computed = zf._commit_check(img, o + n)
+                crc.append(computed)
+                st.append(1 if stored == computed else 0)
+            except ValueError:
+                crc.append(0)
+                st.append(2)
+        as_i32 = lambda v: torch.tensor(np.array(v, np.uint32).view(np.int32))  # noqa: E731
+        return as_i32(crc), as_i32(st)
+
+    def raw(self, buf, off, ln):
+        img = buf.numpy()
+        r = [oracle.crc32c_hw(M32, img[o:o + n]) ^ M32 for o, n in zip(off.tolist(), ln.tolist())]
+        return torch.tensor(np.array(r, np.uint32).view(np.int32))
+
+    def crc(self, buf, off, ln):
+        img = buf.numpy()
+        r = [oracle.crc32c_hw(0, img[o:o + n]) for o, n in zip(off.tolist(), ln.tolist())]
+        return torch.tensor(np.array(r, np.uint32).view(np.int32))
+
+    def sync(self):
+        pass
+
+
+def name(*ix):
+    return "zeroskip-" + UUIDSTR + "".join(f"-{i}" for i in ix)
+
+
+def small_db(long_region: bool = False, seed: int = 7) -> dict:
+    """packed(0-3) [+ long packed(4-5)], finalised 6..8 (with the finalise
+    quirk), active 9, .zsdb -- every CRC from the oracle writer."""
+    rng = np.random.default_rng(seed)
+    db = {}
+    recs = [(b"k%05d" % i, rng.integers(0, 256, int(rng.integers(0, 300)), dtype=np.uint8).tobytes())
+            for i in range(400)]
+    db[name(0, 3)] = zf.packed_file(recs, UUID, 0, 3)
+    idx = 4
+    if long_region:
+        big = [(b"b%05d" % i, rng.integers(0, 256, 70000, dtype=np.uint8).tobytes()) for i in range(250)]
+        db[name(4, 5)] = zf.packed_file(big, UUID, 4, 5)
+        idx = 6
+    for f in range(3):
+        w = zf.FileWriter(UUID, idx)
+        for t in range(40):
+            for j in range(int(rng.integers(1, 4))):
+                w.add(b"f%d-%d-%d" % (f, t, j), rng.integers(0, 256, int(rng.integers(0, 500)), dtype=np.uint8).tobytes())
+            if t % 7 == 3:
+                w.remove(b"f%d-%d-0" % (f, t))
+            w.commit()
+        w.finalise()
+        db[name(idx, idx)] = w.image()
+        idx += 1
+    w = zf.FileWriter(UUID, idx)
+    for t in range(10):
+        w.add(b"a%d" % t, b"v" * t)
+        w.commit()
+    db[name(idx)] = w.image()
+    db[".zsdb"] = zf.dotzsdb_bytes(len(db[name(idx)]), UUIDSTR.encode() + b"\0", idx)
+    return db
+
+
+def run_local(db, world=1, rank=0):
+    return cs.Consistent(cs.open_db(db), rank, world, OracleBackend()).prepare().run()
+
+
+def test_parse_name():
+    assert cs.parse_name(name(5)) == (zsfile.ACTIVE, UUIDSTR, 5, 5)
+    assert cs.parse_name(name(5, 5)) == (zsfile.FINALISED, UUIDSTR, 5, 5)
+    assert cs.parse_name(name(0, 7)) == (zsfile.PACKED, UUIDSTR, 0, 7)
+    assert cs.parse_name(".zsdb") is None
+    assert cs.parse_name("zeroskip-short-1") is None
+
+
+def test_finalise_quirk_matches_reference_semantics():
+    """The finalise commit after a committed txn is zero-length and hashed from
+    the previous span's CRC: the reference verifier (from 0) rejects it."""
+    w = zf.FileWriter(UUID, 1)
+    w.add(b"k", b"v")
+    w.commit()
+    w.finalise()
+    img = w.image()
+    commits, end, why = zf.walk(img)
+    assert why == "end" and end == len(img)
+    assert commits[-1]["span_len"] == 0 and not commits[-1]["ok"]
+    first = commits[0]
+    span_crc = oracle.crc32c_hw(0, img[first["span_off"]:first["span_off"] + first["span_len"]])
+    assert commits[-1]["stored"] == oracle.crc32c_hw(span_crc, zf.le64(zf.REC_COMMIT << 56))
+    # no earlier span: the register is the xcalloc'd 0 and the verifier accepts it
+    w2 = zf.FileWriter(UUID, 2)
+    w2.finalise()
+    assert zf.walk(w2.image())[0][-1]["ok"]
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 5, 8])
+def test_plan_covers_every_byte_once(world):
+    db = cs.open_db(small_db(long_region=True))
+    plan = cs.make_plan(db, world)
+    by_file = {}
+    for u in plan.units:
+        assert 0 <= u.rank < world
+        by_file.setdefault(u.fid, []).append(u)
+    for fid, f in enumerate(db.files):
+        us = sorted(by_file[fid], key=lambda u: u.lo)
+        assert us[0].lo in (0, plan.packed.get(fid, {}).get("roff", 0))
+        for a, b in zip(us, us[1:]):
+            assert a.hi == b.lo
+        assert us[-1].hi == f.size
+    loads = [sum(u.hi - u.lo for u in plan.units if u.rank == r) for r in range(world)]
+    assert sum(loads) == plan.weight
+
+
+def test_consistent_clean_db():
+    rep = run_local(small_db())
+    assert rep.ok, rep.as_dict()
+    assert rep.dotzsdb["ok"] and not rep.issues
+    assert len(rep.stale_empty_commits) == 3 and not rep.bad_commits
+    assert rep.files == 5
+
+
+@pytest.mark.parametrize("what", ["finalised", "packed_records", "packed_ptrs", "header", "dotzsdb"])
+def test_consistent_detects(what):
+    db = small_db()
+    fin = name(5, 5)
+    if what == "finalised":
+        img = bytearray(db[fin])
+        commits, _, _ = zf.walk(img)
+        c = commits[10]
+        img[c["span_off"] + 30] ^= 0x40
+        db[fin] = bytes(img)
+        rep = run_local(db)
+        assert rep.bad_commits == [(fin, c["commit_off"])]
+    elif what in ("packed_records", "packed_ptrs"):
+        img = bytearray(db[name(0, 3)])
+        chk = {c["kind"]: c for c in zf.packed_check(img)}
+        c = chk["records" if what == "packed_records" else "pointers"]
+        img[c["span_off"] + c["span_len"] // 2] ^= 1
+        db[name(0, 3)] = bytes(img)
+        rep = run_local(db)
+        assert rep.bad_commits == [(name(0, 3), c["commit_off"])]
+    elif what == "header":
+        img = bytearray(db[fin])
+        img[20] ^= 1
+        db[fin] = bytes(img)
+        rep = run_local(db)
+        assert [h[0] for h in rep.header_errors] == [fin]
+    else:
+        d = bytearray(db[".zsdb"])
+        d[20] ^= 1
+        db[".zsdb"] = bytes(d)
+        rep = run_local(db)
+        assert rep.dotzsdb["present"] and not rep.dotzsdb["ok"]
+    assert not rep.ok
+
+
+def test_directory_source(tmp_path):
+    for n, v in small_db().items():
+        (tmp_path / n).write_bytes(v)
+    (tmp_path / "unrelated.txt").write_bytes(b"x")
+    rep = run_local(str(tmp_path))
+    assert rep.ok and rep.files == 5
+
+
+def _worker(rank, world, port, db, corrupt, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rep = run_local(db, world, rank)
+        q.put((rank, rep.ok, rep.commits, rep.bad_commits, len(rep.stale_empty_commits), rep.files,
+               rep.bytes_checked))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,corrupt", [(2, False), (3, True)])
+def test_multi_rank_matches_single(world, corrupt):
+    db = small_db(long_region=True)
+    if corrupt:
+        img = bytearray(db[name(4, 5)])
+        chk = {c["kind"]: c for c in zf.packed_check(img)}
+        c = chk["records"]
+        assert c["span_len"] > zf.MAX_SHORT_VAL_LEN        # a long commit, split across ranks
+        img[c["span_off"] + c["span_len"] - 100] ^= 2
+        db[name(4, 5)] = bytes(img)
+    plan = cs.make_plan(cs.open_db(db), world)
+    assert any(u.what == "piece" for u in plan.units)
+    single = run_local(db)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + (os.getpid() % 1000) + world
+    procs = [ctx.Process(target=_worker, args=(r, world, port, db, corrupt, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for _, ok, commits, bad, nstale, files, nbytes in res:
+        assert ok == single.ok == (not corrupt)
+        assert commits == single.commits
+        assert bad == single.bad_commits
+        assert nstale == len(single.stale_empty_commits)
+        assert files == single.files and nbytes == single.bytes_checked
+    if corrupt:
+        assert single.bad_commits == [(name(4, 5), c["commit_off"])]

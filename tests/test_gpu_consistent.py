@@ -1,0 +1,156 @@
+"""zsdb_consistent on the GPU (zeroskip_amd/consistent.py) against the oracle:
+oracle-written DBs, corruptions, the GPU-side DB generator re-checked by the
+oracle walker, a directory on disk, and two ranks exchanging digests."""
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import zs_format as zf
+from tests.test_consistent_host import OracleBackend, name, small_db
+from zeroskip_amd import consistent as cs
+
+pytestmark = pytest.mark.gpu
+
+
+def gpu_report(db, world=1, rank=0):
+    return cs.Consistent(cs.open_db(db), rank, world).prepare().run()
+
+
+def same(a, b):
+    return (a.ok, a.commits, a.bad_commits, a.stale_empty_commits, a.files, a.bytes_checked,
+            sorted(map(tuple, a.header_errors)), a.issues) == \
+           (b.ok, b.commits, b.bad_commits, b.stale_empty_commits, b.files, b.bytes_checked,
+            sorted(map(tuple, b.header_errors)), b.issues)
+
+
+def test_oracle_db_clean(gpu):
+    db = small_db(long_region=True)
+    g = gpu_report(db)
+    o = cs.Consistent(cs.open_db(db), 0, 1, OracleBackend()).prepare().run()
+    assert g.ok and same(g, o), (g.as_dict(), o.as_dict())
+    assert len(g.stale_empty_commits) == 3
+
+
+@pytest.mark.parametrize("what", ["finalised", "long_records", "ptrs", "header"])
+def test_oracle_db_corruption(gpu, what):
+    db = small_db(long_region=True)
+    if what == "finalised":
+        f = name(7, 7)
+        img = bytearray(db[f])
+        c = zf.walk(img)[0][17]
+        img[c["span_off"] + c["span_len"] - 1] ^= 0x80
+        want = [(f, c["commit_off"])]
+    elif what in ("long_records", "ptrs"):
+        f = name(4, 5)
+        img = bytearray(db[f])
+        c = {c["kind"]: c for c in zf.packed_check(img)}["records" if what == "long_records" else "pointers"]
+        img[c["span_off"] + 12345 % c["span_len"]] ^= 4
+        want = [(f, c["commit_off"])]
+    else:
+        f = name(0, 3)
+        img = bytearray(db[f])
+        img[30] ^= 1
+        want = []
+    db[f] = bytes(img)
+    g = gpu_report(db)
+    o = cs.Consistent(cs.open_db(db), 0, 1, OracleBackend()).prepare().run()
+    assert not g.ok and same(g, o)
+    assert g.bad_commits == want
+    if what == "header":
+        assert [h[0] for h in g.header_errors] == [f]
+
+
+def _gen_small(gpu):
+    from tools import zsdb_gen
+    return zsdb_gen.make_db(device=gpu, packed=2, packed_region_bytes=20 << 20, packed_vlen=1000,
+                            finalised=5, active_pairs=100)
+
+
+def test_generator_checked_by_oracle(gpu):
+    """The GPU-written DB (bench config 5) is what the oracle writer would write."""
+    db = _gen_small(gpu)
+    nstale = 0
+    for n, v in db.items():
+        if n == ".zsdb":
+            assert zf.dotzsdb_bytes(int.from_bytes(v[8:16], "big"), v[16:53],
+                                    int.from_bytes(v[53:57], "big")) == v
+            continue
+        img = v.cpu().numpy().tobytes()
+        assert zf.header_check(img)[0], n
+        kind = cs.parse_name(n)[0]
+        if kind == 2:
+            assert all(c["ok"] for c in zf.packed_check(img)), n
+        else:
+            commits, end, why = zf.walk(img)
+            assert why == "end" and end == len(img), n
+            for c in commits[:-1]:
+                assert c["ok"], (n, c)
+            if kind == 1:
+                assert commits[-1]["span_len"] == 0 and not commits[-1]["ok"]
+                nstale += 1
+            else:
+                assert commits[-1]["ok"]
+    assert nstale == 5
+    rep = gpu_report(db)
+    assert rep.ok and len(rep.stale_empty_commits) == 5 and not rep.issues, rep.as_dict()
+
+
+def test_directory_and_cli(gpu, tmp_path):
+    from tools import zsdb_gen
+    db = _gen_small(gpu)
+    zsdb_gen.write_dir(db, str(tmp_path))
+    rep = cs.consistent(str(tmp_path))
+    assert rep.ok and rep.files == len(db) - 1
+    f = sorted(p for p in os.listdir(tmp_path) if cs.parse_name(p) and cs.parse_name(p)[0] == 1)[2]
+    with open(tmp_path / f, "r+b") as fh:
+        fh.seek(1000)
+        b = fh.read(1)
+        fh.seek(1000)
+        fh.write(bytes([b[0] ^ 1]))
+    assert cs.main([str(tmp_path)]) == 1
+    rep = cs.consistent(str(tmp_path))
+    assert [b[0] for b in rep.bad_commits] == [f]
+
+
+def _rank_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        db = small_db(long_region=True)
+        img = bytearray(db[name(4, 5)])
+        c = {c["kind"]: c for c in zf.packed_check(img)}["records"]
+        img[c["span_off"] + 7] ^= 1
+        db[name(4, 5)] = bytes(img)
+        rep = gpu_report(db, world, rank)
+        q.put((rank, rep.ok, rep.commits, rep.bad_commits, len(rep.stale_empty_commits), c["commit_off"]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_split_long_region(gpu):
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    single = cs.Consistent(cs.open_db(small_db(long_region=True)), 0, 1, OracleBackend()).prepare().run()
+    for _, ok, commits, bad, nstale, at in res:
+        assert not ok and commits == single.commits and nstale == 3
+        assert bad == [(name(4, 5), at)]

@@ -1,0 +1,553 @@
+"""zsdb_consistent on the GPU(s): a full re-checksum of a zeroskip DB directory.
+
+The reference declares the operation and implements nothing:
+``zsdb_consistent`` returns ZS_NOTIMPLEMENTED (src/zeroskip.c:1399-1407) and
+``zeroskip consistent`` parses its options and exits 0
+(tool/cmd-consistent.c:23-49).  SURVEY.md §8f-2 defines it for this engine as
+"every CRC the format carries, recomputed":
+
+* ``.zsdb``: signature + CRC over its host-order fields
+  (src/zeroskip-dotzsdb.c:105-119, struct zeroskip-priv.h:83-91);
+* every ``zeroskip-<uuid>-<idx>[-<idx>]`` file (names interpreted like
+  interpret_db_filename, src/zeroskip.c:200-235): header signature + CRC
+  (src/zeroskip-header.c:105-170), header indices against the file name;
+* active / finalised files: the record walk of src/zeroskip-record.c:283-331
+  and every commit CRC (writer semantics, src/zeroskip-file.c:253-350);
+* packed files: the pointer-section commit the reference checks
+  (src/zeroskip-packed.c:278-339) AND the records-region commit it never
+  checks (written by zeroskip-packed.c:442 through one crc32_end).
+
+Zero-length commits whose CRC is the previous span's register hashed with the
+trailer -- what zs_active_file_finalise writes after an already-committed
+transaction (src/zeroskip-active.c:122 + src/mfile.c:534-546) -- are reported
+apart, as ``stale_empty_commits``, because the reference's own verifier
+(zeroskip-record.c:204-232) rejects them although nothing is corrupt.
+
+Work split (one process per GPU, launched by torchrun): the byte weight of the
+DB is cut into `world` equal ranges.  Active / finalised files and packed tails
+(records commit + pointer section + final commit) go whole to the rank holding
+their midpoint; a packed records region crossing a cut is split there.  Every
+rank stages its ranges into one device buffer, walks its files on the host
+(threads; the ctypes calls release the GIL), verifies all its commits in ONE
+device launch and computes RAW registers of its split pieces in another.  The
+per-rank summaries are all-gathered (kilobytes); split regions are folded with
+the zero-shift operator (``shard.fold``) and their commit trailers applied on
+the host.  Input bytes never cross xGMI.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import re
+import struct
+import sys
+import time
+from concurrent.futures import ThreadPoolExecutor
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import zsfile
+from .shard import fold
+
+PREFIX = "zeroskip-"
+DOTZSDB = ".zsdb"
+HDR = 40
+M32 = 0xFFFFFFFF
+T_COMMIT, T_2ND, T_FINAL, T_LONG_COMMIT, T_LONG_FINAL = 4, 8, 16, 36, 48
+_NAME = re.compile(r"zeroskip-(.{36})-(\d+)(?:-(\d+))?$")
+SPLIT_ALIGN = 64 << 10
+SLOT_ALIGN = 256
+
+
+# --------------------------------------------------------------------- the DB
+@dataclass
+class DbFile:
+    name: str
+    kind: int                 # zsfile.ACTIVE / FINALISED / PACKED
+    uuid: str
+    startidx: int
+    endidx: int
+    image: np.ndarray         # the file bytes (np.memmap for a directory)
+    dev: torch.Tensor | None = None   # optional device-resident copy
+
+    @property
+    def size(self) -> int:
+        return int(self.image.nbytes)
+
+
+def parse_name(name: str):
+    """(kind, uuidstr, startidx, endidx) or None, like interpret_db_filename
+    (src/zeroskip.c:200-235): one index = active, two equal = finalised,
+    two different = packed."""
+    m = _NAME.search(name)
+    if not m or not name.startswith(PREFIX):
+        return None
+    s = int(m.group(2))
+    if m.group(3) is None:
+        return zsfile.ACTIVE, m.group(1), s, s
+    e = int(m.group(3))
+    return (zsfile.FINALISED if e == s else zsfile.PACKED), m.group(1), s, e
+
+
+def _as_u8(x) -> np.ndarray:
+    if isinstance(x, torch.Tensor):
+        return x.detach().cpu().numpy().view(np.uint8).reshape(-1)
+    if isinstance(x, np.ndarray):
+        return x.view(np.uint8).reshape(-1)
+    return np.frombuffer(bytes(x), dtype=np.uint8)
+
+
+@dataclass
+class Db:
+    dotzsdb: bytes | None
+    files: list[DbFile]
+
+
+def open_db(src) -> Db:
+    """A DB from a directory (files memory-mapped, nothing read yet) or from a
+    mapping {file name: bytes | np.ndarray | torch.Tensor} (in-memory images;
+    a CUDA tensor is used in place as the device-resident copy)."""
+    files, dot = [], None
+    if isinstance(src, (str, os.PathLike)):
+        names = sorted(os.listdir(src))
+        get = {}
+        for n in names:
+            p = os.path.join(src, n)
+            if not os.path.isfile(p):
+                continue
+            if n == DOTZSDB:
+                with open(p, "rb") as fh:
+                    dot = fh.read()
+            elif parse_name(n):
+                sz = os.path.getsize(p)
+                get[n] = (np.memmap(p, dtype=np.uint8, mode="r") if sz else np.zeros(0, np.uint8), None)
+    else:
+        get = {}
+        for n, v in src.items():
+            if n == DOTZSDB:
+                dot = bytes(_as_u8(v))
+            elif parse_name(n):
+                dev = v if isinstance(v, torch.Tensor) and v.is_cuda else None
+                get[n] = (_as_u8(v), dev)
+    for n, (img, dev) in get.items():
+        kind, uuid, s, e = parse_name(n)
+        files.append(DbFile(n, kind, uuid, s, e, img, dev))
+    files.sort(key=lambda f: (f.startidx, f.endidx, f.name))
+    return Db(dot, files)
+
+
+# ------------------------------------------------------------------ the plan
+@dataclass
+class Unit:
+    fid: int
+    what: str                 # "file" | "tail" | "region" (whole records span) | "piece"
+    lo: int                   # byte range of the file this unit checksums
+    hi: int
+    rank: int = 0
+    piece: int = 0            # for "piece": its index within the region
+
+
+@dataclass
+class Plan:
+    world: int
+    units: list[Unit]
+    packed: dict              # fid -> dict(roff, rlen, poff, plen, rc)
+    weight: int
+
+
+def _packed_layout(img: np.ndarray):
+    off, ln, rc = zsfile.packed_spans(img)
+    return dict(roff=int(off[0]), rlen=int(ln[0]), poff=int(off[1]), plen=int(ln[1]), rc=int(rc))
+
+
+def make_plan(db: Db, world: int) -> Plan:
+    """Deterministic cut of the DB into `world` ranges of equal byte weight
+    (the same on every rank; only packed tails are read to build it)."""
+    seq, packed = [], {}
+    for fid, f in enumerate(db.files):
+        if f.kind == zsfile.PACKED:
+            lay = _packed_layout(f.image)
+            packed[fid] = lay
+            if lay["rc"] == 0:
+                rend = lay["roff"] + lay["rlen"]
+                seq.append((Unit(fid, "region", lay["roff"], rend), True))
+                seq.append((Unit(fid, "tail", rend, f.size), False))
+                continue
+        seq.append((Unit(fid, "file", 0, f.size), False))
+    W = sum(u.hi - u.lo for u, _ in seq)
+    bounds = [(W * r) // world for r in range(world + 1)]
+
+    def rank_of(x):
+        r = 0
+        while r + 1 < world and bounds[r + 1] <= x:
+            r += 1
+        return r
+
+    units, cur = [], 0
+    for u, splittable in seq:
+        w = u.hi - u.lo
+        if not splittable or world == 1:
+            u.rank = rank_of(cur + w // 2)
+            units.append(u)
+        else:
+            cuts = [u.lo]
+            for r in range(1, world):
+                if cur < bounds[r] < cur + w:
+                    c = u.lo + bounds[r] - cur
+                    c = u.lo + ((c - u.lo) // SPLIT_ALIGN) * SPLIT_ALIGN
+                    if cuts[-1] < c < u.hi:
+                        cuts.append(c)
+            cuts.append(u.hi)
+            if len(cuts) == 2:
+                u.rank = rank_of(cur + w // 2)
+                units.append(u)
+            else:
+                for i in range(len(cuts) - 1):
+                    a, b = cuts[i], cuts[i + 1]
+                    units.append(Unit(u.fid, "piece", a, b, rank_of(cur + (a - u.lo) + (b - a) // 2), i))
+        cur += w
+    return Plan(world, units, packed, W)
+
+
+# ---------------------------------------------------------------- device side
+class GpuBackend:
+    """The product path: libzscrc kernels on the staged device buffer."""
+
+    def __init__(self, device: torch.device):
+        self.device = device
+
+    def empty(self, n: int) -> torch.Tensor:
+        return torch.empty(max(n, 1), dtype=torch.uint8, device=self.device)
+
+    def verify(self, buf, off, ln):
+        return zsfile.verify_commits(buf, off, ln)
+
+    def raw(self, buf, off, ln):
+        from .device import crc_batch
+        return crc_batch(buf, off, ln, raw=True)
+
+    def crc(self, buf, off, ln):
+        from .device import crc_batch
+        return crc_batch(buf, off, ln)
+
+    def sync(self):
+        torch.cuda.synchronize(self.device)
+
+
+def _commit_rec(img: np.ndarray, off: int):
+    """(type, span_len, rec_len, stored, trailer words) of the commit at off."""
+    w0 = int.from_bytes(img[off:off + 8].tobytes(), "big")
+    t = w0 >> 56
+    if t in (T_COMMIT, T_FINAL):
+        return t, (w0 >> 32) & 0xFFFFFF, 8, w0 & M32, [w0 & 0xFFFFFFFF00000000]
+    if t in (T_LONG_COMMIT, T_LONG_FINAL) and off + 24 <= img.nbytes:
+        n = int.from_bytes(img[off + 8:off + 16].tobytes(), "big")
+        w2 = int.from_bytes(img[off + 16:off + 24].tobytes(), "big")
+        return t, n, 24, w2 & M32, [w0, n, w2 & 0xFF00000000000000]
+    return t, None, 0, None, None
+
+
+def _trailer_crc(span_crc: int, words) -> int:
+    from .crc32c import crc32c_hw
+    return crc32c_hw(span_crc, b"".join(struct.pack("<Q", w) for w in words))
+
+
+@dataclass
+class Report:
+    ok: bool = True
+    files: int = 0
+    commits: int = 0
+    bytes_checked: int = 0
+    dotzsdb: dict = field(default_factory=dict)
+    bad_commits: list = field(default_factory=list)         # (file, commit offset)
+    stale_empty_commits: list = field(default_factory=list)  # (file, commit offset)
+    header_errors: list = field(default_factory=list)
+    walk_errors: list = field(default_factory=list)
+    issues: list = field(default_factory=list)
+    timing: dict = field(default_factory=dict)
+
+    def as_dict(self):
+        return dict(self.__dict__)
+
+
+class Consistent:
+    """One rank's share of a consistency check.  ``prepare()`` stages the
+    rank's bytes on its device and walks its files (host); ``run()`` is the
+    device pass + exchange + fold and can be repeated (device-resident)."""
+
+    MAX_LISTED = 1000
+
+    def __init__(self, db: Db, rank: int = 0, world: int = 1, backend=None, group=None,
+                 threads: int = 8):
+        self.db, self.rank, self.world, self.group = db, rank, world, group
+        self.backend = backend or GpuBackend(torch.device("cuda", torch.cuda.current_device()))
+        self.threads = threads
+        self.plan = make_plan(db, world)
+        self.mine = [u for u in self.plan.units if u.rank == rank]
+
+    # ---------------------------------------------------------------- prepare
+    def prepare(self):
+        t0 = time.perf_counter()
+        db, be = self.db, self.backend
+        # device layout: one slot per unit; a whole span also needs its commit record
+        slots, pos = [], 0
+        for u in self.mine:
+            f = db.files[u.fid]
+            hi = u.hi
+            if u.what == "region":
+                hi = min(f.size, u.hi + 24)
+            slots.append((u, u.lo, hi, pos))
+            pos += -(-(hi - u.lo) // SLOT_ALIGN) * SLOT_ALIGN
+        self.buf = be.empty(pos)
+        pinned = None
+        if any(db.files[u.fid].dev is None for u, *_ in slots) and self.buf.is_cuda:
+            pinned = torch.empty(max(pos, 1), dtype=torch.uint8, pin_memory=True)
+        host = pinned.numpy() if pinned is not None else (self.buf.numpy() if not self.buf.is_cuda else None)
+        for u, lo, hi, p in slots:
+            f = db.files[u.fid]
+            if f.dev is not None:
+                self.buf[p:p + hi - lo].copy_(f.dev.view(torch.uint8).reshape(-1)[lo:hi], non_blocking=True)
+            else:
+                host[p:p + hi - lo] = f.image[lo:hi]
+        t_read = time.perf_counter()
+        if pinned is not None:
+            self.buf.copy_(pinned[:self.buf.numel()], non_blocking=True)
+
+        # host side: headers, walks, commit descriptors (while the copy runs)
+        self.local = Report()
+        c_off, c_len, c_file, c_rec = [], [], [], []
+        pieces = []           # (fid, piece, lo, hi, slot offset)
+        header_of = set()
+
+        def walk(item):
+            u, lo, hi, p = item
+            return zsfile.walk(db.files[u.fid].image)
+
+        file_units = [s for s in slots if s[0].what == "file" and db.files[s[0].fid].kind != zsfile.PACKED]
+        with ThreadPoolExecutor(max_workers=max(1, self.threads)) as ex:
+            walks = dict(zip([s[0].fid for s in file_units], ex.map(walk, file_units)))
+        for u, lo, hi, p in slots:
+            f = db.files[u.fid]
+            if u.what in ("file", "tail") and u.fid not in header_of:
+                header_of.add(u.fid)
+                self._check_header(f)
+            if u.what == "file" and f.kind == zsfile.PACKED:
+                self.local.walk_errors.append((f.name, self.plan.packed[u.fid]["rc"], 0))
+            elif u.what == "file":
+                so, sl, rc, end = walks[u.fid]
+                self._check_walk(f, so, sl, rc, end)
+                c_off.append(so.astype(np.int64) + (p - lo))
+                c_len.append(sl.astype(np.int64))
+                c_file.append(np.full(len(so), u.fid, np.int64))
+                c_rec.append(so.astype(np.int64) + sl.astype(np.int64))
+            elif u.what == "tail":
+                lay = self.plan.packed[u.fid]
+                c_off += [np.array([lay["poff"] - lo + p], np.int64)]
+                c_len += [np.array([lay["plen"]], np.int64)]
+                c_file += [np.array([u.fid], np.int64)]
+                c_rec += [np.array([lay["poff"] + lay["plen"]], np.int64)]
+            elif u.what == "region":
+                c_off += [np.array([p], np.int64)]
+                c_len += [np.array([u.hi - u.lo], np.int64)]
+                c_file += [np.array([u.fid], np.int64)]
+                c_rec += [np.array([u.hi], np.int64)]
+            else:
+                pieces.append((u.fid, u.piece, u.lo, u.hi, p))
+        cat = (lambda xs: np.concatenate(xs) if xs else np.zeros(0, np.int64))
+        self.c_off, self.c_len, self.c_file, self.c_rec = map(cat, (c_off, c_len, c_file, c_rec))
+        self.pieces = pieces
+        dev = self.buf.device
+        self.d_off = torch.from_numpy(self.c_off).to(dev)
+        self.d_len = torch.from_numpy(self.c_len).to(dev)
+        self.d_poff = torch.tensor([q[4] for q in pieces], dtype=torch.int64, device=dev)
+        self.d_plen = torch.tensor([q[3] - q[2] for q in pieces], dtype=torch.int64, device=dev)
+        self.local.files = len(header_of)
+        self.local.bytes_checked = int(sum(u.hi - u.lo for u in self.mine))
+        be.sync()
+        t1 = time.perf_counter()
+        self.prepare_times = dict(stage_s=t_read - t0, walk_and_copy_s=t1 - t_read, total_s=t1 - t0,
+                                  staged_bytes=pos)
+        return self
+
+    def _check_header(self, f: DbFile):
+        rc, st, cp = zsfile.header_crc(f.image)
+        if rc != 0 or st != cp:
+            self.local.header_errors.append((f.name, "signature" if rc else "crc", st, cp))
+            return
+        sidx = int.from_bytes(f.image[28:32].tobytes(), "big")
+        eidx = int.from_bytes(f.image[32:36].tobytes(), "big")
+        if (sidx, eidx) != (f.startidx, f.endidx):
+            self.local.issues.append(f"{f.name}: header indices {sidx}-{eidx} do not match the name")
+
+    def _check_walk(self, f: DbFile, so, sl, rc, end):
+        if rc != zsfile.END:
+            self.local.walk_errors.append((f.name, int(rc), int(end)))
+            return
+        last = HDR
+        if len(so):
+            e = int(so[-1] + sl[-1])
+            _, _, rl, _, _ = _commit_rec(f.image, e)
+            last = e + rl
+        if last != f.size:
+            self.local.issues.append(f"{f.name}: {f.size - last} bytes after the last commit")
+
+    # -------------------------------------------------------------------- run
+    def run(self, events=None) -> Report:
+        """events: optional (start, end) device events recorded around the
+        device pass (bench.py's kernel timing)."""
+        be = self.backend
+        t0 = time.perf_counter()
+        n = len(self.c_off)
+        loc = self.local
+        bad_idx = np.zeros(0, np.int64)
+        if events:
+            events[0].record()
+        if n:
+            crc, st = be.verify(self.buf, self.d_off, self.d_len)
+        raw = be.raw(self.buf, self.d_poff, self.d_plen) if self.pieces else None
+        if events:
+            events[1].record()
+        if n:
+            bad_idx = torch.nonzero(st != 1).reshape(-1).cpu().numpy()
+        raw_h = [v & M32 for v in raw.cpu().tolist()] if raw is not None else []
+        t_dev = time.perf_counter()
+
+        # zero-length mismatches: the finalise quirk if the CRC chains from the
+        # previous span of the same file
+        bad, stale = [], []
+        quirk = [i for i in bad_idx.tolist() if self.c_len[i] == 0 and i > 0
+                 and self.c_file[i - 1] == self.c_file[i]]
+        if quirk:
+            q = np.array(quirk)
+            prev = be.crc(self.buf, torch.from_numpy(self.c_off[q - 1]).to(self.buf.device),
+                          torch.from_numpy(self.c_len[q - 1]).to(self.buf.device))
+            prev = [v & M32 for v in prev.cpu().tolist()]
+        qset = dict(zip(quirk, prev)) if quirk else {}
+        for i in bad_idx.tolist():
+            f = self.db.files[int(self.c_file[i])]
+            at = int(self.c_rec[i])
+            if i in qset:
+                _, _, _, stored, words = _commit_rec(f.image, at)
+                if stored is not None and _trailer_crc(qset[i], words) == stored:
+                    stale.append((f.name, at))
+                    continue
+            bad.append((f.name, at))
+        summary = dict(rank=self.rank, commits=n, bad=bad[:self.MAX_LISTED], n_bad=len(bad),
+                       stale=stale[:self.MAX_LISTED], n_stale=len(stale),
+                       pieces=[(q[0], q[1], q[3] - q[2], r) for q, r in zip(self.pieces, raw_h)],
+                       files=loc.files, bytes=loc.bytes_checked, header_errors=loc.header_errors,
+                       walk_errors=loc.walk_errors, issues=loc.issues)
+        allsum = self._gather(summary)
+        t_x = time.perf_counter()
+        rep = self._merge(allsum)
+        t1 = time.perf_counter()
+        rep.timing = dict(device_s=t_dev - t0, exchange_s=t_x - t_dev, fold_s=t1 - t_x, total_s=t1 - t0)
+        return rep
+
+    def _gather(self, summary):
+        if self.world == 1:
+            return [summary]
+        import torch.distributed as dist
+        out = [None] * self.world
+        dist.all_gather_object(out, summary, group=self.group)
+        return out
+
+    def _merge(self, allsum) -> Report:
+        rep = Report()
+        rep.dotzsdb = self._check_dotzsdb()
+        pieces = {}
+        for s in allsum:
+            rep.commits += s["commits"]
+            rep.files += s["files"]
+            rep.bytes_checked += s["bytes"]
+            rep.bad_commits += [tuple(b) for b in s["bad"]]
+            rep.stale_empty_commits += [tuple(b) for b in s["stale"]]
+            rep.header_errors += [tuple(h) for h in s["header_errors"]]
+            rep.walk_errors += [tuple(w) for w in s["walk_errors"]]
+            rep.issues += s["issues"]
+            for fid, k, ln, r in s["pieces"]:
+                pieces.setdefault(fid, []).append((k, r, ln))
+            if s["n_bad"] > len(s["bad"]):
+                rep.issues.append(f"rank {s['rank']}: {s['n_bad'] - len(s['bad'])} more bad commits not listed")
+        # split records regions: fold the pieces, then the commit trailer
+        for fid, ps in sorted(pieces.items()):
+            ps.sort()
+            f, lay = self.db.files[fid], self.plan.packed[fid]
+            span = fold([(r, ln) for _, r, ln in ps])
+            rep.commits += 1
+            at = lay["roff"] + lay["rlen"]
+            _, _, _, stored, words = _commit_rec(f.image, at)
+            if stored is None or _trailer_crc(span, words) != stored:
+                rep.bad_commits.append((f.name, at))
+        rep.bad_commits.sort()
+        rep.stale_empty_commits.sort()
+        dz = rep.dotzsdb
+        if dz.get("present"):
+            uu = {f.uuid for f in self.db.files}
+            if uu - {dz["uuid"]}:
+                rep.issues.append(f"files with a uuid other than .zsdb's: {sorted(uu - {dz['uuid']})}")
+            act = [f for f in self.db.files if f.kind == zsfile.ACTIVE]
+            if len(act) > 1:
+                rep.issues.append(f"{len(act)} active files")
+            for f in act:
+                if f.startidx != dz["curidx"]:
+                    rep.issues.append(f"{f.name}: active index {f.startidx} != .zsdb curidx {dz['curidx']}")
+                elif f.size != dz["offset"]:
+                    rep.issues.append(f"{f.name}: size {f.size} != .zsdb offset {dz['offset']}")
+        rep.ok = (not rep.bad_commits and not rep.header_errors and not rep.walk_errors
+                  and dz.get("ok", False))
+        return rep
+
+    def _check_dotzsdb(self) -> dict:
+        d = self.db.dotzsdb
+        if d is None:
+            return dict(present=False, ok=False)
+        rc, st, cp = zsfile.dotzsdb_crc(d)
+        if rc != 0 and len(d) < 61:
+            return dict(present=True, ok=False, rc=rc)
+        return dict(present=True, ok=rc == 0 and st == cp, rc=rc, stored=st, computed=cp,
+                    offset=int.from_bytes(d[8:16], "big"),
+                    uuid=d[16:52].decode("latin-1"), curidx=int.from_bytes(d[53:57], "big"))
+
+
+def consistent(src, rank: int = 0, world: int = 1, group=None, backend=None) -> Report:
+    """Check a DB (directory or in-memory mapping); every rank returns the
+    same merged report."""
+    return Consistent(open_db(src), rank, world, backend, group).prepare().run()
+
+
+def main(argv=None) -> int:
+    """``python -m zeroskip_amd.consistent DBDIR`` (cmd-consistent's slot):
+    exit 0 if consistent, 1 if not.  Under torchrun every rank takes a share."""
+    ap = argparse.ArgumentParser(prog="zeroskip consistent")
+    ap.add_argument("dbdir")
+    ap.add_argument("--json", action="store_true")
+    a = ap.parse_args(argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        dist.init_process_group("nccl")
+    rep = consistent(a.dbdir, rank, world)
+    if rank == 0:
+        if a.json:
+            print(json.dumps(rep.as_dict(), default=str))
+        else:
+            print(f"{a.dbdir}: {'consistent' if rep.ok else 'NOT consistent'} -- {rep.files} files, "
+                  f"{rep.commits} commits, {rep.bytes_checked} bytes; bad commits {len(rep.bad_commits)}, "
+                  f"header errors {len(rep.header_errors)}, walk errors {len(rep.walk_errors)}, "
+                  f"stale empty commits {len(rep.stale_empty_commits)}, .zsdb ok {rep.dotzsdb.get('ok')}")
+            for line in rep.issues:
+                print("  " + line)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+    return 0 if rep.ok else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
