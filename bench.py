@@ -419,7 +419,7 @@ def run_config5(args, world, rank, dev, stream):
     tm = Timer(world, dev)
     elapsed = tm.run(step, args.steps, args.warmup)
     rep = step.rep
-    assert rep.ok and len(rep.stale_empty_commits) == args.finalised, rep.as_dict()
+    assert rep.ok and rep.n_stale == args.finalised, (rep.ok, rep.n_bad, rep.n_stale, rep.walk_errors[:5])
     kern_ms = float(np.mean(tm.kern_ms))
     ncommit = len(job.c_off)
     local_bytes = job.local.bytes_checked

@@ -108,9 +108,9 @@ def test_directory_and_cli(gpu, tmp_path):
     assert rep.ok and rep.files == len(db) - 1
     f = sorted(p for p in os.listdir(tmp_path) if cs.parse_name(p) and cs.parse_name(p)[0] == 1)[2]
     with open(tmp_path / f, "r+b") as fh:
-        fh.seek(1000)
+        fh.seek(40 + 3 * 320 + 100)          # value payload of pair 3
         b = fh.read(1)
-        fh.seek(1000)
+        fh.seek(40 + 3 * 320 + 100)
         fh.write(bytes([b[0] ^ 1]))
     assert cs.main([str(tmp_path)]) == 1
     rep = cs.consistent(str(tmp_path))

@@ -264,6 +264,8 @@ class Report:
     dotzsdb: dict = field(default_factory=dict)
     bad_commits: list = field(default_factory=list)         # (file, commit offset)
     stale_empty_commits: list = field(default_factory=list)  # (file, commit offset)
+    n_bad: int = 0            # counts (the lists hold at most MAX_LISTED per rank)
+    n_stale: int = 0
     header_errors: list = field(default_factory=list)
     walk_errors: list = field(default_factory=list)
     issues: list = field(default_factory=list)
@@ -465,6 +467,8 @@ class Consistent:
             rep.bytes_checked += s["bytes"]
             rep.bad_commits += [tuple(b) for b in s["bad"]]
             rep.stale_empty_commits += [tuple(b) for b in s["stale"]]
+            rep.n_bad += s["n_bad"]
+            rep.n_stale += s["n_stale"]
             rep.header_errors += [tuple(h) for h in s["header_errors"]]
             rep.walk_errors += [tuple(w) for w in s["walk_errors"]]
             rep.issues += s["issues"]
@@ -482,6 +486,7 @@ class Consistent:
             _, _, _, stored, words = _commit_rec(f.image, at)
             if stored is None or _trailer_crc(span, words) != stored:
                 rep.bad_commits.append((f.name, at))
+                rep.n_bad += 1
         rep.bad_commits.sort()
         rep.stale_empty_commits.sort()
         dz = rep.dotzsdb
@@ -497,7 +502,7 @@ class Consistent:
                     rep.issues.append(f"{f.name}: active index {f.startidx} != .zsdb curidx {dz['curidx']}")
                 elif f.size != dz["offset"]:
                     rep.issues.append(f"{f.name}: size {f.size} != .zsdb offset {dz['offset']}")
-        rep.ok = (not rep.bad_commits and not rep.header_errors and not rep.walk_errors
+        rep.ok = (not rep.n_bad and not rep.header_errors and not rep.walk_errors
                   and dz.get("ok", False))
         return rep
 
@@ -538,9 +543,13 @@ def main(argv=None) -> int:
             print(json.dumps(rep.as_dict(), default=str))
         else:
             print(f"{a.dbdir}: {'consistent' if rep.ok else 'NOT consistent'} -- {rep.files} files, "
-                  f"{rep.commits} commits, {rep.bytes_checked} bytes; bad commits {len(rep.bad_commits)}, "
+                  f"{rep.commits} commits, {rep.bytes_checked} bytes; bad commits {rep.n_bad}, "
                   f"header errors {len(rep.header_errors)}, walk errors {len(rep.walk_errors)}, "
-                  f"stale empty commits {len(rep.stale_empty_commits)}, .zsdb ok {rep.dotzsdb.get('ok')}")
+                  f"stale empty commits {rep.n_stale}, .zsdb ok {rep.dotzsdb.get('ok')}")
+            for b in rep.bad_commits[:20]:
+                print(f"  bad commit: {b[0]} at offset {b[1]}")
+            for w in rep.walk_errors[:20]:
+                print(f"  walk stopped: {w[0]} rc {w[1]} at offset {w[2]}")
             for line in rep.issues:
                 print("  " + line)
     if world > 1:
