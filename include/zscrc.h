@@ -127,6 +127,20 @@ int zscrc_diag_stream_read(const void *d_buf, uint64_t len, void *d_scratch4, in
 /* Number of gfx950 devices visible (0 if none / no HIP runtime). */
 int zscrc_device_count(void);
 
+/* Host byte streams: crc32c(seed, everything passed to update), computed on
+ * the GPU chunk by chunk while the caller keeps producing bytes (the shape
+ * of crc32_begin / mfile_write / crc32_end, src/mfile.c:270-290, :526-546,
+ * and of repack's records-region CRC, src/zeroskip-packed.c:442).  Default:
+ * update() copies into pinned staging, the caller may reuse its buffer on
+ * return.  ZSCRC_STREAM_NOCOPY: the GPU copies straight from the caller's
+ * memory, which must stay valid and unchanged until final() (an append-only
+ * mmap).  chunk_bytes 0 = 64 MiB.  final() always frees the stream. */
+typedef struct zscrc_stream zscrc_stream;
+#define ZSCRC_STREAM_NOCOPY 1u
+int zscrc_stream_open(zscrc_stream **s, uint32_t seed, uint64_t chunk_bytes, unsigned flags);
+int zscrc_stream_update(zscrc_stream *s, const void *buf, size_t len);
+int zscrc_stream_final(zscrc_stream *s, uint32_t *crc);
+
 /* ======================================================================
  * Part 3 -- zeroskip file images (verify-on-open / `consistent` / repack).
  * A commit's CRC covers its span (the bytes since crc32_begin, ending where

@@ -1,0 +1,48 @@
+"""zscrc_stream_* (host byte streams checksummed on the GPU) against the
+oracle: irregular update sizes across chunk boundaries, both copy modes,
+seeds, many chunks (register-array growth), empty streams."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+from zeroskip_amd.stream import CrcStream
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("nocopy", [False, True])
+@pytest.mark.parametrize("seed", [0, 0xDEADBEEF])
+def test_irregular_updates(gpu, nocopy, seed):
+    rng = np.random.default_rng(5 + nocopy)
+    data = rng.integers(0, 256, (24 << 20) + 12345, dtype=np.uint8)
+    cuts = [0, 1, 8, 15, 4096, (1 << 20) - 3, (1 << 20) + 5, 7 << 20, (7 << 20) + 1, 19 << 20, len(data)]
+    with CrcStream(seed, chunk_bytes=1 << 20, nocopy=nocopy) as s:
+        for a, b in zip(cuts, cuts[1:]):
+            s.update(data[a:b])
+    assert s.crc == oracle.crc32c_hw(seed, data)
+
+
+def test_many_chunks(gpu):
+    data = np.random.default_rng(9).integers(0, 256, (20 << 20) + 77, dtype=np.uint8)
+    s = CrcStream(7, chunk_bytes=4096)        # > 4096 chunks: the register array grows
+    for i in range(0, len(data), 3 << 20):
+        s.update(data[i:i + (3 << 20)])
+    assert s.final() == oracle.crc32c_hw(7, data)
+
+
+def test_empty_and_tiny(gpu):
+    assert CrcStream(0x1234).final() == 0x1234
+    s = CrcStream(0)
+    s.update(b"")
+    s.update(b"lorem")
+    s.update(b" ipsum")
+    assert s.final() == 0xdfb4e6c9          # tests/unit-crc32c.c:36
+
+
+def test_default_chunk_large(gpu):
+    data = np.random.default_rng(11).integers(0, 256, (200 << 20) + 3, dtype=np.uint8)
+    with CrcStream(0, nocopy=True) as s:
+        s.update(data)
+    assert s.crc == oracle.crc32c_hw(0, data)

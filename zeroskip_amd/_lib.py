@@ -43,9 +43,13 @@ SIGNATURES = {
     "zscrc_device_verify_commits": (_int, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
     "zscrc_zs_verify_image": (_int, [_vp, _u64, _int, _vp]),
     "zscrc_device_write_commits": (_int, [_vp, _vp, _vp, _sz, _vp, _vp]),
+    "zscrc_stream_open": (_int, [_vp, _u32, _u64, ctypes.c_uint]),
+    "zscrc_stream_update": (_int, [_vp, _vp, _sz]),
+    "zscrc_stream_final": (_int, [_vp, _vp]),
 }
 
 ZSCRC_RAW = 1
+ZSCRC_STREAM_NOCOPY = 1
 
 _lib = None
 

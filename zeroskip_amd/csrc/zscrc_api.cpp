@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <vector>
 
 #include "../../include/zscrc.h"
 #include "zscrc_gf2.h"
@@ -364,30 +365,19 @@ int span_impl(DevCtx *c, const void *d_buf, uint64_t len, uint32_t seed, uint32_
     return ZSCRC_OK;
 }
 
-/* Scalar call offloaded to the GPU; returns false to fall back to the CPU. */
+/* Scalar call offloaded to the GPU (chunked copy/CRC pipeline of Part 4,
+ * straight from the caller's memory); returns false to fall back to the CPU. */
 bool gpu_scalar(uint32_t crc, const void *buf, size_t len, uint32_t *res)
 {
-    DevCtx *c = nullptr;
-    if (get_ctx(&c))
+    zscrc_stream *st = nullptr;
+    if (zscrc_stream_open(&st, crc, 0, ZSCRC_STREAM_NOCOPY))
         return false;
-    std::lock_guard<std::recursive_mutex> lk(c->mu);
-    if (grow(&c->stage, &c->stage_bytes, len + 64))
+    const int rc = zscrc_stream_update(st, buf, len);
+    uint32_t r = 0;
+    const int rc2 = zscrc_stream_final(st, &r);
+    if (rc || rc2)
         return false;
-    uint8_t *dbuf = static_cast<uint8_t *>(c->stage);
-    uint32_t *dout = reinterpret_cast<uint32_t *>(dbuf + ((len + 15) & ~size_t(15)));
-    hipError_t e = hipMemcpy(dbuf, buf, len, hipMemcpyHostToDevice);
-    if (e != hipSuccess) {
-        set_err("hipMemcpy H2D", e);
-        return false;
-    }
-    if (span_impl(c, dbuf, len, crc, dout, nullptr, 0, nullptr))
-        return false;
-    e = hipMemcpy(res, dout, 4, hipMemcpyDeviceToHost);
-    if (e != hipSuccess) {
-        set_err("hipMemcpy D2H", e);
-        return false;
-    }
-    g_stat[3] += len;
+    *res = r;
     return true;
 }
 
@@ -674,6 +664,239 @@ int zscrc_device_count(void)
     for (int i = 0; i < n; ++i)
         k += is_gfx950(i);
     return k;
+}
+
+/* ============================================= Part 4: host byte streams */
+/*
+ * Incremental CRC of a host byte stream on the GPU -- the shape of zeroskip's
+ * crc32_begin / mfile_write / crc32_end (src/mfile.c:270-290, :526-546) and
+ * of repack's one huge records-region CRC (src/zeroskip-packed.c:442).
+ * Bytes are cut into fixed chunks; each chunk is copied host->device on a
+ * copy stream and its RAW register computed on a compute stream (span
+ * kernel), NSLOT chunks in flight, so PCIe transfer, CRC and the caller's
+ * production of the next bytes overlap.  final() folds the chunk registers on
+ * the host: reg = shift(reg, len_k) ^ raw_k, then the initial register.
+ */
+} /* extern "C" */
+
+struct zscrc_stream {
+    static constexpr int NSLOT = 3;
+    DevCtx *c = nullptr;
+    int dev = 0;
+    unsigned flags = 0;
+    hipStream_t cs = nullptr, ks = nullptr; /* copy / compute */
+    uint32_t seed = 0;
+    uint64_t chunk = 0;
+    uint8_t *dbuf[NSLOT] = {};
+    uint8_t *hpin[NSLOT] = {};
+    void *scr[NSLOT] = {};
+    hipEvent_t copied[NSLOT] = {}, done[NSLOT] = {};
+    bool used[NSLOT] = {};
+    uint32_t *dparts = nullptr;
+    size_t cap = 0;
+    std::vector<uint64_t> lens;
+    int slot = 0;
+    uint64_t fill = 0;   /* copy mode: bytes staged in hpin[slot] */
+    uint64_t total = 0;
+    int err = 0;
+};
+
+namespace {
+
+int stream_fail(zscrc_stream *s, const char *what, hipError_t e)
+{
+    set_err(what, e);
+    s->err = ZSCRC_EHIP;
+    return s->err;
+}
+
+/* Queue chunk `idx` = n bytes at src (device-visible after the copy) in slot k. */
+int stream_submit(zscrc_stream *s, const void *src, uint64_t n)
+{
+    const int k = s->slot;
+    const size_t idx = s->lens.size();
+    hipError_t e;
+    if (idx >= s->cap) {
+        /* grow the device register array (rare: doubles) */
+        size_t ncap = s->cap ? 2 * s->cap : 4096;
+        uint32_t *np = nullptr;
+        if ((e = hipStreamSynchronize(s->ks)) != hipSuccess)
+            return stream_fail(s, "hipStreamSynchronize", e);
+        if ((e = hipMalloc(&np, ncap * 4)) != hipSuccess)
+            return stream_fail(s, "hipMalloc(stream registers)", e);
+        if (s->dparts) {
+            (void)hipMemcpy(np, s->dparts, s->cap * 4, hipMemcpyDeviceToDevice);
+            (void)hipFree(s->dparts);
+        }
+        s->dparts = np;
+        s->cap = ncap;
+    }
+    /* the slot's device buffer is free once its previous CRC finished */
+    if (s->used[k] && (e = hipStreamWaitEvent(s->cs, s->done[k], 0)) != hipSuccess)
+        return stream_fail(s, "hipStreamWaitEvent", e);
+    if ((e = hipMemcpyAsync(s->dbuf[k], src, n, hipMemcpyHostToDevice, s->cs)) != hipSuccess)
+        return stream_fail(s, "hipMemcpyAsync H2D", e);
+    if ((e = hipEventRecord(s->copied[k], s->cs)) != hipSuccess ||
+        (e = hipStreamWaitEvent(s->ks, s->copied[k], 0)) != hipSuccess)
+        return stream_fail(s, "stream event", e);
+    {
+        std::lock_guard<std::recursive_mutex> lk(s->c->mu);
+        int rc = span_impl(s->c, s->dbuf[k], n, 0, s->dparts + idx, s->scr[k], ZSCRC_RAW, s->ks);
+        if (rc)
+            return s->err = rc;
+    }
+    if ((e = hipEventRecord(s->done[k], s->ks)) != hipSuccess)
+        return stream_fail(s, "hipEventRecord", e);
+    s->used[k] = true;
+    s->lens.push_back(n);
+    s->total += n;
+    g_stat[3] += n;
+    s->slot = (k + 1) % zscrc_stream::NSLOT;
+    return ZSCRC_OK;
+}
+
+void stream_free(zscrc_stream *s)
+{
+    if (s->cs)
+        (void)hipStreamSynchronize(s->cs);
+    if (s->ks)
+        (void)hipStreamSynchronize(s->ks);
+    for (int k = 0; k < zscrc_stream::NSLOT; ++k) {
+        if (s->dbuf[k])
+            (void)hipFree(s->dbuf[k]);
+        if (s->scr[k])
+            (void)hipFree(s->scr[k]);
+        if (s->hpin[k])
+            (void)hipHostFree(s->hpin[k]);
+        if (s->copied[k])
+            (void)hipEventDestroy(s->copied[k]);
+        if (s->done[k])
+            (void)hipEventDestroy(s->done[k]);
+    }
+    if (s->dparts)
+        (void)hipFree(s->dparts);
+    if (s->cs)
+        (void)hipStreamDestroy(s->cs);
+    if (s->ks)
+        (void)hipStreamDestroy(s->ks);
+    delete s;
+}
+
+} /* namespace */
+
+extern "C" {
+
+int zscrc_stream_open(zscrc_stream **out, uint32_t seed, uint64_t chunk_bytes, unsigned flags)
+{
+    if (!out)
+        return ZSCRC_EINVAL;
+    *out = nullptr;
+    DevCtx *c;
+    int rc = get_ctx(&c);
+    if (rc)
+        return rc;
+    zscrc_stream *s = new (std::nothrow) zscrc_stream;
+    if (!s)
+        return ZSCRC_ENOMEM;
+    s->c = c;
+    s->flags = flags;
+    s->seed = seed;
+    s->chunk = chunk_bytes ? ((chunk_bytes + 4095) & ~4095ull) : (64ull << 20);
+    hipError_t e = hipGetDevice(&s->dev);
+    if (e == hipSuccess)
+        e = hipStreamCreateWithFlags(&s->cs, hipStreamNonBlocking);
+    if (e == hipSuccess)
+        e = hipStreamCreateWithFlags(&s->ks, hipStreamNonBlocking);
+    for (int k = 0; e == hipSuccess && k < zscrc_stream::NSLOT; ++k) {
+        e = hipMalloc(&s->dbuf[k], s->chunk);
+        if (e == hipSuccess)
+            e = hipMalloc(&s->scr[k], zscrc_span_scratch_bytes(s->chunk));
+        if (e == hipSuccess && !(flags & ZSCRC_STREAM_NOCOPY))
+            e = hipHostMalloc(reinterpret_cast<void **>(&s->hpin[k]), s->chunk, hipHostMallocDefault);
+        if (e == hipSuccess)
+            e = hipEventCreateWithFlags(&s->copied[k], hipEventDisableTiming);
+        if (e == hipSuccess)
+            e = hipEventCreateWithFlags(&s->done[k], hipEventDisableTiming);
+    }
+    if (e != hipSuccess) {
+        set_err("zscrc_stream_open", e);
+        stream_free(s);
+        return ZSCRC_ENOMEM;
+    }
+    *out = s;
+    return ZSCRC_OK;
+}
+
+int zscrc_stream_update(zscrc_stream *s, const void *buf, size_t len)
+{
+    if (!s || (!buf && len))
+        return ZSCRC_EINVAL;
+    if (s->err)
+        return s->err;
+    const uint8_t *p = static_cast<const uint8_t *>(buf);
+    if (s->flags & ZSCRC_STREAM_NOCOPY) {
+        /* straight from the caller's (unchanging) memory, chunk by chunk */
+        while (len) {
+            const uint64_t n = len < s->chunk ? len : s->chunk;
+            int rc = stream_submit(s, p, n);
+            if (rc)
+                return rc;
+            p += n;
+            len -= n;
+        }
+        return ZSCRC_OK;
+    }
+    while (len) {
+        const int k = s->slot;
+        if (s->fill == 0 && s->used[k]) {
+            /* the staging buffer is free once its copy has left */
+            hipError_t e = hipEventSynchronize(s->copied[k]);
+            if (e != hipSuccess)
+                return stream_fail(s, "hipEventSynchronize", e);
+        }
+        const uint64_t n = len < s->chunk - s->fill ? len : s->chunk - s->fill;
+        memcpy(s->hpin[k] + s->fill, p, n);
+        s->fill += n;
+        p += n;
+        len -= n;
+        if (s->fill == s->chunk) {
+            s->fill = 0;
+            int rc = stream_submit(s, s->hpin[k], s->chunk);
+            if (rc)
+                return rc;
+        }
+    }
+    return ZSCRC_OK;
+}
+
+int zscrc_stream_final(zscrc_stream *s, uint32_t *crc)
+{
+    if (!s)
+        return ZSCRC_EINVAL;
+    int rc = s->err;
+    if (!rc && s->fill) {
+        const uint64_t n = s->fill;
+        s->fill = 0;
+        rc = stream_submit(s, s->hpin[s->slot], n);
+    }
+    std::vector<uint32_t> raw(s->lens.size());
+    if (!rc && !raw.empty()) {
+        hipError_t e = hipStreamSynchronize(s->ks);
+        if (e == hipSuccess)
+            e = hipMemcpy(raw.data(), s->dparts, raw.size() * 4, hipMemcpyDeviceToHost);
+        if (e != hipSuccess)
+            rc = stream_fail(s, "stream final", e);
+    }
+    if (!rc && crc) {
+        const uint32_t kx = zs_gf2_xpow8n(s->chunk);
+        uint32_t reg = 0;
+        for (size_t i = 0; i < raw.size(); ++i)
+            reg = (s->lens[i] == s->chunk ? zs_gf2_mul(reg, kx) : zs_gf2_shift(reg, s->lens[i])) ^ raw[i];
+        reg ^= zs_gf2_shift(s->seed ^ 0xffffffffu, s->total);
+        *crc = reg ^ 0xffffffffu;
+    }
+    stream_free(s);
+    return rc;
 }
 
 } /* extern "C" */
