@@ -197,6 +197,26 @@ typedef struct zscrc_zs_report {
  * current device, verify every commit there.  Synchronous. */
 int zscrc_zs_verify_image(const void *image, uint64_t size, int kind, zscrc_zs_report *rep);
 
+/* `consistent` for one process / one GPU (zsdb_consistent,
+ * src/zeroskip.c:1399-1407, and tool/cmd-consistent.c:23-49 are stubs in the
+ * reference): every .zsdb / header / commit CRC of the DB directory,
+ * recomputed; commits on the GPU.  The multi-GPU driver is
+ * zeroskip_amd/consistent.py. */
+typedef struct zscrc_consistent_report {
+    uint64_t files;               /* zeroskip-* files checked                    */
+    uint64_t commits;             /* commit CRCs recomputed on the GPU           */
+    uint64_t bytes;               /* file bytes staged to the GPU                */
+    uint64_t bad_commits;         /* stored CRC != recomputed                    */
+    uint64_t stale_empty_commits; /* zero-length finalise commits hashed from the
+                                   * previous span (src/mfile.c:534-546 quirk)  */
+    uint64_t header_errors;       /* bad signature or header CRC                 */
+    uint64_t walk_errors;         /* record walk stopped early / packed layout   */
+    int dotzsdb;                  /* 1 ok, 0 bad, -1 missing                     */
+    int consistent;               /* 1 if every check passed                     */
+    char first_bad[512];          /* "file:offset: what" of the first problem    */
+} zscrc_consistent_report;
+int zscrc_zs_consistent(const char *dbdir, zscrc_consistent_report *rep);
+
 #ifdef __cplusplus
 }
 #endif

@@ -154,3 +154,30 @@ def test_two_ranks_split_long_region(gpu):
     for _, ok, commits, bad, nstale, at in res:
         assert not ok and commits == single.commits and nstale == 3
         assert bad == [(name(4, 5), at)]
+
+
+def test_native_entry_point(gpu, tmp_path):
+    """zscrc_zs_consistent (the C entry point for zsdb_consistent) agrees with
+    the Python driver, clean and corrupted, across several device groups."""
+    db = small_db(long_region=True)
+    for n, v in db.items():
+        (tmp_path / n).write_bytes(v)
+    nat = cs.consistent_native(str(tmp_path))
+    py = cs.consistent(str(tmp_path))
+    assert nat["consistent"] == 1 and py.ok
+    assert nat["commits"] == py.commits and nat["stale_empty_commits"] == py.n_stale == 3
+    assert nat["files"] == 6 and nat["dotzsdb"] == 1
+    f = name(7, 7)
+    img = bytearray(db[f])
+    c = zf.walk(img)[0][5]
+    img[c["span_off"] + 3] ^= 0x10
+    (tmp_path / f).write_bytes(bytes(img))
+    os.environ["ZSCRC_CONSISTENT_GROUP"] = str(1 << 20)     # one file per device pass
+    try:
+        nat = cs.consistent_native(str(tmp_path))
+    finally:
+        del os.environ["ZSCRC_CONSISTENT_GROUP"]
+    assert nat["consistent"] == 0 and nat["bad_commits"] == 1
+    assert nat["first_bad"].startswith(f"{f}:{c['commit_off']}:")
+    (tmp_path / ".zsdb").write_bytes(b"short")
+    assert cs.consistent_native(str(tmp_path))["dotzsdb"] == 0

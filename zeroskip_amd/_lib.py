@@ -46,6 +46,7 @@ SIGNATURES = {
     "zscrc_stream_open": (_int, [_vp, _u32, _u64, ctypes.c_uint]),
     "zscrc_stream_update": (_int, [_vp, _vp, _sz]),
     "zscrc_stream_final": (_int, [_vp, _vp]),
+    "zscrc_zs_consistent": (_int, [ctypes.c_char_p, _vp]),
 }
 
 ZSCRC_RAW = 1

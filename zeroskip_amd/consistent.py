@@ -37,6 +37,7 @@ the host.  Input bytes never cross xGMI.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import re
@@ -516,6 +517,27 @@ class Consistent:
         return dict(present=True, ok=rc == 0 and st == cp, rc=rc, stored=st, computed=cp,
                     offset=int.from_bytes(d[8:16], "big"),
                     uuid=d[16:52].decode("latin-1"), curidx=int.from_bytes(d[53:57], "big"))
+
+
+class NativeReport(ctypes.Structure):
+    """zscrc_consistent_report (include/zscrc.h)."""
+    _fields_ = [("files", ctypes.c_uint64), ("commits", ctypes.c_uint64), ("bytes", ctypes.c_uint64),
+                ("bad_commits", ctypes.c_uint64), ("stale_empty_commits", ctypes.c_uint64),
+                ("header_errors", ctypes.c_uint64), ("walk_errors", ctypes.c_uint64),
+                ("dotzsdb", ctypes.c_int), ("consistent", ctypes.c_int), ("first_bad", ctypes.c_char * 512)]
+
+    def as_dict(self):
+        d = {k: getattr(self, k) for k, _ in self._fields_}
+        d["first_bad"] = self.first_bad.decode(errors="replace")
+        return d
+
+
+def consistent_native(dbdir: str) -> dict:
+    """The C entry point (one process, current GPU): zscrc_zs_consistent."""
+    from ._lib import check, lib
+    rep = NativeReport()
+    check(lib().zscrc_zs_consistent(os.fsencode(dbdir), ctypes.byref(rep)), "zscrc_zs_consistent")
+    return rep.as_dict()
 
 
 def consistent(src, rank: int = 0, world: int = 1, group=None, backend=None) -> Report:
