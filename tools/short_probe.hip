@@ -1,0 +1,154 @@
+// short_probe: what bounds one-lane-per-record (G = 1) CRC on short records?
+// Measured ceilings for the product's G = 1 access shape, not product code.
+//   read   : lane l reads record r = its own RLEN bytes at r*RSTRIDE as 64-byte
+//            pieces (4 x 16 B loads each), records grid-strided -- no compute
+//   crc    : the same loads + the product's slice-by-4 chain (32-replica LDS
+//            tables, one v_perm per lookup address) over every word
+//   crc2   : crc with two records per lane interleaved (two independent chains)
+// usage: short_probe  (prints JSON lines)
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u32x4 *g4p;
+
+__device__ __forceinline__ unsigned lds32(const char *L, unsigned a) { return *(const unsigned *)(L + a); }
+
+__device__ __forceinline__ unsigned m4(const char *L, unsigned x, unsigned c_lo, unsigned c_hi)
+{
+    const unsigned a0 = __builtin_amdgcn_perm(x, c_lo, 0x0C020400u);
+    const unsigned a1 = __builtin_amdgcn_perm(x, c_lo, 0x0C020500u);
+    const unsigned a2 = __builtin_amdgcn_perm(x, c_hi, 0x0C020600u);
+    const unsigned a3 = __builtin_amdgcn_perm(x, c_hi, 0x0C020700u);
+    return lds32(L, a0) ^ lds32(L, a1 + 128) ^ lds32(L, a2) ^ lds32(L, a3 + 128);
+}
+
+template <int RSTRIDE, int RLEN, int MODE>  // MODE 0 read, 1 crc, 2 crc2
+__global__ __launch_bounds__(1024) void rec(const char *buf, size_t nrec, unsigned *out)
+{
+    __shared__ __attribute__((aligned(16))) char L[MODE ? 131072 : 16];
+    if (MODE) {
+        uint4 *L4 = reinterpret_cast<uint4 *>(L);
+        for (int i = threadIdx.x; i < 8192; i += 1024) {
+            const unsigned v = 0x9E3779B9u * (unsigned)(i >> 3) + 0x7F4A7C15u;
+            L4[i] = make_uint4(v, v, v, v);
+        }
+        __syncthreads();
+    }
+    const int lane = threadIdx.x & 63;
+    const unsigned c_lo = (unsigned)(lane & 31) << 2, c_hi = c_lo | 0x10000u;
+    const size_t nthr = (size_t)gridDim.x * 1024;
+    const size_t t = (size_t)blockIdx.x * 1024 + threadIdx.x;
+    constexpr int NP = RLEN / 64;
+    unsigned acc = 0;
+    if (MODE < 2) {
+        for (size_t r = t; r < nrec; r += nthr) {
+            const char *p = buf + r * RSTRIDE;
+            unsigned reg = 0;
+#pragma unroll
+            for (int pc = 0; pc < NP; ++pc) {
+                u32x4 v[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    v[i] = *(g4p)(p + pc * 64 + 16 * i);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    if (MODE == 0) {
+                        reg ^= v[i].x ^ v[i].y ^ v[i].z ^ v[i].w;
+                    } else {
+                        reg = m4(L, reg ^ v[i].x, c_lo, c_hi);
+                        reg = m4(L, reg ^ v[i].y, c_lo, c_hi);
+                        reg = m4(L, reg ^ v[i].z, c_lo, c_hi);
+                        reg = m4(L, reg ^ v[i].w, c_lo, c_hi);
+                    }
+                }
+            }
+            acc ^= reg;
+        }
+    } else {
+        for (size_t r = 2 * t; r < nrec; r += 2 * nthr) {
+            const char *p = buf + r * RSTRIDE;
+            const char *q = p + (r + 1 < nrec ? RSTRIDE : 0);
+            unsigned ra = 0, rb = 0;
+#pragma unroll
+            for (int pc = 0; pc < NP; ++pc) {
+                u32x4 a[4], b[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    a[i] = *(g4p)(p + pc * 64 + 16 * i);
+                    b[i] = *(g4p)(q + pc * 64 + 16 * i);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    ra = m4(L, ra ^ a[i].x, c_lo, c_hi);
+                    rb = m4(L, rb ^ b[i].x, c_lo, c_hi);
+                    ra = m4(L, ra ^ a[i].y, c_lo, c_hi);
+                    rb = m4(L, rb ^ b[i].y, c_lo, c_hi);
+                    ra = m4(L, ra ^ a[i].z, c_lo, c_hi);
+                    rb = m4(L, rb ^ b[i].z, c_lo, c_hi);
+                    ra = m4(L, ra ^ a[i].w, c_lo, c_hi);
+                    rb = m4(L, rb ^ b[i].w, c_lo, c_hi);
+                }
+            }
+            acc ^= ra ^ rb;
+        }
+    }
+    if (acc == 0x12345678u)
+        out[0] = acc;
+}
+
+template <int RS, int RL, int MODE>
+void run(const char *d, size_t total, unsigned *o, int cu)
+{
+    const size_t nrec = total / RS;
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    for (int mult : {1, 2}) {
+        const int grid = cu * mult;
+        for (int i = 0; i < 3; ++i)
+            hipLaunchKernelGGL((rec<RS, RL, MODE>), dim3(grid), dim3(1024), 0, 0, d, nrec, o);
+        std::vector<float> t;
+        for (int r = 0; r < 10; ++r) {
+            hipEventRecord(a);
+            hipLaunchKernelGGL((rec<RS, RL, MODE>), dim3(grid), dim3(1024), 0, 0, d, nrec, o);
+            hipEventRecord(b);
+            hipEventSynchronize(b);
+            float ms;
+            hipEventElapsedTime(&ms, a, b);
+            t.push_back(ms);
+        }
+        std::sort(t.begin(), t.end());
+        const double ms = t[t.size() / 2];
+        printf("{\"stride\": %d, \"len\": %d, \"mode\": \"%s\", \"grid\": %d, \"ms\": %.4f, \"GBs\": %.1f}\n", RS, RL,
+               MODE == 0 ? "read" : MODE == 1 ? "crc" : "crc2", grid, ms, nrec * (double)RL / ms / 1e6);
+        fflush(stdout);
+    }
+}
+
+int main()
+{
+    size_t n = (size_t)4 << 30;
+    char *d;
+    unsigned *o;
+    if (hipMalloc(&d, n) != hipSuccess || hipMalloc(&o, 64) != hipSuccess) {
+        printf("alloc failed\n");
+        return 1;
+    }
+    hipMemset(d, 1, n);
+    hipDeviceSynchronize();
+    int cu = 0;
+    hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, 0);
+    run<64, 64, 0>(d, n, o, cu);
+    run<64, 64, 1>(d, n, o, cu);
+    run<64, 64, 2>(d, n, o, cu);
+    run<320, 320, 0>(d, n, o, cu);
+    run<320, 320, 1>(d, n, o, cu);
+    run<320, 320, 2>(d, n, o, cu);
+    run<1024, 1024, 0>(d, n, o, cu);
+    run<1024, 1024, 1>(d, n, o, cu);
+    run<1024, 1024, 2>(d, n, o, cu);
+    return 0;
+}
