@@ -42,6 +42,37 @@ def teams(request, gpu):
     lib().zscrc_set_teams(1024, 1 << 20)
 
 
+@pytest.fixture(params=[-1, 1, 2, 3, 4], ids=["g1-auto", "g1-ring1", "g1-ring2", "g1-short", "g1-short-pf"])
+def g1_walk(request, gpu):
+    lib().zscrc_set_prefetch(1, request.param)
+    yield request.param
+    lib().zscrc_set_prefetch(1, -1)
+
+
+def test_golden_cases_g1_walks(gpu, g1_walk):
+    """Every one-lane-per-record walk (team ring / short kernel) on the golden
+    cases, the fixed-stride shapes and a commit batch."""
+    lib().zscrc_set_teams(1 << 40, 1 << 40)
+    try:
+        data = xorshift64_bytes(GOLDEN["data"]["bytes"])
+        rows = np.array(GOLDEN["cases"], dtype=np.uint64)
+        d = to_dev(data, gpu)
+        offs = to_dev(rows[:, 0].astype(np.int64), gpu)
+        lens = to_dev(rows[:, 1].astype(np.int64), gpu)
+        seeds = to_dev(rows[:, 2].astype(np.uint32).view(np.int32), gpu)
+        assert np.array_equal(u32(zd.crc_batch(d, offs, lens, seeds)), rows[:, 3].astype(np.uint32))
+        for stride, length, n in [(64, 64, 70000), (320, 312, 20000), (1040, 1037, 3000), (7, 7, 500)]:
+            data = rand_bytes(stride * (n - 1) + length, stride * 7 + length)
+            out = u32(zd.crc_fixed(to_dev(data, gpu), stride, length, n, seed=0x77))
+            assert np.array_equal(out, _oracle_seeded(data, stride, length, n, 0x77)), (stride, length)
+            raw = u32(zd.crc_fixed(to_dev(data[3:], gpu), stride, length - 3, n - 1, raw=True))
+            ref = oracle.batch(data[3:], n=n - 1, stride=stride, fixed_len=length - 3, impl="hw",
+                               seeds=np.full(n - 1, M32, np.uint32)) ^ np.uint32(M32)
+            assert np.array_equal(raw, ref), (stride, length, "raw")
+    finally:
+        lib().zscrc_set_teams(1024, 1 << 20)
+
+
 def test_golden_cases_variable_batch(gpu, teams):
     data = xorshift64_bytes(GOLDEN["data"]["bytes"])
     rows = np.array(GOLDEN["cases"], dtype=np.uint64)

@@ -30,6 +30,7 @@ void zscrc_cpu_init(void);
 int zs_launch_team(int g, int fixed, int depth, const zs::BatchDesc *d, const uint32_t *gtab, int grid,
                    hipStream_t stream);
 int zs_launch_span_fold(const zs::SpanFold *f, hipStream_t stream);
+int zs_launch_short(int fixed, int pf, const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
 int zs_launch_stream_read(const void *buf, uint64_t n, uint32_t *out, int grid, hipStream_t stream);
 int zs_launch_classify(const zs::Classify *c, hipStream_t stream);
 int zs_launch_part_fold(const zs::BatchDesc *d, const uint32_t *gtab, hipStream_t stream);
@@ -48,7 +49,9 @@ std::atomic<uint64_t> g_g1_max{1024};
 std::atomic<uint64_t> g_g16_max{1u << 20};
 int g_strict = 0;
 /* record-walk override per team size (index 0/1/2 = G 1/16/64): -1 = automatic
- * (walk_for), 0 = two-level loop, 1/2 = flattened loop with a 1/2-item ring */
+ * (walk_for), 0 = two-level loop, 1/2 = flattened loop with a 1/2-item ring;
+ * G = 1 only: 3 / 4 = short_kernel (per-lane records; next piece loaded if it
+ * exists / always four loads) */
 std::atomic<int> g_depth[3] = {{-1}, {-1}, {-1}};
 
 struct DevCtx {
@@ -199,6 +202,8 @@ zs::BatchDesc make_desc()
  * items deep where the batch is fixed-stride, except 4-8 KiB G16 records. */
 int walk_for(int g, int fixed, uint64_t len)
 {
+    if (g == 1)
+        return 3;
     if (len >= 8192)
         return 0;
     if (!fixed)
@@ -214,9 +219,12 @@ int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s, int depth_hi
     int depth = g_depth[g == 1 ? 0 : g == 16 ? 1 : 2];
     if (depth < 0)
         depth = depth_hint >= 0 ? depth_hint : walk_for(g, fixed, typical);
+    if (g != 1 && depth > 2)
+        depth = 2;
     if (!fixed && depth == 2)
         depth = 1;
-    int rc = zs_launch_team(g, fixed, depth, &d, c->gtab, c->ncu, s);
+    int rc = depth >= 3 ? zs_launch_short(fixed, depth == 4, &d, c->gtab, c->ncu, s)
+                        : zs_launch_team(g, fixed, depth, &d, c->gtab, c->ncu, s);
     if (rc) {
         set_err("team kernel launch", hipGetLastError());
         return ZSCRC_EHIP;
@@ -279,7 +287,7 @@ int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s)
         g_stat[2]++;
     }
     const int team[4] = {1, 16, 16, 64};
-    const int walk[4] = {1, 1, 0, 0};
+    const int walk[4] = {-1, 1, 0, 0};
     d.len_lo = 0;
     d.len_hi = ~0ull;
     d.desc = desc;
@@ -630,7 +638,7 @@ void zscrc_set_gpu_min(uint64_t min_bytes)
 
 void zscrc_set_prefetch(int g, int depth)
 {
-    if (depth < -1 || depth > 2)
+    if (depth < -1 || depth > (g == 1 ? 4 : 2))
         return;
     if (g == 1)
         g_depth[0] = depth;

@@ -631,6 +631,113 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
     }
 }
 
+/* ------------------------------------------------------ short records */
+/*
+ * One lane per record, records <= g1_max bytes (zsbench's 312-byte commit
+ * spans, 64-byte config-2 records): each lane walks its own record piece by
+ * piece with the next piece's loads in flight, nothing carried across
+ * records.  Same end-aligned 64-byte piece grid, fix-ups, tail and emit() as
+ * team_kernel<1>, without the generic (record, step) cursor: the per-record
+ * overhead is a handful of scalar/vector ops.  (tools/short_probe: this
+ * shape reads at the streaming ceiling on 64 B and 320 B records.)
+ * PF: 0 = next piece loaded only if it exists; 1 = always four loads (a
+ * dummy address past the record) so the wait counts stay static.
+ */
+template <bool FIXED, int PF>
+__global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
+{
+    __shared__ __attribute__((aligned(16))) char L[OFF_U];
+    fill_lds<1>(L, gtab);
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const uint32_t c_lo = (uint32_t)(lane & 31) << 2;
+    const uint32_t c_hi = c_lo | 0x10000u;
+    uint64_t count = d.n;
+    const RecDesc *list = nullptr;
+    if (!FIXED) {
+        uint32_t base = 0;
+        for (uint32_t k = 0; k < d.klass; ++k)
+            base += __builtin_amdgcn_readfirstlane(((g32p)d.class_count)[k]);
+        count = __builtin_amdgcn_readfirstlane(((g32p)d.class_count)[d.klass]);
+        list = d.desc + base;
+    }
+    const uintptr_t dummy = reinterpret_cast<uintptr_t>(gtab);
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(d.base) & ~uintptr_t(3);
+    const uint64_t nthr = (uint64_t)gridDim.x * WG;
+    for (uint64_t i = (uint64_t)blockIdx.x * WG + threadIdx.x; i < count; i += nthr) {
+        Item it;
+        uint64_t off, len;
+        uint32_t seed;
+        if (FIXED) {
+            len = (d.last_len != ~0ull && i + 1 == d.n) ? d.last_len : d.fixed_len;
+            off = i * d.stride;
+            seed = d.fixed_seed;
+            it.rec = i;
+        } else {
+            typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+            typedef const __attribute__((address_space(1))) u32x2 *g2p;
+            const g2p q = (g2p)(list + i);
+            const u32x2 a = q[0], b = q[1], c = q[2];
+            off = ((uint64_t)a.y << 32) | a.x;
+            len = ((uint64_t)b.y << 32) | b.x;
+            seed = c.x;
+            it.rec = c.y;
+        }
+        const uintptr_t A = reinterpret_cast<uintptr_t>(d.base) + off;
+        it.A = A;
+        it.len = len;
+        it.R0 = seed ^ d.xor_io;
+        if (!FIXED && d.commit) {
+            it.c0 = ((g32p)(A + len))[0];
+            it.c1 = ((g32p)(A + len))[1];
+        }
+        if (len < 8) {
+            uint32_t r = it.R0;
+            for (uint64_t k = 0; k < len; ++k)
+                r = byte_step(L, r, ((g8p)A)[k], c_hi);
+            emit(d, it, r, L, c_lo, c_hi);
+            continue;
+        }
+        const uintptr_t E = (A + len) & ~uintptr_t(3);
+        const uint64_t np = (E - A + 63) >> 6;
+        it.E = E;
+        it.V0 = E - np * 64;
+        it.S = np;
+        uint32_t w[16];
+        {
+            const uintptr_t p = it.V0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uintptr_t q = p + 16 * k;
+                const u32x4 v = *(g4p)(q < lo ? lo : q);
+                w[4 * k + 0] = v.x;
+                w[4 * k + 1] = v.y;
+                w[4 * k + 2] = v.z;
+                w[4 * k + 3] = v.w;
+            }
+        }
+        uint32_t r = 0;
+        for (uint64_t k = 0; k < np; ++k) {
+            uint32_t nx[16];
+            if (PF == 1) {
+                issue_plain(k + 1 < np ? it.V0 + 64 * (k + 1) : dummy, nx);
+            } else if (k + 1 < np) {
+                issue_plain(it.V0 + 64 * (k + 1), nx);
+            }
+            fixup<1>(it, k, 0, lo, w);
+            r = piece<false>(L, r, w, c_lo, c_hi);
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+                w[q] = nx[q];
+        }
+        const g8p t = (g8p)E;
+        const uint32_t tail = (uint32_t)((A + len) - E);
+        for (uint32_t k = 0; k < tail; ++k)
+            r = byte_step(L, r, t[k], c_hi);
+        emit(d, it, r, L, c_lo, c_hi);
+    }
+}
+
 /* ------------------------------------------------------------ span fold */
 /* K^m from the table K^(2^b). */
 __device__ __forceinline__ uint32_t kpow(const uint32_t *kp2, uint32_t m)
@@ -910,6 +1017,20 @@ extern "C" int zs_launch_team(int g, int fixed, int depth, const zs::BatchDesc *
     }
 #undef ZS_CASES
 #undef ZS_LAUNCH
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int zs_launch_short(int fixed, int pf, const zs::BatchDesc *d, const uint32_t *gtab, int grid,
+                               hipStream_t stream)
+{
+    if (fixed && pf)
+        hipLaunchKernelGGL((zs::short_kernel<true, 1>), dim3(grid), dim3(zs::WG), 0, stream, *d, gtab);
+    else if (fixed)
+        hipLaunchKernelGGL((zs::short_kernel<true, 0>), dim3(grid), dim3(zs::WG), 0, stream, *d, gtab);
+    else if (pf)
+        hipLaunchKernelGGL((zs::short_kernel<false, 1>), dim3(grid), dim3(zs::WG), 0, stream, *d, gtab);
+    else
+        hipLaunchKernelGGL((zs::short_kernel<false, 0>), dim3(grid), dim3(zs::WG), 0, stream, *d, gtab);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
