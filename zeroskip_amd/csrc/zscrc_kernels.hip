@@ -700,35 +700,56 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
         }
         const uintptr_t E = (A + len) & ~uintptr_t(3);
         const uint64_t np = (E - A + 63) >> 6;
-        it.E = E;
-        it.V0 = E - np * 64;
-        it.S = np;
-        uint32_t w[16];
-        {
-            const uintptr_t p = it.V0;
+        const uintptr_t V0 = E - np * 64;
+        uint32_t w[16], nx[16];
+        issue_plain(V0 < lo ? dummy : V0, w);
+        if (PF == 1 || np > 1)
+            issue_plain(np > 1 ? V0 + 64 : dummy, nx);
+        uint32_t r;
+        if (V0 < lo) {
+            /* record within 64 B of the buffer start: its first piece byte-wise */
+            r = it.R0;
+            for (uintptr_t b = A; b < V0 + 64; ++b)
+                r = byte_step(L, r, ((g8p)b)[0], c_hi);
+        } else {
+            const int32_t d0 = (int32_t)(A - V0); /* front padding, 0..63 */
+            if ((A & 3) == 0) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uintptr_t q = p + 16 * k;
-                const u32x4 v = *(g4p)(q < lo ? lo : q);
-                w[4 * k + 0] = v.x;
-                w[4 * k + 1] = v.y;
-                w[4 * k + 2] = v.z;
-                w[4 * k + 3] = v.w;
+                for (int k = 0; k < 16; ++k) {
+                    const int32_t dk = d0 - 4 * k;
+                    w[k] = dk > 0 ? 0u : (dk == 0 ? w[k] ^ it.R0 : w[k]);
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    const int32_t dk = d0 - 4 * k;
+                    uint32_t v = w[k];
+                    if (dk >= 4)
+                        v = 0;
+                    else if (dk > 0)
+                        v &= 0xffffffffu << (8 * dk);
+                    if (dk >= 0 && dk < 4)
+                        v ^= it.R0 << (8 * dk);
+                    else if (dk < 0 && dk > -4)
+                        v ^= it.R0 >> (8 * -dk);
+                    w[k] = v;
+                }
             }
+            r = piece<false>(L, 0u, w, c_lo, c_hi);
         }
-        uint32_t r = 0;
-        for (uint64_t k = 0; k < np; ++k) {
-            uint32_t nx[16];
-            if (PF == 1) {
-                issue_plain(k + 1 < np ? it.V0 + 64 * (k + 1) : dummy, nx);
-            } else if (k + 1 < np) {
-                issue_plain(it.V0 + 64 * (k + 1), nx);
-            }
-            fixup<1>(it, k, 0, lo, w);
-            r = piece<false>(L, r, w, c_lo, c_hi);
+        /* R0 bytes that spill past the first piece (front padding > 60) */
+        const uint32_t spill = (V0 >= lo && A + 4 > V0 + 64) ? it.R0 >> (8 * (uint32_t)(V0 + 64 - A)) : 0u;
+        for (uint64_t k = 1; k < np; ++k) {
 #pragma unroll
             for (int q = 0; q < 16; ++q)
                 w[q] = nx[q];
+            if (PF == 1)
+                issue_plain(k + 1 < np ? V0 + 64 * (k + 1) : dummy, nx);
+            else if (k + 1 < np)
+                issue_plain(V0 + 64 * (k + 1), nx);
+            if (k == 1)
+                w[0] ^= spill;
+            r = piece<false>(L, r, w, c_lo, c_hi);
         }
         const g8p t = (g8p)E;
         const uint32_t tail = (uint32_t)((A + len) - E);
