@@ -713,6 +713,18 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
                 r = byte_step(L, r, ((g8p)b)[0], c_hi);
         } else {
             const int32_t d0 = (int32_t)(A - V0); /* front padding, 0..63 */
+            const int32_t d0u = __builtin_amdgcn_readfirstlane(d0);
+            if (__ballot(d0 != d0u || (A & 3) != 0) == 0) {
+                /* every record of the wave starts at the same 4-aligned word f
+                 * of its first piece (fixed-stride batches, zsbench spans):
+                 * skip the zero prefix with scalar branches, R0 enters at f */
+                const int32_t f = d0u >> 2;
+                r = 0;
+#pragma unroll
+                for (int k = 0; k < 16; ++k)
+                    if (k >= f)
+                        r = m4(L, r ^ w[k] ^ (k == f ? it.R0 : 0u), c_lo, c_hi);
+            } else {
             if ((A & 3) == 0) {
 #pragma unroll
                 for (int k = 0; k < 16; ++k) {
@@ -736,6 +748,7 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
                 }
             }
             r = piece<false>(L, 0u, w, c_lo, c_hi);
+            }
         }
         /* R0 bytes that spill past the first piece (front padding > 60) */
         const uint32_t spill = (V0 >= lo && A + 4 > V0 + 64) ? it.R0 >> (8 * (uint32_t)(V0 + 64 - A)) : 0u;
