@@ -479,17 +479,6 @@ template <int G, bool FIXED, int DEPTH>
 __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
 {
     __shared__ __attribute__((aligned(16))) char L[LDS_BYTES];
-    fill_lds<G>(L, gtab);
-    __syncthreads();
-
-    const int lane = threadIdx.x & 63;
-    const int j = lane % G;
-    const uint32_t c_lo = (uint32_t)(lane & 31) << 2;
-    const uint32_t c_hi = c_lo | 0x10000u;
-    uint64_t team = ((uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6)) * (64 / G) + lane / G;
-    if (G == 64)
-        team = uni64(team); /* whole-wave team: keep record state in SGPRs */
-    const uint64_t nteams = (uint64_t)gridDim.x * WAVES * (64 / G);
     /* work items: records, or records x 2^lp parts; a device-built class list
      * supplies the record count without a host round trip */
     uint64_t count = d.n;
@@ -503,6 +492,20 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
     }
     const uint32_t lp = (!FIXED && d.split) ? split_log_parts(count) : 0;
     const uint64_t nitems = count << lp;
+    /* blocks without work (empty or small classes) leave before the LDS fill */
+    if ((uint64_t)blockIdx.x * WAVES * (64 / G) >= nitems)
+        return;
+    fill_lds<G>(L, gtab);
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const int j = lane % G;
+    const uint32_t c_lo = (uint32_t)(lane & 31) << 2;
+    const uint32_t c_hi = c_lo | 0x10000u;
+    uint64_t team = ((uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6)) * (64 / G) + lane / G;
+    if (G == 64)
+        team = uni64(team); /* whole-wave team: keep record state in SGPRs */
+    const uint64_t nteams = (uint64_t)gridDim.x * WAVES * (64 / G);
     Meta pre;
     pre.idx = ~0ull;
 
@@ -647,11 +650,6 @@ template <bool FIXED, int PF>
 __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
 {
     __shared__ __attribute__((aligned(16))) char L[OFF_U];
-    fill_lds<1>(L, gtab);
-    __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const uint32_t c_lo = (uint32_t)(lane & 31) << 2;
-    const uint32_t c_hi = c_lo | 0x10000u;
     uint64_t count = d.n;
     const RecDesc *list = nullptr;
     if (!FIXED) {
@@ -661,6 +659,13 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
         count = __builtin_amdgcn_readfirstlane(((g32p)d.class_count)[d.klass]);
         list = d.desc + base;
     }
+    if ((uint64_t)blockIdx.x * WG >= count)
+        return;
+    fill_lds<1>(L, gtab);
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const uint32_t c_lo = (uint32_t)(lane & 31) << 2;
+    const uint32_t c_hi = c_lo | 0x10000u;
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(gtab);
     const uintptr_t lo = reinterpret_cast<uintptr_t>(d.base) & ~uintptr_t(3);
     const uint64_t nthr = (uint64_t)gridDim.x * WG;
