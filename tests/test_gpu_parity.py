@@ -42,7 +42,8 @@ def teams(request, gpu):
     lib().zscrc_set_teams(1024, 1 << 20)
 
 
-@pytest.fixture(params=[-1, 1, 2, 3, 4], ids=["g1-auto", "g1-ring1", "g1-ring2", "g1-short", "g1-short-pf"])
+@pytest.fixture(params=[-1, 1, 2, 3, 4, 5],
+                ids=["g1-auto", "g1-ring1", "g1-ring2", "g1-short", "g1-short-pf", "g1-short-pf2"])
 def g1_walk(request, gpu):
     lib().zscrc_set_prefetch(1, request.param)
     yield request.param

@@ -644,7 +644,8 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
  * overhead is a handful of scalar/vector ops.  (tools/short_probe: this
  * shape reads at the streaming ceiling on 64 B and 320 B records.)
  * PF: 0 = next piece loaded only if it exists; 1 = always four loads (a
- * dummy address past the record) so the wait counts stay static.
+ * dummy address past the record) so the wait counts stay static; 2 = two
+ * pieces ahead (loaded only if they exist).
  */
 template <bool FIXED, int PF>
 __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
@@ -706,10 +707,12 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
         const uintptr_t E = (A + len) & ~uintptr_t(3);
         const uint64_t np = (E - A + 63) >> 6;
         const uintptr_t V0 = E - np * 64;
-        uint32_t w[16], nx[16];
+        uint32_t w[16], nx[16], nx2[16];
         issue_plain(V0 < lo ? dummy : V0, w);
         if (PF == 1 || np > 1)
             issue_plain(np > 1 ? V0 + 64 : dummy, nx);
+        if (PF == 2 && np > 2)
+            issue_plain(V0 + 128, nx2);
         uint32_t r;
         if (V0 < lo) {
             /* record within 64 B of the buffer start: its first piece byte-wise */
@@ -761,7 +764,13 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
 #pragma unroll
             for (int q = 0; q < 16; ++q)
                 w[q] = nx[q];
-            if (PF == 1)
+            if (PF == 2) {
+#pragma unroll
+                for (int q = 0; q < 16; ++q)
+                    nx[q] = nx2[q];
+                if (k + 2 < np)
+                    issue_plain(V0 + 64 * (k + 2), nx2);
+            } else if (PF == 1)
                 issue_plain(k + 1 < np ? V0 + 64 * (k + 1) : dummy, nx);
             else if (k + 1 < np)
                 issue_plain(V0 + 64 * (k + 1), nx);
@@ -1062,14 +1071,23 @@ extern "C" int zs_launch_team(int g, int fixed, int depth, const zs::BatchDesc *
 extern "C" int zs_launch_short(int fixed, int pf, const zs::BatchDesc *d, const uint32_t *gtab, int grid,
                                hipStream_t stream)
 {
-    if (fixed && pf)
-        hipLaunchKernelGGL((zs::short_kernel<true, 1>), dim3(grid), dim3(zs::WG), 0, stream, *d, gtab);
-    else if (fixed)
-        hipLaunchKernelGGL((zs::short_kernel<true, 0>), dim3(grid), dim3(zs::WG), 0, stream, *d, gtab);
-    else if (pf)
-        hipLaunchKernelGGL((zs::short_kernel<false, 1>), dim3(grid), dim3(zs::WG), 0, stream, *d, gtab);
-    else
-        hipLaunchKernelGGL((zs::short_kernel<false, 0>), dim3(grid), dim3(zs::WG), 0, stream, *d, gtab);
+#define ZS_SHORT(F, P) hipLaunchKernelGGL((zs::short_kernel<F, P>), dim3(grid), dim3(zs::WG), 0, stream, *d, gtab)
+    if (fixed) {
+        if (pf == 2)
+            ZS_SHORT(true, 2);
+        else if (pf == 1)
+            ZS_SHORT(true, 1);
+        else
+            ZS_SHORT(true, 0);
+    } else {
+        if (pf == 2)
+            ZS_SHORT(false, 2);
+        else if (pf == 1)
+            ZS_SHORT(false, 1);
+        else
+            ZS_SHORT(false, 0);
+    }
+#undef ZS_SHORT
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
