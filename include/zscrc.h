@@ -115,8 +115,9 @@ void zscrc_set_gpu_min(uint64_t min_bytes);
 void zscrc_set_teams(uint64_t g1_max, uint64_t g16_max);
 /* tuning: record walk for team size g (1, 16 or 64): -1 = automatic (default),
  * 0 = two-level loop, 1 / 2 = flattened (record, step) loop with a 1- / 2-item
- * register ring; g = 1 only: 3 / 4 / 5 = per-lane short-record kernel (next
- * piece loaded when it exists / always / two pieces ahead) */
+ * register ring; g = 1 only: 3..8 = per-lane short-record kernel (next
+ * piece loaded when it exists / always / two pieces ahead / bursts of 2, 3,
+ * 4 pieces) */
 void zscrc_set_prefetch(int g, int depth);
 /* team size the fixed-stride path picks for n records of len bytes (1/16/64;
  * 0 if no device) */

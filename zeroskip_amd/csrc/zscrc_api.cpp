@@ -50,8 +50,8 @@ std::atomic<uint64_t> g_g16_max{1u << 20};
 int g_strict = 0;
 /* record-walk override per team size (index 0/1/2 = G 1/16/64): -1 = automatic
  * (walk_for), 0 = two-level loop, 1/2 = flattened loop with a 1/2-item ring;
- * G = 1 only: 3 / 4 / 5 = short_kernel (per-lane records; next piece loaded
- * if it exists / always four loads / two pieces ahead) */
+ * G = 1 only: 3..8 = short_kernel (per-lane records; next piece loaded if it
+ * exists / always four loads / two pieces ahead / bursts of 2, 3, 4 pieces) */
 std::atomic<int> g_depth[3] = {{-1}, {-1}, {-1}};
 
 struct DevCtx {
@@ -638,7 +638,7 @@ void zscrc_set_gpu_min(uint64_t min_bytes)
 
 void zscrc_set_prefetch(int g, int depth)
 {
-    if (depth < -1 || depth > (g == 1 ? 5 : 2))
+    if (depth < -1 || depth > (g == 1 ? 8 : 2))
         return;
     if (g == 1)
         g_depth[0] = depth;

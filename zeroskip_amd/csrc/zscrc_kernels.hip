@@ -645,8 +645,63 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
  * shape reads at the streaming ceiling on 64 B and 320 B records.)
  * PF: 0 = next piece loaded only if it exists; 1 = always four loads (a
  * dummy address past the record) so the wait counts stay static; 2 = two
- * pieces ahead (loaded only if they exist).
+ * pieces ahead (loaded only if they exist); 3 / 4 / 5 = bursts: the loads of
+ * 2 / 3 / 4 pieces issued together, then hashed.
  */
+/* Register after the first 64-byte piece of a record whose piece grid starts
+ * at V0 <= A: bytes before A are zero, the initial register enters at A.
+ * A piece below the buffer's first aligned dword (V0 < lo) is hashed
+ * byte-wise from A instead (its loads went to a dummy address). */
+__device__ __forceinline__ uint32_t first_piece(const char *L, const Item &it, uintptr_t V0, uintptr_t lo,
+                                                uint32_t (&w)[16], uint32_t c_lo, uint32_t c_hi)
+{
+    const uintptr_t A = it.A;
+    uint32_t r;
+    if (V0 < lo) {
+        r = it.R0;
+        for (uintptr_t b = A; b < V0 + 64; ++b)
+            r = byte_step(L, r, ((g8p)b)[0], c_hi);
+        return r;
+    }
+    const int32_t d0 = (int32_t)(A - V0); /* front padding, 0..63 */
+    const int32_t d0u = __builtin_amdgcn_readfirstlane(d0);
+    if (__ballot(d0 != d0u || (A & 3) != 0) == 0) {
+        /* every record of the wave starts at the same 4-aligned word f of its
+         * first piece (fixed-stride batches, zsbench spans): skip the zero
+         * prefix with scalar branches, R0 enters at f */
+        const int32_t f = d0u >> 2;
+        r = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (k >= f)
+                r = m4(L, r ^ w[k] ^ (k == f ? it.R0 : 0u), c_lo, c_hi);
+        return r;
+    }
+    if ((A & 3) == 0) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int32_t dk = d0 - 4 * k;
+            w[k] = dk > 0 ? 0u : (dk == 0 ? w[k] ^ it.R0 : w[k]);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int32_t dk = d0 - 4 * k;
+            uint32_t v = w[k];
+            if (dk >= 4)
+                v = 0;
+            else if (dk > 0)
+                v &= 0xffffffffu << (8 * dk);
+            if (dk >= 0 && dk < 4)
+                v ^= it.R0 << (8 * dk);
+            else if (dk < 0 && dk > -4)
+                v ^= it.R0 >> (8 * -dk);
+            w[k] = v;
+        }
+    }
+    return piece<false>(L, 0u, w, c_lo, c_hi);
+}
+
 template <bool FIXED, int PF>
 __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
 {
@@ -707,59 +762,42 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
         const uintptr_t E = (A + len) & ~uintptr_t(3);
         const uint64_t np = (E - A + 63) >> 6;
         const uintptr_t V0 = E - np * 64;
+        /* R0 bytes that spill past the first piece (front padding > 60) */
+        const uint32_t spill = (V0 >= lo && A + 4 > V0 + 64) ? it.R0 >> (8 * (uint32_t)(V0 + 64 - A)) : 0u;
+        uint32_t r = 0;
+        if (PF >= 3) {
+            /* bursts of up to NPC pieces: all loads of a burst in flight
+             * before the first word is hashed */
+            constexpr int NPC = PF - 1; /* PF 3/4/5: bursts of 2/3/4 pieces */
+            /* every burst issues exactly NPC x 4 loads (static wait counts, no
+             * loads under branches); pieces past the record re-read its first
+             * piece, which is in the cache */
+            const uintptr_t P0 = V0 < lo ? dummy : V0;
+#pragma nounroll
+            for (uint64_t base = 0; base < np; base += NPC) {
+                uint32_t buf[NPC][16];
+#pragma unroll
+                for (int p = 0; p < NPC; ++p)
+                    issue_plain(base + p == 0 ? P0 : (base + p < np ? V0 + 64 * (base + p) : P0), buf[p]);
+                int p0 = 0;
+                if (base == 0) {
+                    r = first_piece(L, it, V0, lo, buf[0], c_lo, c_hi);
+                    buf[1][0] ^= spill;
+                    p0 = 1;
+                }
+#pragma unroll
+                for (int p = 0; p < NPC; ++p)
+                    if (p >= p0 && base + p < np)
+                        r = piece<false>(L, r, buf[p], c_lo, c_hi);
+            }
+        } else {
         uint32_t w[16], nx[16], nx2[16];
         issue_plain(V0 < lo ? dummy : V0, w);
         if (PF == 1 || np > 1)
             issue_plain(np > 1 ? V0 + 64 : dummy, nx);
         if (PF == 2 && np > 2)
             issue_plain(V0 + 128, nx2);
-        uint32_t r;
-        if (V0 < lo) {
-            /* record within 64 B of the buffer start: its first piece byte-wise */
-            r = it.R0;
-            for (uintptr_t b = A; b < V0 + 64; ++b)
-                r = byte_step(L, r, ((g8p)b)[0], c_hi);
-        } else {
-            const int32_t d0 = (int32_t)(A - V0); /* front padding, 0..63 */
-            const int32_t d0u = __builtin_amdgcn_readfirstlane(d0);
-            if (__ballot(d0 != d0u || (A & 3) != 0) == 0) {
-                /* every record of the wave starts at the same 4-aligned word f
-                 * of its first piece (fixed-stride batches, zsbench spans):
-                 * skip the zero prefix with scalar branches, R0 enters at f */
-                const int32_t f = d0u >> 2;
-                r = 0;
-#pragma unroll
-                for (int k = 0; k < 16; ++k)
-                    if (k >= f)
-                        r = m4(L, r ^ w[k] ^ (k == f ? it.R0 : 0u), c_lo, c_hi);
-            } else {
-            if ((A & 3) == 0) {
-#pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                    const int32_t dk = d0 - 4 * k;
-                    w[k] = dk > 0 ? 0u : (dk == 0 ? w[k] ^ it.R0 : w[k]);
-                }
-            } else {
-#pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                    const int32_t dk = d0 - 4 * k;
-                    uint32_t v = w[k];
-                    if (dk >= 4)
-                        v = 0;
-                    else if (dk > 0)
-                        v &= 0xffffffffu << (8 * dk);
-                    if (dk >= 0 && dk < 4)
-                        v ^= it.R0 << (8 * dk);
-                    else if (dk < 0 && dk > -4)
-                        v ^= it.R0 >> (8 * -dk);
-                    w[k] = v;
-                }
-            }
-            r = piece<false>(L, 0u, w, c_lo, c_hi);
-            }
-        }
-        /* R0 bytes that spill past the first piece (front padding > 60) */
-        const uint32_t spill = (V0 >= lo && A + 4 > V0 + 64) ? it.R0 >> (8 * (uint32_t)(V0 + 64 - A)) : 0u;
+        r = first_piece(L, it, V0, lo, w, c_lo, c_hi);
         for (uint64_t k = 1; k < np; ++k) {
 #pragma unroll
             for (int q = 0; q < 16; ++q)
@@ -777,6 +815,7 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
             if (k == 1)
                 w[0] ^= spill;
             r = piece<false>(L, r, w, c_lo, c_hi);
+        }
         }
         const g8p t = (g8p)E;
         const uint32_t tail = (uint32_t)((A + len) - E);
@@ -1072,21 +1111,21 @@ extern "C" int zs_launch_short(int fixed, int pf, const zs::BatchDesc *d, const 
                                hipStream_t stream)
 {
 #define ZS_SHORT(F, P) hipLaunchKernelGGL((zs::short_kernel<F, P>), dim3(grid), dim3(zs::WG), 0, stream, *d, gtab)
-    if (fixed) {
-        if (pf == 2)
-            ZS_SHORT(true, 2);
-        else if (pf == 1)
-            ZS_SHORT(true, 1);
-        else
-            ZS_SHORT(true, 0);
-    } else {
-        if (pf == 2)
-            ZS_SHORT(false, 2);
-        else if (pf == 1)
-            ZS_SHORT(false, 1);
-        else
-            ZS_SHORT(false, 0);
+#define ZS_SHORT_PF(F)     \
+    switch (pf) {          \
+    case 0: ZS_SHORT(F, 0); break; \
+    case 1: ZS_SHORT(F, 1); break; \
+    case 2: ZS_SHORT(F, 2); break; \
+    case 3: ZS_SHORT(F, 3); break; \
+    case 4: ZS_SHORT(F, 4); break; \
+    default: ZS_SHORT(F, 5); break; \
     }
+    if (fixed) {
+        ZS_SHORT_PF(true);
+    } else {
+        ZS_SHORT_PF(false);
+    }
+#undef ZS_SHORT_PF
 #undef ZS_SHORT
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
