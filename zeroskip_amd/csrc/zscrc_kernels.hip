@@ -768,7 +768,7 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
         if (PF >= 3) {
             /* bursts of up to NPC pieces: all loads of a burst in flight
              * before the first word is hashed */
-            constexpr int NPC = PF - 1; /* PF 3/4/5: bursts of 2/3/4 pieces */
+            constexpr int NPC = PF >= 3 ? PF - 1 : 2; /* PF 3/4/5: bursts of 2/3/4 pieces */
             /* every burst issues exactly NPC x 4 loads (static wait counts, no
              * loads under branches); pieces past the record re-read its first
              * piece, which is in the cache */
