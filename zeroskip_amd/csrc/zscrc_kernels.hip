@@ -643,9 +643,9 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
  * team_kernel<1>, without the generic (record, step) cursor: the per-record
  * overhead is a handful of scalar/vector ops.  (tools/short_probe: this
  * shape reads at the streaming ceiling on 64 B and 320 B records.)
- * PF: 0 = next piece loaded only if it exists; 1 = always four loads (a
- * dummy address past the record) so the wait counts stay static; 2 = two
- * pieces ahead (loaded only if they exist); 3 / 4 / 5 = bursts: the loads of
+ * PF: 0 = next piece loaded only if it exists; 1 = always four loads (past
+ * the record: the record's own first piece again) so the wait counts stay
+ * static; 2 = the same two pieces ahead; 3 / 4 / 5 = bursts: the loads of
  * 2 / 3 / 4 pieces issued together, then hashed.
  */
 /* Register after the first 64-byte piece of a record whose piece grid starts
@@ -765,6 +765,7 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
         /* R0 bytes that spill past the first piece (front padding > 60) */
         const uint32_t spill = (V0 >= lo && A + 4 > V0 + 64) ? it.R0 >> (8 * (uint32_t)(V0 + 64 - A)) : 0u;
         uint32_t r = 0;
+        const uintptr_t P0 = V0 < lo ? dummy : V0;
         if (PF >= 3) {
             /* bursts of up to NPC pieces: all loads of a burst in flight
              * before the first word is hashed */
@@ -772,7 +773,6 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
             /* every burst issues exactly NPC x 4 loads (static wait counts, no
              * loads under branches); pieces past the record re-read its first
              * piece, which is in the cache */
-            const uintptr_t P0 = V0 < lo ? dummy : V0;
 #pragma nounroll
             for (uint64_t base = 0; base < np; base += NPC) {
                 uint32_t buf[NPC][16];
@@ -792,11 +792,22 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
             }
         } else {
         uint32_t w[16], nx[16], nx2[16];
-        issue_plain(V0 < lo ? dummy : V0, w);
-        if (PF == 1 || np > 1)
-            issue_plain(np > 1 ? V0 + 64 : dummy, nx);
-        if (PF == 2 && np > 2)
-            issue_plain(V0 + 128, nx2);
+        /* PF 1/2 issue a fixed number of loads per piece (static wait
+         * counts); past the record they re-read its first piece (cached) */
+        /* sched_barrier: keep the issue order (piece 0 first) -- the wait
+         * counter is in-order, and hipcc otherwise issues piece 0 last, so
+         * hashing it would wait for every piece in flight */
+        issue_plain(P0, w);
+        __builtin_amdgcn_sched_barrier(0);
+        if (PF == 0) {
+            if (np > 1)
+                issue_plain(V0 + 64, nx);
+        } else {
+            issue_plain(np > 1 ? V0 + 64 : P0, nx);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (PF == 2)
+            issue_plain(np > 2 ? V0 + 128 : P0, nx2);
         r = first_piece(L, it, V0, lo, w, c_lo, c_hi);
         for (uint64_t k = 1; k < np; ++k) {
 #pragma unroll
@@ -806,12 +817,13 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
 #pragma unroll
                 for (int q = 0; q < 16; ++q)
                     nx[q] = nx2[q];
-                if (k + 2 < np)
-                    issue_plain(V0 + 64 * (k + 2), nx2);
-            } else if (PF == 1)
-                issue_plain(k + 1 < np ? V0 + 64 * (k + 1) : dummy, nx);
-            else if (k + 1 < np)
+                issue_plain(k + 2 < np ? V0 + 64 * (k + 2) : P0, nx2);
+            } else if (PF == 1) {
+                issue_plain(k + 1 < np ? V0 + 64 * (k + 1) : P0, nx);
+            } else if (k + 1 < np) {
                 issue_plain(V0 + 64 * (k + 1), nx);
+            }
+            __builtin_amdgcn_sched_barrier(0);
             if (k == 1)
                 w[0] ^= spill;
             r = piece<false>(L, r, w, c_lo, c_hi);
