@@ -646,7 +646,8 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
  * PF: 0 = next piece loaded only if it exists; 1 = always four loads (past
  * the record: the record's own first piece again) so the wait counts stay
  * static; 2 = the same two pieces ahead; 3 / 4 / 5 = bursts: the loads of
- * 2 / 3 / 4 pieces issued together, then hashed.
+ * 3 / 4 / 5 pieces issued together (buffer loads, zero-cost past the
+ * record), then hashed.
  */
 /* Register after the first 64-byte piece of a record whose piece grid starts
  * at V0 <= A: bytes before A are zero, the initial register enters at A.
@@ -766,29 +767,59 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
         const uint32_t spill = (V0 >= lo && A + 4 > V0 + 64) ? it.R0 >> (8 * (uint32_t)(V0 + 64 - A)) : 0u;
         uint32_t r = 0;
         const uintptr_t P0 = V0 < lo ? dummy : V0;
+        constexpr uint32_t OOB = 0x80000000u, RANGE = 0x7ffffff0u;
+        uintptr_t W = 0;
+        __amdgpu_buffer_rsrc_t rsrc;
+        bool inwin = true;
         if (PF >= 3) {
-            /* bursts of up to NPC pieces: all loads of a burst in flight
-             * before the first word is hashed */
-            constexpr int NPC = PF >= 3 ? PF - 1 : 2; /* PF 3/4/5: bursts of 2/3/4 pieces */
-            /* every burst issues exactly NPC x 4 loads (static wait counts, no
-             * loads under branches); pieces past the record re-read its first
-             * piece, which is in the cache */
+            const uintptr_t first = __builtin_amdgcn_readfirstlane((uint32_t)V0) |
+                                    ((uintptr_t)__builtin_amdgcn_readfirstlane((uint32_t)(V0 >> 32)) << 32);
+            W = first >= (1ull << 30) ? first - (1ull << 30) : 0;
+            rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)W, (short)0, (int)RANGE, 0x00020000);
+            inwin = V0 >= W && V0 + 64 * np - W < RANGE;
+        }
+        const bool simple = (A & 3) == 0 && V0 >= lo && inwin;
+        if (PF >= 3 && __ballot(!simple) == 0) {
+            /* bursts of NPB pieces, all their loads in flight before the first
+             * word is hashed.  Buffer loads against a per-wave resource: a
+             * piece past the record gets an out-of-range offset, which loads
+             * zeros without a memory request, so every burst is exactly
+             * NPB x 4 loads (static wait counts) at no extra traffic.  Only
+             * for waves whose records are 4-aligned and inside a 2 GiB window
+             * (everything else takes the PF 0 walk below). */
+            constexpr int NPB = PF >= 3 ? PF : 3;
+            const int32_t d0 = (int32_t)(A - V0); /* front padding, 0..60 */
 #pragma nounroll
-            for (uint64_t base = 0; base < np; base += NPC) {
-                uint32_t buf[NPC][16];
+            for (uint64_t base = 0; base < np; base += NPB) {
+                uint32_t buf[NPB][16];
 #pragma unroll
-                for (int p = 0; p < NPC; ++p)
-                    issue_plain(base + p == 0 ? P0 : (base + p < np ? V0 + 64 * (base + p) : P0), buf[p]);
-                int p0 = 0;
-                if (base == 0) {
-                    r = first_piece(L, it, V0, lo, buf[0], c_lo, c_hi);
-                    buf[1][0] ^= spill;
-                    p0 = 1;
+                for (int p = 0; p < NPB; ++p) {
+                    const uint32_t o = base + p < np ? (uint32_t)(V0 + 64 * (base + p) - W) : OOB;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const u32x4 v = __builtin_bit_cast(
+                            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, o + 16 * q, 0, 0));
+                        buf[p][4 * q + 0] = v.x;
+                        buf[p][4 * q + 1] = v.y;
+                        buf[p][4 * q + 2] = v.z;
+                        buf[p][4 * q + 3] = v.w;
+                    }
                 }
 #pragma unroll
-                for (int p = 0; p < NPC; ++p)
-                    if (p >= p0 && base + p < np)
-                        r = piece<false>(L, r, buf[p], c_lo, c_hi);
+                for (int p = 0; p < NPB; ++p) {
+                    if (base + p < np) {
+                        if (base == 0 && p == 0) {
+#pragma unroll
+                            for (int k = 0; k < 16; ++k) {
+                                const int32_t dk = d0 - 4 * k;
+                                const uint32_t x = dk > 0 ? 0u : (dk == 0 ? buf[0][k] ^ it.R0 : buf[0][k]);
+                                r = m4(L, r ^ x, c_lo, c_hi);
+                            }
+                        } else {
+                            r = piece<false>(L, r, buf[p], c_lo, c_hi);
+                        }
+                    }
+                }
             }
         } else {
         uint32_t w[16], nx[16], nx2[16];
