@@ -726,6 +726,13 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(gtab);
     const uintptr_t lo = reinterpret_cast<uintptr_t>(d.base) & ~uintptr_t(3);
     const uint64_t nthr = (uint64_t)gridDim.x * WG;
+    /* The result store of a record is issued after the NEXT record's first
+     * loads: on gfx9 stores share the in-order vmcnt counter with loads, so a
+     * store issued before them would make the first wait of every record
+     * include a write round trip. */
+    Item pend;
+    uint32_t pend_r = 0;
+    bool have = false;
     for (uint64_t i = (uint64_t)blockIdx.x * WG + threadIdx.x; i < count; i += nthr) {
         Item it;
         uint64_t off, len;
@@ -754,6 +761,9 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
             it.c1 = ((g32p)(A + len))[1];
         }
         if (len < 8) {
+            if (have)
+                emit(d, pend, pend_r, L, c_lo, c_hi);
+            have = false;
             uint32_t r = it.R0;
             for (uint64_t k = 0; k < len; ++k)
                 r = byte_step(L, r, ((g8p)A)[k], c_hi);
@@ -805,6 +815,9 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
                         buf[p][4 * q + 3] = v.w;
                     }
                 }
+                if (have)
+                    emit(d, pend, pend_r, L, c_lo, c_hi);
+                have = false;
 #pragma unroll
                 for (int p = 0; p < NPB; ++p) {
                     if (base + p < np) {
@@ -839,6 +852,9 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
         __builtin_amdgcn_sched_barrier(0);
         if (PF == 2)
             issue_plain(np > 2 ? V0 + 128 : P0, nx2);
+        if (have)
+            emit(d, pend, pend_r, L, c_lo, c_hi);
+        have = false;
         r = first_piece(L, it, V0, lo, w, c_lo, c_hi);
         for (uint64_t k = 1; k < np; ++k) {
 #pragma unroll
@@ -864,8 +880,12 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
         const uint32_t tail = (uint32_t)((A + len) - E);
         for (uint32_t k = 0; k < tail; ++k)
             r = byte_step(L, r, t[k], c_hi);
-        emit(d, it, r, L, c_lo, c_hi);
+        pend = it;
+        pend_r = r;
+        have = true;
     }
+    if (have)
+        emit(d, pend, pend_r, L, c_lo, c_hi);
 }
 
 /* ------------------------------------------------------------ span fold */
