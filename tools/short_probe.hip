@@ -25,7 +25,18 @@ __device__ __forceinline__ unsigned m4(const char *L, unsigned x, unsigned c_lo,
     return lds32(L, a0) ^ lds32(L, a1 + 128) ^ lds32(L, a2) ^ lds32(L, a3 + 128);
 }
 
-template <int RSTRIDE, int RLEN, int MODE>  // MODE 0 read, 1 crc, 2 crc2
+__global__ void fill_random(unsigned *p, size_t n)
+{
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        unsigned long long x = (i + 1) * 0x9E3779B97F4A7C15ull;
+        x ^= x >> 29;
+        x *= 0xBF58476D1CE4E5B9ull;
+        x ^= x >> 32;
+        p[i] = (unsigned)x;
+    }
+}
+
+template <int RSTRIDE, int RLEN, int MODE>  // MODE 0 read, 1 crc, 2 crc2, 3 crc + store per record
 __global__ __launch_bounds__(1024) void rec(const char *buf, size_t nrec, unsigned *out)
 {
     __shared__ __attribute__((aligned(16))) char L[MODE ? 131072 : 16];
@@ -43,7 +54,7 @@ __global__ __launch_bounds__(1024) void rec(const char *buf, size_t nrec, unsign
     const size_t t = (size_t)blockIdx.x * 1024 + threadIdx.x;
     constexpr int NP = RLEN / 64;
     unsigned acc = 0;
-    if (MODE < 2) {
+    if (MODE < 2 || MODE == 3) {
         for (size_t r = t; r < nrec; r += nthr) {
             const char *p = buf + r * RSTRIDE;
             unsigned reg = 0;
@@ -65,7 +76,10 @@ __global__ __launch_bounds__(1024) void rec(const char *buf, size_t nrec, unsign
                     }
                 }
             }
-            acc ^= reg;
+            if (MODE == 3)
+                out[16 + r] = reg;
+            else
+                acc ^= reg;
         }
     } else {
         for (size_t r = 2 * t; r < nrec; r += 2 * nthr) {
@@ -123,7 +137,7 @@ void run(const char *d, size_t total, unsigned *o, int cu)
         std::sort(t.begin(), t.end());
         const double ms = t[t.size() / 2];
         printf("{\"stride\": %d, \"len\": %d, \"mode\": \"%s\", \"grid\": %d, \"ms\": %.4f, \"GBs\": %.1f}\n", RS, RL,
-               MODE == 0 ? "read" : MODE == 1 ? "crc" : "crc2", grid, ms, nrec * (double)RL / ms / 1e6);
+               MODE == 0 ? "read" : MODE == 1 ? "crc" : MODE == 2 ? "crc2" : "crc+store", grid, ms, nrec * (double)RL / ms / 1e6);
         fflush(stdout);
     }
 }
@@ -133,14 +147,22 @@ int main()
     size_t n = (size_t)4 << 30;
     char *d;
     unsigned *o;
-    if (hipMalloc(&d, n) != hipSuccess || hipMalloc(&o, 64) != hipSuccess) {
+    if (hipMalloc(&d, n) != hipSuccess || hipMalloc(&o, (64 << 20) * 4) != hipSuccess) {
         printf("alloc failed\n");
         return 1;
     }
-    hipMemset(d, 1, n);
-    hipDeviceSynchronize();
     int cu = 0;
     hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, 0);
+    hipMemset(d, 1, n);
+    hipDeviceSynchronize();
+    printf("{\"data\": \"memset 1\"}\n");
+    run<320, 320, 1>(d, n, o, cu);
+    hipLaunchKernelGGL(fill_random, dim3(4096), dim3(256), 0, 0, (unsigned *)d, n / 4);
+    hipDeviceSynchronize();
+    printf("{\"data\": \"random\"}\n");
+    run<320, 320, 1>(d, n, o, cu);
+    run<320, 320, 3>(d, n, o, cu);
+    return 0;
     run<64, 64, 0>(d, n, o, cu);
     run<64, 64, 1>(d, n, o, cu);
     run<64, 64, 2>(d, n, o, cu);

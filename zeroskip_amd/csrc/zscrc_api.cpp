@@ -31,6 +31,7 @@ int zs_launch_team(int g, int fixed, int depth, const zs::BatchDesc *d, const ui
                    hipStream_t stream);
 int zs_launch_span_fold(const zs::SpanFold *f, hipStream_t stream);
 int zs_launch_short(int fixed, int pf, const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
+int zs_launch_tiny(int fixed, const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
 int zs_launch_stream_read(const void *buf, uint64_t n, uint32_t *out, int grid, hipStream_t stream);
 int zs_launch_classify(const zs::Classify *c, hipStream_t stream);
 int zs_launch_part_fold(const zs::BatchDesc *d, const uint32_t *gtab, hipStream_t stream);
@@ -223,7 +224,13 @@ int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s, int depth_hi
         depth = 2;
     if (!fixed && depth == 2)
         depth = 1;
-    int rc = depth >= 3 ? zs_launch_short(fixed, depth - 3, &d, c->gtab, c->ncu, s)
+    zs::BatchDesc dx = d;
+    if (depth == 9) { /* experiment: short kernel without result stores */
+        dx.split = 0xDEADu;
+        depth = 3;
+    }
+    int rc = depth == 10 ? zs_launch_tiny(fixed, &dx, c->gtab, c->ncu, s)
+             : depth >= 3 ? zs_launch_short(fixed, depth - 3, &dx, c->gtab, c->ncu, s)
                         : zs_launch_team(g, fixed, depth, &d, c->gtab, c->ncu, s);
     if (rc) {
         set_err("team kernel launch", hipGetLastError());
@@ -638,7 +645,7 @@ void zscrc_set_gpu_min(uint64_t min_bytes)
 
 void zscrc_set_prefetch(int g, int depth)
 {
-    if (depth < -1 || depth > (g == 1 ? 8 : 2))
+    if (depth < -1 || depth > (g == 1 ? 10 : 2))
         return;
     if (g == 1)
         g_depth[0] = depth;
