@@ -180,6 +180,15 @@ int zscrc_zs_dotzsdb_crc(const void *image, uint64_t size, uint32_t *stored, uin
 int zscrc_device_verify_commits(const void *d_image, const uint64_t *d_span_off, const uint64_t *d_span_len,
                                 size_t n, uint32_t *d_crc, uint32_t *d_status, void *stream);
 
+/* Device: as zscrc_device_verify_commits, but span i's CRC continues from
+ * d_seed[i] (a crc32c value, crc32c(d_seed[i], span) chaining) instead of
+ * crc32c(0, 0, 0) = 0.  Resolves the reference's zero-length finalise commit
+ * (zeroskip-file.c:253-350 after crc32_end without crc32_begin, mfile.c:534-546):
+ * its stored CRC continues from the previous span's CRC.  d_seed NULL = 0. */
+int zscrc_device_verify_commits_seeded(const void *d_image, const uint64_t *d_span_off,
+                                       const uint64_t *d_span_len, const uint32_t *d_seed, size_t n,
+                                       uint32_t *d_crc, uint32_t *d_status, void *stream);
+
 /* Device: compute n commit CRCs (the writer's side, zeroskip-file.c:253-350)
  * and store each one big-endian into its commit record; d_crc[i] receives it. */
 int zscrc_device_write_commits(void *d_image, const uint64_t *d_span_off, const uint64_t *d_span_len, size_t n,

@@ -184,19 +184,22 @@ def packed_file(records, uuid: bytes, startidx: int, endidx: int) -> bytes:
 
 
 # ------------------------------------------------------------------ verify
-def _commit_check(img, off: int):
+def _commit_check(img, off: int, seed: int = 0):
     """Decode the commit record at `off`; return (span_off, span_len, rec_len,
-    stored, computed) with the writer's trailer semantics."""
+    stored, computed) with the writer's trailer semantics.  `seed`: the CRC
+    the span continues from (crc32_begin stores crc32c(0,0,0) = 0,
+    mfile.c:526-532; a finalise without crc32_begin continues from the
+    previous span's CRC, mfile.c:534-546)."""
     w0, = struct.unpack_from(">Q", img, off)
     t = w0 >> 56
     if t in (REC_COMMIT, REC_FINAL):
         n = (w0 >> 32) & 0xFFFFFF
-        c = oracle.crc32c_hw(0, bytes(img[off - n:off]))
+        c = oracle.crc32c_hw(seed, bytes(img[off - n:off]))
         c = oracle.crc32c_hw(c, le64(w0 & 0xFFFFFFFF00000000))
         return off - n, n, 8, w0 & 0xFFFFFFFF, c
     if t in (REC_LONG_COMMIT, REC_LONG_FINAL):
         n, w2 = struct.unpack_from(">QQ", img, off + 8)
-        c = oracle.crc32c_hw(0, bytes(img[off - n:off]))
+        c = oracle.crc32c_hw(seed, bytes(img[off - n:off]))
         c = oracle.crc32c_hw(c, le64(w0))
         c = oracle.crc32c_hw(c, le64(n))
         c = oracle.crc32c_hw(c, le64(w2 & 0xFF00000000000000))

@@ -29,12 +29,13 @@ class OracleBackend:
     def empty(self, n):
         return torch.zeros(max(n, 1), dtype=torch.uint8)
 
-    def verify(self, buf, off, ln):
+    def verify(self, buf, off, ln, seed=None):
         img = buf.numpy()
         crc, st = [], []
-        for o, n in zip(off.tolist(), ln.tolist()):
+        seeds = [0] * len(off) if seed is None else [v & M32 for v in seed.tolist()]
+        for o, n, sd in zip(off.tolist(), ln.tolist(), seeds):
             try:
-                _, _, _, stored, computed = zf._commit_check(img, o + n)
+                _, _, _, stored, computed = zf._commit_check(img, o + n, sd)
                 crc.append(computed)
                 st.append(1 if stored == computed else 0)
             except ValueError:

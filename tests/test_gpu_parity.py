@@ -140,6 +140,22 @@ def test_variable_random_batch(gpu, teams):
     assert bad.size == 0, [(int(i), int(offs[i]), int(lens[i])) for i in bad[:10]]
 
 
+@pytest.mark.parametrize("lens", [[(1 << 20) + 1], [3 * (1 << 20) + 13], [(64 << 20) + 5],
+                                  [(1 << 20) + 7, 100, (5 << 20) + 3, 8, (2 << 20)]],
+                         ids=["1MiB+1", "3MiB+13", "64MiB+5", "mixed"])
+def test_few_long_records_split(gpu, lens):
+    """A handful of long records: each is split into up to 8192 parts (every
+    CU busy) and the parts are folded per record by a block-parallel fold."""
+    lens = np.array(lens, np.int64)
+    offs = np.cumsum(np.concatenate([[3], lens[:-1] + 5])).astype(np.int64)
+    data = rand_bytes(int(offs[-1] + lens[-1]) + 8, 2024)
+    seeds = (np.arange(len(lens), dtype=np.uint32) * 0x9E3779B9).astype(np.uint32)
+    out = u32(zd.crc_batch(to_dev(data, gpu), to_dev(offs, gpu), to_dev(lens, gpu),
+                           to_dev(seeds.view(np.int32), gpu)))
+    ref = oracle.batch(data, offs.astype(np.uint64), lens.astype(np.uint64), seeds, impl="hw", threads=8)
+    assert np.array_equal(out, ref), (out, ref)
+
+
 def test_raw_registers(gpu):
     data = rand_bytes(64 * 4096, 5)
     reg_in = 0x0BADF00D

@@ -54,7 +54,7 @@ __global__ __launch_bounds__(1024) void rec(const char *buf, size_t nrec, unsign
     const size_t t = (size_t)blockIdx.x * 1024 + threadIdx.x;
     constexpr int NP = RLEN / 64;
     unsigned acc = 0;
-    if (MODE < 2 || MODE == 3) {
+    if (MODE < 2 || MODE == 3 || MODE == 5 || MODE >= 12) {
         for (size_t r = t; r < nrec; r += nthr) {
             const char *p = buf + r * RSTRIDE;
             unsigned reg = 0;
@@ -76,10 +76,124 @@ __global__ __launch_bounds__(1024) void rec(const char *buf, size_t nrec, unsign
                     }
                 }
             }
+            if (MODE == 13 && r == t + 5 * nthr)
+                out[16 + t] = reg;
+            if (MODE == 14 && ((r - t) / nthr) % 64 == 63)
+                out[16 + r] = reg;
+            if (MODE == 15 && ((r - t) / nthr) % 8 == 7)
+                out[16 + r] = reg;
             if (MODE == 3)
                 out[16 + r] = reg;
+            else if (MODE == 5)
+                __builtin_nontemporal_store(reg, out + 16 + r);
             else
                 acc ^= reg;
+        }
+    } else if (MODE == 4) {
+        /* deferred: the store of record r goes out after record r+nthr's loads */
+        size_t pr = ~(size_t)0;
+        unsigned preg = 0;
+        for (size_t r = t; r < nrec; r += nthr) {
+            const char *p = buf + r * RSTRIDE;
+            u32x4 v[NP][4];
+#pragma unroll
+            for (int pc = 0; pc < NP; ++pc)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    v[pc][i] = *(g4p)(p + pc * 64 + 16 * i);
+            __builtin_amdgcn_sched_barrier(0);
+            if (pr != ~(size_t)0)
+                out[16 + pr] = preg;
+            unsigned reg = 0;
+#pragma unroll
+            for (int pc = 0; pc < NP; ++pc)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    reg = m4(L, reg ^ v[pc][i].x, c_lo, c_hi);
+                    reg = m4(L, reg ^ v[pc][i].y, c_lo, c_hi);
+                    reg = m4(L, reg ^ v[pc][i].z, c_lo, c_hi);
+                    reg = m4(L, reg ^ v[pc][i].w, c_lo, c_hi);
+                }
+            pr = r;
+            preg = reg;
+        }
+        if (pr != ~(size_t)0)
+            out[16 + pr] = preg;
+    } else if (MODE == 7 || MODE == 8) {
+        /* wave-contiguous chunks: wave v owns records [v*CH, (v+1)*CH); each
+         * iteration = 64 consecutive records (lane = record).  Results are
+         * batched over 8 iterations: MODE 7 via a 2 KiB LDS slot per wave and
+         * two dwordx4 stores, MODE 8 as 8 dword stores from registers. */
+        __shared__ __attribute__((aligned(16))) unsigned R[16][512];
+        const size_t nw = (size_t)gridDim.x * 16;
+        const size_t wv = (size_t)blockIdx.x * 16 + (threadIdx.x >> 6);
+        const size_t CH = ((nrec + nw - 1) / nw + 511) & ~(size_t)511;
+        const size_t r0 = wv * CH, r1 = r0 + CH < nrec ? r0 + CH : nrec;
+        unsigned keep[8];
+        for (size_t rb = r0; rb < r1; rb += 512) {
+#pragma unroll 1
+            for (int it = 0; it < 8; ++it) {
+                const size_t r = rb + 64 * it + lane;
+                const char *p = buf + (r < r1 ? r : r0) * RSTRIDE;
+                unsigned reg = 0;
+#pragma unroll
+                for (int pc = 0; pc < NP; ++pc) {
+                    u32x4 v[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        v[i] = *(g4p)(p + pc * 64 + 16 * i);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        reg = m4(L, reg ^ v[i].x, c_lo, c_hi);
+                        reg = m4(L, reg ^ v[i].y, c_lo, c_hi);
+                        reg = m4(L, reg ^ v[i].z, c_lo, c_hi);
+                        reg = m4(L, reg ^ v[i].w, c_lo, c_hi);
+                    }
+                }
+                if (MODE == 7)
+                    R[threadIdx.x >> 6][64 * it + lane] = reg;
+                else
+                    keep[it & 7] = reg;
+            }
+            if (MODE == 7) {
+                const uint4 a = *(const uint4 *)&R[threadIdx.x >> 6][4 * lane];
+                const uint4 b = *(const uint4 *)&R[threadIdx.x >> 6][256 + 4 * lane];
+                if (rb + 512 <= r1) {
+                    *(uint4 *)(out + 16 + rb + 4 * lane) = a;
+                    *(uint4 *)(out + 16 + rb + 256 + 4 * lane) = b;
+                }
+            } else {
+#pragma unroll
+                for (int it = 0; it < 8; ++it)
+                    if (rb + 64 * it + lane < r1)
+                        out[16 + rb + 64 * it + lane] = keep[it];
+            }
+        }
+    } else if (MODE == 6) {
+        /* 4 consecutive records per lane, one 16-byte store */
+        for (size_t r0 = 4 * t; r0 + 3 < nrec; r0 += 4 * nthr) {
+            unsigned res[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const char *p = buf + (r0 + q) * RSTRIDE;
+                unsigned reg = 0;
+#pragma unroll
+                for (int pc = 0; pc < NP; ++pc) {
+                    u32x4 v[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        v[i] = *(g4p)(p + pc * 64 + 16 * i);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        reg = m4(L, reg ^ v[i].x, c_lo, c_hi);
+                        reg = m4(L, reg ^ v[i].y, c_lo, c_hi);
+                        reg = m4(L, reg ^ v[i].z, c_lo, c_hi);
+                        reg = m4(L, reg ^ v[i].w, c_lo, c_hi);
+                    }
+                }
+                res[q] = reg;
+            }
+            *(uint4 *)(out + 16 + r0) = make_uint4(res[0], res[1], res[2], res[3]);
         }
     } else {
         for (size_t r = 2 * t; r < nrec; r += 2 * nthr) {
@@ -109,7 +223,9 @@ __global__ __launch_bounds__(1024) void rec(const char *buf, size_t nrec, unsign
             acc ^= ra ^ rb;
         }
     }
-    if (acc == 0x12345678u)
+    if (MODE == 12)
+        out[16 + t] = acc;
+    else if (acc == 0x12345678u)
         out[0] = acc;
 }
 
@@ -120,7 +236,7 @@ void run(const char *d, size_t total, unsigned *o, int cu)
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    for (int mult : {1, 2}) {
+    for (int mult : {1}) {
         const int grid = cu * mult;
         for (int i = 0; i < 3; ++i)
             hipLaunchKernelGGL((rec<RS, RL, MODE>), dim3(grid), dim3(1024), 0, 0, d, nrec, o);
@@ -137,7 +253,7 @@ void run(const char *d, size_t total, unsigned *o, int cu)
         std::sort(t.begin(), t.end());
         const double ms = t[t.size() / 2];
         printf("{\"stride\": %d, \"len\": %d, \"mode\": \"%s\", \"grid\": %d, \"ms\": %.4f, \"GBs\": %.1f}\n", RS, RL,
-               MODE == 0 ? "read" : MODE == 1 ? "crc" : MODE == 2 ? "crc2" : "crc+store", grid, ms, nrec * (double)RL / ms / 1e6);
+               MODE == 0 ? "read" : MODE == 1 ? "crc" : MODE == 2 ? "crc2" : MODE == 3 ? "crc+store" : MODE == 4 ? "crc+deferred" : MODE == 5 ? "crc+ntstore" : MODE == 6 ? "crc4+x4store" : MODE == 7 ? "wavechunk+lds8" : MODE == 8 ? "wavechunk+reg8" : MODE == 12 ? "store at end" : MODE == 13 ? "one store mid-stream" : MODE == 14 ? "store 1/64 iters" : "store 1/8 iters", grid, ms, nrec * (double)RL / ms / 1e6);
         fflush(stdout);
     }
 }
@@ -147,7 +263,7 @@ int main()
     size_t n = (size_t)4 << 30;
     char *d;
     unsigned *o;
-    if (hipMalloc(&d, n) != hipSuccess || hipMalloc(&o, (64 << 20) * 4) != hipSuccess) {
+    if (hipMalloc(&d, n) != hipSuccess || hipMalloc(&o, (64 << 20) * 4 + 256) != hipSuccess) {
         printf("alloc failed\n");
         return 1;
     }
@@ -156,21 +272,14 @@ int main()
     hipMemset(d, 1, n);
     hipDeviceSynchronize();
     printf("{\"data\": \"memset 1\"}\n");
-    run<320, 320, 1>(d, n, o, cu);
     hipLaunchKernelGGL(fill_random, dim3(4096), dim3(256), 0, 0, (unsigned *)d, n / 4);
     hipDeviceSynchronize();
     printf("{\"data\": \"random\"}\n");
     run<320, 320, 1>(d, n, o, cu);
     run<320, 320, 3>(d, n, o, cu);
-    return 0;
-    run<64, 64, 0>(d, n, o, cu);
-    run<64, 64, 1>(d, n, o, cu);
-    run<64, 64, 2>(d, n, o, cu);
-    run<320, 320, 0>(d, n, o, cu);
-    run<320, 320, 1>(d, n, o, cu);
-    run<320, 320, 2>(d, n, o, cu);
-    run<1024, 1024, 0>(d, n, o, cu);
-    run<1024, 1024, 1>(d, n, o, cu);
-    run<1024, 1024, 2>(d, n, o, cu);
+    run<320, 320, 12>(d, n, o, cu);
+    run<320, 320, 13>(d, n, o, cu);
+    run<320, 320, 14>(d, n, o, cu);
+    run<320, 320, 15>(d, n, o, cu);
     return 0;
 }

@@ -1,0 +1,180 @@
+// team_probe: access-shape ceilings for short records (diagnostic, not product code).
+// A team of G lanes owns one record of RS bytes (records back to back, stride RS,
+// offset OFS from a 4 KiB-aligned base).  The record is cut into SUB-byte
+// sub-pieces; team lane j owns sub-pieces j, j+G, ...  Each sub-piece is SUB/16
+// 16-byte loads.
+//   mode 0 read : loads only (XOR into one register)
+//   mode 1 crc  : slice-by-4 chain over every word (32-replica LDS tables);
+//                 the last word of a sub-piece uses a compact (non-replicated)
+//                 "word then skip" table when G > 1; team fold via shuffles +
+//                 compact tables; the record's register stored per record
+// usage: team_probe  (JSON lines)
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u32x4 *g4p;
+
+__device__ __forceinline__ unsigned lds32(const char *L, unsigned a) { return *(const unsigned *)(L + a); }
+
+__device__ __forceinline__ unsigned m4(const char *L, unsigned x, unsigned c_lo, unsigned c_hi)
+{
+    const unsigned a0 = __builtin_amdgcn_perm(x, c_lo, 0x0C020400u);
+    const unsigned a1 = __builtin_amdgcn_perm(x, c_lo, 0x0C020500u);
+    const unsigned a2 = __builtin_amdgcn_perm(x, c_hi, 0x0C020600u);
+    const unsigned a3 = __builtin_amdgcn_perm(x, c_hi, 0x0C020700u);
+    return lds32(L, a0) ^ lds32(L, a1 + 128) ^ lds32(L, a2) ^ lds32(L, a3 + 128);
+}
+
+// compact table at byte base B: entry (t, e) at B + 1024 t + 4 e
+__device__ __forceinline__ unsigned op4(const char *L, unsigned B, unsigned x)
+{
+    return lds32(L, B + ((x & 0xff) << 2)) ^ lds32(L, B + 1024 + ((x >> 6) & 0x3fc)) ^
+           lds32(L, B + 2048 + ((x >> 14) & 0x3fc)) ^ lds32(L, B + 3072 + ((x >> 22) & 0x3fc));
+}
+
+__global__ void fill_random(unsigned *p, size_t n)
+{
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        unsigned long long x = (i + 1) * 0x9E3779B97F4A7C15ull;
+        x ^= x >> 29;
+        x *= 0xBF58476D1CE4E5B9ull;
+        x ^= x >> 32;
+        p[i] = (unsigned)x;
+    }
+}
+
+template <int G, int SUB, int RS, int MODE>
+__global__ __launch_bounds__(1024) void rec(const char *buf, size_t nrec, unsigned *out)
+{
+    constexpr int NSUB = RS / SUB;                 // sub-pieces per record
+    constexpr int IT = (NSUB + G - 1) / G;         // sub-pieces per lane (max)
+    constexpr int NL = SUB / 16;                   // loads per sub-piece
+    __shared__ __attribute__((aligned(16))) char L[MODE ? 131072 + 4096 * 8 : 16];
+    if (MODE) {
+        uint4 *L4 = reinterpret_cast<uint4 *>(L);
+        for (int i = threadIdx.x; i < (131072 + 4096 * 8) / 16; i += 1024) {
+            const unsigned v = 0x9E3779B9u * (unsigned)(i >> 3) + 0x7F4A7C15u;
+            L4[i] = make_uint4(v, v ^ 1, v ^ 2, v ^ 3);
+        }
+        __syncthreads();
+    }
+    const int lane = threadIdx.x & 63;
+    const int j = lane % G;
+    const unsigned c_lo = (unsigned)(lane & 31) << 2, c_hi = c_lo | 0x10000u;
+    const size_t nteam = (size_t)gridDim.x * (1024 / G);
+    const size_t team = (size_t)blockIdx.x * (1024 / G) + threadIdx.x / G;
+    unsigned acc = 0;
+    for (size_t r = team; r < nrec; r += nteam) {
+        const char *p = buf + r * RS;
+        u32x4 v[IT][NL];
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int sp = j + it * G;
+#pragma unroll
+            for (int i = 0; i < NL; ++i)
+                v[it][i] = (sp < NSUB) ? *(g4p)(p + sp * SUB + 16 * i) : u32x4{0, 0, 0, 0};
+        }
+        unsigned reg = 0;
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+#pragma unroll
+            for (int i = 0; i < NL; ++i) {
+                if (MODE == 0) {
+                    reg ^= v[it][i].x ^ v[it][i].y ^ v[it][i].z ^ v[it][i].w;
+                } else {
+                    reg = m4(L, reg ^ v[it][i].x, c_lo, c_hi);
+                    reg = m4(L, reg ^ v[it][i].y, c_lo, c_hi);
+                    reg = m4(L, reg ^ v[it][i].z, c_lo, c_hi);
+                    if (G > 1 && i == NL - 1)
+                        reg = op4(L, 131072, reg ^ v[it][i].w);
+                    else
+                        reg = m4(L, reg ^ v[it][i].w, c_lo, c_hi);
+                }
+            }
+        }
+        if (MODE) {
+#pragma unroll
+            for (int k = 1; k < G; k <<= 1) {
+                const unsigned o = __shfl_xor(reg, k, 64);
+                reg = ((j & k) ? reg : op4(L, 131072 + 4096 * (1 + __builtin_ctz(k)), reg)) ^
+                      ((j & k) ? 0u : o);
+            }
+            if (j == 0)
+                out[r] = reg;
+        } else {
+            acc ^= reg;
+        }
+    }
+    if (acc == 0x12345678u)
+        out[0] = acc;
+}
+
+template <int G, int SUB, int RS, int MODE>
+void run(const char *d, size_t total, unsigned *o, int cu)
+{
+    const size_t nrec = std::min(total / RS, (size_t)(64 << 20));
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    const int grid = cu;
+    for (int i = 0; i < 3; ++i)
+        hipLaunchKernelGGL((rec<G, SUB, RS, MODE>), dim3(grid), dim3(1024), 0, 0, d, nrec, o);
+    std::vector<float> t;
+    for (int r = 0; r < 10; ++r) {
+        hipEventRecord(a);
+        hipLaunchKernelGGL((rec<G, SUB, RS, MODE>), dim3(grid), dim3(1024), 0, 0, d, nrec, o);
+        hipEventRecord(b);
+        hipEventSynchronize(b);
+        float ms;
+        hipEventElapsedTime(&ms, a, b);
+        t.push_back(ms);
+    }
+    std::sort(t.begin(), t.end());
+    const double ms = t[t.size() / 2];
+    printf("{\"G\": %d, \"sub\": %d, \"rs\": %d, \"mode\": \"%s\", \"nrec\": %zu, \"ms\": %.4f, \"GBs\": %.1f}\n", G,
+           SUB, RS, MODE == 0 ? "read" : "crc", nrec, ms, nrec * (double)RS / ms / 1e6);
+    fflush(stdout);
+}
+
+template <int G, int SUB, int RS>
+void both(const char *d, size_t total, unsigned *o, int cu)
+{
+    run<G, SUB, RS, 0>(d, total, o, cu);
+    run<G, SUB, RS, 1>(d, total, o, cu);
+}
+
+int main()
+{
+    size_t n = (size_t)4 << 30;
+    char *d;
+    unsigned *o;
+    if (hipMalloc(&d, n) != hipSuccess || hipMalloc(&o, (64 << 20) * 4 + 64) != hipSuccess) {
+        printf("alloc failed\n");
+        return 1;
+    }
+    int cu = 0;
+    hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, 0);
+    hipLaunchKernelGGL(fill_random, dim3(4096), dim3(256), 0, 0, (unsigned *)d, n / 4);
+    hipDeviceSynchronize();
+    both<1, 64, 320>(d, n, o, cu);
+    both<2, 16, 320>(d, n, o, cu);
+    both<4, 16, 320>(d, n, o, cu);
+    both<4, 64, 320>(d, n, o, cu);
+    both<8, 16, 320>(d, n, o, cu);
+    both<16, 16, 320>(d, n, o, cu);
+    both<1, 64, 64>(d, n, o, cu);
+    both<2, 16, 64>(d, n, o, cu);
+    both<4, 16, 64>(d, n, o, cu);
+    both<1, 64, 256>(d, n, o, cu);
+    both<4, 16, 256>(d, n, o, cu);
+    both<8, 16, 256>(d, n, o, cu);
+    both<16, 16, 256>(d, n, o, cu);
+    both<1, 64, 1024>(d, n, o, cu);
+    both<4, 16, 1024>(d, n, o, cu);
+    both<16, 16, 1024>(d, n, o, cu);
+    both<16, 64, 1024>(d, n, o, cu);
+    return 0;
+}

@@ -223,8 +223,8 @@ class GpuBackend:
     def empty(self, n: int) -> torch.Tensor:
         return torch.empty(max(n, 1), dtype=torch.uint8, device=self.device)
 
-    def verify(self, buf, off, ln):
-        return zsfile.verify_commits(buf, off, ln)
+    def verify(self, buf, off, ln, seed=None):
+        return zsfile.verify_commits(buf, off, ln, seed)
 
     def raw(self, buf, off, ln):
         from .device import crc_batch
@@ -418,28 +418,29 @@ class Consistent:
         raw_h = [v & M32 for v in raw.cpu().tolist()] if raw is not None else []
         t_dev = time.perf_counter()
 
-        # zero-length mismatches: the finalise quirk if the CRC chains from the
-        # previous span of the same file
-        bad, stale = [], []
-        quirk = [i for i in bad_idx.tolist() if self.c_len[i] == 0 and i > 0
-                 and self.c_file[i - 1] == self.c_file[i]]
-        if quirk:
-            q = np.array(quirk)
-            prev = be.crc(self.buf, torch.from_numpy(self.c_off[q - 1]).to(self.buf.device),
-                          torch.from_numpy(self.c_len[q - 1]).to(self.buf.device))
-            prev = [v & M32 for v in prev.cpu().tolist()]
-        qset = dict(zip(quirk, prev)) if quirk else {}
-        for i in bad_idx.tolist():
-            f = self.db.files[int(self.c_file[i])]
-            at = int(self.c_rec[i])
-            if i in qset:
-                _, _, _, stored, words = _commit_rec(f.image, at)
-                if stored is not None and _trailer_crc(qset[i], words) == stored:
-                    stale.append((f.name, at))
-                    continue
-            bad.append((f.name, at))
-        summary = dict(rank=self.rank, commits=n, bad=bad[:self.MAX_LISTED], n_bad=len(bad),
-                       stale=stale[:self.MAX_LISTED], n_stale=len(stale),
+        # zero-length mismatches: the finalise quirk if the stored CRC chains
+        # from the previous span of the same file (re-verified on the device
+        # with the previous span's CRC as seed)
+        qm = (self.c_len[bad_idx] == 0) & (bad_idx > 0)
+        qm[qm] = self.c_file[bad_idx[qm] - 1] == self.c_file[bad_idx[qm]]
+        q = bad_idx[qm]
+        stale_i = np.zeros(0, np.int64)
+        if len(q):
+            dq = torch.from_numpy(q).to(self.d_off.device)
+            prev = be.crc(self.buf, self.d_off[dq - 1], self.d_len[dq - 1])
+            _, st2 = be.verify(self.buf, self.d_off[dq], self.d_len[dq], prev)
+            stale_i = q[(st2 == 1).cpu().numpy()]
+        bad_i = np.setdiff1d(bad_idx, stale_i, assume_unique=True)
+
+        def listed(ix):
+            out = []
+            for i in ix[:self.MAX_LISTED].tolist():
+                out.append((self.db.files[int(self.c_file[i])].name, int(self.c_rec[i])))
+            return out
+
+        bad, stale = listed(bad_i), listed(stale_i)
+        summary = dict(rank=self.rank, commits=n, bad=bad, n_bad=len(bad_i),
+                       stale=stale, n_stale=len(stale_i),
                        pieces=[(q[0], q[1], q[3] - q[2], r) for q, r in zip(self.pieces, raw_h)],
                        files=loc.files, bytes=loc.bytes_checked, header_errors=loc.header_errors,
                        walk_errors=loc.walk_errors, issues=loc.issues)

@@ -607,7 +607,8 @@ int zscrc_diag_stream_read(const void *d_buf, uint64_t len, void *d_scratch4, in
 }
 
 int zscrc_internal_verify_commits(const void *d_image, const uint64_t *d_off, const uint64_t *d_len,
-                                  uint32_t *d_crc, uint32_t *d_status, size_t n, void *stream, int write)
+                                  const uint32_t *d_seed, uint32_t *d_crc, uint32_t *d_status, size_t n,
+                                  void *stream, int write)
 {
     if (n == 0)
         return ZSCRC_OK;
@@ -621,6 +622,7 @@ int zscrc_internal_verify_commits(const void *d_image, const uint64_t *d_off, co
     d.base = static_cast<const uint8_t *>(d_image);
     d.off = d_off;
     d.len = d_len;
+    d.seed = d_seed;
     d.out = d_crc;
     d.status = d_status;
     d.commit = write ? 2u : 1u;

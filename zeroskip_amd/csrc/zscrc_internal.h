@@ -70,11 +70,13 @@ struct Classify {
     int pass;             /* 0 = count, 1 = scatter */
 };
 
-/* parts per long record for `count` records: >= 16 and >= 8192 items */
+/* parts per long record for `count` records: >= 16 per record and >= 8192
+ * items in all (two per wave team of the chip), so even one long record
+ * keeps every CU busy; at most 8192 parts per record */
 __host__ __device__ inline uint32_t split_log_parts(uint64_t count)
 {
     uint32_t lp = 4;
-    while ((count << lp) < 8192 && lp < 10)
+    while ((count << lp) < 8192 && lp < 13)
         ++lp;
     return lp;
 }

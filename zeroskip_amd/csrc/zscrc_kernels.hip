@@ -1134,9 +1134,23 @@ __device__ __forceinline__ uint32_t xpow8(const uint32_t *pow2, uint64_t n)
 
 /* Fold the 2^lp part registers of every listed record (register after part p
  * = shift(register before, |part p|) ^ raw_p), then finish like emit(): plain
- * CRC, or the commit trailer + comparison in commit mode. */
+ * CRC, or the commit trailer + comparison in commit mode.  One block per
+ * record: the m non-empty parts are m-1 parts of P bytes and a last one of
+ * Lm bytes, so  reg = (XOR_p<m-1 raw_p * XP^(m-2-p)) * x^(8 Lm) ^ raw_(m-1)
+ * with XP = x^(8P).  Thread t Horner-folds a contiguous run of parts and
+ * shifts its partial by XP^(parts after its run); the block XOR-reduces. */
+__device__ __forceinline__ uint32_t ppow(const uint32_t (&lad)[16], uint32_t e)
+{
+    uint32_t r = 0x80000000u;
+    for (int b = 0; e; ++b, e >>= 1)
+        if (e & 1)
+            r = gmul(r, lad[b]);
+    return r;
+}
+
 __global__ __launch_bounds__(256) void part_fold_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
 {
+    __shared__ uint32_t red[4];
     const uint32_t *pow2 = gtab + GT_POW2;
     uint32_t base = 0;
     for (uint32_t k = 0; k < d.klass; ++k)
@@ -1146,37 +1160,55 @@ __global__ __launch_bounds__(256) void part_fold_kernel(BatchDesc d, const uint3
     const uint32_t lp = split_log_parts(count);
     const uint64_t K = 1ull << lp;
     const uint32_t X4 = pow2[2]; /* x^32: one slice-by-4 step */
-    for (uint64_t idx = (uint64_t)blockIdx.x * 256 + threadIdx.x; idx < count;
-         idx += (uint64_t)gridDim.x * 256) {
+    const int t = threadIdx.x;
+    for (uint64_t idx = blockIdx.x; idx < count; idx += gridDim.x) {
         const RecDesc r = list[idx];
         const uint64_t len = r.len;
         const uint64_t P = (((len + K - 1) >> lp) + 63) & ~63ull;
-        const uint32_t XP = xpow8(pow2, P);
+        const uint32_t m = (uint32_t)((len + P - 1) / P); /* non-empty parts, 1..K */
         const uint32_t *parts = d.part_out + (idx << lp);
-        uint32_t reg = parts[0];
-        for (uint64_t p = 1; p < K; ++p) {
-            const uint64_t lo = p * P;
-            if (lo >= len)
-                break;
-            const uint64_t plen = len - lo < P ? len - lo : P;
-            reg = gmul(reg, plen == P ? XP : xpow8(pow2, plen)) ^ parts[p];
+        const uint32_t nu = m - 1;                        /* uniform parts */
+        const uint32_t run = (nu + 255) / 256;
+        const uint32_t lo = t * run < nu ? t * run : nu;
+        const uint32_t hi = lo + run < nu ? lo + run : nu;
+        uint32_t part = 0;
+        if (lo < hi) {
+            uint32_t lad[16];
+            lad[0] = xpow8(pow2, P);
+#pragma unroll
+            for (int b = 1; b < 16; ++b)
+                lad[b] = gmul(lad[b - 1], lad[b - 1]);
+            for (uint32_t p = lo; p < hi; ++p)
+                part = gmul(part, lad[0]) ^ parts[p];
+            part = gmul(part, ppow(lad, nu - hi));
         }
+        for (int o = 32; o > 0; o >>= 1)
+            part ^= __shfl_xor(part, o);
+        if ((t & 63) == 0)
+            red[t >> 6] = part;
+        __syncthreads();
+        const uint32_t H = red[0] ^ red[1] ^ red[2] ^ red[3];
+        __syncthreads();
+        if (t != 0)
+            continue;
+        const uint64_t Lm = len - (uint64_t)nu * P;
+        uint32_t reg = (nu ? gmul(H, xpow8(pow2, Lm)) : 0u) ^ parts[nu];
         if (!d.commit) {
             d.out[r.rec] = reg ^ d.xor_io;
             continue;
         }
         const uintptr_t end = reinterpret_cast<uintptr_t>(d.base) + r.off + len;
         const uint64_t w0 = load_be64(end);
-        const uint32_t t = (uint32_t)(w0 >> 56);
+        const uint32_t ty = (uint32_t)(w0 >> 56);
         uint64_t tw[3];
         int nt = 0;
         uint32_t stored = 0;
         uintptr_t crc_at = 0;
-        if (t == REC_COMMIT || t == REC_FINAL) {
+        if (ty == REC_COMMIT || ty == REC_FINAL) {
             tw[nt++] = w0 & 0xFFFFFFFF00000000ull;
             stored = (uint32_t)w0;
             crc_at = end + 4;
-        } else if (t == REC_LONG_COMMIT || t == REC_LONG_FINAL) {
+        } else if (ty == REC_LONG_COMMIT || ty == REC_LONG_FINAL) {
             const uint64_t w2 = load_be64(end + 16);
             tw[nt++] = w0;
             tw[nt++] = load_be64(end + 8);
@@ -1238,7 +1270,7 @@ extern "C" int zs_launch_classify(const zs::Classify *c, hipStream_t stream)
 
 extern "C" int zs_launch_part_fold(const zs::BatchDesc *d, const uint32_t *gtab, hipStream_t stream)
 {
-    hipLaunchKernelGGL(zs::part_fold_kernel, dim3(1024), dim3(256), 0, stream, *d, gtab);
+    hipLaunchKernelGGL(zs::part_fold_kernel, dim3(2048), dim3(256), 0, stream, *d, gtab);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

@@ -30,6 +30,7 @@
 #include "zscrc_internal.h"
 
 extern "C" int zscrc_internal_verify_commits(const void *d_image, const uint64_t *d_off, const uint64_t *d_len,
+                                             const uint32_t *d_seed,
                                              uint32_t *d_crc, uint32_t *d_status, size_t n, void *stream,
                                              int write);
 
@@ -219,13 +220,20 @@ int zscrc_zs_dotzsdb_crc(const void *image, uint64_t size, uint32_t *stored, uin
 int zscrc_device_verify_commits(const void *d_image, const uint64_t *d_span_off, const uint64_t *d_span_len,
                                 size_t n, uint32_t *d_crc, uint32_t *d_status, void *stream)
 {
-    return zscrc_internal_verify_commits(d_image, d_span_off, d_span_len, d_crc, d_status, n, stream, 0);
+    return zscrc_internal_verify_commits(d_image, d_span_off, d_span_len, nullptr, d_crc, d_status, n, stream, 0);
+}
+
+int zscrc_device_verify_commits_seeded(const void *d_image, const uint64_t *d_span_off,
+                                       const uint64_t *d_span_len, const uint32_t *d_seed, size_t n,
+                                       uint32_t *d_crc, uint32_t *d_status, void *stream)
+{
+    return zscrc_internal_verify_commits(d_image, d_span_off, d_span_len, d_seed, d_crc, d_status, n, stream, 0);
 }
 
 int zscrc_device_write_commits(void *d_image, const uint64_t *d_span_off, const uint64_t *d_span_len, size_t n,
                                uint32_t *d_crc, void *stream)
 {
-    return zscrc_internal_verify_commits(d_image, d_span_off, d_span_len, d_crc, nullptr, n, stream, 1);
+    return zscrc_internal_verify_commits(d_image, d_span_off, d_span_len, nullptr, d_crc, nullptr, n, stream, 1);
 }
 
 int zscrc_zs_verify_image(const void *image, uint64_t size, int kind, zscrc_zs_report *rep)

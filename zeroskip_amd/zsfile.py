@@ -79,17 +79,27 @@ def verify_image(image, kind: int = ACTIVE) -> dict:
     return rep.as_dict()
 
 
-def verify_commits(d_image: torch.Tensor, span_off: torch.Tensor, span_len: torch.Tensor):
+def verify_commits(d_image: torch.Tensor, span_off: torch.Tensor, span_len: torch.Tensor,
+                   seed: torch.Tensor | None = None):
     """Device-resident commit verification: (crc, status) int32 tensors;
-    status 1 = stored CRC matches, 0 = mismatch, 2 = no commit record."""
+    status 1 = stored CRC matches, 0 = mismatch, 2 = no commit record.
+    seed (int32, optional): span i's CRC continues from seed[i]
+    (zscrc_device_verify_commits_seeded) -- the reference's zero-length
+    finalise commit chains from the previous span's CRC."""
     n = span_off.numel()
     crc = torch.empty(n, dtype=torch.int32, device=d_image.device)
     st = torch.empty(n, dtype=torch.int32, device=d_image.device)
     with torch.cuda.device(d_image.device):
-        check(lib().zscrc_device_verify_commits(
-            d_image.data_ptr(), span_off.data_ptr(), span_len.data_ptr(), n, crc.data_ptr(),
-            st.data_ptr(), torch.cuda.current_stream(d_image.device).cuda_stream),
-            "zscrc_device_verify_commits")
+        stream = torch.cuda.current_stream(d_image.device).cuda_stream
+        if seed is None:
+            check(lib().zscrc_device_verify_commits(
+                d_image.data_ptr(), span_off.data_ptr(), span_len.data_ptr(), n, crc.data_ptr(),
+                st.data_ptr(), stream), "zscrc_device_verify_commits")
+        else:
+            assert seed.numel() == n and seed.dtype == torch.int32 and seed.device == d_image.device
+            check(lib().zscrc_device_verify_commits_seeded(
+                d_image.data_ptr(), span_off.data_ptr(), span_len.data_ptr(), seed.data_ptr(), n,
+                crc.data_ptr(), st.data_ptr(), stream), "zscrc_device_verify_commits_seeded")
     return crc, st
 
 
