@@ -1,5 +1,7 @@
 """Run one fixed-stride batch case repeatedly (profiling target).
-usage: python tools/crc_case.py STRIDE LEN N [G1_MAX G16_MAX] [REPS]"""
+usage: python tools/crc_case.py STRIDE LEN N [G1_MAX G16_MAX] [REPS]
+env: ZS_DEPTH = G1 walk override (zscrc_set_prefetch(1, depth)), ZS_SHIFT = byte
+offset of record 0 in the buffer"""
 import os
 import sys
 
@@ -13,7 +15,10 @@ stride, length, n = (int(x) for x in sys.argv[1:4])
 if len(sys.argv) > 5:
     lib().zscrc_set_teams(int(sys.argv[4]), int(sys.argv[5]))
 reps = int(sys.argv[6]) if len(sys.argv) > 6 else 5
-d = torch.randint(0, 256, (stride * (n - 1) + length,), dtype=torch.uint8, device="cuda")
+if "ZS_DEPTH" in os.environ:
+    lib().zscrc_set_prefetch(1, int(os.environ["ZS_DEPTH"]))
+shift = int(os.environ.get("ZS_SHIFT", "0"))
+d = torch.randint(0, 256, (shift + stride * (n - 1) + length,), dtype=torch.uint8, device="cuda")[shift:]
 out = torch.empty(n, dtype=torch.int32, device="cuda")
 for _ in range(reps):
     zd.crc_fixed(d, stride, length, n, out=out)

@@ -84,6 +84,12 @@ __global__ __launch_bounds__(1024) void rec(const char *buf, size_t nrec, unsign
                 out[16 + r] = reg;
             if (MODE == 3)
                 out[16 + r] = reg;
+            if (MODE == 16)
+                out[16 + lane] = reg;
+            if (MODE == 17)
+                ((volatile unsigned *)L)[threadIdx.x] = reg;
+            if (MODE == 18)
+                out[16 + (r & 0xfffff)] = reg;
             else if (MODE == 5)
                 __builtin_nontemporal_store(reg, out + 16 + r);
             else
@@ -253,7 +259,7 @@ void run(const char *d, size_t total, unsigned *o, int cu)
         std::sort(t.begin(), t.end());
         const double ms = t[t.size() / 2];
         printf("{\"stride\": %d, \"len\": %d, \"mode\": \"%s\", \"grid\": %d, \"ms\": %.4f, \"GBs\": %.1f}\n", RS, RL,
-               MODE == 0 ? "read" : MODE == 1 ? "crc" : MODE == 2 ? "crc2" : MODE == 3 ? "crc+store" : MODE == 4 ? "crc+deferred" : MODE == 5 ? "crc+ntstore" : MODE == 6 ? "crc4+x4store" : MODE == 7 ? "wavechunk+lds8" : MODE == 8 ? "wavechunk+reg8" : MODE == 12 ? "store at end" : MODE == 13 ? "one store mid-stream" : MODE == 14 ? "store 1/64 iters" : "store 1/8 iters", grid, ms, nrec * (double)RL / ms / 1e6);
+               MODE == 0 ? "read" : MODE == 1 ? "crc" : MODE == 2 ? "crc2" : MODE == 3 ? "crc+store" : MODE == 4 ? "crc+deferred" : MODE == 5 ? "crc+ntstore" : MODE == 6 ? "crc4+x4store" : MODE == 7 ? "wavechunk+lds8" : MODE == 8 ? "wavechunk+reg8" : MODE == 12 ? "store at end" : MODE == 13 ? "one store mid-stream" : MODE == 14 ? "store 1/64 iters" : MODE == 15 ? "store 1/8 iters" : MODE == 16 ? "store same 256B" : MODE == 17 ? "lds store" : "store 4MiB window", grid, ms, nrec * (double)RL / ms / 1e6);
         fflush(stdout);
     }
 }
@@ -277,9 +283,13 @@ int main()
     printf("{\"data\": \"random\"}\n");
     run<320, 320, 1>(d, n, o, cu);
     run<320, 320, 3>(d, n, o, cu);
-    run<320, 320, 12>(d, n, o, cu);
-    run<320, 320, 13>(d, n, o, cu);
-    run<320, 320, 14>(d, n, o, cu);
-    run<320, 320, 15>(d, n, o, cu);
+    run<320, 320, 16>(d, n, o, cu);
+    run<320, 320, 17>(d, n, o, cu);
+    run<320, 320, 18>(d, n, o, cu);
+    run<64, 64, 1>(d, n, o, cu);
+    run<64, 64, 3>(d, n, o, cu);
+    run<64, 64, 16>(d, n, o, cu);
+    run<64, 64, 17>(d, n, o, cu);
+    run<64, 64, 18>(d, n, o, cu);
     return 0;
 }
