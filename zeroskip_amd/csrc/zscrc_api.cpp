@@ -31,7 +31,6 @@ int zs_launch_team(int g, int fixed, int depth, const zs::BatchDesc *d, const ui
                    hipStream_t stream);
 int zs_launch_span_fold(const zs::SpanFold *f, hipStream_t stream);
 int zs_launch_short(int fixed, int pf, const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
-int zs_launch_tiny(int fixed, const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
 int zs_launch_stream_read(const void *buf, uint64_t n, uint32_t *out, int grid, hipStream_t stream);
 int zs_launch_classify(const zs::Classify *c, hipStream_t stream);
 int zs_launch_part_fold(const zs::BatchDesc *d, const uint32_t *gtab, hipStream_t stream);
@@ -225,12 +224,7 @@ int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s, int depth_hi
     if (!fixed && depth == 2)
         depth = 1;
     zs::BatchDesc dx = d;
-    if (depth == 9) { /* experiment: short kernel without result stores */
-        dx.split = 0xDEADu;
-        depth = 3;
-    }
-    int rc = depth == 10 ? zs_launch_tiny(fixed, &dx, c->gtab, c->ncu, s)
-             : depth >= 3 ? zs_launch_short(fixed, depth - 3, &dx, c->gtab, c->ncu, s)
+    int rc = depth >= 3 ? zs_launch_short(fixed, depth - 3, &dx, c->gtab, c->ncu, s)
                         : zs_launch_team(g, fixed, depth, &d, c->gtab, c->ncu, s);
     if (rc) {
         set_err("team kernel launch", hipGetLastError());
@@ -285,6 +279,12 @@ int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s)
     cl.bound[2] = b2;
     cl.count = cnt;
     cl.desc = desc;
+    {
+        /* class 0 goes to the short kernel (walks 3..9), which can read the
+         * caller's arrays when every record is class 0 */
+        const int w0 = g_depth[0];
+        cl.direct_ok = g1 > 0 && (w0 < 0 || w0 >= 3);
+    }
     for (int pass = 0; pass < 2; ++pass) {
         cl.pass = pass;
         if (zs_launch_classify(&cl, s)) {
@@ -647,7 +647,7 @@ void zscrc_set_gpu_min(uint64_t min_bytes)
 
 void zscrc_set_prefetch(int g, int depth)
 {
-    if (depth < -1 || depth > (g == 1 ? 10 : 2))
+    if (depth < -1 || depth > (g == 1 ? 8 : 2))
         return;
     if (g == 1)
         g_depth[0] = depth;

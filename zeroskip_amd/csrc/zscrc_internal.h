@@ -68,6 +68,8 @@ struct Classify {
     uint32_t *count;      /* [0..3] class sizes, [4..7] scatter cursors; zeroed */
     RecDesc *desc;        /* n entries, class-sorted after the scatter pass */
     int pass;             /* 0 = count, 1 = scatter */
+    int direct_ok;        /* the class-0 kernel can read the caller's arrays:
+                             skip the scatter when every record is class 0 */
 };
 
 /* parts per long record for `count` records: >= 16 per record and >= 8192

@@ -716,6 +716,9 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
         count = __builtin_amdgcn_readfirstlane(((g32p)d.class_count)[d.klass]);
         list = d.desc + base;
     }
+    /* every record of the batch in this (first) class: the classify scatter
+     * was skipped, read the caller's off/len/seed arrays */
+    const bool direct = !FIXED && d.klass == 0 && count == d.n;
     if ((uint64_t)blockIdx.x * WG >= count)
         return;
     fill_lds<1>(L, gtab);
@@ -741,6 +744,12 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
             len = (d.last_len != ~0ull && i + 1 == d.n) ? d.last_len : d.fixed_len;
             off = i * d.stride;
             seed = d.fixed_seed;
+            it.rec = i;
+        } else if (direct) {
+            typedef const __attribute__((address_space(1))) uint64_t *g64p;
+            off = ((g64p)d.off)[i];
+            len = ((g64p)d.len)[i];
+            seed = d.seed ? ((g32p)d.seed)[i] : 0u;
             it.rec = i;
         } else {
             typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -882,119 +891,10 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
             r = byte_step(L, r, t[k], c_hi);
         pend = it;
         pend_r = r;
-        have = d.split != 0xDEADu; /* experiment: 0xDEAD = no result stores */
+        have = true;
     }
     if (have)
         emit(d, pend, pend_r, L, c_lo, c_hi);
-}
-
-/*
- * tiny_kernel<FIXED, NP>: records of at most NP 64-byte pieces (len <= 64*NP - 3),
- * 4-byte aligned.  Each lane issues all 4*NP loads of its record at once
- * (buffer loads; pieces past the record are out of range: zeros, no memory
- * request) and then hashes -- the shape tools/short_probe measures at the
- * streaming ceiling.  Records that do not fit the fast shape (< 8 bytes,
- * unaligned, near the buffer start, outside the wave's 2 GiB window) are
- * hashed byte-wise (the launcher only sends batches where that is rare).
- */
-template <bool FIXED, int NP>
-__global__ __launch_bounds__(WG) void tiny_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
-{
-    __shared__ __attribute__((aligned(16))) char L[OFF_U];
-    uint64_t count = d.n;
-    const RecDesc *list = nullptr;
-    if (!FIXED) {
-        uint32_t base = 0;
-        for (uint32_t k = 0; k < d.klass; ++k)
-            base += __builtin_amdgcn_readfirstlane(((g32p)d.class_count)[k]);
-        count = __builtin_amdgcn_readfirstlane(((g32p)d.class_count)[d.klass]);
-        list = d.desc + base;
-    }
-    if ((uint64_t)blockIdx.x * WG >= count)
-        return;
-    fill_lds<1>(L, gtab);
-    __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const uint32_t c_lo = (uint32_t)(lane & 31) << 2;
-    const uint32_t c_hi = c_lo | 0x10000u;
-    const uintptr_t lo = reinterpret_cast<uintptr_t>(d.base) & ~uintptr_t(3);
-    const uint64_t nthr = (uint64_t)gridDim.x * WG;
-    constexpr uint32_t OOB = 0x80000000u, RANGE = 0x7ffffff0u;
-    for (uint64_t i = (uint64_t)blockIdx.x * WG + threadIdx.x; i < count; i += nthr) {
-        Item it;
-        uint64_t off, len;
-        uint32_t seed;
-        if (FIXED) {
-            len = (d.last_len != ~0ull && i + 1 == d.n) ? d.last_len : d.fixed_len;
-            off = i * d.stride;
-            seed = d.fixed_seed;
-            it.rec = i;
-        } else {
-            typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-            typedef const __attribute__((address_space(1))) u32x2 *g2p;
-            const g2p q = (g2p)(list + i);
-            const u32x2 a = q[0], b = q[1], c = q[2];
-            off = ((uint64_t)a.y << 32) | a.x;
-            len = ((uint64_t)b.y << 32) | b.x;
-            seed = c.x;
-            it.rec = c.y;
-        }
-        const uintptr_t A = reinterpret_cast<uintptr_t>(d.base) + off;
-        it.A = A;
-        it.len = len;
-        it.R0 = seed ^ d.xor_io;
-        if (!FIXED && d.commit) {
-            it.c0 = ((g32p)(A + len))[0];
-            it.c1 = ((g32p)(A + len))[1];
-        }
-        const uintptr_t E = (A + len) & ~uintptr_t(3);
-        const uint64_t np = (E - A + 63) >> 6;
-        const uintptr_t V0 = E - np * 64;
-        const uintptr_t first = __builtin_amdgcn_readfirstlane((uint32_t)V0) |
-                                ((uintptr_t)__builtin_amdgcn_readfirstlane((uint32_t)(V0 >> 32)) << 32);
-        const uintptr_t W = first >= (1ull << 30) ? first - (1ull << 30) : 0;
-        const __amdgpu_buffer_rsrc_t rsrc =
-            __builtin_amdgcn_make_buffer_rsrc((void *)W, (short)0, (int)RANGE, 0x00020000);
-        const bool fast = len >= 8 && (A & 3) == 0 && V0 >= lo && np <= NP && V0 >= W &&
-                          V0 + 64 * np - W < RANGE;
-        uint32_t buf[NP][16];
-#pragma unroll
-        for (int p = 0; p < NP; ++p) {
-            const uint32_t o = fast && (uint64_t)p < np ? (uint32_t)(V0 + 64 * p - W) : OOB;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const u32x4 v =
-                    __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, o + 16 * q, 0, 0));
-                buf[p][4 * q + 0] = v.x;
-                buf[p][4 * q + 1] = v.y;
-                buf[p][4 * q + 2] = v.z;
-                buf[p][4 * q + 3] = v.w;
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0); /* every load issued before hashing starts */
-        uint32_t r = 0;
-        if (fast) {
-            const int32_t d0 = (int32_t)(A - V0); /* 0..60, multiple of 4 */
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const int32_t dk = d0 - 4 * k;
-                const uint32_t x = dk > 0 ? 0u : (dk == 0 ? buf[0][k] ^ it.R0 : buf[0][k]);
-                r = m4(L, r ^ x, c_lo, c_hi);
-            }
-#pragma unroll
-            for (int p = 1; p < NP; ++p)
-                if ((uint64_t)p < np)
-                    r = piece<false>(L, r, buf[p], c_lo, c_hi);
-            const uint32_t tail = (uint32_t)((A + len) - E);
-            for (uint32_t k = 0; k < tail; ++k)
-                r = byte_step(L, r, ((g8p)E)[k], c_hi);
-        } else {
-            r = it.R0;
-            for (uint64_t k = 0; k < len; ++k)
-                r = byte_step(L, r, ((g8p)A)[k], c_hi);
-        }
-        emit(d, it, r, L, c_lo, c_hi);
-    }
 }
 
 /* ------------------------------------------------------------ span fold */
@@ -1059,6 +959,8 @@ __device__ __forceinline__ int class_of(const Classify &c, uint64_t len)
 __global__ __launch_bounds__(256) void classify_kernel(Classify c)
 {
     __shared__ uint32_t cnt[4], slot[4], pos[4];
+    if (c.pass == 1 && c.direct_ok && ((const volatile uint32_t *)c.count)[0] == c.n)
+        return; /* one class: its kernel reads the caller's arrays directly */
     const uint64_t per = (c.n + gridDim.x - 1) / gridDim.x;
     const uint64_t r0 = (uint64_t)blockIdx.x * per;
     const uint64_t r1 = r0 + per < c.n ? r0 + per : c.n;
@@ -1331,15 +1233,6 @@ extern "C" int zs_launch_short(int fixed, int pf, const zs::BatchDesc *d, const 
     }
 #undef ZS_SHORT_PF
 #undef ZS_SHORT
-    return hipGetLastError() == hipSuccess ? 0 : -3;
-}
-
-extern "C" int zs_launch_tiny(int fixed, const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream)
-{
-    if (fixed)
-        hipLaunchKernelGGL((zs::tiny_kernel<true, 5>), dim3(grid), dim3(zs::WG), 0, stream, *d, gtab);
-    else
-        hipLaunchKernelGGL((zs::tiny_kernel<false, 5>), dim3(grid), dim3(zs::WG), 0, stream, *d, gtab);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
