@@ -47,6 +47,7 @@ std::atomic<uint64_t> g_stat[4];
 std::atomic<uint64_t> g_gpu_min{0};
 std::atomic<uint64_t> g_g1_max{1024};
 std::atomic<uint64_t> g_g16_max{1u << 20};
+std::atomic<int> g_split_team{64}; /* team size on split long records */
 int g_strict = 0;
 /* record-walk override per team size (index 0/1/2 = G 1/16/64): -1 = automatic
  * (walk_for), 0 = two-level loop, 1/2 = flattened loop with a 1/2-item ring;
@@ -86,6 +87,9 @@ void env_init()
     s = getenv("ZSCRC_G1_MAX");
     if (s)
         g_g1_max = strtoull(s, nullptr, 0);
+    s = getenv("ZSCRC_SPLIT_TEAM");
+    if (s && (atoi(s) == 16 || atoi(s) == 64))
+        g_split_team = atoi(s);
     s = getenv("ZSCRC_G16_MAX");
     if (s)
         g_g16_max = strtoull(s, nullptr, 0);
@@ -252,7 +256,10 @@ int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s)
         b1 = g1;
     const uint64_t b2 = g16 > b1 ? g16 : b1;
     const size_t list_bytes = 64 + n * sizeof(zs::RecDesc);
-    const size_t part_bytes = (n * 16 + 16384) * sizeof(uint32_t);
+    const int gs = g_split_team;
+    /* split target per class: two items per team of the launch */
+    auto split_items = [&](int g) { return 2u * (uint32_t)c->ncu * 16u * (uint32_t)(64 / g); };
+    const size_t part_bytes = (n * 16 + 2 * (size_t)split_items(16)) * sizeof(uint32_t);
     {
         std::lock_guard<std::recursive_mutex> lk(c->mu);
         int rc = grow(&c->classes, &c->classes_bytes, list_bytes);
@@ -293,7 +300,7 @@ int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s)
         }
         g_stat[2]++;
     }
-    const int team[4] = {1, 16, 16, 64};
+    const int team[4] = {1, 16, 16, gs};
     const int walk[4] = {-1, 1, 0, 0};
     d.len_lo = 0;
     d.len_hi = ~0ull;
@@ -302,14 +309,18 @@ int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s)
     for (int k = 0; k < 4; ++k) {
         zs::BatchDesc dk = d;
         dk.klass = (uint32_t)k;
-        if (k == 3) {
-            dk.split = 1;
+        if (k >= 2) {
+            /* classes 2-3 split their records into parts when there are too
+             * few to fill the chip (a lone 1 MiB record would otherwise be one
+             * team's serial walk); class 3 always into >= 16 parts */
+            dk.split = split_items(team[k]);
+            dk.split_lpmin = k == 3 ? 4u : 0u;
             dk.part_out = static_cast<uint32_t *>(c->parts);
         }
         int rc = launch(c, team[k], dk, s, walk[k]);
         if (rc)
             return rc;
-        if (k == 3) {
+        if (k >= 2) {
             if (zs_launch_part_fold(&dk, c->gtab, s)) {
                 set_err("part fold launch", hipGetLastError());
                 return ZSCRC_EHIP;

@@ -45,10 +45,12 @@ struct BatchDesc {
     const struct RecDesc *desc;
     const uint32_t *class_count;
     uint32_t klass;
-    /* split long records into 2^lp equal parts (lp chosen in-kernel from the
-     * record count) whose raw registers go to part_out[idx << lp | part];
+    /* split != 0: split long records into 2^lp equal parts, lp chosen
+     * in-kernel from the record count so that there are >= split items
+     * (split_log_parts); raw part registers go to part_out[idx << lp | part],
      * part_fold_kernel folds them per record */
     uint32_t split;
+    uint32_t split_lpmin;
     uint32_t *part_out;
 };
 
@@ -72,13 +74,13 @@ struct Classify {
                              skip the scatter when every record is class 0 */
 };
 
-/* parts per long record for `count` records: >= 16 per record and >= 8192
- * items in all (two per wave team of the chip), so even one long record
- * keeps every CU busy; at most 8192 parts per record */
-__host__ __device__ inline uint32_t split_log_parts(uint64_t count)
+/* log2 parts per record for `count` records: at least lpmin, and at least
+ * `target` items in all (two per team of the launch), so that even one long
+ * record keeps every CU busy */
+__host__ __device__ inline uint32_t split_log_parts(uint64_t count, uint32_t target, uint32_t lpmin)
 {
-    uint32_t lp = 4;
-    while ((count << lp) < 8192 && lp < 13)
+    uint32_t lp = lpmin;
+    while ((count << lp) < target && lp < 16)
         ++lp;
     return lp;
 }

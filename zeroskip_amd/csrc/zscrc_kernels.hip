@@ -476,8 +476,9 @@ __device__ __forceinline__ void compute(const BatchDesc &d, const Cursor &c, uin
 }
 
 template <int G, bool FIXED, int DEPTH>
-__global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
+__global__ __launch_bounds__(WG) void team_kernel(BatchDesc d_in, const uint32_t *__restrict__ gtab)
 {
+    BatchDesc d = d_in;
     __shared__ __attribute__((aligned(16))) char L[LDS_BYTES];
     /* work items: records, or records x 2^lp parts; a device-built class list
      * supplies the record count without a host round trip */
@@ -490,7 +491,9 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d, const uint32_t *_
         count = __builtin_amdgcn_readfirstlane(((g32p)d.class_count)[d.klass]);
         list = d.desc + base;
     }
-    const uint32_t lp = (!FIXED && d.split) ? split_log_parts(count) : 0;
+    const uint32_t lp = (!FIXED && d.split) ? split_log_parts(count, d.split, d.split_lpmin) : 0;
+    if (lp == 0)
+        d.part_out = nullptr; /* enough records: no split, results go out directly */
     const uint64_t nitems = count << lp;
     /* blocks without work (empty or small classes) leave before the LDS fill */
     if ((uint64_t)blockIdx.x * WAVES * (64 / G) >= nitems)
@@ -1059,7 +1062,9 @@ __global__ __launch_bounds__(256) void part_fold_kernel(BatchDesc d, const uint3
         base += d.class_count[k];
     const uint64_t count = d.class_count[d.klass];
     const RecDesc *list = d.desc + base;
-    const uint32_t lp = split_log_parts(count);
+    const uint32_t lp = split_log_parts(count, d.split, d.split_lpmin);
+    if (lp == 0)
+        return; /* the team kernel emitted every record itself */
     const uint64_t K = 1ull << lp;
     const uint32_t X4 = pow2[2]; /* x^32: one slice-by-4 step */
     const int t = threadIdx.x;
