@@ -34,6 +34,7 @@ int zs_launch_short(int fixed, int pf, const zs::BatchDesc *d, const uint32_t *g
 int zs_launch_stream_read(const void *buf, uint64_t n, uint32_t *out, int grid, hipStream_t stream);
 int zs_launch_classify(const zs::Classify *c, hipStream_t stream);
 int zs_launch_part_fold(const zs::BatchDesc *d, const uint32_t *gtab, hipStream_t stream);
+int zs_launch_plan(const zs::PlanArgs *a, hipStream_t stream);
 }
 
 namespace {
@@ -244,9 +245,10 @@ int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s, int depth_hi
  *   <= g1_max          one lane per record, flattened walk
  *   <= 8 KiB           16-lane teams, flattened walk
  *   <= g16_max         16-lane teams, two-level walk
- *   longer             whole-wave teams on 2^k equal parts per record (k from
- *                      the class count, >= 8192 parts in all), then a fold
- *                      kernel combines each record's part registers. */
+ *   longer             whole-wave teams
+ * Classes 2-3 with fewer records than two per team are cut into equal parts
+ * (unit ~ class bytes / items wanted, plan_kernel) and a fold kernel combines
+ * each record's part registers. */
 int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s)
 {
     const uint64_t g1 = g_g1_max, g16 = g_g16_max;
@@ -255,11 +257,16 @@ int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s)
     if (b1 < g1)
         b1 = g1;
     const uint64_t b2 = g16 > b1 ? g16 : b1;
-    const size_t list_bytes = 64 + n * sizeof(zs::RecDesc);
+    /* classes buffer: [0,32) class sizes + scatter cursors, [32,64) class
+     * byte totals, [64,128) split plans, [256, ...) class-sorted descriptors */
+    constexpr size_t HEAD = 256;
+    const size_t list_bytes = HEAD + n * sizeof(zs::RecDesc);
     const int gs = g_split_team;
     /* split target per class: two items per team of the launch */
     auto split_items = [&](int g) { return 2u * (uint32_t)c->ncu * 16u * (uint32_t)(64 / g); };
-    const size_t part_bytes = (n * 16 + 2 * (size_t)split_items(16)) * sizeof(uint32_t);
+    const size_t T = split_items(16) > split_items(gs) ? split_items(16) : split_items(gs);
+    /* parts buffer: part registers (< 2T), part_rec (< 2T), part_base (< T) */
+    const size_t part_bytes = 5 * T * sizeof(uint32_t);
     {
         std::lock_guard<std::recursive_mutex> lk(c->mu);
         int rc = grow(&c->classes, &c->classes_bytes, list_bytes);
@@ -269,8 +276,13 @@ int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s)
             return rc;
     }
     uint32_t *cnt = static_cast<uint32_t *>(c->classes);
-    zs::RecDesc *desc = reinterpret_cast<zs::RecDesc *>(static_cast<char *>(c->classes) + 64);
-    hipError_t e = hipMemsetAsync(cnt, 0, 64, s);
+    uint64_t *cbytes = reinterpret_cast<uint64_t *>(static_cast<char *>(c->classes) + 32);
+    zs::SplitPlan *plans = reinterpret_cast<zs::SplitPlan *>(static_cast<char *>(c->classes) + 64);
+    zs::RecDesc *desc = reinterpret_cast<zs::RecDesc *>(static_cast<char *>(c->classes) + HEAD);
+    uint32_t *part_out = static_cast<uint32_t *>(c->parts);
+    uint32_t *part_rec = part_out + 2 * T;
+    uint32_t *part_base = part_rec + 2 * T;
+    hipError_t e = hipMemsetAsync(cnt, 0, HEAD, s);
     if (e != hipSuccess) {
         set_err("hipMemsetAsync(class counters)", e);
         return ZSCRC_EHIP;
@@ -285,6 +297,7 @@ int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s)
     cl.bound[1] = b1;
     cl.bound[2] = b2;
     cl.count = cnt;
+    cl.bytes = cbytes;
     cl.desc = desc;
     {
         /* class 0 goes to the short kernel (walks 3..9), which can read the
@@ -310,12 +323,30 @@ int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s)
         zs::BatchDesc dk = d;
         dk.klass = (uint32_t)k;
         if (k >= 2) {
-            /* classes 2-3 split their records into parts when there are too
-             * few to fill the chip (a lone 1 MiB record would otherwise be one
-             * team's serial walk); class 3 always into >= 16 parts */
-            dk.split = split_items(team[k]);
-            dk.split_lpmin = k == 3 ? 4u : 0u;
-            dk.part_out = static_cast<uint32_t *>(c->parts);
+            /* classes 2-3 with fewer records than two per team are cut into
+             * equal parts (a lone 1 MiB record would otherwise be one team's
+             * serial walk; a few 3 GiB regions beside small records would
+             * leave most teams idle), folded per record afterwards */
+            zs::PlanArgs pa;
+            pa.count = cnt;
+            pa.bytes = cbytes;
+            pa.desc = desc;
+            pa.klass = (uint32_t)k;
+            pa.target = split_items(team[k]);
+            pa.unit_min = (uint64_t)team[k] * 64 * 16; /* 16 steps of the team */
+            pa.plan = plans;
+            pa.part_base = part_base;
+            pa.part_rec = part_rec;
+            if (zs_launch_plan(&pa, s)) {
+                set_err("split plan launch", hipGetLastError());
+                return ZSCRC_EHIP;
+            }
+            g_stat[2]++;
+            dk.split = 1;
+            dk.plan = plans;
+            dk.part_base = part_base;
+            dk.part_rec = part_rec;
+            dk.part_out = part_out;
         }
         int rc = launch(c, team[k], dk, s, walk[k]);
         if (rc)

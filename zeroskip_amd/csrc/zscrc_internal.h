@@ -45,13 +45,15 @@ struct BatchDesc {
     const struct RecDesc *desc;
     const uint32_t *class_count;
     uint32_t klass;
-    /* split != 0: split long records into 2^lp equal parts, lp chosen
-     * in-kernel from the record count so that there are >= split items
-     * (split_log_parts); raw part registers go to part_out[idx << lp | part],
-     * part_fold_kernel folds them per record */
+    /* split != 0: this class may be split into parts (plan_kernel decides
+     * from the class's record count and bytes, plan[klass]); part p of
+     * record part_rec[p] covers bytes [(p - part_base[rec]) * unit, +unit);
+     * raw part registers go to part_out[p], part_fold_kernel folds them */
     uint32_t split;
-    uint32_t split_lpmin;
     uint32_t *part_out;
+    const struct SplitPlan *plan;
+    const uint32_t *part_base;
+    const uint32_t *part_rec;
 };
 
 struct RecDesc {
@@ -68,22 +70,31 @@ struct Classify {
     uint64_t n;
     uint64_t bound[3];    /* class c holds bound[c-1] < len <= bound[c] */
     uint32_t *count;      /* [0..3] class sizes, [4..7] scatter cursors; zeroed */
+    uint64_t *bytes;      /* [0..3] class byte totals; zeroed */
     RecDesc *desc;        /* n entries, class-sorted after the scatter pass */
     int pass;             /* 0 = count, 1 = scatter */
     int direct_ok;        /* the class-0 kernel can read the caller's arrays:
                              skip the scatter when every record is class 0 */
 };
 
-/* log2 parts per record for `count` records: at least lpmin, and at least
- * `target` items in all (two per team of the launch), so that even one long
- * record keeps every CU busy */
-__host__ __device__ inline uint32_t split_log_parts(uint64_t count, uint32_t target, uint32_t lpmin)
-{
-    uint32_t lp = lpmin;
-    while ((count << lp) < target && lp < 16)
-        ++lp;
-    return lp;
-}
+/* How a length class is split (written by plan_kernel on the device). */
+struct SplitPlan {
+    uint64_t unit;   /* bytes per part (the last part of a record: the rest) */
+    uint32_t parts;  /* work items: parts in all, or records when direct     */
+    uint32_t direct; /* 1 = enough records: no split                          */
+};
+
+struct PlanArgs {
+    const uint32_t *count; /* class sizes */
+    const uint64_t *bytes; /* class byte totals */
+    const struct RecDesc *desc;
+    uint32_t klass;
+    uint32_t target;       /* items wanted: two per team of the launch */
+    uint64_t unit_min;     /* smallest part worth a team */
+    SplitPlan *plan;
+    uint32_t *part_base;   /* per record of the class: its first part */
+    uint32_t *part_rec;    /* per part: its record */
+};
 
 struct SpanFold {
     const uint32_t *part; /* W raw segment registers */

@@ -159,7 +159,7 @@ __device__ __forceinline__ void load_meta(const RecDesc *list, uint64_t idx, uin
 
 template <int G, bool FIXED>
 __device__ __forceinline__ bool fetch_record(const BatchDesc &d, const RecDesc *list, uint64_t count,
-                                             uint64_t w, uint64_t nteams, uint64_t nitems, uint32_t lp,
+                                             uint64_t w, uint64_t nteams, uint64_t nitems, uint32_t sp,
                                              Meta &pre, Item &it)
 {
     constexpr uint64_t STEP = (uint64_t)G * 64;
@@ -172,12 +172,13 @@ __device__ __forceinline__ bool fetch_record(const BatchDesc &d, const RecDesc *
         off = rec * d.stride;
         seed = d.fixed_seed;
     } else {
-        const uint64_t idx = w >> lp;
+        const uint64_t idx = sp ? ((g32p)d.part_rec)[w] : w;
         Meta m = pre;
         if (m.idx != idx)
             load_meta(list, idx, count - 1, m);
         /* prefetch the descriptor of this team's next work item's record */
-        const uint64_t nidx = (w + nteams) >> lp;
+        const uint64_t nw = w + nteams < nitems ? w + nteams : nitems - 1;
+        const uint64_t nidx = sp ? ((g32p)d.part_rec)[nw] : nw;
         if (nidx != idx)
             load_meta(list, nidx, count - 1, pre);
         else
@@ -186,12 +187,12 @@ __device__ __forceinline__ bool fetch_record(const BatchDesc &d, const RecDesc *
         off = m.off;
         seed = m.seed;
         rec = m.rec;
-        if (lp) {
-            /* part (w mod 2^lp) of the record: equal 64-byte-multiple parts */
-            const uint64_t P = (((len + (1ull << lp) - 1) >> lp) + 63) & ~63ull;
-            const uint64_t part = w & ((1ull << lp) - 1);
-            lo = part * P < len ? part * P : len;
-            const uint64_t hi = lo + P < len ? lo + P : len;
+        if (sp) {
+            /* part p of the record: bytes [p * unit, +unit), the last one the rest */
+            const uint64_t U = d.plan[d.klass].unit;
+            const uint64_t part = w - ((g32p)d.part_base)[idx];
+            lo = part * U < len ? part * U : len;
+            const uint64_t hi = lo + U < len ? lo + U : len;
             len = hi - lo;
             if (part)
                 seed = d.xor_io; /* parts after the first start from a zero register */
@@ -209,7 +210,7 @@ __device__ __forceinline__ bool fetch_record(const BatchDesc &d, const RecDesc *
     it.rec = rec;
     it.w = w;
     it.R0 = seed ^ d.xor_io;
-    if (!FIXED && d.commit && !lp) {
+    if (!FIXED && d.commit && !sp) {
         /* the commit record's first word, fetched with the record so the
          * check at the record end never waits on a late load */
         it.c0 = ((g32p)(A + len))[0];
@@ -430,7 +431,7 @@ __device__ void fill_lds(char *L, const uint32_t *__restrict__ gtab)
 
 template <int G, bool FIXED>
 __device__ __forceinline__ Cursor next_cursor(const BatchDesc &d, const RecDesc *list, uint64_t count,
-                                              const Cursor &c, uint64_t nteams, uint64_t nitems, uint32_t lp,
+                                              const Cursor &c, uint64_t nteams, uint64_t nitems, uint32_t sp,
                                               Meta &pre)
 {
     Cursor n = c;
@@ -441,7 +442,7 @@ __device__ __forceinline__ Cursor next_cursor(const BatchDesc &d, const RecDesc 
         return n;
     }
     n.s = 0;
-    n.ok = fetch_record<G, FIXED>(d, list, count, c.it.w + nteams, nteams, nitems, lp, pre, n.it);
+    n.ok = fetch_record<G, FIXED>(d, list, count, c.it.w + nteams, nteams, nitems, sp, pre, n.it);
     return n;
 }
 
@@ -480,8 +481,9 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d_in, const uint32_t
 {
     BatchDesc d = d_in;
     __shared__ __attribute__((aligned(16))) char L[LDS_BYTES];
-    /* work items: records, or records x 2^lp parts; a device-built class list
-     * supplies the record count without a host round trip */
+    /* work items: records, or parts of records (split classes, plan_kernel);
+     * a device-built class list supplies the record count without a host
+     * round trip */
     uint64_t count = d.n;
     const RecDesc *list = nullptr;
     if (!FIXED) {
@@ -491,10 +493,15 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d_in, const uint32_t
         count = __builtin_amdgcn_readfirstlane(((g32p)d.class_count)[d.klass]);
         list = d.desc + base;
     }
-    const uint32_t lp = (!FIXED && d.split) ? split_log_parts(count, d.split, d.split_lpmin) : 0;
-    if (lp == 0)
+    uint32_t sp = 0;
+    uint64_t nitems = count;
+    if (!FIXED && d.split) {
+        sp = __builtin_amdgcn_readfirstlane(((const volatile uint32_t *)&d.plan[d.klass].direct)[0]) ? 0u : 1u;
+        if (sp)
+            nitems = __builtin_amdgcn_readfirstlane(((const volatile uint32_t *)&d.plan[d.klass].parts)[0]);
+    }
+    if (!sp)
         d.part_out = nullptr; /* enough records: no split, results go out directly */
-    const uint64_t nitems = count << lp;
     /* blocks without work (empty or small classes) leave before the LDS fill */
     if ((uint64_t)blockIdx.x * WAVES * (64 / G) >= nitems)
         return;
@@ -518,7 +525,7 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d_in, const uint32_t
      * their per-record metadata loads wait on the same vmcnt counter. */
     Cursor c0;
     c0.s = 0;
-    c0.ok = fetch_record<G, FIXED>(d, list, count, team, nteams, nitems, lp, pre, c0.it);
+    c0.ok = fetch_record<G, FIXED>(d, list, count, team, nteams, nitems, sp, pre, c0.it);
     uint32_t acc = 0;
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(gtab);
     const uintptr_t lo = reinterpret_cast<uintptr_t>(d.base) & ~uintptr_t(3);
@@ -534,7 +541,7 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d_in, const uint32_t
         while (ok) {
             Cursor cn;
             cn.s = 0;
-            cn.ok = fetch_record<G, FIXED>(d, list, count, cur.w + nteams, nteams, nitems, lp, pre, cn.it);
+            cn.ok = fetch_record<G, FIXED>(d, list, count, cur.w + nteams, nteams, nitems, sp, pre, cn.it);
             uint32_t w[16];
 #pragma unroll
             for (int k = 0; k < 16; ++k)
@@ -590,7 +597,7 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d_in, const uint32_t
             ok = cn.ok;
         }
     } else if (FIXED && DEPTH == 2) {
-        Cursor c1 = next_cursor<G, FIXED>(d, list, count, c0, nteams, nitems, lp, pre);
+        Cursor c1 = next_cursor<G, FIXED>(d, list, count, c0, nteams, nitems, sp, pre);
         uint32_t bb[16];
         issue<G>(c1, j, dummy, lo, bb);
         for (;;) {
@@ -602,7 +609,7 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d_in, const uint32_t
                 for (int k = 0; k < 16; ++k)
                     w[k] = ba[k];
                 const Cursor cur = c0;
-                const Cursor c2 = next_cursor<G, FIXED>(d, list, count, c1, nteams, nitems, lp, pre);
+                const Cursor c2 = next_cursor<G, FIXED>(d, list, count, c1, nteams, nitems, sp, pre);
                 issue<G>(c2, j, dummy, lo, ba);
                 c0 = c1;
                 c1 = c2;
@@ -616,7 +623,7 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d_in, const uint32_t
                 for (int k = 0; k < 16; ++k)
                     w[k] = bb[k];
                 const Cursor cur = c0;
-                const Cursor c2 = next_cursor<G, FIXED>(d, list, count, c1, nteams, nitems, lp, pre);
+                const Cursor c2 = next_cursor<G, FIXED>(d, list, count, c1, nteams, nitems, sp, pre);
                 issue<G>(c2, j, dummy, lo, bb);
                 c0 = c1;
                 c1 = c2;
@@ -630,7 +637,7 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d_in, const uint32_t
 #pragma unroll
             for (int k = 0; k < 16; ++k)
                 w[k] = ba[k];
-            c0 = next_cursor<G, FIXED>(d, list, count, cur, nteams, nitems, lp, pre);
+            c0 = next_cursor<G, FIXED>(d, list, count, cur, nteams, nitems, sp, pre);
             issue<G>(c0, j, dummy, lo, ba);
             compute<G>(d, cur, w, acc, j, lane, L, c_lo, c_hi, lo);
         }
@@ -975,8 +982,18 @@ __global__ __launch_bounds__(256) void classify_kernel(Classify c)
     }
     __syncthreads();
     uint32_t local[4] = {0, 0, 0, 0};
-    for (uint64_t rec = r0 + threadIdx.x; rec < r1; rec += 256)
-        local[class_of(c, lens[rec])]++;
+    uint64_t lbytes[4] = {0, 0, 0, 0};
+    for (uint64_t rec = r0 + threadIdx.x; rec < r1; rec += 256) {
+        const uint64_t len = lens[rec];
+        const int k = class_of(c, len);
+        local[k]++;
+        if (c.pass == 0)
+            lbytes[k] += len;
+    }
+    __shared__ unsigned long long bsum[4];
+    if (threadIdx.x < 4)
+        bsum[threadIdx.x] = 0;
+    __syncthreads();
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         uint32_t v = local[k];
@@ -984,11 +1001,20 @@ __global__ __launch_bounds__(256) void classify_kernel(Classify c)
             v += __shfl_xor(v, o);
         if (lane == 0 && v)
             atomicAdd(&cnt[k], v);
+        if (c.pass == 0) {
+            unsigned long long b = lbytes[k];
+            for (int o = 32; o > 0; o >>= 1)
+                b += __shfl_xor(b, o);
+            if (lane == 0 && b)
+                atomicAdd(&bsum[k], b);
+        }
     }
     __syncthreads();
     if (c.pass == 0) {
-        if (threadIdx.x < 4 && cnt[threadIdx.x])
+        if (threadIdx.x < 4 && cnt[threadIdx.x]) {
             atomicAdd(&c.count[threadIdx.x], cnt[threadIdx.x]);
+            atomicAdd((unsigned long long *)&c.bytes[threadIdx.x], bsum[threadIdx.x]);
+        }
         return;
     }
     if (threadIdx.x < 4) {
@@ -1028,6 +1054,86 @@ __global__ __launch_bounds__(256) void classify_kernel(Classify c)
     }
 }
 
+/* Split plan of one length class (one block; runs after the scatter): with
+ * fewer records than `target`, every record is cut into ceil(len / unit)
+ * parts, unit ~ class bytes / target -- parts of equal size whatever the mix
+ * of record lengths, so the work items balance over the chip.  Writes
+ * part_base (first part of each record, a block-wide scan) and part_rec
+ * (record of each part, a search in the chunk's bases in LDS). */
+__global__ __launch_bounds__(1024) void plan_kernel(PlanArgs a)
+{
+    __shared__ uint32_t sbase[1025];
+    __shared__ uint32_t wsum[16];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    uint32_t first = 0;
+    for (uint32_t k = 0; k < a.klass; ++k)
+        first += a.count[k];
+    const uint32_t count = a.count[a.klass];
+    const RecDesc *list = a.desc + first;
+    SplitPlan *pl = a.plan + a.klass;
+    if (count == 0 || count >= a.target) {
+        if (t == 0) {
+            pl->unit = 0;
+            pl->parts = count;
+            pl->direct = 1;
+        }
+        return;
+    }
+    /* each record adds at most one partial part: with unit >= bytes /
+     * (target - count) the parts never exceed target, so no team gets one
+     * item more than the others (a 2% overshoot of 2 items per team would
+     * leave the kernel waiting on teams with 3) */
+    const uint64_t room = a.target - count;
+    uint64_t unit = (a.bytes[a.klass] + room - 1) / room;
+    unit = (unit + 63) & ~63ull;
+    if (unit < a.unit_min)
+        unit = a.unit_min;
+    uint32_t running = 0;
+    for (uint32_t c0 = 0; c0 < count; c0 += 1024) {
+        const uint32_t r = c0 + t;
+        const uint32_t np = r < count ? (uint32_t)((list[r].len + unit - 1) / unit) : 0u;
+        uint32_t v = np;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t u = __shfl_up(v, o);
+            if (lane >= o)
+                v += u;
+        }
+        if (lane == 63)
+            wsum[wv] = v;
+        __syncthreads();
+        uint32_t woff = 0;
+        for (int i = 0; i < wv; ++i)
+            woff += wsum[i];
+        const uint32_t incl = running + woff + v;
+        sbase[t] = incl - np;
+        if (t == 1023)
+            sbase[1024] = incl;
+        if (r < count)
+            a.part_base[r] = incl - np;
+        __syncthreads();
+        const uint32_t lo = sbase[0], hi = sbase[1024];
+        for (uint32_t q = lo + t; q < hi; q += 1024) {
+            /* largest i with sbase[i] <= q: the record holding part q */
+            uint32_t a0 = 0, a1 = 1024;
+            while (a1 - a0 > 1) {
+                const uint32_t mid = (a0 + a1) >> 1;
+                if (sbase[mid] <= q)
+                    a0 = mid;
+                else
+                    a1 = mid;
+            }
+            a.part_rec[q] = c0 + a0;
+        }
+        running = hi;
+        __syncthreads();
+    }
+    if (t == 0) {
+        pl->unit = unit;
+        pl->parts = running;
+        pl->direct = 0;
+    }
+}
+
 __device__ __forceinline__ uint32_t xpow8(const uint32_t *pow2, uint64_t n)
 {
     uint32_t r = 0x80000000u;
@@ -1037,11 +1143,11 @@ __device__ __forceinline__ uint32_t xpow8(const uint32_t *pow2, uint64_t n)
     return r;
 }
 
-/* Fold the 2^lp part registers of every listed record (register after part p
- * = shift(register before, |part p|) ^ raw_p), then finish like emit(): plain
- * CRC, or the commit trailer + comparison in commit mode.  One block per
- * record: the m non-empty parts are m-1 parts of P bytes and a last one of
- * Lm bytes, so  reg = (XOR_p<m-1 raw_p * XP^(m-2-p)) * x^(8 Lm) ^ raw_(m-1)
+/* Fold the part registers of every record of a split class (register after
+ * part p = shift(register before, |part p|) ^ raw_p), then finish like
+ * emit(): plain CRC, or the commit trailer + comparison in commit mode.  One
+ * block per record: its m parts are m-1 parts of P = unit bytes and a last one
+ * of Lm bytes, so  reg = (XOR_p<m-1 raw_p * XP^(m-2-p)) * x^(8 Lm) ^ raw_(m-1)
  * with XP = x^(8P).  Thread t Horner-folds a contiguous run of parts and
  * shifts its partial by XP^(parts after its run); the block XOR-reduces. */
 __device__ __forceinline__ uint32_t ppow(const uint32_t (&lad)[16], uint32_t e)
@@ -1062,18 +1168,18 @@ __global__ __launch_bounds__(256) void part_fold_kernel(BatchDesc d, const uint3
         base += d.class_count[k];
     const uint64_t count = d.class_count[d.klass];
     const RecDesc *list = d.desc + base;
-    const uint32_t lp = split_log_parts(count, d.split, d.split_lpmin);
-    if (lp == 0)
+    if (((const volatile uint32_t *)&d.plan[d.klass].direct)[0])
         return; /* the team kernel emitted every record itself */
-    const uint64_t K = 1ull << lp;
+    const uint64_t P = d.plan[d.klass].unit;
+    const uint32_t nparts = ((const volatile uint32_t *)&d.plan[d.klass].parts)[0];
     const uint32_t X4 = pow2[2]; /* x^32: one slice-by-4 step */
     const int t = threadIdx.x;
     for (uint64_t idx = blockIdx.x; idx < count; idx += gridDim.x) {
         const RecDesc r = list[idx];
         const uint64_t len = r.len;
-        const uint64_t P = (((len + K - 1) >> lp) + 63) & ~63ull;
-        const uint32_t m = (uint32_t)((len + P - 1) / P); /* non-empty parts, 1..K */
-        const uint32_t *parts = d.part_out + (idx << lp);
+        const uint32_t pb = d.part_base[idx];
+        const uint32_t m = (idx + 1 < count ? d.part_base[idx + 1] : nparts) - pb; /* 1.. parts */
+        const uint32_t *parts = d.part_out + pb;
         const uint32_t nu = m - 1;                        /* uniform parts */
         const uint32_t run = (nu + 255) / 256;
         const uint32_t lo = t * run < nu ? t * run : nu;
@@ -1172,6 +1278,12 @@ extern "C" int zs_launch_classify(const zs::Classify *c, hipStream_t stream)
     if (blocks == 0)
         blocks = 1;
     hipLaunchKernelGGL(zs::classify_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, *c);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int zs_launch_plan(const zs::PlanArgs *a, hipStream_t stream)
+{
+    hipLaunchKernelGGL(zs::plan_kernel, dim3(1), dim3(1024), 0, stream, *a);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
