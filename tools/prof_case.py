@@ -1,0 +1,70 @@
+"""Profiling target: exactly REPS device passes of one BASELINE config and
+nothing else on the GPU after setup, so rocprofv3 per-dispatch counters sum to
+REPS passes (traffic per pass = sum over the zs:: dispatches / REPS).
+
+usage: python tools/prof_case.py config2|config3|config4|config5 [REPS]"""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from zeroskip_amd import device as zd  # noqa: E402
+from zeroskip_amd import zsfile  # noqa: E402
+
+
+def main():
+    cfg = sys.argv[1]
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev)
+    g.manual_seed(7)
+    if cfg == "config3":
+        data = torch.randint(0, 256, (65536 * 65536,), dtype=torch.uint8, device=dev, generator=g)
+        out = torch.empty(65536, dtype=torch.int32, device=dev)
+        run = lambda k: zd.crc_fixed(data, 65536, 65536, 65536, out=out)  # noqa: E731
+    elif cfg == "config2":
+        bufs = torch.randint(0, 256, (32, 64 << 20), dtype=torch.uint8, device=dev, generator=g)
+        out = torch.empty(1 << 20, dtype=torch.int32, device=dev)
+        run = lambda k: zd.crc_fixed(bufs[k % 32], 64, 64, 1 << 20, out=out)  # noqa: E731
+    elif cfg == "config4":
+        from tools import zsdb_gen as zg
+        ppf = zg.pairs_per_file(True)
+        nfiles = -(-10_000_000 // ppf)
+        img = zg.log_files(bytes(range(16)), 0, nfiles, ppf, 0, True, g, dev)
+        offs, lens = zg.log_spans(nfiles, ppf, True, True, dev)
+        run = lambda k: zsfile.verify_commits(img.view(-1), offs, lens)  # noqa: E731
+    elif cfg == "config5":
+        from tools import zsdb_gen as zg
+        from zeroskip_amd import consistent as cs
+        db = zg.make_db(device=dev)
+        job = cs.Consistent(cs.open_db(db), 0, 1)
+        job.prepare()
+        run = lambda k: job.run()  # noqa: E731
+    elif cfg.startswith("fixed"):
+        # fixedSTRIDE_LEN_SHIFT: 10M records of LEN bytes every STRIDE bytes, record 0 at SHIFT
+        stride, ln, shift = (int(x) for x in cfg[5:].split("_"))
+        n = 10_000_000
+        data = torch.randint(0, 256, (shift + stride * n,), dtype=torch.uint8, device=dev, generator=g)
+        out = torch.empty(n, dtype=torch.int32, device=dev)
+        run = lambda k: zd.crc_fixed(data[shift:], stride, ln, n, out=out)  # noqa: E731
+    else:
+        raise SystemExit(f"unknown config {cfg}")
+    if "ZS_DEPTH" in os.environ:
+        from zeroskip_amd._lib import lib as _l
+        _l().zscrc_set_prefetch(1, int(os.environ["ZS_DEPTH"]))
+    torch.cuda.synchronize()
+    # marker dispatch: the passes are the zs:: dispatches after this one
+    from zeroskip_amd._lib import check, lib
+    scratch = torch.zeros(4096, dtype=torch.int32, device=dev)
+    check(lib().zscrc_diag_stream_read(scratch.data_ptr(), 8192, scratch.data_ptr(), 1,
+                                       torch.cuda.current_stream().cuda_stream), "marker")
+    for k in range(reps):
+        run(k)
+    torch.cuda.synchronize()
+    print("done", cfg, reps)
+
+
+if __name__ == "__main__":
+    main()
