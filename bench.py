@@ -400,7 +400,7 @@ def run_config4(args, world, rank, dev, stream):
         e2e["note"] = "the walk and the H2D copy can overlap per file; summed here"
 
     nbytes = span_bytes + 8 * ncommit + 16 * ncommit + 8 * ncommit   # spans + trailers + descriptors + crc/status
-    r = roof(nbytes, kern_ms, "verify_commits: classify + zs::team_kernel<1> (312 B spans)",
+    r = roof(nbytes, kern_ms, "verify_commits: classify (count) + zs::burst_kernel (312 B spans)",
              traffic_for("config4_bytes_per_launch"), None)
     out_line = line(args, world, elapsed, span_bytes * world * args.steps,
                     {"workload": f"config4: zsbench writeseqtxn replay, {pairs_total} pairs per GPU, "
@@ -447,7 +447,7 @@ def run_config5(args, world, rank, dev, stream):
     ncommit = len(job.c_off)
     local_bytes = job.local.bytes_checked
     nbytes = local_bytes + 24 * ncommit + 16 * len(job.pieces)
-    r = roof(nbytes, kern_ms, "verify_commits (classify + team<1> spans + team<64> split long "
+    r = roof(nbytes, kern_ms, "verify_commits (classify + burst_kernel spans + team<64> split long "
                               "regions + part_fold) + raw pieces, this rank",
              traffic_for("config5_bytes_per_launch"), None)
     out_line = line(args, world, elapsed, job.plan.weight * args.steps,

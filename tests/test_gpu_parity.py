@@ -42,9 +42,9 @@ def teams(request, gpu):
     lib().zscrc_set_teams(1024, 1 << 20)
 
 
-@pytest.fixture(params=[-1, 1, 2, 3, 4, 5, 6, 7, 8],
+@pytest.fixture(params=[-1, 1, 2, 3, 4, 5, 6, 7, 8, 9],
                 ids=["g1-auto", "g1-ring1", "g1-ring2", "g1-short", "g1-short-pf", "g1-short-pf2",
-                     "g1-burst2", "g1-burst3", "g1-burst4"])
+                     "g1-burst2", "g1-burst3", "g1-burst4", "g1-record-burst"])
 def g1_walk(request, gpu):
     lib().zscrc_set_prefetch(1, request.param)
     yield request.param
@@ -229,6 +229,17 @@ def test_config2_full_size_vs_oracle(gpu):
     d = torch.randint(0, 256, (n * 64,), dtype=torch.uint8, device=gpu)
     out = u32(zd.crc_fixed(d, 64, 64, n))
     ref = oracle.batch(d.cpu().numpy(), n=n, stride=64, fixed_len=64, impl="hw", threads=8)
+    assert np.array_equal(out, ref)
+
+
+@pytest.mark.parametrize("n,rl,stride", [(3 << 20, 64, 64), (2_500_000, 312, 320)])
+def test_short_records_beyond_stash(gpu, n, rl, stride):
+    """More records than the short kernel keeps in LDS (8 per thread): results
+    stored per record; zeroskip-like 312/320 layout too."""
+    d = torch.randint(0, 256, (stride * (n - 1) + rl + 40,), dtype=torch.uint8, device=gpu)
+    out = u32(zd.crc_fixed(d[40:], stride, rl, n, seed=0xabc))
+    ref = oracle.batch(d[40:].cpu().numpy(), n=n, stride=stride, fixed_len=rl, impl="hw", threads=8,
+                       seeds=np.full(n, 0xabc, np.uint32))
     assert np.array_equal(out, ref)
 
 

@@ -35,6 +35,7 @@ int zs_launch_stream_read(const void *buf, uint64_t n, uint32_t *out, int grid, 
 int zs_launch_classify(const zs::Classify *c, hipStream_t stream);
 int zs_launch_part_fold(const zs::BatchDesc *d, const uint32_t *gtab, hipStream_t stream);
 int zs_launch_plan(const zs::PlanArgs *a, hipStream_t stream);
+int zs_launch_burst(int fixed, const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
 }
 
 namespace {
@@ -207,8 +208,10 @@ zs::BatchDesc make_desc()
  * items deep where the batch is fixed-stride, except 4-8 KiB G16 records. */
 int walk_for(int g, int fixed, uint64_t len)
 {
-    if (g == 1)
-        return 3;
+    if (g == 1) /* record bursts (burst_kernel) for 65..320-byte records and
+                 * variable batches; one-piece and > 5-piece fixed-stride
+                 * records: the piece walk (tools/g1_sweep.py) */
+        return fixed && (len <= 64 || len > 320) ? 3 : 9;
     if (len >= 8192)
         return 0;
     if (!fixed)
@@ -229,7 +232,8 @@ int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s, int depth_hi
     if (!fixed && depth == 2)
         depth = 1;
     zs::BatchDesc dx = d;
-    int rc = depth >= 3 ? zs_launch_short(fixed, depth - 3, &dx, c->gtab, c->ncu, s)
+    int rc = depth == 9  ? zs_launch_burst(fixed, &dx, c->gtab, c->ncu, s)
+             : depth >= 3 ? zs_launch_short(fixed, depth - 3, &dx, c->gtab, c->ncu, s)
                         : zs_launch_team(g, fixed, depth, &d, c->gtab, c->ncu, s);
     if (rc) {
         set_err("team kernel launch", hipGetLastError());
@@ -689,7 +693,7 @@ void zscrc_set_gpu_min(uint64_t min_bytes)
 
 void zscrc_set_prefetch(int g, int depth)
 {
-    if (depth < -1 || depth > (g == 1 ? 8 : 2))
+    if (depth < -1 || depth > (g == 1 ? 9 : 2))
         return;
     if (g == 1)
         g_depth[0] = depth;

@@ -926,6 +926,210 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
     }
 }
 
+/*
+ * burst_kernel: one lane per record of at most 5 pieces, all its pieces loaded
+ * at once (a burst) and then hashed, so a line the record shares with the
+ * neighbouring lane's record is requested by both lanes together and fetched
+ * once (the piece walk of short_kernel re-fetches it a record later:
+ * profiles/r01/short_record_traffic.json).  Double-buffered: the next record's
+ * burst is in flight while the current one is hashed.  512-thread workgroups
+ * (8 waves per CU, 256 VGPRs per lane) hold the two 80-VGPR bursts without
+ * spilling.  Every burst is exactly 20 loads (pieces past the record repeat
+ * its last piece, lanes without a burst load a cached dummy), so the waits are
+ * static.  Records of more pieces, or whose grid starts below the buffer's
+ * first dword: piece by piece with clamped dword loads.
+ */
+constexpr int BWG = 512;
+
+struct BRec {
+    Item it;
+    uintptr_t V0;
+    uint64_t np;
+    bool ok;    /* a record */
+    bool burst; /* <= 5 pieces, grid inside the buffer */
+};
+
+template <bool FIXED>
+__device__ __forceinline__ void burst_meta(const BatchDesc &d, const RecDesc *list, bool direct, uint64_t count,
+                                           uint64_t i, uintptr_t lo, BRec &b)
+{
+    b.ok = i < count;
+    if (!b.ok) {
+        b.burst = false;
+        b.np = 0;
+        b.V0 = lo;
+        b.it.len = 0;
+        return;
+    }
+    uint64_t off, len;
+    uint32_t seed;
+    if (FIXED) {
+        len = (d.last_len != ~0ull && i + 1 == d.n) ? d.last_len : d.fixed_len;
+        off = i * d.stride;
+        seed = d.fixed_seed;
+        b.it.rec = i;
+    } else if (direct) {
+        typedef const __attribute__((address_space(1))) uint64_t *g64p;
+        off = ((g64p)d.off)[i];
+        len = ((g64p)d.len)[i];
+        seed = d.seed ? ((g32p)d.seed)[i] : 0u;
+        b.it.rec = i;
+    } else {
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+        typedef const __attribute__((address_space(1))) u32x2 *g2p;
+        const g2p q = (g2p)(list + i);
+        const u32x2 a = q[0], c2 = q[1], c = q[2];
+        off = ((uint64_t)a.y << 32) | a.x;
+        len = ((uint64_t)c2.y << 32) | c2.x;
+        seed = c.x;
+        b.it.rec = c.y;
+    }
+    const uintptr_t A = reinterpret_cast<uintptr_t>(d.base) + off;
+    b.it.A = A;
+    b.it.len = len;
+    b.it.R0 = seed ^ d.xor_io;
+    if (!FIXED && d.commit) {
+        b.it.c0 = ((g32p)(A + len))[0];
+        b.it.c1 = ((g32p)(A + len))[1];
+    }
+    const uintptr_t E = (A + len) & ~uintptr_t(3);
+    b.it.E = E;
+    b.np = len < 8 ? 0 : (E - A + 63) >> 6;
+    b.V0 = E - b.np * 64;
+    b.burst = b.np >= 1 && b.V0 >= lo;
+}
+
+__device__ __forceinline__ void burst_issue(const BRec &b, uintptr_t dummy, uint32_t (&w)[5][16])
+{
+#pragma unroll
+    for (int p = 0; p < 5; ++p)
+        issue_plain(b.burst ? b.V0 + 64 * ((uint64_t)p < b.np ? (uint64_t)p : b.np - 1) : dummy, w[p]);
+}
+
+__device__ __forceinline__ void burst_hash(const BatchDesc &d, BRec &b, uint32_t (&w)[5][16], const char *L,
+                                           uintptr_t lo, uint32_t c_lo, uint32_t c_hi)
+{
+    Item &it = b.it;
+    const uintptr_t A = it.A, E = it.E;
+    uint32_t r;
+    if (b.np == 0) {
+        r = it.R0;
+        for (uint64_t k = 0; k < it.len; ++k)
+            r = byte_step(L, r, ((g8p)A)[k], c_hi);
+        emit(d, it, r, L, c_lo, c_hi);
+        return;
+    }
+    const uintptr_t V0 = b.V0;
+    const uint32_t spill = A + 4 > V0 + 64 ? it.R0 >> (8 * (uint32_t)(V0 + 64 - A)) : 0u;
+    if (b.burst) {
+        w[1][0] ^= b.np > 1 ? spill : 0u;
+        r = first_piece(L, it, V0, 0, w[0], c_lo, c_hi); /* V0 >= lo here */
+#pragma unroll
+        for (int p = 1; p < 5; ++p)
+            if ((uint64_t)p < b.np)
+                r = piece<false>(L, r, w[p], c_lo, c_hi);
+        /* longer records: further bursts of five pieces into the same
+         * registers (the next record's burst, issued earlier, lands first) */
+        for (uint64_t base = 5; base < b.np; base += 5) {
+#pragma unroll
+            for (int p = 0; p < 5; ++p)
+                issue_plain(V0 + 64 * (base + p < b.np ? base + p : b.np - 1), w[p]);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int p = 0; p < 5; ++p)
+                if (base + p < b.np)
+                    r = piece<false>(L, r, w[p], c_lo, c_hi);
+        }
+    } else {
+        r = 0;
+        const int32_t d0 = (int32_t)(A - V0);
+        for (uint64_t p = 0; p < b.np; ++p) {
+            const uintptr_t q = V0 + 64 * p;
+            uint32_t x[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                x[k] = *(g32p)(q + 4 * k < lo ? lo : q + 4 * k);
+            if (p < 2) {
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    const int32_t dk = d0 - 64 * (int32_t)p - 4 * k;
+                    uint32_t v = x[k];
+                    if (dk >= 4)
+                        v = 0;
+                    else if (dk > 0)
+                        v &= 0xffffffffu << (8 * dk);
+                    if (dk >= 0 && dk < 4)
+                        v ^= it.R0 << (8 * dk);
+                    else if (dk < 0 && dk > -4)
+                        v ^= it.R0 >> (8 * -dk);
+                    x[k] = v;
+                }
+            }
+            r = piece<false>(L, r, x, c_lo, c_hi);
+        }
+    }
+    const uint32_t tail = (uint32_t)((A + it.len) - E);
+    for (uint32_t k = 0; k < tail; ++k)
+        r = byte_step(L, r, ((g8p)E)[k], c_hi);
+    emit(d, it, r, L, c_lo, c_hi);
+}
+
+template <bool FIXED>
+__global__ __launch_bounds__(BWG) void burst_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
+{
+    __shared__ __attribute__((aligned(16))) char L[OFF_U];
+    uint64_t count = d.n;
+    const RecDesc *list = nullptr;
+    if (!FIXED) {
+        uint32_t base = 0;
+        for (uint32_t k = 0; k < d.klass; ++k)
+            base += __builtin_amdgcn_readfirstlane(((g32p)d.class_count)[k]);
+        count = __builtin_amdgcn_readfirstlane(((g32p)d.class_count)[d.klass]);
+        list = d.desc + base;
+    }
+    const bool direct = !FIXED && d.klass == 0 && count == d.n;
+    if ((uint64_t)blockIdx.x * BWG >= count)
+        return;
+    {
+        uint4 *L4 = reinterpret_cast<uint4 *>(L);
+        for (int i = threadIdx.x; i < 8192; i += BWG) {
+            const int dw = i * 4;
+            const int e = (dw >> 6) & 255;
+            const int tj = (dw >> 14) * 2 + ((dw >> 5) & 1);
+            const uint32_t v = gtab[GT_S4 + tj * 256 + e];
+            L4[i] = make_uint4(v, v, v, v);
+        }
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const uint32_t c_lo = (uint32_t)(lane & 31) << 2;
+    const uint32_t c_hi = c_lo | 0x10000u;
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(d.base) & ~uintptr_t(3);
+    const uintptr_t dummy = reinterpret_cast<uintptr_t>(gtab);
+    const uint64_t nthr = (uint64_t)gridDim.x * BWG;
+    uint64_t i = (uint64_t)blockIdx.x * BWG + threadIdx.x;
+    BRec ra, rb;
+    uint32_t wa[5][16], wb[5][16];
+    burst_meta<FIXED>(d, list, direct, count, i, lo, ra);
+    burst_issue(ra, dummy, wa);
+    for (;;) {
+        burst_meta<FIXED>(d, list, direct, count, i + nthr, lo, rb);
+        burst_issue(rb, dummy, wb);
+        __builtin_amdgcn_sched_barrier(0);
+        if (!ra.ok)
+            break;
+        burst_hash(d, ra, wa, L, lo, c_lo, c_hi);
+        i += nthr;
+        burst_meta<FIXED>(d, list, direct, count, i + nthr, lo, ra);
+        burst_issue(ra, dummy, wa);
+        __builtin_amdgcn_sched_barrier(0);
+        if (!rb.ok)
+            break;
+        burst_hash(d, rb, wb, L, lo, c_lo, c_hi);
+        i += nthr;
+    }
+}
+
 /* ------------------------------------------------------------ span fold */
 /* K^m from the table K^(2^b). */
 __device__ __forceinline__ uint32_t kpow(const uint32_t *kp2, uint32_t m)
@@ -1369,6 +1573,15 @@ extern "C" int zs_launch_short(int fixed, int pf, const zs::BatchDesc *d, const 
     }
 #undef ZS_SHORT_PF
 #undef ZS_SHORT
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int zs_launch_burst(int fixed, const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream)
+{
+    if (fixed)
+        hipLaunchKernelGGL((zs::burst_kernel<true>), dim3(grid), dim3(zs::BWG), 0, stream, *d, gtab);
+    else
+        hipLaunchKernelGGL((zs::burst_kernel<false>), dim3(grid), dim3(zs::BWG), 0, stream, *d, gtab);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
