@@ -54,7 +54,8 @@ int g_strict = 0;
 /* record-walk override per team size (index 0/1/2 = G 1/16/64): -1 = automatic
  * (walk_for), 0 = two-level loop, 1/2 = flattened loop with a 1/2-item ring;
  * G = 1 only: 3..8 = short_kernel (per-lane records; next piece loaded if it
- * exists / always four loads / two pieces ahead / bursts of 2, 3, 4 pieces) */
+ * exists / always four loads / two pieces ahead / bursts of 2, 3, 4 pieces),
+ * 9 = burst_kernel (a record's pieces loaded at once, next record in flight) */
 std::atomic<int> g_depth[3] = {{-1}, {-1}, {-1}};
 
 struct DevCtx {
