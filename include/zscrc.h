@@ -110,17 +110,22 @@ void zscrc_stats(uint64_t out[4]);
 /* scalar calls of at least `min_bytes` go to the GPU (0 = never; default from
  * env ZSCRC_GPU_MIN, else never). */
 void zscrc_set_gpu_min(uint64_t min_bytes);
-/* team size tuning: records <= g1_max bytes use one lane each, <= g16_max a
- * 16-lane team, larger a 64-lane (whole wavefront) team. */
+/* team size tuning: records <= g1_max bytes (default 640) use one lane each,
+ * <= g16_max (default 1 MiB) a 16-lane team, larger a 64-lane (whole
+ * wavefront) team. */
 void zscrc_set_teams(uint64_t g1_max, uint64_t g16_max);
+/* tuning: 2-lane teams on fixed-stride batches -- 0 = automatic (records of
+ * 128..1024 bytes whose length, stride and base are multiples of 128; the
+ * default), 1 = never, 2 = every record <= g1_max */
+void zscrc_set_small_team(int mode);
 /* tuning: record walk for team size g (1, 16 or 64): -1 = automatic (default),
  * 0 = two-level loop, 1 / 2 = flattened (record, step) loop with a 1- / 2-item
  * register ring; g = 1 only: 3..8 = per-lane short-record kernel (next
  * piece loaded when it exists / always / two pieces ahead / bursts of 2, 3,
  * 4 pieces) */
 void zscrc_set_prefetch(int g, int depth);
-/* team size the fixed-stride path picks for n records of len bytes (1/16/64;
- * 0 if no device) */
+/* team size the fixed-stride path picks for n packed records of len bytes
+ * from a 128-byte-aligned base (1/2/16/64; 0 if no device) */
 int zscrc_team_for(uint64_t len, uint64_t n);
 /* Diagnostic: plain streaming read of len bytes (multiple of 8192) -- the
  * measured HBM read ceiling on this GPU.  d_scratch4: 4 writable device bytes. */

@@ -13,7 +13,7 @@ from oracle import oracle
 from tests.golden.datagen import xorshift64_bytes
 from zeroskip_amd import device as zd
 from zeroskip_amd import crc32c as zc
-from zeroskip_amd._lib import lib, stats
+from zeroskip_amd._lib import DEFAULT_TEAMS, lib, stats
 
 pytestmark = pytest.mark.gpu
 
@@ -34,12 +34,12 @@ def rand_bytes(n, seed):
     return np.random.default_rng(seed).integers(0, 256, n, dtype=np.uint8)
 
 
-@pytest.fixture(params=[(1024, 1 << 20), (0, 0), (1 << 40, 1 << 40), (0, 1 << 40)],
+@pytest.fixture(params=[DEFAULT_TEAMS, (0, 0), (1 << 40, 1 << 40), (0, 1 << 40)],
                 ids=["default", "all-g64", "all-g1", "all-g16"])
 def teams(request, gpu):
     lib().zscrc_set_teams(*request.param)
     yield request.param
-    lib().zscrc_set_teams(1024, 1 << 20)
+    lib().zscrc_set_teams(*DEFAULT_TEAMS)
 
 
 @pytest.fixture(params=[-1, 1, 2, 3, 4, 5, 6, 7, 8, 9],
@@ -72,7 +72,7 @@ def test_golden_cases_g1_walks(gpu, g1_walk):
                                seeds=np.full(n - 1, M32, np.uint32)) ^ np.uint32(M32)
             assert np.array_equal(raw, ref), (stride, length, "raw")
     finally:
-        lib().zscrc_set_teams(1024, 1 << 20)
+        lib().zscrc_set_teams(*DEFAULT_TEAMS)
 
 
 def test_golden_cases_variable_batch(gpu, teams):
@@ -113,6 +113,32 @@ def test_fixed_stride(gpu, stride, length, n):
     ref = _oracle_seeded(data, stride, length, n, 0x1234)
     bad = np.nonzero(out != ref)[0]
     assert bad.size == 0, bad[:10]
+
+
+@pytest.mark.parametrize("mode,shapes", [
+    (0, [(128, 128, 50000), (256, 256, 30000), (1024, 1024, 5000), (768, 640, 8000)]),
+    (2, [(64, 64, 70000), (320, 312, 20000), (1040, 1000, 3000), (200, 200, 9000),
+         (130, 129, 5000), (7, 7, 500), (1, 1, 100), (256, 256, 3000)]),
+], ids=["auto-aligned", "forced-ragged"])
+def test_two_lane_teams(gpu, mode, shapes):
+    """2-lane teams (zscrc_set_small_team): chosen automatically on 128-byte
+    aligned records, forced onto ragged lengths, odd strides and a base 3 bytes
+    off alignment."""
+    lib().zscrc_set_small_team(mode)
+    lib().zscrc_set_teams(1024, 1 << 20)
+    try:
+        if mode == 0:
+            assert lib().zscrc_team_for(256, 1 << 20) == 2
+            assert lib().zscrc_team_for(312, 1 << 20) == 1
+        for stride, length, n in shapes:
+            data = rand_bytes(stride * (n - 1) + length + 3, stride * 3 + length)
+            out = u32(zd.crc_fixed(to_dev(data, gpu), stride, length, n, seed=0x5a5a))
+            assert np.array_equal(out, _oracle_seeded(data, stride, length, n, 0x5a5a)), (stride, length)
+            out = u32(zd.crc_fixed(to_dev(data[3:], gpu), stride, length, n, seed=7))
+            assert np.array_equal(out, _oracle_seeded(data[3:], stride, length, n, 7)), (stride, length, "+3")
+    finally:
+        lib().zscrc_set_small_team(0)
+        lib().zscrc_set_teams(*DEFAULT_TEAMS)
 
 
 def _oracle_seeded(data, stride, length, n, seed):

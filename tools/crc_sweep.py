@@ -7,7 +7,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from zeroskip_amd import device as zd  # noqa: E402
-from zeroskip_amd._lib import lib  # noqa: E402
+from zeroskip_amd._lib import DEFAULT_TEAMS, lib  # noqa: E402
 
 
 def timeit(fn, reps=10, warm=3):
@@ -34,14 +34,14 @@ def main():
         ("cfg3 64KiB g64", 65536, 65536, 65536, (0, 0)),
         ("cfg3 64KiB g16", 65536, 65536, 65536, (0, 1 << 40)),
         ("cfg3 64KiB g1", 65536, 65536, 65536, (1 << 40, 1 << 40)),
-        ("cfg2 64B g1", 64, 64, 1 << 20, (1024, 1 << 20)),
-        ("cfg2 64B g1 x16 (1 GiB)", 64, 64, 1 << 24, (1024, 1 << 20)),
-        ("zsbench 312B g1", 320, 312, 10_000_000, (1024, 1 << 20)),
+        ("cfg2 64B g1", 64, 64, 1 << 20, DEFAULT_TEAMS),
+        ("cfg2 64B g1 x16 (1 GiB)", 64, 64, 1 << 24, DEFAULT_TEAMS),
+        ("zsbench 312B g1", 320, 312, 10_000_000, DEFAULT_TEAMS),
         ("zsbench 312B g16", 320, 312, 10_000_000, (0, 1 << 40)),
         ("4KiB g1", 4096, 4096, 1 << 20, (1 << 40, 1 << 40)),
         ("4KiB g16", 4096, 4096, 1 << 20, (0, 1 << 40)),
         ("4KiB g64", 4096, 4096, 1 << 20, (0, 0)),
-        ("zsbench 312B default", 320, 312, 10_000_000, (1024, 1 << 20)),
+        ("zsbench 312B default", 320, 312, 10_000_000, DEFAULT_TEAMS),
         ("1KiB g1", 1024, 1024, 1 << 22, (1 << 40, 1 << 40)),
         ("1KiB g16", 1024, 1024, 1 << 22, (0, 1 << 40)),
         ("256KiB g16", 262144, 262144, 16384, (0, 1 << 40)),
@@ -66,7 +66,7 @@ def main():
                               "GiBs": round(byt / ms / 1e6 * 1e9 / (1 << 30), 1)}), flush=True)
     for g in (1, 16, 64):
         lib().zscrc_set_prefetch(g, -1)
-    lib().zscrc_set_teams(1024, 1 << 20)
+    lib().zscrc_set_teams(*DEFAULT_TEAMS)
     ms = timeit(lambda: zd.crc_span(big))
     print(json.dumps({"case": "span 4 GiB", "ms": round(ms, 4), "GBs": round((4 << 30) / ms / 1e6, 1)}))
 

@@ -8,6 +8,9 @@ import subprocess
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libzscrc.so")
 
+# library defaults of zscrc_set_teams(g1_max, g16_max) (zscrc_api.cpp g_g1_max, g_g16_max)
+DEFAULT_TEAMS = (640, 1 << 20)
+
 _u32, _u64, _vp, _sz, _int = (ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p,
                               ctypes.c_size_t, ctypes.c_int)
 
@@ -32,6 +35,7 @@ SIGNATURES = {
     "zscrc_stats": (None, [_vp]),
     "zscrc_set_gpu_min": (None, [_u64]),
     "zscrc_set_teams": (None, [_u64, _u64]),
+    "zscrc_set_small_team": (None, [_int]),
     "zscrc_team_for": (_int, [_u64, _u64]),
     "zscrc_set_prefetch": (None, [_int, _int]),
     "zscrc_diag_stream_read": (_int, [_vp, _u64, _vp, _int, _vp]),

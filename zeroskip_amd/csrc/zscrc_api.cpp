@@ -47,9 +47,12 @@ constexpr uint64_t SEG_MIN = 64u << 10;
 thread_local char t_err[256];
 std::atomic<uint64_t> g_stat[4];
 std::atomic<uint64_t> g_gpu_min{0};
-std::atomic<uint64_t> g_g1_max{1024};
+std::atomic<uint64_t> g_g1_max{640};
 std::atomic<uint64_t> g_g16_max{1u << 20};
 std::atomic<int> g_split_team{64}; /* team size on split long records */
+/* 2-lane teams on fixed-stride records: 0 = automatic (128-byte-aligned
+ * records of 128..1024 bytes), 1 = never, 2 = every record <= g1_max */
+std::atomic<int> g_small_team{0};
 int g_strict = 0;
 /* record-walk override per team size (index 0/1/2 = G 1/16/64): -1 = automatic
  * (walk_for), 0 = two-level loop, 1/2 = flattened loop with a 1/2-item ring;
@@ -93,6 +96,9 @@ void env_init()
     s = getenv("ZSCRC_SPLIT_TEAM");
     if (s && (atoi(s) == 16 || atoi(s) == 64))
         g_split_team = atoi(s);
+    s = getenv("ZSCRC_SMALL_TEAM");
+    if (s && atoi(s) >= 0 && atoi(s) <= 2)
+        g_small_team = atoi(s);
     s = getenv("ZSCRC_G16_MAX");
     if (s)
         g_g16_max = strtoull(s, nullptr, 0);
@@ -115,6 +121,7 @@ void build_gtab(uint32_t *t)
         zs_gf2_shift_table(t + GT_Z + 1024 * k, 64ull << k);
     for (int k = 0; k < 64; ++k)
         t[GT_POW2 + k] = zs_gf2_xpow8n(1ull << k);
+    zs_gf2_shift_table(t + GT_U2, 4 + 64);
 }
 
 /* Context of the current device, initialised on first use. */
@@ -180,11 +187,24 @@ int grow(void **p, size_t *have, size_t need)
     return ZSCRC_OK;
 }
 
-/* Team size for n records of `len` bytes: 16-lane teams keep four records
- * per wave in flight (best on >= 1 KiB records, profiles/r01/sweep), but only
- * when there are enough records to give every team one. */
-int team_for(uint64_t len, uint64_t n, int ncu)
+/* Team size for n fixed-stride records of `len` bytes at `stride` from
+ * `base` (profiles/r01/team_sweep.jsonl, same-GPU A/B of G 1 / 2 / 16):
+ *  - 2-lane teams where every record starts and ends on a 128-byte line
+ *    (each lane reads one half of each line: 4.7-5.3 TB/s from 128 B to
+ *    1 KiB, vs 2.8-4.6 one lane per record and 0.7-5.1 with 16 lanes);
+ *    unaligned records leave the two lanes' 64-byte pieces straddling lines
+ *    and one lane a piece behind, and lose to one lane per record;
+ *  - one lane per record up to g1_max (640) bytes;
+ *  - 16-lane teams above it (best from ~700 B unaligned), which keep four
+ *    records per wave in flight, when there are enough records to give every
+ *    team one; otherwise whole-wave teams. */
+int team_for(uint64_t len, uint64_t n, int ncu, uint64_t stride, uintptr_t base)
 {
+    const int st = g_small_team;
+    if (st == 2 && len <= g_g1_max)
+        return 2;
+    if (st == 0 && len >= 128 && len <= 1024 && ((len | stride | base) & 127) == 0)
+        return 2;
     if (len <= g_g1_max)
         return 1;
     if (len <= g_g16_max && n >= (uint64_t)ncu * 16 * 4)
@@ -225,7 +245,7 @@ int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s, int depth_hi
     /* fixed-stride form when no per-record arrays are involved */
     const int fixed = !d.desc && !d.off && !d.len && !d.seed && !d.commit && d.len_lo == 0 && d.len_hi == ~0ull;
     const uint64_t typical = fixed ? d.fixed_len : (d.len_lo > 0 ? d.len_lo : 1);
-    int depth = g_depth[g == 1 ? 0 : g == 16 ? 1 : 2];
+    int depth = g == 2 ? -1 : g_depth[g == 1 ? 0 : g == 16 ? 1 : 2].load();
     if (depth < 0)
         depth = depth_hint >= 0 ? depth_hint : walk_for(g, fixed, typical);
     if (g != 1 && depth > 2)
@@ -547,7 +567,8 @@ int zscrc_device_fixed(const void *d_base, uint64_t stride, uint64_t len, uint32
     d.out = d_out;
     d.n = n;
     d.xor_io = (flags & ZSCRC_RAW) ? 0u : 0xffffffffu;
-    return launch(c, team_for(len, n, c->ncu), d, static_cast<hipStream_t>(stream));
+    return launch(c, team_for(len, n, c->ncu, stride, reinterpret_cast<uintptr_t>(d_base)), d,
+                  static_cast<hipStream_t>(stream));
 }
 
 size_t zscrc_span_scratch_bytes(uint64_t len)
@@ -709,7 +730,14 @@ int zscrc_team_for(uint64_t len, uint64_t n)
     DevCtx *c;
     if (get_ctx(&c))
         return 0;
-    return team_for(len, n, c->ncu);
+    return team_for(len, n, c->ncu, len, 0);
+}
+
+void zscrc_set_small_team(int mode)
+{
+    std::call_once(g_env_once, env_init);
+    if (mode >= 0 && mode <= 2)
+        g_small_team = mode;
 }
 
 void zscrc_set_teams(uint64_t g1_max, uint64_t g16_max)

@@ -11,7 +11,8 @@ enum {
     GT_U64 = 2048,   /* shift(b<<8j, 4 + 63*64): word then skip, 64-lane team */
     GT_Z = 3072,     /* GT_Z + k*1024: shift(b<<8j, 64<<k), k = 0..5          */
     GT_POW2 = 3072 + 6 * 1024, /* 64 words: x^(8*2^k) mod P, k = 0..63          */
-    GT_WORDS = 3072 + 6 * 1024 + 64,
+    GT_U2 = 3072 + 6 * 1024 + 64, /* shift(b<<8j, 4 + 64): word then skip, 2-lane team */
+    GT_WORDS = 3072 + 6 * 1024 + 64 + 1024,
 };
 
 namespace zs {

@@ -420,11 +420,11 @@ __device__ void fill_lds(char *L, const uint32_t *__restrict__ gtab)
     }
     if (G > 1) {
         uint32_t *U = reinterpret_cast<uint32_t *>(L + OFF_U);
-        const int src = G == 16 ? GT_U16 : GT_U64;
+        const int src = G == 2 ? GT_U2 : G == 16 ? GT_U16 : GT_U64;
         for (int i = threadIdx.x; i < 1024; i += WG)
             U[i] = gtab[src + i];
         uint32_t *Z = reinterpret_cast<uint32_t *>(L + OFF_Z);
-        constexpr int NZ = G == 16 ? 4 : 6;
+        constexpr int NZ = G == 2 ? 1 : G == 16 ? 4 : 6;
         for (int i = threadIdx.x; i < NZ * 1024; i += WG)
             Z[i] = gtab[GT_Z + i];
     }
@@ -1543,6 +1543,7 @@ extern "C" int zs_launch_team(int g, int fixed, int depth, const zs::BatchDesc *
     }
     switch (g) {
     case 1: ZS_CASES(1); break;
+    case 2: ZS_CASES(2); break;
     case 16: ZS_CASES(16); break;
     case 64: ZS_CASES(64); break;
     default:
