@@ -325,10 +325,10 @@ int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s)
     cl.bytes = cbytes;
     cl.desc = desc;
     {
-        /* class 0 goes to the short kernel (walks 3..9), which can read the
-         * caller's arrays when every record is class 0 */
+        /* class 0 goes to burst_kernel (walk 9, the default), which walks
+         * the caller's arrays and skips longer records: no class-0 list */
         const int w0 = g_depth[0];
-        cl.direct_ok = g1 > 0 && (w0 < 0 || w0 >= 3);
+        cl.direct_ok = g1 > 0 && (w0 < 0 || w0 == 9);
     }
     for (int pass = 0; pass < 2; ++pass) {
         cl.pass = pass;
@@ -347,6 +347,8 @@ int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s)
     for (int k = 0; k < 4; ++k) {
         zs::BatchDesc dk = d;
         dk.klass = (uint32_t)k;
+        if (k == 0 && cl.direct_ok)
+            dk.direct_max = g1;
         if (k >= 2) {
             /* classes 2-3 with fewer records than two per team are cut into
              * equal parts (a lone 1 MiB record would otherwise be one team's

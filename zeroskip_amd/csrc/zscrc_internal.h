@@ -46,6 +46,10 @@ struct BatchDesc {
     const struct RecDesc *desc;
     const uint32_t *class_count;
     uint32_t klass;
+    /* class 0 of a variable batch, direct_max != 0: the class kernel walks the
+     * caller's off/len/seed arrays itself and skips records longer than
+     * direct_max (the other classes' kernels take them); no class-0 list */
+    uint64_t direct_max;
     /* split != 0: this class may be split into parts (plan_kernel decides
      * from the class's record count and bytes, plan[klass]); part p of
      * record part_rec[p] covers bytes [(p - part_base[rec]) * unit, +unit);
@@ -74,8 +78,10 @@ struct Classify {
     uint64_t *bytes;      /* [0..3] class byte totals; zeroed */
     RecDesc *desc;        /* n entries, class-sorted after the scatter pass */
     int pass;             /* 0 = count, 1 = scatter */
-    int direct_ok;        /* the class-0 kernel can read the caller's arrays:
-                             skip the scatter when every record is class 0 */
+    int direct_ok;        /* the class-0 kernel reads the caller's arrays
+                             (BatchDesc::direct_max): no class-0 scatter, and
+                             no scatter pass at all when every record is
+                             class 0 */
 };
 
 /* How a length class is split (written by plan_kernel on the device). */

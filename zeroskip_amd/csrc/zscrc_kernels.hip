@@ -947,6 +947,7 @@ struct BRec {
     uint64_t np;
     bool ok;    /* a record */
     bool burst; /* <= 5 pieces, grid inside the buffer */
+    bool skip;  /* another class's record (direct_max) */
 };
 
 template <bool FIXED>
@@ -954,6 +955,7 @@ __device__ __forceinline__ void burst_meta(const BatchDesc &d, const RecDesc *li
                                            uint64_t i, uintptr_t lo, BRec &b)
 {
     b.ok = i < count;
+    b.skip = false;
     if (!b.ok) {
         b.burst = false;
         b.np = 0;
@@ -970,10 +972,18 @@ __device__ __forceinline__ void burst_meta(const BatchDesc &d, const RecDesc *li
         b.it.rec = i;
     } else if (direct) {
         typedef const __attribute__((address_space(1))) uint64_t *g64p;
-        off = ((g64p)d.off)[i];
         len = ((g64p)d.len)[i];
-        seed = d.seed ? ((g32p)d.seed)[i] : 0u;
         b.it.rec = i;
+        if (d.direct_max && len > d.direct_max) {
+            b.skip = true;
+            b.burst = false;
+            b.np = 0;
+            b.V0 = lo;
+            b.it.len = 0;
+            return;
+        }
+        off = ((g64p)d.off)[i];
+        seed = d.seed ? ((g32p)d.seed)[i] : 0u;
     } else {
         typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
         typedef const __attribute__((address_space(1))) u32x2 *g2p;
@@ -1009,6 +1019,8 @@ __device__ __forceinline__ void burst_issue(const BRec &b, uintptr_t dummy, uint
 __device__ __forceinline__ void burst_hash(const BatchDesc &d, BRec &b, uint32_t (&w)[5][16], const char *L,
                                            uintptr_t lo, uint32_t c_lo, uint32_t c_hi)
 {
+    if (b.skip)
+        return;
     Item &it = b.it;
     const uintptr_t A = it.A, E = it.E;
     uint32_t r;
@@ -1086,6 +1098,8 @@ __global__ __launch_bounds__(BWG) void burst_kernel(BatchDesc d, const uint32_t 
             base += __builtin_amdgcn_readfirstlane(((g32p)d.class_count)[k]);
         count = __builtin_amdgcn_readfirstlane(((g32p)d.class_count)[d.klass]);
         list = d.desc + base;
+        if (d.direct_max && count)
+            count = d.n; /* walk every record, skip the other classes' */
     }
     const bool direct = !FIXED && d.klass == 0 && count == d.n;
     if ((uint64_t)blockIdx.x * BWG >= count)
@@ -1184,12 +1198,16 @@ __global__ __launch_bounds__(1024) void span_fold_kernel(SpanFold f)
  * in every class with one atomic per class, and scatters with LDS atomics.
  * (One global atomic per wave serialises: ~12 ns each on one address.)
  * Order inside a class is irrelevant: results go to their record index. */
+constexpr int CWG = 1024; /* classify: one block per CU at most -- the per-block
+                            class counters are same-address global atomics,
+                            which serialise at ~12 ns each */
+
 __device__ __forceinline__ int class_of(const Classify &c, uint64_t len)
 {
     return len <= c.bound[0] ? 0 : len <= c.bound[1] ? 1 : len <= c.bound[2] ? 2 : 3;
 }
 
-__global__ __launch_bounds__(256) void classify_kernel(Classify c)
+__global__ __launch_bounds__(CWG) void classify_kernel(Classify c)
 {
     __shared__ uint32_t cnt[4], slot[4], pos[4];
     if (c.pass == 1 && c.direct_ok && ((const volatile uint32_t *)c.count)[0] == c.n)
@@ -1206,12 +1224,21 @@ __global__ __launch_bounds__(256) void classify_kernel(Classify c)
     __syncthreads();
     uint32_t local[4] = {0, 0, 0, 0};
     uint64_t lbytes[4] = {0, 0, 0, 0};
-    for (uint64_t rec = r0 + threadIdx.x; rec < r1; rec += 256) {
-        const uint64_t len = lens[rec];
-        const int k = class_of(c, len);
-        local[k]++;
-        if (c.pass == 0)
-            lbytes[k] += len;
+    constexpr int CL = 8; /* lengths in flight per thread */
+    for (uint64_t rb = r0 + threadIdx.x; rb < r1; rb += CWG * CL) {
+        uint64_t v[CL];
+#pragma unroll
+        for (int j = 0; j < CL; ++j)
+            v[j] = rb + CWG * j < r1 ? lens[rb + CWG * j] : ~0ull;
+#pragma unroll
+        for (int j = 0; j < CL; ++j) {
+            if (rb + CWG * j >= r1)
+                continue;
+            const int k = class_of(c, v[j]);
+            local[k]++;
+            if (c.pass == 0)
+                lbytes[k] += v[j];
+        }
     }
     __shared__ unsigned long long bsum[4];
     if (threadIdx.x < 4)
@@ -1247,13 +1274,15 @@ __global__ __launch_bounds__(256) void classify_kernel(Classify c)
         slot[threadIdx.x] = base + (cnt[threadIdx.x] ? atomicAdd(&c.count[4 + threadIdx.x], cnt[threadIdx.x]) : 0);
     }
     __syncthreads();
-    for (uint64_t b = r0 + (threadIdx.x & ~63u); b < r1; b += 256) {
+    for (uint64_t b = r0 + (threadIdx.x & ~63u); b < r1; b += CWG) {
         const uint64_t rec = b + lane;
         int cls = -1;
         uint64_t len = 0;
         if (rec < r1) {
             len = lens[rec];
             cls = class_of(c, len);
+            if (cls == 0 && c.direct_ok)
+                cls = -1; /* the class-0 kernel reads the caller's arrays */
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -1495,12 +1524,12 @@ __global__ __launch_bounds__(1024) void stream_read_kernel(const uint8_t *buf, u
 /* ------------------------------------------------------------ launchers */
 extern "C" int zs_launch_classify(const zs::Classify *c, hipStream_t stream)
 {
-    uint64_t blocks = (c->n + 4095) / 4096;
-    if (blocks > 2048)
-        blocks = 2048;
+    uint64_t blocks = (c->n + 8191) / 8192;
+    if (blocks > 256)
+        blocks = 256;
     if (blocks == 0)
         blocks = 1;
-    hipLaunchKernelGGL(zs::classify_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, *c);
+    hipLaunchKernelGGL(zs::classify_kernel, dim3((uint32_t)blocks), dim3(zs::CWG), 0, stream, *c);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
