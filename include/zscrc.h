@@ -86,6 +86,16 @@ int zscrc_device_batch(const void *d_base, const uint64_t *d_off, const uint64_t
                        const uint32_t *d_seed, uint32_t *d_out, size_t n,
                        unsigned flags, void *stream);
 
+/* As zscrc_device_batch, with a caller-known bound on the record lengths:
+ * max_len >= every d_len[i] (ZSCRC_LEN_UNBOUNDED: none known).  A bound of
+ * short records (<= 640 bytes by default) skips the device-side length
+ * classification: one kernel over the caller's arrays.  Results never depend
+ * on the bound; a wrong one costs only time. */
+#define ZSCRC_LEN_UNBOUNDED UINT64_MAX
+int zscrc_device_batch_bounded(const void *d_base, const uint64_t *d_off, const uint64_t *d_len,
+                               const uint32_t *d_seed, uint32_t *d_out, size_t n, unsigned flags,
+                               uint64_t max_len, void *stream);
+
 /* Device-resident fixed-stride batch: record i = d_base[i*stride .. +len). */
 int zscrc_device_fixed(const void *d_base, uint64_t stride, uint64_t len, uint32_t seed,
                        uint32_t *d_out, size_t n, unsigned flags, void *stream);
@@ -193,6 +203,13 @@ int zscrc_device_verify_commits(const void *d_image, const uint64_t *d_span_off,
 int zscrc_device_verify_commits_seeded(const void *d_image, const uint64_t *d_span_off,
                                        const uint64_t *d_span_len, const uint32_t *d_seed, size_t n,
                                        uint32_t *d_crc, uint32_t *d_status, void *stream);
+
+/* Device: zscrc_device_verify_commits_seeded (d_seed may be NULL) with a
+ * caller-known bound on the span lengths, as zscrc_device_batch_bounded --
+ * the host walk that found the commits knows it. */
+int zscrc_device_verify_commits_bounded(const void *d_image, const uint64_t *d_span_off,
+                                        const uint64_t *d_span_len, const uint32_t *d_seed, size_t n,
+                                        uint64_t max_len, uint32_t *d_crc, uint32_t *d_status, void *stream);
 
 /* Device: compute n commit CRCs (the writer's side, zeroskip-file.c:253-350)
  * and store each one big-endian into its commit record; d_crc[i] receives it. */

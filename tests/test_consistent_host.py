@@ -29,7 +29,9 @@ class OracleBackend:
     def empty(self, n):
         return torch.zeros(max(n, 1), dtype=torch.uint8)
 
-    def verify(self, buf, off, ln, seed=None):
+    def verify(self, buf, off, ln, seed=None, max_len=None):
+        # the bound the product passes to zscrc_device_verify_commits_bounded must hold
+        assert max_len is None or all(n <= max_len for n in ln.tolist())
         img = buf.numpy()
         crc, st = [], []
         seeds = [0] * len(off) if seed is None else [v & M32 for v in seed.tolist()]
@@ -49,7 +51,8 @@ class OracleBackend:
         r = [oracle.crc32c_hw(M32, img[o:o + n]) ^ M32 for o, n in zip(off.tolist(), ln.tolist())]
         return torch.tensor(np.array(r, np.uint32).view(np.int32))
 
-    def crc(self, buf, off, ln):
+    def crc(self, buf, off, ln, max_len=None):
+        assert max_len is None or all(n <= max_len for n in ln.tolist())
         img = buf.numpy()
         r = [oracle.crc32c_hw(0, img[o:o + n]) for o, n in zip(off.tolist(), ln.tolist())]
         return torch.tensor(np.array(r, np.uint32).view(np.int32))

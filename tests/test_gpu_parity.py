@@ -141,6 +141,31 @@ def test_two_lane_teams(gpu, mode, shapes):
         lib().zscrc_set_teams(*DEFAULT_TEAMS)
 
 
+@pytest.mark.parametrize("bound", ["exact", "loose", "wrong", "none"])
+def test_bounded_batch(gpu, bound):
+    """zscrc_device_batch_bounded: a length bound of short records takes one
+    kernel over the caller's arrays; results never depend on the bound (a
+    wrong one included)."""
+    rng = np.random.default_rng(11)
+    n = 40000
+    lens = rng.integers(0, 400, n).astype(np.uint64)
+    lens[::97] = rng.integers(401, 5000, lens[::97].size)   # a few longer ones
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1] + rng.integers(0, 9, n - 1).astype(np.uint64))
+    data = rand_bytes(int(offs[-1] + lens[-1]) + 8, 5)
+    seeds = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    ref = oracle.batch(data, offs, lens, seeds, impl="hw", threads=8)
+    mx = {"exact": int(lens.max()), "loose": 640, "wrong": 300, "none": None}[bound]
+    if bound == "exact":
+        lens = np.minimum(lens, 600).astype(np.uint64)      # all short: the one-kernel path
+        ref = oracle.batch(data, offs, lens, seeds, impl="hw", threads=8)
+        mx = int(lens.max())
+    d = to_dev(data, gpu)
+    out = u32(zd.crc_batch(d, to_dev(offs.astype(np.int64), gpu), to_dev(lens.astype(np.int64), gpu),
+                           to_dev(seeds.view(np.int32), gpu), max_len=mx))
+    assert np.array_equal(out, ref), np.nonzero(out != ref)[0][:10]
+
+
 def _oracle_seeded(data, stride, length, n, seed):
     offs = np.arange(n, dtype=np.uint64) * stride
     lens = np.full(n, length, dtype=np.uint64)

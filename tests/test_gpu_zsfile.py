@@ -73,11 +73,18 @@ def test_device_commits_match_oracle_crcs(gpu):
         imgs.append(img)
         base += len(img)
     d = torch.from_numpy(np.frombuffer(b"".join(imgs), dtype=np.uint8).copy()).cuda()
-    crc, st = zsfile.verify_commits(d, torch.tensor(offs, dtype=torch.int64, device="cuda"),
-                                    torch.tensor(lens, dtype=torch.int64, device="cuda"))
-    torch.cuda.synchronize()
-    assert (st.cpu().numpy() == 1).all()
-    assert (crc.cpu().numpy().view(np.uint32) == np.array(want, dtype=np.uint32)).all()
+    d_off = torch.tensor(offs, dtype=torch.int64, device="cuda")
+    d_len = torch.tensor(lens, dtype=torch.int64, device="cuda")
+    # unbounded, the walk's exact bound, a short (wrong) bound, and the
+    # one-kernel path over the short spans only
+    short = [i for i, n in enumerate(lens) if n <= 640]
+    for mx, ix in [(None, None), (max(lens), None), (64, None), (640, short)]:
+        o, ln = (d_off, d_len) if ix is None else (d_off[ix], d_len[ix])
+        crc, st = zsfile.verify_commits(d, o, ln, max_len=mx)
+        torch.cuda.synchronize()
+        w = np.array(want, dtype=np.uint32) if ix is None else np.array(want, dtype=np.uint32)[ix]
+        assert (st.cpu().numpy() == 1).all(), mx
+        assert (crc.cpu().numpy().view(np.uint32) == w).all(), mx
 
 
 def test_write_commits_matches_writer(gpu):

@@ -34,7 +34,8 @@ def main():
         nfiles = -(-10_000_000 // ppf)
         img = zg.log_files(bytes(range(16)), 0, nfiles, ppf, 0, True, g, dev)
         offs, lens = zg.log_spans(nfiles, ppf, True, True, dev)
-        run = lambda k: zsfile.verify_commits(img.view(-1), offs, lens)  # noqa: E731
+        mx = int(lens.max().item())
+        run = lambda k: zsfile.verify_commits(img.view(-1), offs, lens, max_len=mx)  # noqa: E731
     elif cfg == "config5":
         from tools import zsdb_gen as zg
         from zeroskip_amd import consistent as cs

@@ -46,6 +46,8 @@ SIGNATURES = {
     "zscrc_zs_dotzsdb_crc": (_int, [_vp, _u64, _vp, _vp]),
     "zscrc_device_verify_commits": (_int, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
     "zscrc_device_verify_commits_seeded": (_int, [_vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp]),
+    "zscrc_device_verify_commits_bounded": (_int, [_vp, _vp, _vp, _vp, _sz, _u64, _vp, _vp, _vp]),
+    "zscrc_device_batch_bounded": (_int, [_vp, _vp, _vp, _vp, _vp, _sz, ctypes.c_uint, _u64, _vp]),
     "zscrc_zs_verify_image": (_int, [_vp, _u64, _int, _vp]),
     "zscrc_device_write_commits": (_int, [_vp, _vp, _vp, _sz, _vp, _vp]),
     "zscrc_stream_open": (_int, [_vp, _u32, _u64, ctypes.c_uint]),
@@ -55,6 +57,7 @@ SIGNATURES = {
 }
 
 ZSCRC_RAW = 1
+LEN_UNBOUNDED = (1 << 64) - 1  # ZSCRC_LEN_UNBOUNDED
 ZSCRC_STREAM_NOCOPY = 1
 
 _lib = None

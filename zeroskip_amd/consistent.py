@@ -223,16 +223,16 @@ class GpuBackend:
     def empty(self, n: int) -> torch.Tensor:
         return torch.empty(max(n, 1), dtype=torch.uint8, device=self.device)
 
-    def verify(self, buf, off, ln, seed=None):
-        return zsfile.verify_commits(buf, off, ln, seed)
+    def verify(self, buf, off, ln, seed=None, max_len=None):
+        return zsfile.verify_commits(buf, off, ln, seed, max_len)
 
     def raw(self, buf, off, ln):
         from .device import crc_batch
         return crc_batch(buf, off, ln, raw=True)
 
-    def crc(self, buf, off, ln):
+    def crc(self, buf, off, ln, max_len=None):
         from .device import crc_batch
-        return crc_batch(buf, off, ln)
+        return crc_batch(buf, off, ln, max_len=max_len)
 
     def sync(self):
         torch.cuda.synchronize(self.device)
@@ -361,6 +361,8 @@ class Consistent:
                 pieces.append((u.fid, u.piece, u.lo, u.hi, p))
         cat = (lambda xs: np.concatenate(xs) if xs else np.zeros(0, np.int64))
         self.c_off, self.c_len, self.c_file, self.c_rec = map(cat, (c_off, c_len, c_file, c_rec))
+        # longest span, for zscrc_device_verify_commits_bounded (the host walk knows it)
+        self.c_max = int(self.c_len.max()) if len(self.c_len) else 0
         self.pieces = pieces
         dev = self.buf.device
         self.d_off = torch.from_numpy(self.c_off).to(dev)
@@ -409,7 +411,9 @@ class Consistent:
         if events:
             events[0].record()
         if n:
-            crc, st = be.verify(self.buf, self.d_off, self.d_len)
+            # the host walk knows the longest span: short-span batches skip
+            # the device-side length classes (zscrc_device_verify_commits_bounded)
+            crc, st = be.verify(self.buf, self.d_off, self.d_len, max_len=self.c_max)
         raw = be.raw(self.buf, self.d_poff, self.d_plen) if self.pieces else None
         if events:
             events[1].record()
@@ -427,8 +431,9 @@ class Consistent:
         stale_i = np.zeros(0, np.int64)
         if len(q):
             dq = torch.from_numpy(q).to(self.d_off.device)
-            prev = be.crc(self.buf, self.d_off[dq - 1], self.d_len[dq - 1])
-            _, st2 = be.verify(self.buf, self.d_off[dq], self.d_len[dq], prev)
+            prev = be.crc(self.buf, self.d_off[dq - 1], self.d_len[dq - 1],
+                          max_len=int(self.c_len[q - 1].max()))
+            _, st2 = be.verify(self.buf, self.d_off[dq], self.d_len[dq], prev, max_len=0)
             stale_i = q[(st2 == 1).cpu().numpy()]
         bad_i = np.setdiff1d(bad_idx, stale_i, assume_unique=True)
 

@@ -274,9 +274,17 @@ int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s, int depth_hi
  * Classes 2-3 with fewer records than two per team are cut into equal parts
  * (unit ~ class bytes / items wanted, plan_kernel) and a fold kernel combines
  * each record's part registers. */
-int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s)
+int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t max_len = ZSCRC_LEN_UNBOUNDED)
 {
     const uint64_t g1 = g_g1_max, g16 = g_g16_max;
+    {
+        /* the caller bounds every length by one-lane records: burst_kernel
+         * straight over the caller's arrays, no classify (it is correct for
+         * any length, so a wrong bound costs only time) */
+        const int w0 = g_depth[0];
+        if (max_len <= g1 && (w0 < 0 || w0 == 9))
+            return launch(c, 1, d, s, 9);
+    }
     const uint64_t n = d.n;
     uint64_t b1 = g16 < 8191 ? g16 : 8191;
     if (b1 < g1)
@@ -530,6 +538,14 @@ int zscrc_device_batch(const void *d_base, const uint64_t *d_off, const uint64_t
                        const uint32_t *d_seed, uint32_t *d_out, size_t n, unsigned flags,
                        void *stream)
 {
+    return zscrc_device_batch_bounded(d_base, d_off, d_len, d_seed, d_out, n, flags, ZSCRC_LEN_UNBOUNDED,
+                                      stream);
+}
+
+int zscrc_device_batch_bounded(const void *d_base, const uint64_t *d_off, const uint64_t *d_len,
+                               const uint32_t *d_seed, uint32_t *d_out, size_t n, unsigned flags,
+                               uint64_t max_len, void *stream)
+{
     if (n == 0)
         return ZSCRC_OK;
     if (!d_base || !d_off || !d_len || !d_out)
@@ -547,7 +563,7 @@ int zscrc_device_batch(const void *d_base, const uint64_t *d_off, const uint64_t
     d.out = d_out;
     d.n = n;
     d.xor_io = (flags & ZSCRC_RAW) ? 0u : 0xffffffffu;
-    return launch_classes(c, d, s);
+    return launch_classes(c, d, s, max_len);
 }
 
 int zscrc_device_fixed(const void *d_base, uint64_t stride, uint64_t len, uint32_t seed,
@@ -678,7 +694,7 @@ int zscrc_diag_stream_read(const void *d_buf, uint64_t len, void *d_scratch4, in
 
 int zscrc_internal_verify_commits(const void *d_image, const uint64_t *d_off, const uint64_t *d_len,
                                   const uint32_t *d_seed, uint32_t *d_crc, uint32_t *d_status, size_t n,
-                                  void *stream, int write)
+                                  void *stream, int write, uint64_t max_len)
 {
     if (n == 0)
         return ZSCRC_OK;
@@ -698,7 +714,7 @@ int zscrc_internal_verify_commits(const void *d_image, const uint64_t *d_off, co
     d.commit = write ? 2u : 1u;
     d.n = n;
     d.xor_io = 0xffffffffu;
-    return launch_classes(c, d, static_cast<hipStream_t>(stream));
+    return launch_classes(c, d, static_cast<hipStream_t>(stream), max_len);
 }
 
 const char *zscrc_last_error(void) { return t_err; }

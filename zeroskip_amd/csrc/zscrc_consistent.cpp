@@ -117,8 +117,11 @@ int verify_group(std::vector<DbFile> &files, size_t a, size_t b, zscrc_consisten
         e = hipMemcpy(dlen, hlen.data(), ncommit * 8, hipMemcpyHostToDevice);
     int rc = e == hipSuccess ? ZSCRC_OK : ZSCRC_EHIP;
     std::vector<uint32_t> st(ncommit);
+    uint64_t max_len = 0;
+    for (uint64_t l : hlen)
+        max_len = l > max_len ? l : max_len;
     if (!rc)
-        rc = zscrc_device_verify_commits(dimg, doff, dlen, ncommit, dcrc, dst, nullptr);
+        rc = zscrc_device_verify_commits_bounded(dimg, doff, dlen, nullptr, ncommit, max_len, dcrc, dst, nullptr);
     if (!rc && hipMemcpy(st.data(), dst, ncommit * 4, hipMemcpyDeviceToHost) != hipSuccess)
         rc = ZSCRC_EHIP;
     /* zero-length mismatches right after a commit of the same file: the
@@ -133,7 +136,9 @@ int verify_group(std::vector<DbFile> &files, size_t a, size_t b, zscrc_consisten
     if (!rc && !cand.empty()) {
         const size_t m = cand.size();
         std::vector<uint64_t> q(4 * m);
+        uint64_t prev_max = 0;
         for (size_t c = 0; c < m; ++c) {
+            prev_max = hlen[cand[c] - 1] > prev_max ? hlen[cand[c] - 1] : prev_max;
             q[c] = hoff[cand[c] - 1];
             q[m + c] = hlen[cand[c] - 1];
             q[2 * m + c] = hoff[cand[c]];
@@ -148,10 +153,10 @@ int verify_group(std::vector<DbFile> &files, size_t a, size_t b, zscrc_consisten
         }
         rc = e == hipSuccess ? ZSCRC_OK : ZSCRC_EHIP;
         if (!rc)
-            rc = zscrc_device_batch(dimg, dq, dq + m, nullptr, dprev, m, 0, nullptr);
-        if (!rc)
-            rc = zscrc_device_verify_commits_seeded(dimg, dq + 2 * m, dq + 3 * m, dprev, m, dprev + m,
-                                                    dprev + 2 * m, nullptr);
+            rc = zscrc_device_batch_bounded(dimg, dq, dq + m, nullptr, dprev, m, 0, prev_max, nullptr);
+        if (!rc) /* the candidates are zero-length spans */
+            rc = zscrc_device_verify_commits_bounded(dimg, dq + 2 * m, dq + 3 * m, dprev, m, 0, dprev + m,
+                                                     dprev + 2 * m, nullptr);
         if (!rc && hipMemcpy(st2.data(), dprev + 2 * m, m * 4, hipMemcpyDeviceToHost) != hipSuccess)
             rc = ZSCRC_EHIP;
         if (dq)

@@ -1092,7 +1092,7 @@ __global__ __launch_bounds__(BWG) void burst_kernel(BatchDesc d, const uint32_t 
     __shared__ __attribute__((aligned(16))) char L[OFF_U];
     uint64_t count = d.n;
     const RecDesc *list = nullptr;
-    if (!FIXED) {
+    if (!FIXED && d.class_count) { /* no classes: every record, caller's arrays */
         uint32_t base = 0;
         for (uint32_t k = 0; k < d.klass; ++k)
             base += __builtin_amdgcn_readfirstlane(((g32p)d.class_count)[k]);

@@ -32,7 +32,7 @@
 extern "C" int zscrc_internal_verify_commits(const void *d_image, const uint64_t *d_off, const uint64_t *d_len,
                                              const uint32_t *d_seed,
                                              uint32_t *d_crc, uint32_t *d_status, size_t n, void *stream,
-                                             int write);
+                                             int write, uint64_t max_len);
 
 namespace {
 
@@ -220,20 +220,31 @@ int zscrc_zs_dotzsdb_crc(const void *image, uint64_t size, uint32_t *stored, uin
 int zscrc_device_verify_commits(const void *d_image, const uint64_t *d_span_off, const uint64_t *d_span_len,
                                 size_t n, uint32_t *d_crc, uint32_t *d_status, void *stream)
 {
-    return zscrc_internal_verify_commits(d_image, d_span_off, d_span_len, nullptr, d_crc, d_status, n, stream, 0);
+    return zscrc_internal_verify_commits(d_image, d_span_off, d_span_len, nullptr, d_crc, d_status, n, stream, 0,
+                                         ZSCRC_LEN_UNBOUNDED);
 }
 
 int zscrc_device_verify_commits_seeded(const void *d_image, const uint64_t *d_span_off,
                                        const uint64_t *d_span_len, const uint32_t *d_seed, size_t n,
                                        uint32_t *d_crc, uint32_t *d_status, void *stream)
 {
-    return zscrc_internal_verify_commits(d_image, d_span_off, d_span_len, d_seed, d_crc, d_status, n, stream, 0);
+    return zscrc_internal_verify_commits(d_image, d_span_off, d_span_len, d_seed, d_crc, d_status, n, stream, 0,
+                                         ZSCRC_LEN_UNBOUNDED);
+}
+
+int zscrc_device_verify_commits_bounded(const void *d_image, const uint64_t *d_span_off,
+                                        const uint64_t *d_span_len, const uint32_t *d_seed, size_t n,
+                                        uint64_t max_len, uint32_t *d_crc, uint32_t *d_status, void *stream)
+{
+    return zscrc_internal_verify_commits(d_image, d_span_off, d_span_len, d_seed, d_crc, d_status, n, stream, 0,
+                                         max_len);
 }
 
 int zscrc_device_write_commits(void *d_image, const uint64_t *d_span_off, const uint64_t *d_span_len, size_t n,
                                uint32_t *d_crc, void *stream)
 {
-    return zscrc_internal_verify_commits(d_image, d_span_off, d_span_len, nullptr, d_crc, nullptr, n, stream, 1);
+    return zscrc_internal_verify_commits(d_image, d_span_off, d_span_len, nullptr, d_crc, nullptr, n, stream, 1,
+                                         ZSCRC_LEN_UNBOUNDED);
 }
 
 int zscrc_zs_verify_image(const void *image, uint64_t size, int kind, zscrc_zs_report *rep)
@@ -289,7 +300,10 @@ int zscrc_zs_verify_image(const void *image, uint64_t size, int kind, zscrc_zs_r
         if (e != hipSuccess) {
             rc = ZSCRC_EHIP;
         } else {
-            rc = zscrc_device_verify_commits(dimg, doff, dlen, n, dcrc, dst, nullptr);
+            uint64_t max_len = 0;
+            for (size_t i = 0; i < n; ++i)
+                max_len = len[i] > max_len ? len[i] : max_len;
+            rc = zscrc_device_verify_commits_bounded(dimg, doff, dlen, nullptr, n, max_len, dcrc, dst, nullptr);
             uint32_t *st = static_cast<uint32_t *>(malloc(n * 4));
             if (!rc && st && hipMemcpy(st, dst, n * 4, hipMemcpyDeviceToHost) == hipSuccess) {
                 for (size_t i = 0; i < n; ++i) {

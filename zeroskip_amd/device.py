@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import torch
 
-from ._lib import ZSCRC_RAW, check, lib
+from ._lib import LEN_UNBOUNDED, ZSCRC_RAW, check, lib
 
 
 def _stream(device: torch.device) -> int:
@@ -41,8 +41,10 @@ def crc_fixed(data: torch.Tensor, stride: int, length: int, n: int, seed: int = 
 
 def crc_batch(data: torch.Tensor, offs: torch.Tensor, lens: torch.Tensor,
               seeds: torch.Tensor | None = None, out: torch.Tensor | None = None,
-              raw: bool = False) -> torch.Tensor:
-    """out[i] = crc32c(seeds[i], data[offs[i] : offs[i]+lens[i]]) (int64 offs/lens)."""
+              raw: bool = False, max_len: int | None = None) -> torch.Tensor:
+    """out[i] = crc32c(seeds[i], data[offs[i] : offs[i]+lens[i]]) (int64 offs/lens).
+    max_len: a known bound on every lens[i] (zscrc_device_batch_bounded);
+    results never depend on it."""
     dev = _dev(data)
     n = offs.numel()
     if offs.dtype != torch.int64 or lens.dtype != torch.int64:
@@ -52,10 +54,11 @@ def crc_batch(data: torch.Tensor, offs: torch.Tensor, lens: torch.Tensor,
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=dev)
     with torch.cuda.device(dev):
-        check(lib().zscrc_device_batch(data.data_ptr(), offs.data_ptr(), lens.data_ptr(),
-                                       None if seeds is None else seeds.data_ptr(),
-                                       out.data_ptr(), n, ZSCRC_RAW if raw else 0,
-                                       _stream(dev)), "zscrc_device_batch")
+        check(lib().zscrc_device_batch_bounded(data.data_ptr(), offs.data_ptr(), lens.data_ptr(),
+                                               None if seeds is None else seeds.data_ptr(),
+                                               out.data_ptr(), n, ZSCRC_RAW if raw else 0,
+                                               LEN_UNBOUNDED if max_len is None else max_len,
+                                               _stream(dev)), "zscrc_device_batch_bounded")
     return out
 
 

@@ -80,18 +80,26 @@ def verify_image(image, kind: int = ACTIVE) -> dict:
 
 
 def verify_commits(d_image: torch.Tensor, span_off: torch.Tensor, span_len: torch.Tensor,
-                   seed: torch.Tensor | None = None):
+                   seed: torch.Tensor | None = None, max_len: int | None = None):
     """Device-resident commit verification: (crc, status) int32 tensors;
     status 1 = stored CRC matches, 0 = mismatch, 2 = no commit record.
     seed (int32, optional): span i's CRC continues from seed[i]
     (zscrc_device_verify_commits_seeded) -- the reference's zero-length
-    finalise commit chains from the previous span's CRC."""
+    finalise commit chains from the previous span's CRC.
+    max_len (optional): a known bound on the span lengths, e.g. from the host
+    walk (zscrc_device_verify_commits_bounded); results never depend on it."""
     n = span_off.numel()
     crc = torch.empty(n, dtype=torch.int32, device=d_image.device)
     st = torch.empty(n, dtype=torch.int32, device=d_image.device)
     with torch.cuda.device(d_image.device):
         stream = torch.cuda.current_stream(d_image.device).cuda_stream
-        if seed is None:
+        if max_len is not None:
+            assert seed is None or (seed.numel() == n and seed.dtype == torch.int32)
+            check(lib().zscrc_device_verify_commits_bounded(
+                d_image.data_ptr(), span_off.data_ptr(), span_len.data_ptr(),
+                None if seed is None else seed.data_ptr(), n, max_len, crc.data_ptr(), st.data_ptr(),
+                stream), "zscrc_device_verify_commits_bounded")
+        elif seed is None:
             check(lib().zscrc_device_verify_commits(
                 d_image.data_ptr(), span_off.data_ptr(), span_len.data_ptr(), n, crc.data_ptr(),
                 st.data_ptr(), stream), "zscrc_device_verify_commits")
