@@ -329,3 +329,34 @@ def test_sharded_span_gpu_partials(gpu):
         assert p.exitcode == 0
     want = oracle.crc32c_hw(0x77, np.random.default_rng(321).integers(0, 256, total, dtype=np.uint8))
     assert all(c == want for _, c in res)
+
+
+def test_beyond_4gib(gpu):
+    """64-bit offsets and lengths: a 4.5 GiB buffer -- the whole-buffer span,
+    one record longer than 4 GiB (split plan), records straddling and past the
+    4 GiB offset (one-lane and team kernels), bounded and unbounded."""
+    total = (4 << 30) + (512 << 20) + 77
+    g = torch.Generator(device=gpu)
+    g.manual_seed(4242)
+    d = torch.randint(0, 256, (total,), dtype=torch.uint8, device=gpu, generator=g)
+    h = d.cpu().numpy()
+    four = 1 << 32
+    rng = np.random.default_rng(3)
+    offs = [0, four - 100, four - 3, four + 5, four + 1000, total - 5000, 7]
+    lens = [four + 77, 300, 70, 64, 20000, 5000, 1 << 20]
+    so = rng.integers(four, total - 700, 20000).astype(np.uint64)   # short records past 4 GiB
+    offs = np.concatenate([np.array(offs, np.uint64), so])
+    lens = np.concatenate([np.array(lens, np.uint64), rng.integers(0, 640, so.size).astype(np.uint64)])
+    ref = oracle.batch(h, offs, lens, impl="hw", threads=8)
+    d_off = to_dev(offs.astype(np.int64), gpu)
+    d_len = to_dev(lens.astype(np.int64), gpu)
+    assert np.array_equal(u32(zd.crc_batch(d, d_off, d_len)), ref)
+    short = slice(7, None)
+    assert np.array_equal(u32(zd.crc_batch(d, d_off[short], d_len[short], max_len=640)), ref[short])
+    whole = oracle.batch(h, np.array([0], np.uint64), np.array([total], np.uint64), impl="hw", threads=1)[0]
+    assert u32(zd.crc_span(d))[0] == whole
+    # fixed stride with record i at i * 600 MiB: offsets past 4 GiB in the fixed path
+    stride, ln = 600 << 20, 1 << 20
+    n = (total - ln) // stride + 1
+    ref_f = oracle.batch(h, n=n, stride=stride, fixed_len=ln, impl="hw", threads=8)
+    assert np.array_equal(u32(zd.crc_fixed(d, stride, ln, n)), ref_f)
