@@ -360,3 +360,33 @@ def test_beyond_4gib(gpu):
     n = (total - ln) // stride + 1
     ref_f = oracle.batch(h, n=n, stride=stride, fixed_len=ln, impl="hw", threads=8)
     assert np.array_equal(u32(zd.crc_fixed(d, stride, ln, n)), ref_f)
+
+
+def test_two_streams_share_scratch(gpu):
+    """Variable batches and spans enqueued alternately on two streams without
+    host synchronisation: the device's shared class lists / part registers
+    must be ordered across the streams (scratch_acquire/release)."""
+    rng = np.random.default_rng(21)
+    cases = []
+    for k in range(2):
+        n = 3000
+        lens = rng.integers(0, 3000, n).astype(np.uint64)
+        lens[:3] = [5 << 20, 3 << 20, 70000]                  # split classes too
+        offs = np.zeros(n, np.uint64)
+        offs[1:] = np.cumsum(lens[:-1])
+        data = rand_bytes(int(offs[-1] + lens[-1]), 50 + k)
+        cases.append((to_dev(data, gpu), to_dev(offs.astype(np.int64), gpu), to_dev(lens.astype(np.int64), gpu),
+                      oracle.batch(data, offs, lens, impl="hw", threads=8),
+                      oracle.batch(data, np.array([0], np.uint64), np.array([data.size], np.uint64),
+                                   impl="hw")[0]))
+    streams = [torch.cuda.Stream(gpu), torch.cuda.Stream(gpu)]
+    outs = []
+    for rep in range(6):
+        for k, st in enumerate(streams):
+            d, o, ln, _, _ = cases[k]
+            with torch.cuda.stream(st):
+                outs.append((k, zd.crc_batch(d, o, ln), zd.crc_span(d)))
+    torch.cuda.synchronize()
+    for k, b, sp in outs:
+        assert np.array_equal(b.cpu().numpy().view(np.uint32), cases[k][3])
+        assert (sp.cpu().numpy().view(np.uint32)[0]) == cases[k][4]

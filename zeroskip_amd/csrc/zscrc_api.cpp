@@ -74,6 +74,9 @@ struct DevCtx {
     size_t classes_bytes = 0;
     void *parts = nullptr;     /* part registers of split long records */
     size_t parts_bytes = 0;
+    hipEvent_t last = nullptr; /* end of the last scratch user's work ... */
+    hipStream_t last_stream = nullptr; /* ... enqueued on this stream */
+    bool last_valid = false;
 };
 DevCtx g_ctx[MAX_DEV];
 std::once_flag g_env_once;
@@ -187,6 +190,51 @@ int grow(void **p, size_t *have, size_t need)
     return ZSCRC_OK;
 }
 
+/* The scratch buffers (class lists, part registers, span partials) are
+ * shared by every call on a device.  A call on another stream than the last
+ * user's waits for that user's work (hipStreamWaitEvent) -- concurrent calls
+ * on two streams would otherwise race on the lists.  Call with c->mu held for
+ * the whole enqueue.  Streams under hipGraph capture are left alone (an
+ * event recorded outside the capture cannot be waited on inside it). */
+bool capturing(hipStream_t s)
+{
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
+}
+
+int scratch_acquire(DevCtx *c, hipStream_t s)
+{
+    if (!c->last_valid || c->last_stream == s || capturing(s))
+        return ZSCRC_OK;
+    hipError_t e = hipStreamWaitEvent(s, c->last, 0);
+    if (e != hipSuccess) {
+        set_err("hipStreamWaitEvent(scratch)", e);
+        return ZSCRC_EHIP;
+    }
+    return ZSCRC_OK;
+}
+
+int scratch_release(DevCtx *c, hipStream_t s)
+{
+    if (capturing(s)) {
+        c->last_valid = false;
+        return ZSCRC_OK;
+    }
+    hipError_t e = hipSuccess;
+    if (!c->last)
+        e = hipEventCreateWithFlags(&c->last, hipEventDisableTiming);
+    if (e == hipSuccess)
+        e = hipEventRecord(c->last, s);
+    if (e != hipSuccess) {
+        set_err("hipEventRecord(scratch)", e);
+        c->last_valid = false;
+        return ZSCRC_EHIP;
+    }
+    c->last_stream = s;
+    c->last_valid = true;
+    return ZSCRC_OK;
+}
+
 /* Team size for n fixed-stride records of `len` bytes at `stride` from
  * `base` (profiles/r01/team_sweep.jsonl, same-GPU A/B of G 1 / 2 / 16):
  *  - 2-lane teams where every record starts and ends on a 128-byte line
@@ -274,6 +322,8 @@ int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s, int depth_hi
  * Classes 2-3 with fewer records than two per team are cut into equal parts
  * (unit ~ class bytes / items wanted, plan_kernel) and a fold kernel combines
  * each record's part registers. */
+int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1, uint64_t g16);
+
 int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t max_len = ZSCRC_LEN_UNBOUNDED)
 {
     const uint64_t g1 = g_g1_max, g16 = g_g16_max;
@@ -285,6 +335,16 @@ int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t max_len =
         if (max_len <= g1 && (w0 < 0 || w0 == 9))
             return launch(c, 1, d, s, 9);
     }
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    int rc = scratch_acquire(c, s);
+    if (!rc)
+        rc = launch_classes_locked(c, d, s, g1, g16);
+    const int rc2 = scratch_release(c, s);
+    return rc ? rc : rc2;
+}
+
+int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1, uint64_t g16)
+{
     const uint64_t n = d.n;
     uint64_t b1 = g16 < 8191 ? g16 : 8191;
     if (b1 < g1)
@@ -301,7 +361,6 @@ int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t max_len =
     /* parts buffer: part registers (< 2T), part_rec (< 2T), part_base (< T) */
     const size_t part_bytes = 5 * T * sizeof(uint32_t);
     {
-        std::lock_guard<std::recursive_mutex> lk(c->mu);
         int rc = grow(&c->classes, &c->classes_bytes, list_bytes);
         if (!rc)
             rc = grow(&c->parts, &c->parts_bytes, part_bytes);
@@ -605,7 +664,14 @@ int zscrc_device_span(const void *d_buf, uint64_t len, uint32_t seed, uint32_t *
     if (rc)
         return rc;
     std::lock_guard<std::recursive_mutex> lk(c->mu);
-    return span_impl(c, d_buf, len, seed, d_out, scratch, flags, static_cast<hipStream_t>(stream));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (scratch) /* the caller's own partials buffer */
+        return span_impl(c, d_buf, len, seed, d_out, scratch, flags, s);
+    rc = scratch_acquire(c, s);
+    if (!rc)
+        rc = span_impl(c, d_buf, len, seed, d_out, nullptr, flags, s);
+    const int rc2 = scratch_release(c, s);
+    return rc ? rc : rc2;
 }
 
 int zscrc_host_batch(const void *base, const uint64_t *off, const uint64_t *len,
