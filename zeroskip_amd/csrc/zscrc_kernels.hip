@@ -44,6 +44,9 @@ constexpr uint32_t LDS_BYTES = 163840;
 constexpr uint32_t OFF_U = 131072;
 constexpr uint32_t OFF_Z = 135168;
 constexpr uint32_t STASH = 8; /* short_kernel: results per thread kept in LDS */
+#ifndef ZS_WARM
+#define ZS_WARM 1
+#endif
 
 /* Global-address-space views: flat pointers would tie every load to the LDS
  * counter (lgkmcnt) and serialise them against the table lookups. */
@@ -733,6 +736,15 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
     const bool direct = !FIXED && d.klass == 0 && count == d.n;
     if ((uint64_t)blockIdx.x * WG >= count)
         return;
+    /* fixed stride: touch the line of the thread's first record before the
+     * table fill, so its HBM round trip overlaps the fill (the record's own
+     * loads then hit L2); the value is only kept live */
+    u32x4 warm = {0, 0, 0, 0};
+    if (FIXED && ZS_WARM) {
+        const uint64_t i0 = (uint64_t)blockIdx.x * WG + threadIdx.x;
+        if (i0 < count && d.fixed_len >= 16)
+            warm = *(g4p)((reinterpret_cast<uintptr_t>(d.base) + i0 * d.stride) & ~uintptr_t(15));
+    }
     fill_lds<1>(L, gtab);
     __syncthreads();
     const int lane = threadIdx.x & 63;
@@ -924,6 +936,8 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
         for (uint64_t i = first; i < count; i += nthr, slot += WG)
             d.out[i] = stash_buf[slot];
     }
+    if (FIXED && ZS_WARM && (warm.x & warm.y & warm.z & warm.w) == 0xFFFFFFFFu && d.n == 0)
+        d.out[0] = 0; /* never taken (n > 0 here): keeps the warm-up load */
 }
 
 /*
