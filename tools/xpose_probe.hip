@@ -1,0 +1,197 @@
+// xpose_probe: one lane per record with quad-cooperative loads (diagnostic,
+// not product code).  Records of RS bytes back to back from base + SHIFT.
+// Lane (row g = lane / 16, column c = lane % 16) owns record wave_base + lane.
+// For piece p and t = 0..3, lane (g, c) loads bytes [16g, 16g + 16) of piece p
+// of the record owned by lane (t, c): each load instruction reads 16 pieces of
+// 64 contiguous bytes (16-32 cache lines) instead of 64 scattered 16-byte
+// pieces (64 lines).  A 4 x 4 transpose of 16-byte blocks across the four
+// rows (v_permlane32_swap then v_permlane16_swap, 16 per 64-byte piece) hands
+// every lane its own record's piece; hashing is the one-lane slice-by-4 chain
+// on 32-replica LDS tables (no per-team operators).
+//   mode 0: loads only; 1: loads + transpose; 2: + slice-by-4 CRC chain
+//   xpose 0: plain one-lane loads (lane reads its own record) for comparison
+// Output: JSON lines.
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u32x4 *g4p;
+
+__device__ __forceinline__ unsigned lds32(const char *L, unsigned a) { return *(const unsigned *)(L + a); }
+
+__device__ __forceinline__ unsigned m4(const char *L, unsigned x, unsigned c_lo, unsigned c_hi)
+{
+    const unsigned a0 = __builtin_amdgcn_perm(x, c_lo, 0x0C020400u);
+    const unsigned a1 = __builtin_amdgcn_perm(x, c_lo, 0x0C020500u);
+    const unsigned a2 = __builtin_amdgcn_perm(x, c_hi, 0x0C020600u);
+    const unsigned a3 = __builtin_amdgcn_perm(x, c_hi, 0x0C020700u);
+    return lds32(L, a0) ^ lds32(L, a1 + 128) ^ lds32(L, a2) ^ lds32(L, a3 + 128);
+}
+
+__global__ void fill_random(unsigned *p, size_t n)
+{
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        unsigned long long x = (i + 1) * 0x9E3779B97F4A7C15ull;
+        x ^= x >> 29;
+        x *= 0xBF58476D1CE4E5B9ull;
+        x ^= x >> 32;
+        p[i] = (unsigned)x;
+    }
+}
+
+/* 4 x 4 transpose of 16-byte blocks over the rows {c, c+16, c+32, c+48} */
+__device__ __forceinline__ void xpose(u32x4 (&r)[4])
+{
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        auto a = __builtin_amdgcn_permlane32_swap(r[0][k], r[2][k], false, false);
+        auto b = __builtin_amdgcn_permlane32_swap(r[1][k], r[3][k], false, false);
+        r[0][k] = a[0];
+        r[2][k] = a[1];
+        r[1][k] = b[0];
+        r[3][k] = b[1];
+        auto c = __builtin_amdgcn_permlane16_swap(r[0][k], r[1][k], false, false);
+        auto d = __builtin_amdgcn_permlane16_swap(r[2][k], r[3][k], false, false);
+        r[0][k] = c[0];
+        r[1][k] = c[1];
+        r[2][k] = d[0];
+        r[3][k] = d[1];
+    }
+}
+
+template <int RS, int MODE, int XP>
+__global__ __launch_bounds__(1024) void rec(const char *buf, size_t nrec, unsigned *out)
+{
+    constexpr int NP = RS / 64; /* pieces per record (RS multiple of 64 here) */
+    __shared__ __attribute__((aligned(16))) char L[MODE == 2 ? 131072 : 16];
+    if (MODE == 2) {
+        uint4 *L4 = reinterpret_cast<uint4 *>(L);
+        for (int i = threadIdx.x; i < 131072 / 16; i += 1024) {
+            const unsigned v = 0x9E3779B9u * (unsigned)(i >> 3) + 0x7F4A7C15u;
+            L4[i] = make_uint4(v, v ^ 1, v ^ 2, v ^ 3);
+        }
+        __syncthreads();
+    }
+    const int lane = threadIdx.x & 63;
+    const int g = lane >> 4, c = lane & 15;
+    const unsigned c_lo = (unsigned)(lane & 31) << 2, c_hi = c_lo | 0x10000u;
+    const size_t nwave = (size_t)gridDim.x * 16;
+    unsigned acc = 0;
+    for (size_t w = (size_t)blockIdx.x * 16 + (threadIdx.x >> 6); w * 64 < nrec; w += nwave) {
+        const size_t rbase = w * 64;
+        u32x4 v[NP][4];
+        if (XP) {
+#pragma unroll
+            for (int p = 0; p < NP; ++p)
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const size_t r = rbase + 16 * t + c; /* record of lane (t, c) */
+                    v[p][t] = r < nrec ? *(g4p)(buf + r * RS + 64 * p + 16 * g) : u32x4{0, 0, 0, 0};
+                }
+        } else {
+#pragma unroll
+            for (int p = 0; p < NP; ++p)
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const size_t r = rbase + lane;
+                    v[p][t] = r < nrec ? *(g4p)(buf + r * RS + 64 * p + 16 * t) : u32x4{0, 0, 0, 0};
+                }
+        }
+        unsigned reg = 0;
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+            if (XP && MODE >= 1)
+                xpose(v[p]);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                if (MODE == 2) {
+                    reg = m4(L, reg ^ v[p][t].x, c_lo, c_hi);
+                    reg = m4(L, reg ^ v[p][t].y, c_lo, c_hi);
+                    reg = m4(L, reg ^ v[p][t].z, c_lo, c_hi);
+                    reg = m4(L, reg ^ v[p][t].w, c_lo, c_hi);
+                } else {
+                    reg ^= v[p][t].x ^ v[p][t].y ^ v[p][t].z ^ v[p][t].w;
+                }
+            }
+        }
+        if (MODE == 2) {
+            if (rbase + lane < nrec)
+                out[rbase + lane] = reg;
+        } else {
+            acc ^= reg;
+        }
+    }
+    if (acc == 0x12345678u)
+        out[0] = acc;
+}
+
+template <int RS, int MODE, int XP>
+void run(const char *d, size_t total, unsigned *o, int cu)
+{
+    const size_t nrec = std::min(total / RS, (size_t)(64 << 20));
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    for (int i = 0; i < 3; ++i)
+        hipLaunchKernelGGL((rec<RS, MODE, XP>), dim3(cu), dim3(1024), 0, 0, d, nrec, o);
+    std::vector<float> t;
+    for (int r = 0; r < 10; ++r) {
+        hipEventRecord(a);
+        hipLaunchKernelGGL((rec<RS, MODE, XP>), dim3(cu), dim3(1024), 0, 0, d, nrec, o);
+        hipEventRecord(b);
+        hipEventSynchronize(b);
+        float ms;
+        hipEventElapsedTime(&ms, a, b);
+        t.push_back(ms);
+    }
+    std::sort(t.begin(), t.end());
+    const double ms = t[t.size() / 2];
+    printf("{\"rs\": %d, \"mode\": %d, \"xpose\": %d, \"nrec\": %zu, \"ms\": %.4f, \"GBs\": %.1f}\n", RS, MODE, XP,
+           nrec, ms, nrec * (double)RS / ms / 1e6);
+    fflush(stdout);
+}
+
+/* self-check: transposed loads + chain == plain loads + chain, record by record */
+template <int RS>
+int check(const char *d, size_t total, unsigned *o, int cu)
+{
+    const size_t nrec = std::min(total / RS, (size_t)(1 << 20));
+    std::vector<unsigned> x(nrec), y(nrec);
+    hipLaunchKernelGGL((rec<RS, 2, 0>), dim3(cu), dim3(1024), 0, 0, d, nrec, o);
+    hipMemcpy(x.data(), o, nrec * 4, hipMemcpyDeviceToHost);
+    hipLaunchKernelGGL((rec<RS, 2, 1>), dim3(cu), dim3(1024), 0, 0, d, nrec, o);
+    hipMemcpy(y.data(), o, nrec * 4, hipMemcpyDeviceToHost);
+    const bool same = x == y;
+    printf("{\"rs\": %d, \"check\": \"%s\"}\n", RS, same ? "xpose == plain" : "MISMATCH");
+    return same ? 0 : 1;
+}
+
+int main()
+{
+    size_t n = (size_t)4 << 30;
+    char *d;
+    unsigned *o;
+    if (hipMalloc(&d, n) != hipSuccess || hipMalloc(&o, (64 << 20) * 4 + 64) != hipSuccess) {
+        printf("alloc failed\n");
+        return 1;
+    }
+    int cu = 0;
+    hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, 0);
+    hipLaunchKernelGGL(fill_random, dim3(4096), dim3(256), 0, 0, (unsigned *)d, n / 4);
+    hipDeviceSynchronize();
+    int bad = check<320>(d, n, o, cu) | check<256>(d, n, o, cu);
+    run<320, 0, 0>(d, n, o, cu);
+    run<320, 0, 1>(d, n, o, cu);
+    run<320, 1, 1>(d, n, o, cu);
+    run<320, 2, 0>(d, n, o, cu);
+    run<320, 2, 1>(d, n, o, cu);
+    run<256, 2, 0>(d, n, o, cu);
+    run<256, 2, 1>(d, n, o, cu);
+    run<64, 2, 0>(d, n, o, cu);
+    run<64, 2, 1>(d, n, o, cu);
+    run<512, 2, 0>(d, n, o, cu);
+    run<512, 2, 1>(d, n, o, cu);
+    return bad;
+}
