@@ -132,7 +132,7 @@ void zscrc_set_small_team(int mode);
  * 0 = two-level loop, 1 / 2 = flattened (record, step) loop with a 1- / 2-item
  * register ring; g = 1 only: 3..8 = per-lane short-record kernel (next
  * piece loaded when it exists / always / two pieces ahead / bursts of 2, 3,
- * 4 pieces) */
+ * 4 pieces), 9 / 10 = record bursts with per-lane / quad-cooperative loads */
 void zscrc_set_prefetch(int g, int depth);
 /* team size the fixed-stride path picks for n packed records of len bytes
  * from a 128-byte-aligned base (1/2/16/64; 0 if no device) */

@@ -42,9 +42,9 @@ def teams(request, gpu):
     lib().zscrc_set_teams(*DEFAULT_TEAMS)
 
 
-@pytest.fixture(params=[-1, 1, 2, 3, 4, 5, 6, 7, 8, 9],
+@pytest.fixture(params=[-1, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10],
                 ids=["g1-auto", "g1-ring1", "g1-ring2", "g1-short", "g1-short-pf", "g1-short-pf2",
-                     "g1-burst2", "g1-burst3", "g1-burst4", "g1-record-burst"])
+                     "g1-burst2", "g1-burst3", "g1-burst4", "g1-record-burst", "g1-record-burst-quad"])
 def g1_walk(request, gpu):
     lib().zscrc_set_prefetch(1, request.param)
     yield request.param

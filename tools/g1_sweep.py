@@ -26,7 +26,7 @@ def main():
               ("312B/320 +8 (pieces 64B-aligned)", 320, 312, 10_000_000, 8),
               ("312B/320 +40 (zeroskip layout)", 320, 312, 10_000_000, 40),
               ("256B/256 aligned", 256, 256, 10_000_000, 0), ("256B/256 +4", 256, 256, 10_000_000, 4)]
-    depths = (3, 9)
+    depths = (3, 9, 10)
     for name, stride, length, n, shift in cases:
         for dp in depths:
             lib().zscrc_set_prefetch(1, dp)
@@ -37,7 +37,7 @@ def main():
     n = 10_000_000
     offs = torch.arange(n, dtype=torch.int64, device=dev) * 320 + 40
     lens = torch.full((n,), 312, dtype=torch.int64, device=dev)
-    for dp in (3, 9):
+    for dp in (3, 9, 10):
         lib().zscrc_set_prefetch(1, dp)
         ms = timeit(lambda: zd.crc_batch(big, offs, lens, out=out[:n]))
         print(json.dumps({"case": "variable 312B x10M", "depth": dp, "ms": round(ms, 4),
@@ -50,7 +50,7 @@ def main():
     del big
     img = zg.log_files(bytes(16), 0, 1526, ppf, 0, True, g, dev)
     o, ln = zg.log_spans(1526, ppf, True, True, dev)
-    for dp in (3, 9):
+    for dp in (3, 9, 10):
         lib().zscrc_set_prefetch(1, dp)
         ms = timeit(lambda: zsfile.verify_commits(img.view(-1), o, ln))
         _, st = zsfile.verify_commits(img.view(-1), o, ln)

@@ -35,7 +35,7 @@ int zs_launch_stream_read(const void *buf, uint64_t n, uint32_t *out, int grid, 
 int zs_launch_classify(const zs::Classify *c, hipStream_t stream);
 int zs_launch_part_fold(const zs::BatchDesc *d, const uint32_t *gtab, hipStream_t stream);
 int zs_launch_plan(const zs::PlanArgs *a, hipStream_t stream);
-int zs_launch_burst(int fixed, const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
+int zs_launch_burst(int fixed, int xp, const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
 }
 
 namespace {
@@ -58,7 +58,8 @@ int g_strict = 0;
  * (walk_for), 0 = two-level loop, 1/2 = flattened loop with a 1/2-item ring;
  * G = 1 only: 3..8 = short_kernel (per-lane records; next piece loaded if it
  * exists / always four loads / two pieces ahead / bursts of 2, 3, 4 pieces),
- * 9 = burst_kernel (a record's pieces loaded at once, next record in flight) */
+ * 9 = burst_kernel (a record's pieces loaded at once, next record in flight),
+ * 10 = burst_kernel with quad-cooperative loads and a lane transpose */
 std::atomic<int> g_depth[3] = {{-1}, {-1}, {-1}};
 
 struct DevCtx {
@@ -277,10 +278,11 @@ zs::BatchDesc make_desc()
  * items deep where the batch is fixed-stride, except 4-8 KiB G16 records. */
 int walk_for(int g, int fixed, uint64_t len)
 {
-    if (g == 1) /* record bursts (burst_kernel) for 65..320-byte records and
-                 * variable batches; one-piece and > 5-piece fixed-stride
-                 * records: the piece walk (tools/g1_sweep.py) */
-        return fixed && (len <= 64 || len > 320) ? 3 : 9;
+    if (g == 1) /* record bursts with quad-cooperative loads (burst_kernel,
+                 * walk 10) for 65..320-byte records and variable batches;
+                 * one-piece and > 5-piece fixed-stride records: the piece
+                 * walk (tools/g1_sweep.py) */
+        return fixed && (len <= 64 || len > 320) ? 3 : 10;
     if (len >= 8192)
         return 0;
     if (!fixed)
@@ -301,7 +303,7 @@ int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s, int depth_hi
     if (!fixed && depth == 2)
         depth = 1;
     zs::BatchDesc dx = d;
-    int rc = depth == 9  ? zs_launch_burst(fixed, &dx, c->gtab, c->ncu, s)
+    int rc = depth >= 9  ? zs_launch_burst(fixed, depth == 10, &dx, c->gtab, c->ncu, s)
              : depth >= 3 ? zs_launch_short(fixed, depth - 3, &dx, c->gtab, c->ncu, s)
                         : zs_launch_team(g, fixed, depth, &d, c->gtab, c->ncu, s);
     if (rc) {
@@ -332,8 +334,8 @@ int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t max_len =
          * straight over the caller's arrays, no classify (it is correct for
          * any length, so a wrong bound costs only time) */
         const int w0 = g_depth[0];
-        if (max_len <= g1 && (w0 < 0 || w0 == 9))
-            return launch(c, 1, d, s, 9);
+        if (max_len <= g1 && (w0 < 0 || w0 >= 9))
+            return launch(c, 1, d, s, walk_for(1, 0, 1));
     }
     std::lock_guard<std::recursive_mutex> lk(c->mu);
     int rc = scratch_acquire(c, s);
@@ -395,7 +397,7 @@ int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1
         /* class 0 goes to burst_kernel (walk 9, the default), which walks
          * the caller's arrays and skips longer records: no class-0 list */
         const int w0 = g_depth[0];
-        cl.direct_ok = g1 > 0 && (w0 < 0 || w0 == 9);
+        cl.direct_ok = g1 > 0 && (w0 < 0 || w0 >= 9);
     }
     for (int pass = 0; pass < 2; ++pass) {
         cl.pass = pass;
@@ -799,7 +801,7 @@ void zscrc_set_gpu_min(uint64_t min_bytes)
 
 void zscrc_set_prefetch(int g, int depth)
 {
-    if (depth < -1 || depth > (g == 1 ? 9 : 2))
+    if (depth < -1 || depth > (g == 1 ? 10 : 2))
         return;
     if (g == 1)
         g_depth[0] = depth;

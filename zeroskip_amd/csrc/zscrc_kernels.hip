@@ -1030,6 +1030,58 @@ __device__ __forceinline__ void burst_issue(const BRec &b, uintptr_t dummy, uint
         issue_plain(b.burst ? b.V0 + 64 * ((uint64_t)p < b.np ? (uint64_t)p : b.np - 1) : dummy, w[p]);
 }
 
+/* Quad-cooperative burst (XP): lane (row g = lane/16, column c = lane%16)
+ * loads bytes [16g, 16g+16) of every piece of the records owned by lanes
+ * (t, c), t = 0..3 -- each load instruction reads 16 pieces of 64 contiguous
+ * bytes (16-32 cache lines) instead of 64 scattered 16-byte pieces (64 lines,
+ * the TA-bound shape of the plain burst).  xpose_burst then
+ * hands every lane its own record's pieces (tools/xpose_probe.hip).  The
+ * owners' grid base, piece count and burst flag come over ds_bpermute.  Call
+ * with every lane of the wave active. */
+__device__ __forceinline__ void burst_issue_x(const BRec &b, uintptr_t dummy, uint32_t (&w)[5][16], int lane)
+{
+    const int g = lane >> 4, c = lane & 15;
+    const uint32_t v_lo = (uint32_t)b.V0, v_hi = (uint32_t)((uint64_t)b.V0 >> 32);
+    const uint32_t pk = (b.burst ? 0x100u : 0u) | (uint32_t)(b.np < 5 ? b.np : 5);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int src = 16 * t + c;
+        const uint32_t lo_t = __shfl(v_lo, src), hi_t = __shfl(v_hi, src), pk_t = __shfl(pk, src);
+        const uintptr_t V = ((uintptr_t)hi_t << 32) | lo_t;
+        const uint32_t np_t = pk_t & 0xffu;
+        const bool bt = (pk_t & 0x100u) != 0;
+#pragma unroll
+        for (int p = 0; p < 5; ++p) {
+            const uintptr_t q = bt ? V + 64 * (uint32_t)(p < (int)np_t ? p : np_t - 1) + 16 * g : dummy + 16 * g;
+            const u32x4 v = *(g4p)q;
+            w[p][4 * t + 0] = v.x;
+            w[p][4 * t + 1] = v.y;
+            w[p][4 * t + 2] = v.z;
+            w[p][4 * t + 3] = v.w;
+        }
+    }
+}
+
+/* 4 x 4 transpose of 16-byte blocks across the rows {c, c+16, c+32, c+48}:
+ * block t of lane (g, c) <-> block g of lane (t, c) (v_permlane32_swap, then
+ * v_permlane16_swap; gfx950).  Every lane of the wave active. */
+__device__ __forceinline__ void xpose_burst(uint32_t (&w)[5][16])
+{
+#pragma unroll
+    for (int p = 0; p < 5; ++p)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const auto a = __builtin_amdgcn_permlane32_swap(w[p][k], w[p][8 + k], false, false);
+            const auto b = __builtin_amdgcn_permlane32_swap(w[p][4 + k], w[p][12 + k], false, false);
+            const auto e = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
+            const auto f = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
+            w[p][k] = e[0];
+            w[p][4 + k] = e[1];
+            w[p][8 + k] = f[0];
+            w[p][12 + k] = f[1];
+        }
+}
+
 __device__ __forceinline__ void burst_hash(const BatchDesc &d, BRec &b, uint32_t (&w)[5][16], const char *L,
                                            uintptr_t lo, uint32_t c_lo, uint32_t c_hi)
 {
@@ -1100,7 +1152,7 @@ __device__ __forceinline__ void burst_hash(const BatchDesc &d, BRec &b, uint32_t
     emit(d, it, r, L, c_lo, c_hi);
 }
 
-template <bool FIXED>
+template <bool FIXED, bool XP>
 __global__ __launch_bounds__(BWG) void burst_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
 {
     __shared__ __attribute__((aligned(16))) char L[OFF_U];
@@ -1138,6 +1190,32 @@ __global__ __launch_bounds__(BWG) void burst_kernel(BatchDesc d, const uint32_t 
     uint64_t i = (uint64_t)blockIdx.x * BWG + threadIdx.x;
     BRec ra, rb;
     uint32_t wa[5][16], wb[5][16];
+    if (XP) {
+        /* wave-uniform trip count: the transpose needs every lane */
+        burst_meta<FIXED>(d, list, direct, count, i, lo, ra);
+        burst_issue_x(ra, dummy, wa, lane);
+        for (;;) {
+            burst_meta<FIXED>(d, list, direct, count, i + nthr, lo, rb);
+            burst_issue_x(rb, dummy, wb, lane);
+            __builtin_amdgcn_sched_barrier(0);
+            if (!__any(ra.ok))
+                break;
+            xpose_burst(wa);
+            if (ra.ok)
+                burst_hash(d, ra, wa, L, lo, c_lo, c_hi);
+            i += nthr;
+            burst_meta<FIXED>(d, list, direct, count, i + nthr, lo, ra);
+            burst_issue_x(ra, dummy, wa, lane);
+            __builtin_amdgcn_sched_barrier(0);
+            if (!__any(rb.ok))
+                break;
+            xpose_burst(wb);
+            if (rb.ok)
+                burst_hash(d, rb, wb, L, lo, c_lo, c_hi);
+            i += nthr;
+        }
+        return;
+    }
     burst_meta<FIXED>(d, list, direct, count, i, lo, ra);
     burst_issue(ra, dummy, wa);
     for (;;) {
@@ -1620,12 +1698,17 @@ extern "C" int zs_launch_short(int fixed, int pf, const zs::BatchDesc *d, const 
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
-extern "C" int zs_launch_burst(int fixed, const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream)
+extern "C" int zs_launch_burst(int fixed, int xp, const zs::BatchDesc *d, const uint32_t *gtab, int grid,
+                               hipStream_t stream)
 {
-    if (fixed)
-        hipLaunchKernelGGL((zs::burst_kernel<true>), dim3(grid), dim3(zs::BWG), 0, stream, *d, gtab);
+    if (fixed && xp)
+        hipLaunchKernelGGL((zs::burst_kernel<true, true>), dim3(grid), dim3(zs::BWG), 0, stream, *d, gtab);
+    else if (fixed)
+        hipLaunchKernelGGL((zs::burst_kernel<true, false>), dim3(grid), dim3(zs::BWG), 0, stream, *d, gtab);
+    else if (xp)
+        hipLaunchKernelGGL((zs::burst_kernel<false, true>), dim3(grid), dim3(zs::BWG), 0, stream, *d, gtab);
     else
-        hipLaunchKernelGGL((zs::burst_kernel<false>), dim3(grid), dim3(zs::BWG), 0, stream, *d, gtab);
+        hipLaunchKernelGGL((zs::burst_kernel<false, false>), dim3(grid), dim3(zs::BWG), 0, stream, *d, gtab);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
