@@ -35,7 +35,8 @@ int zs_launch_stream_read(const void *buf, uint64_t n, uint32_t *out, int grid, 
 int zs_launch_classify(const zs::Classify *c, hipStream_t stream);
 int zs_launch_part_fold(const zs::BatchDesc *d, const uint32_t *gtab, hipStream_t stream);
 int zs_launch_plan(const zs::PlanArgs *a, hipStream_t stream);
-int zs_launch_burst(int fixed, int xp, const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
+int zs_launch_burst(int fixed, int xp, int nb, const zs::BatchDesc *d, const uint32_t *gtab, int grid,
+                    hipStream_t stream);
 }
 
 namespace {
@@ -303,7 +304,10 @@ int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s, int depth_hi
     if (!fixed && depth == 2)
         depth = 1;
     zs::BatchDesc dx = d;
-    int rc = depth >= 9  ? zs_launch_burst(fixed, depth == 10, &dx, c->gtab, c->ncu, s)
+    /* pieces per burst: a fixed-stride record spans at most ceil(len/64) */
+    const int nb = fixed && d.fixed_len <= 64 && d.last_len == ~0ull ? 1
+                   : fixed && d.fixed_len <= 128 && d.last_len == ~0ull ? 2 : 5;
+    int rc = depth >= 9  ? zs_launch_burst(fixed, depth == 10, nb, &dx, c->gtab, c->ncu, s)
              : depth >= 3 ? zs_launch_short(fixed, depth - 3, &dx, c->gtab, c->ncu, s)
                         : zs_launch_team(g, fixed, depth, &d, c->gtab, c->ncu, s);
     if (rc) {

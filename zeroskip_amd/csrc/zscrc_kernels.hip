@@ -1023,10 +1023,11 @@ __device__ __forceinline__ void burst_meta(const BatchDesc &d, const RecDesc *li
     b.burst = b.np >= 1 && b.V0 >= lo;
 }
 
-__device__ __forceinline__ void burst_issue(const BRec &b, uintptr_t dummy, uint32_t (&w)[5][16])
+template <int NB>
+__device__ __forceinline__ void burst_issue(const BRec &b, uintptr_t dummy, uint32_t (&w)[NB][16])
 {
 #pragma unroll
-    for (int p = 0; p < 5; ++p)
+    for (int p = 0; p < NB; ++p)
         issue_plain(b.burst ? b.V0 + 64 * ((uint64_t)p < b.np ? (uint64_t)p : b.np - 1) : dummy, w[p]);
 }
 
@@ -1038,11 +1039,12 @@ __device__ __forceinline__ void burst_issue(const BRec &b, uintptr_t dummy, uint
  * hands every lane its own record's pieces (tools/xpose_probe.hip).  The
  * owners' grid base, piece count and burst flag come over ds_bpermute.  Call
  * with every lane of the wave active. */
-__device__ __forceinline__ void burst_issue_x(const BRec &b, uintptr_t dummy, uint32_t (&w)[5][16], int lane)
+template <int NB>
+__device__ __forceinline__ void burst_issue_x(const BRec &b, uintptr_t dummy, uint32_t (&w)[NB][16], int lane)
 {
     const int g = lane >> 4, c = lane & 15;
     const uint32_t v_lo = (uint32_t)b.V0, v_hi = (uint32_t)((uint64_t)b.V0 >> 32);
-    const uint32_t pk = (b.burst ? 0x100u : 0u) | (uint32_t)(b.np < 5 ? b.np : 5);
+    const uint32_t pk = (b.burst ? 0x100u : 0u) | (uint32_t)(b.np < NB ? b.np : NB);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
         const int src = 16 * t + c;
@@ -1051,7 +1053,7 @@ __device__ __forceinline__ void burst_issue_x(const BRec &b, uintptr_t dummy, ui
         const uint32_t np_t = pk_t & 0xffu;
         const bool bt = (pk_t & 0x100u) != 0;
 #pragma unroll
-        for (int p = 0; p < 5; ++p) {
+        for (int p = 0; p < NB; ++p) {
             const uintptr_t q = bt ? V + 64 * (uint32_t)(p < (int)np_t ? p : np_t - 1) + 16 * g : dummy + 16 * g;
             const u32x4 v = *(g4p)q;
             w[p][4 * t + 0] = v.x;
@@ -1065,10 +1067,11 @@ __device__ __forceinline__ void burst_issue_x(const BRec &b, uintptr_t dummy, ui
 /* 4 x 4 transpose of 16-byte blocks across the rows {c, c+16, c+32, c+48}:
  * block t of lane (g, c) <-> block g of lane (t, c) (v_permlane32_swap, then
  * v_permlane16_swap; gfx950).  Every lane of the wave active. */
-__device__ __forceinline__ void xpose_burst(uint32_t (&w)[5][16])
+template <int NB>
+__device__ __forceinline__ void xpose_burst(uint32_t (&w)[NB][16])
 {
 #pragma unroll
-    for (int p = 0; p < 5; ++p)
+    for (int p = 0; p < NB; ++p)
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const auto a = __builtin_amdgcn_permlane32_swap(w[p][k], w[p][8 + k], false, false);
@@ -1082,7 +1085,8 @@ __device__ __forceinline__ void xpose_burst(uint32_t (&w)[5][16])
         }
 }
 
-__device__ __forceinline__ void burst_hash(const BatchDesc &d, BRec &b, uint32_t (&w)[5][16], const char *L,
+template <int NB>
+__device__ __forceinline__ void burst_hash(const BatchDesc &d, BRec &b, uint32_t (&w)[NB][16], const char *L,
                                            uintptr_t lo, uint32_t c_lo, uint32_t c_hi)
 {
     if (b.skip)
@@ -1100,21 +1104,24 @@ __device__ __forceinline__ void burst_hash(const BatchDesc &d, BRec &b, uint32_t
     const uintptr_t V0 = b.V0;
     const uint32_t spill = A + 4 > V0 + 64 ? it.R0 >> (8 * (uint32_t)(V0 + 64 - A)) : 0u;
     if (b.burst) {
-        w[1][0] ^= b.np > 1 ? spill : 0u;
+        if (NB > 1)
+            w[NB > 1 ? 1 : 0][0] ^= b.np > 1 ? spill : 0u; /* NB = 1: below */
         r = first_piece(L, it, V0, 0, w[0], c_lo, c_hi); /* V0 >= lo here */
 #pragma unroll
-        for (int p = 1; p < 5; ++p)
+        for (int p = 1; p < NB; ++p)
             if ((uint64_t)p < b.np)
                 r = piece<false>(L, r, w[p], c_lo, c_hi);
-        /* longer records: further bursts of five pieces into the same
+        /* longer records: further bursts of NB pieces into the same
          * registers (the next record's burst, issued earlier, lands first) */
-        for (uint64_t base = 5; base < b.np; base += 5) {
+        for (uint64_t base = NB; base < b.np; base += NB) {
 #pragma unroll
-            for (int p = 0; p < 5; ++p)
+            for (int p = 0; p < NB; ++p)
                 issue_plain(V0 + 64 * (base + p < b.np ? base + p : b.np - 1), w[p]);
             __builtin_amdgcn_sched_barrier(0);
+            if (NB == 1 && base == 1)
+                w[0][0] ^= spill;
 #pragma unroll
-            for (int p = 0; p < 5; ++p)
+            for (int p = 0; p < NB; ++p)
                 if (base + p < b.np)
                     r = piece<false>(L, r, w[p], c_lo, c_hi);
         }
@@ -1152,7 +1159,7 @@ __device__ __forceinline__ void burst_hash(const BatchDesc &d, BRec &b, uint32_t
     emit(d, it, r, L, c_lo, c_hi);
 }
 
-template <bool FIXED, bool XP>
+template <bool FIXED, bool XP, int NB>
 __global__ __launch_bounds__(BWG) void burst_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
 {
     __shared__ __attribute__((aligned(16))) char L[OFF_U];
@@ -1189,7 +1196,7 @@ __global__ __launch_bounds__(BWG) void burst_kernel(BatchDesc d, const uint32_t 
     const uint64_t nthr = (uint64_t)gridDim.x * BWG;
     uint64_t i = (uint64_t)blockIdx.x * BWG + threadIdx.x;
     BRec ra, rb;
-    uint32_t wa[5][16], wb[5][16];
+    uint32_t wa[NB][16], wb[NB][16];
     if (XP) {
         /* wave-uniform trip count: the transpose needs every lane */
         burst_meta<FIXED>(d, list, direct, count, i, lo, ra);
@@ -1698,17 +1705,24 @@ extern "C" int zs_launch_short(int fixed, int pf, const zs::BatchDesc *d, const 
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
-extern "C" int zs_launch_burst(int fixed, int xp, const zs::BatchDesc *d, const uint32_t *gtab, int grid,
+extern "C" int zs_launch_burst(int fixed, int xp, int nb, const zs::BatchDesc *d, const uint32_t *gtab, int grid,
                                hipStream_t stream)
 {
-    if (fixed && xp)
-        hipLaunchKernelGGL((zs::burst_kernel<true, true>), dim3(grid), dim3(zs::BWG), 0, stream, *d, gtab);
+#define ZS_BURST(F, X, N) \
+    hipLaunchKernelGGL((zs::burst_kernel<F, X, N>), dim3(grid), dim3(zs::BWG), 0, stream, *d, gtab)
+    if (fixed && xp && nb == 1)
+        ZS_BURST(true, true, 1);
+    else if (fixed && xp && nb == 2)
+        ZS_BURST(true, true, 2);
+    else if (fixed && xp)
+        ZS_BURST(true, true, 5);
     else if (fixed)
-        hipLaunchKernelGGL((zs::burst_kernel<true, false>), dim3(grid), dim3(zs::BWG), 0, stream, *d, gtab);
+        ZS_BURST(true, false, 5);
     else if (xp)
-        hipLaunchKernelGGL((zs::burst_kernel<false, true>), dim3(grid), dim3(zs::BWG), 0, stream, *d, gtab);
+        ZS_BURST(false, true, 5);
     else
-        hipLaunchKernelGGL((zs::burst_kernel<false, false>), dim3(grid), dim3(zs::BWG), 0, stream, *d, gtab);
+        ZS_BURST(false, false, 5);
+#undef ZS_BURST
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
