@@ -1160,7 +1160,7 @@ __device__ __forceinline__ void burst_hash(const BatchDesc &d, BRec &b, uint32_t
 }
 
 template <bool FIXED, bool XP, int NB>
-__global__ __launch_bounds__(BWG) void burst_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
+__global__ __launch_bounds__(NB == 1 ? 1024 : BWG) void burst_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
 {
     __shared__ __attribute__((aligned(16))) char L[OFF_U];
     uint64_t count = d.n;
@@ -1175,11 +1175,12 @@ __global__ __launch_bounds__(BWG) void burst_kernel(BatchDesc d, const uint32_t 
             count = d.n; /* walk every record, skip the other classes' */
     }
     const bool direct = !FIXED && d.klass == 0 && count == d.n;
-    if ((uint64_t)blockIdx.x * BWG >= count)
+    constexpr int T = NB == 1 ? 1024 : BWG; /* one-piece bursts fit 16 waves per CU */
+    if ((uint64_t)blockIdx.x * T >= count)
         return;
     {
         uint4 *L4 = reinterpret_cast<uint4 *>(L);
-        for (int i = threadIdx.x; i < 8192; i += BWG) {
+        for (int i = threadIdx.x; i < 8192; i += T) {
             const int dw = i * 4;
             const int e = (dw >> 6) & 255;
             const int tj = (dw >> 14) * 2 + ((dw >> 5) & 1);
@@ -1193,8 +1194,8 @@ __global__ __launch_bounds__(BWG) void burst_kernel(BatchDesc d, const uint32_t 
     const uint32_t c_hi = c_lo | 0x10000u;
     const uintptr_t lo = reinterpret_cast<uintptr_t>(d.base) & ~uintptr_t(3);
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(gtab);
-    const uint64_t nthr = (uint64_t)gridDim.x * BWG;
-    uint64_t i = (uint64_t)blockIdx.x * BWG + threadIdx.x;
+    const uint64_t nthr = (uint64_t)gridDim.x * T;
+    uint64_t i = (uint64_t)blockIdx.x * T + threadIdx.x;
     BRec ra, rb;
     uint32_t wa[NB][16], wb[NB][16];
     if (XP) {
@@ -1709,7 +1710,7 @@ extern "C" int zs_launch_burst(int fixed, int xp, int nb, const zs::BatchDesc *d
                                hipStream_t stream)
 {
 #define ZS_BURST(F, X, N) \
-    hipLaunchKernelGGL((zs::burst_kernel<F, X, N>), dim3(grid), dim3(zs::BWG), 0, stream, *d, gtab)
+    hipLaunchKernelGGL((zs::burst_kernel<F, X, N>), dim3(grid), dim3(N == 1 ? 1024 : zs::BWG), 0, stream, *d, gtab)
     if (fixed && xp && nb == 1)
         ZS_BURST(true, true, 1);
     else if (fixed && xp && nb == 2)
