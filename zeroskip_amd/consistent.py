@@ -238,6 +238,26 @@ class GpuBackend:
         torch.cuda.synchronize(self.device)
 
 
+_RAW8 = None
+
+
+def _raw8(x: np.ndarray) -> np.ndarray:
+    """raw CRC-32C register (from 0, no conditioning) of the 8 little-endian
+    bytes of each uint64 in x: XOR of per-byte tables (CRC linearity)."""
+    global _RAW8
+    if _RAW8 is None:
+        from .crc32c import crc32c_hw
+        t = np.zeros((8, 256), np.uint32)
+        for k in range(8):
+            for v in range(256):
+                t[k, v] = crc32c_hw(M32, bytes(k) + bytes([v]) + bytes(7 - k)) ^ M32
+        _RAW8 = t
+    r = np.zeros(x.shape, np.uint32)
+    for k in range(8):
+        r ^= _RAW8[k][((x >> np.uint64(8 * k)) & np.uint64(255)).astype(np.intp)]
+    return r
+
+
 def _commit_rec(img: np.ndarray, off: int):
     """(type, span_len, rec_len, stored, trailer words) of the commit at off."""
     w0 = int.from_bytes(img[off:off + 8].tobytes(), "big")
@@ -290,6 +310,7 @@ class Consistent:
         self.threads = threads
         self.plan = make_plan(db, world)
         self.mine = [u for u in self.plan.units if u.rank == rank]
+        self._names = None   # file names by id, for the bad / stale lists
 
     # ---------------------------------------------------------------- prepare
     def prepare(self):
@@ -417,31 +438,60 @@ class Consistent:
         raw = be.raw(self.buf, self.d_poff, self.d_plen) if self.pieces else None
         if events:
             events[1].record()
+        pack = np.zeros((0, 18), np.int64)
         if n:
-            bad_idx = torch.nonzero(st != 1).reshape(-1).cpu().numpy()
+            # one round trip: the mismatches, their predecessors' computed
+            # commit CRCs, and the commit words after both spans
+            bad = torch.nonzero(st != 1).reshape(-1)
+            prv = (bad - 1).clamp(min=0)
+            ar = torch.arange(8, device=bad.device)
+            lim = self.buf.numel() - 1
+            at = ((self.d_off[bad] + self.d_len[bad])[:, None] + ar).clamp(max=lim)
+            pat = ((self.d_off[prv] + self.d_len[prv])[:, None] + ar).clamp(max=lim)
+            pack = torch.cat([bad[:, None], crc[prv].to(torch.int64)[:, None] & M32,
+                              self.buf[at].to(torch.int64), self.buf[pat].to(torch.int64)], 1).cpu().numpy()
+            bad_idx = pack[:, 0]
         raw_h = [v & M32 for v in raw.cpu().tolist()] if raw is not None else []
         t_dev = time.perf_counter()
 
-        # zero-length mismatches: the finalise quirk if the stored CRC chains
-        # from the previous span of the same file (re-verified on the device
-        # with the previous span's CRC as seed)
+        # zero-length mismatches right after a span of the same file: the
+        # finalise quirk if the stored CRC chains from the previous span's CRC
+        # S: stored = crc32c(S, T).  The device computed crc32c(S, T_prev) for
+        # the previous commit, and with 8-byte trailers
+        #   crc32c(S, T) = crc32c(S, T_prev) ^ raw(T ^ T_prev)
+        # (CRC linearity: same register before both trailers), so the check is
+        # a host-side 8-byte correction -- no second device pass.  Long (24-byte)
+        # trailers, rare, are re-verified on the device with S as the seed.
         qm = (self.c_len[bad_idx] == 0) & (bad_idx > 0)
         qm[qm] = self.c_file[bad_idx[qm] - 1] == self.c_file[bad_idx[qm]]
         q = bad_idx[qm]
         stale_i = np.zeros(0, np.int64)
         if len(q):
-            dq = torch.from_numpy(q).to(self.d_off.device)
-            prev = be.crc(self.buf, self.d_off[dq - 1], self.d_len[dq - 1],
-                          max_len=int(self.c_len[q - 1].max()))
-            _, st2 = be.verify(self.buf, self.d_off[dq], self.d_len[dq], prev, max_len=0)
-            stale_i = q[(st2 == 1).cpu().numpy()]
+            k = pack[qm]
+            w = k[:, 2:18].astype(np.uint8)
+            w_i = np.ascontiguousarray(w[:, :8]).view(">u8").ravel().astype(np.uint64)
+            w_p = np.ascontiguousarray(w[:, 8:]).view(">u8").ravel().astype(np.uint64)
+            short = np.isin(w_i >> np.uint64(56), (T_COMMIT, T_FINAL)) & \
+                np.isin(w_p >> np.uint64(56), (T_COMMIT, T_FINAL))
+            x = (w_i ^ w_p) & np.uint64(0xFFFFFFFF00000000)
+            expect = k[:, 1].astype(np.uint32) ^ _raw8(x)
+            good = short & (expect == (w_i & np.uint64(M32)).astype(np.uint32))
+            stale_i = q[good]
+            ql = q[~short]
+            if len(ql):
+                dq = torch.from_numpy(ql).to(self.d_off.device)
+                prev = be.crc(self.buf, self.d_off[dq - 1], self.d_len[dq - 1],
+                              max_len=int(self.c_len[ql - 1].max()))
+                _, st2 = be.verify(self.buf, self.d_off[dq], self.d_len[dq], prev, max_len=0)
+                stale_i = np.sort(np.concatenate([stale_i, ql[(st2 == 1).cpu().numpy()]]))
         bad_i = np.setdiff1d(bad_idx, stale_i, assume_unique=True)
 
+        if self._names is None:
+            self._names = np.array([f.name for f in self.db.files], dtype=object)
+
         def listed(ix):
-            out = []
-            for i in ix[:self.MAX_LISTED].tolist():
-                out.append((self.db.files[int(self.c_file[i])].name, int(self.c_rec[i])))
-            return out
+            ix = ix[:self.MAX_LISTED]
+            return list(zip(self._names[self.c_file[ix]].tolist(), self.c_rec[ix].tolist()))
 
         bad, stale = listed(bad_i), listed(stale_i)
         summary = dict(rank=self.rank, commits=n, bad=bad, n_bad=len(bad_i),
