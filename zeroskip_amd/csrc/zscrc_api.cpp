@@ -280,10 +280,10 @@ zs::BatchDesc make_desc()
 int walk_for(int g, int fixed, uint64_t len)
 {
     if (g == 1) /* record bursts with quad-cooperative loads (burst_kernel,
-                 * walk 10) for 65..320-byte records and variable batches;
-                 * one-piece and > 5-piece fixed-stride records: the piece
-                 * walk (tools/g1_sweep.py) */
-        return fixed && (len <= 64 || len > 320) ? 3 : 10;
+                 * walk 10) for records over 64 bytes and variable batches;
+                 * one-piece fixed-stride records: the piece walk
+                 * (tools/g1_sweep.py, profiles/r01/mid_sweep.jsonl) */
+        return fixed && len <= 64 ? 3 : 10;
     if (len >= 8192)
         return 0;
     if (!fixed)
