@@ -1260,31 +1260,42 @@ __device__ __forceinline__ uint32_t kpow(const uint32_t *kp2, uint32_t m)
  * SEG bytes long except the last:
  *   H = Horner_{i<W-1}(P_i, K = x^(8 SEG));  reg = H * x^(8 lastlen) ^ P_{W-1}
  *   reg ^= R0 * x^(8 L)                       (initial register)
+ * Spread over blocks (one part per thread up to 256 x 256 parts): a thread
+ * Horner-folds its run of parts and shifts it by K^(parts after the run)
+ * (square-and-multiply: ~14 gmul chains, latency-bound, so one wave per
+ * SIMD); each block XOR-reduces, multiplies by
+ * x^(8 lastlen) and XORs into *out, which the host preset to the constant
+ * R0 * x^(8 L) ^ xor_out (hipMemsetD32Async); block 0 adds P_{W-1}.
  */
-__global__ __launch_bounds__(1024) void span_fold_kernel(SpanFold f)
+constexpr int FWG = 256; /* span fold: one wave per SIMD, the gmul chains are latency-bound */
+
+__global__ __launch_bounds__(FWG) void span_fold_kernel(SpanFold f)
 {
-    __shared__ uint32_t red[1024];
+    __shared__ uint32_t red[FWG / 64];
     const uint32_t W = f.w;
     const uint32_t nh = W - 1; /* Horner terms */
-    const uint32_t per = (nh + 1023) / 1024;
-    const uint32_t s = threadIdx.x * per;
+    const uint32_t nt = gridDim.x * (uint32_t)FWG;
+    const uint32_t per = (nh + nt - 1) / nt;
+    const uint32_t s = (blockIdx.x * (uint32_t)FWG + threadIdx.x) * per;
     const uint32_t e = s + per < nh ? s + per : nh;
     uint32_t h = 0;
     for (uint32_t i = s; i < e; ++i)
         h = gmul(h, f.k) ^ f.part[i];
     if (s < e)
         h = gmul(h, kpow(f.kp2, nh - e));
-    red[threadIdx.x] = h;
+    for (int o = 32; o > 0; o >>= 1)
+        h ^= __shfl_xor(h, o);
+    if ((threadIdx.x & 63) == 0)
+        red[threadIdx.x >> 6] = h;
     __syncthreads();
-    for (int o = 512; o > 0; o >>= 1) {
-        if ((int)threadIdx.x < o)
-            red[threadIdx.x] ^= red[threadIdx.x + o];
-        __syncthreads();
-    }
     if (threadIdx.x == 0) {
-        uint32_t reg = gmul(red[0], f.x_last) ^ f.part[W - 1];
-        reg ^= gmul(f.r0, f.x_total);
-        *f.out = reg ^ f.xor_out;
+        uint32_t x = 0;
+        for (int k = 0; k < FWG / 64; ++k)
+            x ^= red[k];
+        x = gmul(x, f.x_last);
+        if (blockIdx.x == 0)
+            x ^= f.part[W - 1];
+        atomicXor(f.out, x);
     }
 }
 
@@ -1729,6 +1740,9 @@ extern "C" int zs_launch_burst(int fixed, int xp, int nb, const zs::BatchDesc *d
 
 extern "C" int zs_launch_span_fold(const zs::SpanFold *f, hipStream_t stream)
 {
-    hipLaunchKernelGGL(zs::span_fold_kernel, dim3(1), dim3(1024), 0, stream, *f);
+    /* one part per thread, at most one block per CU's worth (256) */
+    uint32_t blocks = (f->w + zs::FWG - 1) / zs::FWG;
+    blocks = blocks < 1 ? 1 : blocks > 256 ? 256 : blocks;
+    hipLaunchKernelGGL(zs::span_fold_kernel, dim3(blocks), dim3(zs::FWG), 0, stream, *f);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
