@@ -29,7 +29,7 @@ int zscrc_cpu_have_sse42(void);
 void zscrc_cpu_init(void);
 int zs_launch_team(int g, int fixed, int depth, const zs::BatchDesc *d, const uint32_t *gtab, int grid,
                    hipStream_t stream);
-int zs_launch_span_fold(const zs::SpanFold *f, hipStream_t stream);
+int zs_launch_span_fold(const zs::SpanFold *f, const uint32_t *gtab, hipStream_t stream);
 int zs_launch_short(int fixed, int pf, const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
 int zs_launch_stream_read(const void *buf, uint64_t n, uint32_t *out, int grid, hipStream_t stream);
 int zs_launch_classify(const zs::Classify *c, hipStream_t stream);
@@ -527,7 +527,7 @@ int span_impl(DevCtx *c, const void *d_buf, uint64_t len, uint32_t seed, uint32_
         set_err("hipMemsetD32Async(span result)", e);
         return ZSCRC_EHIP;
     }
-    if (zs_launch_span_fold(&f, s)) {
+    if (zs_launch_span_fold(&f, c->gtab, s)) {
         set_err("span fold launch", hipGetLastError());
         return ZSCRC_EHIP;
     }
