@@ -353,7 +353,7 @@ def run_config4(args, world, rank, dev, stream):
     for i in range(6):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(stream)
-        zsfile.write_commits(flat, offs_w, lens_w)
+        zsfile.write_commits(flat, offs_w, lens_w, max_len=max_span)
         b.record(stream)
         torch.cuda.synchronize()
         if i:

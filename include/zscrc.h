@@ -215,6 +215,10 @@ int zscrc_device_verify_commits_bounded(const void *d_image, const uint64_t *d_s
  * and store each one big-endian into its commit record; d_crc[i] receives it. */
 int zscrc_device_write_commits(void *d_image, const uint64_t *d_span_off, const uint64_t *d_span_len, size_t n,
                                uint32_t *d_crc, void *stream);
+/* As zscrc_device_write_commits with a caller-known bound on the span
+ * lengths (see zscrc_device_batch_bounded). */
+int zscrc_device_write_commits_bounded(void *d_image, const uint64_t *d_span_off, const uint64_t *d_span_len,
+                                       size_t n, uint64_t max_len, uint32_t *d_crc, void *stream);
 
 typedef struct zscrc_zs_report {
     int header_rc;            /* zscrc_zs_header_crc result */

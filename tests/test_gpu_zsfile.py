@@ -101,4 +101,9 @@ def test_write_commits_matches_writer(gpu):
     crc = zsfile.write_commits(d, offs, lens)
     torch.cuda.synchronize()
     assert d.cpu().numpy().tobytes() == img
+    # bounded by the walk's longest span: one kernel, same bytes
+    d2 = torch.from_numpy(np.frombuffer(bytes(blank), dtype=np.uint8).copy()).cuda()
+    crc2 = zsfile.write_commits(d2, offs, lens, max_len=int(lens.max().item()))
+    torch.cuda.synchronize()
+    assert d2.cpu().numpy().tobytes() == img and torch.equal(crc2, crc)
     assert (crc.cpu().numpy().view(np.uint32) == np.array([c["stored"] for c in commits], np.uint32)).all()

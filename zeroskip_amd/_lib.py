@@ -47,6 +47,7 @@ SIGNATURES = {
     "zscrc_device_verify_commits": (_int, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
     "zscrc_device_verify_commits_seeded": (_int, [_vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp]),
     "zscrc_device_verify_commits_bounded": (_int, [_vp, _vp, _vp, _vp, _sz, _u64, _vp, _vp, _vp]),
+    "zscrc_device_write_commits_bounded": (_int, [_vp, _vp, _vp, _sz, _u64, _vp, _vp]),
     "zscrc_device_batch_bounded": (_int, [_vp, _vp, _vp, _vp, _vp, _sz, ctypes.c_uint, _u64, _vp]),
     "zscrc_zs_verify_image": (_int, [_vp, _u64, _int, _vp]),
     "zscrc_device_write_commits": (_int, [_vp, _vp, _vp, _sz, _vp, _vp]),

@@ -240,6 +240,13 @@ int zscrc_device_verify_commits_bounded(const void *d_image, const uint64_t *d_s
                                          max_len);
 }
 
+int zscrc_device_write_commits_bounded(void *d_image, const uint64_t *d_span_off, const uint64_t *d_span_len,
+                                       size_t n, uint64_t max_len, uint32_t *d_crc, void *stream)
+{
+    return zscrc_internal_verify_commits(d_image, d_span_off, d_span_len, nullptr, d_crc, nullptr, n, stream, 1,
+                                         max_len);
+}
+
 int zscrc_device_write_commits(void *d_image, const uint64_t *d_span_off, const uint64_t *d_span_len, size_t n,
                                uint32_t *d_crc, void *stream)
 {

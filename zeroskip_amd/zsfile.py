@@ -12,7 +12,7 @@ import ctypes
 import numpy as np
 import torch
 
-from ._lib import check, lib
+from ._lib import LEN_UNBOUNDED, check, lib
 
 END, STOPPED, TRUNCATED, OVERFLOW, BADSIG = 0, 1, 2, 3, 4
 ACTIVE, FINALISED, PACKED = 0, 1, 2
@@ -111,13 +111,16 @@ def verify_commits(d_image: torch.Tensor, span_off: torch.Tensor, span_len: torc
     return crc, st
 
 
-def write_commits(d_image: torch.Tensor, span_off: torch.Tensor, span_len: torch.Tensor) -> torch.Tensor:
+def write_commits(d_image: torch.Tensor, span_off: torch.Tensor, span_len: torch.Tensor,
+                  max_len: int | None = None) -> torch.Tensor:
     """Writer side on the GPU: compute every commit CRC and store it
-    big-endian into its commit record in `d_image` (in place)."""
+    big-endian into its commit record in `d_image` (in place).  max_len: a
+    known bound on the span lengths (zscrc_device_write_commits_bounded)."""
     n = span_off.numel()
     crc = torch.empty(n, dtype=torch.int32, device=d_image.device)
     with torch.cuda.device(d_image.device):
-        check(lib().zscrc_device_write_commits(
-            d_image.data_ptr(), span_off.data_ptr(), span_len.data_ptr(), n, crc.data_ptr(),
-            torch.cuda.current_stream(d_image.device).cuda_stream), "zscrc_device_write_commits")
+        check(lib().zscrc_device_write_commits_bounded(
+            d_image.data_ptr(), span_off.data_ptr(), span_len.data_ptr(), n,
+            LEN_UNBOUNDED if max_len is None else max_len, crc.data_ptr(),
+            torch.cuda.current_stream(d_image.device).cuda_stream), "zscrc_device_write_commits_bounded")
     return crc
