@@ -190,35 +190,46 @@ int zscrc_zs_packed_spans(const void *image, uint64_t size, uint64_t span_off[2]
 int zscrc_zs_header_crc(const void *image, uint64_t size, uint32_t *stored, uint32_t *computed);
 /* 61-byte .zsdb CRC over host-order fields (zeroskip-dotzsdb.c:160-235). */
 int zscrc_zs_dotzsdb_crc(const void *image, uint64_t size, uint32_t *stored, uint32_t *computed);
-/* Device: verify n commits of a device-resident image.  d_crc[i] = computed
- * commit CRC, d_status[i] = 1 match / 0 mismatch / 2 no commit record. */
-int zscrc_device_verify_commits(const void *d_image, const uint64_t *d_span_off, const uint64_t *d_span_len,
-                                size_t n, uint32_t *d_crc, uint32_t *d_status, void *stream);
+/* Device: verify n commits of a device-resident image of image_size bytes.
+ * Commit i's span is [d_span_off[i], +d_span_len[i]) and its commit record
+ * starts right after it.  d_crc[i] = computed commit CRC, d_status[i] = 1
+ * match / 0 mismatch / 2 no commit record there -- also when the span, the
+ * 8-byte commit word or a long commit's 24 bytes do not lie inside the image:
+ * nothing outside [d_image, d_image + image_size) is ever read. */
+int zscrc_device_verify_commits(const void *d_image, uint64_t image_size, const uint64_t *d_span_off,
+                                const uint64_t *d_span_len, size_t n, uint32_t *d_crc, uint32_t *d_status,
+                                void *stream);
 
 /* Device: as zscrc_device_verify_commits, but span i's CRC continues from
  * d_seed[i] (a crc32c value, crc32c(d_seed[i], span) chaining) instead of
  * crc32c(0, 0, 0) = 0.  Resolves the reference's zero-length finalise commit
  * (zeroskip-file.c:253-350 after crc32_end without crc32_begin, mfile.c:534-546):
  * its stored CRC continues from the previous span's CRC.  d_seed NULL = 0. */
-int zscrc_device_verify_commits_seeded(const void *d_image, const uint64_t *d_span_off,
+int zscrc_device_verify_commits_seeded(const void *d_image, uint64_t image_size, const uint64_t *d_span_off,
                                        const uint64_t *d_span_len, const uint32_t *d_seed, size_t n,
                                        uint32_t *d_crc, uint32_t *d_status, void *stream);
 
 /* Device: zscrc_device_verify_commits_seeded (d_seed may be NULL) with a
  * caller-known bound on the span lengths, as zscrc_device_batch_bounded --
  * the host walk that found the commits knows it. */
-int zscrc_device_verify_commits_bounded(const void *d_image, const uint64_t *d_span_off,
+int zscrc_device_verify_commits_bounded(const void *d_image, uint64_t image_size, const uint64_t *d_span_off,
                                         const uint64_t *d_span_len, const uint32_t *d_seed, size_t n,
                                         uint64_t max_len, uint32_t *d_crc, uint32_t *d_status, void *stream);
 
 /* Device: compute n commit CRCs (the writer's side, zeroskip-file.c:253-350)
- * and store each one big-endian into its commit record; d_crc[i] receives it. */
-int zscrc_device_write_commits(void *d_image, const uint64_t *d_span_off, const uint64_t *d_span_len, size_t n,
-                               uint32_t *d_crc, void *stream);
+ * and store each one big-endian into its commit record; d_crc[i] receives it.
+ * The commit record's header word (type, and for long commits the length
+ * words) must already be in the image: only the CRC field is written.
+ * d_status (may be NULL): 1 written, 2 not written (no commit record there,
+ * or outside the image -- nothing outside the image is read or written). */
+int zscrc_device_write_commits(void *d_image, uint64_t image_size, const uint64_t *d_span_off,
+                               const uint64_t *d_span_len, size_t n, uint32_t *d_crc, uint32_t *d_status,
+                               void *stream);
 /* As zscrc_device_write_commits with a caller-known bound on the span
  * lengths (see zscrc_device_batch_bounded). */
-int zscrc_device_write_commits_bounded(void *d_image, const uint64_t *d_span_off, const uint64_t *d_span_len,
-                                       size_t n, uint64_t max_len, uint32_t *d_crc, void *stream);
+int zscrc_device_write_commits_bounded(void *d_image, uint64_t image_size, const uint64_t *d_span_off,
+                                       const uint64_t *d_span_len, size_t n, uint64_t max_len, uint32_t *d_crc,
+                                       uint32_t *d_status, void *stream);
 
 typedef struct zscrc_zs_report {
     int header_rc;            /* zscrc_zs_header_crc result */

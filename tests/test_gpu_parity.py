@@ -274,6 +274,27 @@ def test_scalar_offload(gpu):
     assert after[0] - before[0] == 1   # the 37-byte call stayed on the CPU
 
 
+def test_config3_headline_dispatch(gpu):
+    """BASELINE config 3 at full size through the exact call bench.py times:
+    zscrc_device_fixed on 65,536 x 64 KiB chunks (4 GiB), seed 0, flags 0 --
+    the 16-lane team walk with xor_io = ~0 -- every CRC against the oracle."""
+    n, L = 65536, 65536
+    assert lib().zscrc_team_for(L, n) == 16
+    g = torch.Generator(device=gpu)
+    g.manual_seed(0x9E3779B9)
+    d = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=gpu, generator=g)
+    out = torch.empty(n, dtype=torch.int32, device=gpu)
+    from zeroskip_amd._lib import check
+    check(lib().zscrc_device_fixed(d.data_ptr(), L, L, 0, out.data_ptr(), n, 0,
+                                   torch.cuda.current_stream(gpu).cuda_stream), "zscrc_device_fixed")
+    got = u32(out)
+    host = d.cpu().numpy()
+    del d
+    ref = oracle.batch(host, n=n, stride=L, fixed_len=L, impl="hw", threads=min(16, os.cpu_count() or 1))
+    bad = np.nonzero(got != ref)[0]
+    assert bad.size == 0, bad[:10]
+
+
 def test_config2_full_size_vs_oracle(gpu):
     # BASELINE config 2 at full size: 1,048,576 x 64 B records, every CRC checked
     n = 1 << 20

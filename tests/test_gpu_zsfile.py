@@ -107,3 +107,62 @@ def test_write_commits_matches_writer(gpu):
     torch.cuda.synchronize()
     assert d2.cpu().numpy().tobytes() == img and torch.equal(crc2, crc)
     assert (crc.cpu().numpy().view(np.uint32) == np.array([c["stored"] for c in commits], np.uint32)).all()
+
+
+@pytest.mark.parametrize("bound", ["none", "exact", "short"])
+def test_commits_bounded_by_image(gpu, bound):
+    """d_status 2 (and no read or write outside the image) for spans whose
+    commit word, or a long commit's 24 bytes, do not lie inside image_size;
+    a commit whose word ends exactly at the image end still verifies."""
+    w = zf.FileWriter(UUID)
+    rng = np.random.default_rng(77)
+    for t in range(40):
+        w.add(b"%016d" % t, rng.integers(0, 256, int(rng.integers(0, 900)), dtype=np.uint8).tobytes())
+        w.commit()
+    w.add(b"L" * 16, rng.integers(0, 256, (16 << 20) + 40, dtype=np.uint8).tobytes())   # long commit last
+    w.commit()
+    img = w.image()
+    commits, _, _ = zf.walk(img)
+    assert img[commits[-1]["commit_off"]] == zf.REC_LONG_COMMIT and commits[-1]["commit_off"] + 24 == len(img)
+    host = np.frombuffer(img + b"\xab" * 64, dtype=np.uint8).copy()
+    full = torch.from_numpy(host).cuda()
+    offs = [c["span_off"] for c in commits]
+    lens = [c["span_len"] for c in commits]
+    c39 = commits[39]
+    # extra descriptors: span past the end, offset past the end, huge length
+    offs += [c39["span_off"], len(img) + 100, 40]
+    lens += [c39["span_len"] + 64, 0, 1 << 62]
+    d_off = torch.tensor(offs, dtype=torch.int64, device="cuda")
+    d_len = torch.tensor(lens, dtype=torch.int64, device="cuda")
+    mx = {"none": None, "exact": max(lens), "short": 640}[bound]
+    n = len(commits)
+
+    def status(size):
+        _, st = zsfile.verify_commits(full[:size], d_off, d_len, max_len=mx)
+        torch.cuda.synchronize()
+        return st.cpu().numpy()
+
+    st = status(len(img))                        # the long commit's 24 bytes end at the image end
+    assert (st[:n] == 1).all() and (st[n:] == 2).all(), st
+    st = status(len(img) - 1)                    # one byte short: the long commit has no room
+    assert (st[:n - 1] == 1).all() and st[n - 1] == 2 and (st[n:] == 2).all()
+    st = status(commits[-1]["commit_off"] + 8)   # the long commit's first word only
+    assert (st[:n - 1] == 1).all() and st[n - 1] == 2
+    st = status(c39["commit_off"] + 8)           # short commit word ends at the image end
+    assert (st[:40] == 1).all() and st[40] == 2
+    st = status(c39["commit_off"])               # span ends at the image end: no commit word
+    assert (st[:39] == 1).all() and st[39] == 2 and st[40] == 2
+    # writer: a commit word outside the image is neither read nor written
+    blank = host.copy()
+    for c in commits:
+        blank[c["commit_off"] + (20 if c is commits[-1] else 4):][:4] = 0
+    d = torch.from_numpy(blank).cuda()
+    size = c39["commit_off"] + 6
+    _, wst = zsfile.write_commits(d[:size], d_off, d_len, max_len=mx, status=True)
+    torch.cuda.synchronize()
+    wst = wst.cpu().numpy()
+    assert (wst[:39] == 1).all() and (wst[39:] == 2).all()
+    got = d.cpu().numpy()
+    want = blank.copy()
+    want[:c39["commit_off"]] = host[:c39["commit_off"]]
+    assert np.array_equal(got, want)

@@ -1,6 +1,7 @@
 """Host-side zeroskip parsing in libzscrc (walk, packed spans, header and .zsdb
 CRC) agrees with the format oracle.  No GPU."""
 import numpy as np
+import pytest
 
 from oracle import zs_format as zf
 from tests.test_format_oracle import UUID, build_active
@@ -45,3 +46,40 @@ def test_header_and_dotzsdb_crc():
     bad[20] ^= 1
     rc, st, cp = zsfile.dotzsdb_crc(bytes(bad))
     assert st != cp
+
+
+def _key_then_long_value(voff_extra: int, vlen: int) -> bytes:
+    """Header, one short key record (16-byte key) and a LONG_VALUE record
+    whose 64-bit length word is `vlen` (corrupt on purpose)."""
+    hdr = build_active(1)[:zf.HDR_SIZE]
+    voff = 24 + 16 + voff_extra
+    key = zf.be64((zf.REC_KEY << 56) | (16 << 40) | voff) + bytes(16) + b"k" * 16 + bytes(voff_extra)
+    val = zf.be64(zf.REC_LONG_VALUE << 56) + zf.be64(vlen) + b"v" * 64
+    return hdr + key + val
+
+
+@pytest.mark.timeout(20)
+@pytest.mark.parametrize("case", ["wrapped_vlen", "self_loop", "vlen_past_end", "long_delete_at_end",
+                                  "long_delete_huge_klen", "long_key_huge_voff"])
+def test_walk_survives_corrupt_lengths(case):
+    """Every length word is file data: a corrupt one must stop the walk with
+    TRUNCATED -- never loop, go backwards or read past the image."""
+    voff = 24 + 16
+    if case == "wrapped_vlen":
+        img = _key_then_long_value(0, (1 << 64) - 8)
+    elif case == "self_loop":
+        # v + 16 + rup8(vlen) == off (mod 2^64): the old walk stood still forever
+        img = _key_then_long_value(0, (1 << 64) - 16 - voff)
+    elif case == "vlen_past_end":
+        img = _key_then_long_value(0, 4096)
+    elif case == "long_delete_at_end":
+        # a long delete's key length sits at off + 8, past the image end
+        img = build_active(2) + zf.be64(zf.REC_LONG_DELETED << 56)
+    elif case == "long_delete_huge_klen":
+        img = build_active(2) + zf.be64(zf.REC_LONG_DELETED << 56) + zf.be64((1 << 64) - 24) + bytes(8)
+    else:
+        hdr = build_active(1)[:zf.HDR_SIZE]
+        img = hdr + zf.be64(zf.REC_LONG_KEY << 56) + zf.be64(16) + zf.be64((1 << 64) - 1) + b"k" * 16
+    off, ln, rc, end = zsfile.walk(img)
+    assert rc == zsfile.TRUNCATED, (case, rc, end)
+    assert zf.HDR_SIZE <= end <= len(img)

@@ -44,13 +44,13 @@ SIGNATURES = {
     "zscrc_zs_packed_spans": (_int, [_vp, _u64, _vp, _vp]),
     "zscrc_zs_header_crc": (_int, [_vp, _u64, _vp, _vp]),
     "zscrc_zs_dotzsdb_crc": (_int, [_vp, _u64, _vp, _vp]),
-    "zscrc_device_verify_commits": (_int, [_vp, _vp, _vp, _sz, _vp, _vp, _vp]),
-    "zscrc_device_verify_commits_seeded": (_int, [_vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp]),
-    "zscrc_device_verify_commits_bounded": (_int, [_vp, _vp, _vp, _vp, _sz, _u64, _vp, _vp, _vp]),
-    "zscrc_device_write_commits_bounded": (_int, [_vp, _vp, _vp, _sz, _u64, _vp, _vp]),
+    "zscrc_device_verify_commits": (_int, [_vp, _u64, _vp, _vp, _sz, _vp, _vp, _vp]),
+    "zscrc_device_verify_commits_seeded": (_int, [_vp, _u64, _vp, _vp, _vp, _sz, _vp, _vp, _vp]),
+    "zscrc_device_verify_commits_bounded": (_int, [_vp, _u64, _vp, _vp, _vp, _sz, _u64, _vp, _vp, _vp]),
+    "zscrc_device_write_commits_bounded": (_int, [_vp, _u64, _vp, _vp, _sz, _u64, _vp, _vp, _vp]),
     "zscrc_device_batch_bounded": (_int, [_vp, _vp, _vp, _vp, _vp, _sz, ctypes.c_uint, _u64, _vp]),
     "zscrc_zs_verify_image": (_int, [_vp, _u64, _int, _vp]),
-    "zscrc_device_write_commits": (_int, [_vp, _vp, _vp, _sz, _vp, _vp]),
+    "zscrc_device_write_commits": (_int, [_vp, _u64, _vp, _vp, _sz, _vp, _vp, _vp]),
     "zscrc_stream_open": (_int, [_vp, _u32, _u64, ctypes.c_uint]),
     "zscrc_stream_update": (_int, [_vp, _vp, _sz]),
     "zscrc_stream_final": (_int, [_vp, _vp]),

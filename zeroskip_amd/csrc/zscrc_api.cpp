@@ -401,6 +401,8 @@ int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1
     cl.count = cnt;
     cl.bytes = cbytes;
     cl.desc = desc;
+    cl.commit = d.commit != 0;
+    cl.img_size = d.img_size;
     {
         /* class 0 goes to burst_kernel (walk 9, the default), which walks
          * the caller's arrays and skips longer records: no class-0 list */
@@ -777,9 +779,9 @@ int zscrc_diag_stream_read(const void *d_buf, uint64_t len, void *d_scratch4, in
     return ZSCRC_OK;
 }
 
-int zscrc_internal_verify_commits(const void *d_image, const uint64_t *d_off, const uint64_t *d_len,
-                                  const uint32_t *d_seed, uint32_t *d_crc, uint32_t *d_status, size_t n,
-                                  void *stream, int write, uint64_t max_len)
+int zscrc_internal_verify_commits(const void *d_image, uint64_t image_size, const uint64_t *d_off,
+                                  const uint64_t *d_len, const uint32_t *d_seed, uint32_t *d_crc,
+                                  uint32_t *d_status, size_t n, void *stream, int write, uint64_t max_len)
 {
     if (n == 0)
         return ZSCRC_OK;
@@ -797,6 +799,7 @@ int zscrc_internal_verify_commits(const void *d_image, const uint64_t *d_off, co
     d.out = d_crc;
     d.status = d_status;
     d.commit = write ? 2u : 1u;
+    d.img_size = image_size;
     d.n = n;
     d.xor_io = 0xffffffffu;
     return launch_classes(c, d, static_cast<hipStream_t>(stream), max_len);

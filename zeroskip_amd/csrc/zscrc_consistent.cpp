@@ -121,7 +121,8 @@ int verify_group(std::vector<DbFile> &files, size_t a, size_t b, zscrc_consisten
     for (uint64_t l : hlen)
         max_len = l > max_len ? l : max_len;
     if (!rc)
-        rc = zscrc_device_verify_commits_bounded(dimg, doff, dlen, nullptr, ncommit, max_len, dcrc, dst, nullptr);
+        rc = zscrc_device_verify_commits_bounded(dimg, total, doff, dlen, nullptr, ncommit, max_len, dcrc, dst,
+                                                 nullptr);
     if (!rc && hipMemcpy(st.data(), dst, ncommit * 4, hipMemcpyDeviceToHost) != hipSuccess)
         rc = ZSCRC_EHIP;
     /* zero-length mismatches right after a commit of the same file: the
@@ -155,7 +156,7 @@ int verify_group(std::vector<DbFile> &files, size_t a, size_t b, zscrc_consisten
         if (!rc)
             rc = zscrc_device_batch_bounded(dimg, dq, dq + m, nullptr, dprev, m, 0, prev_max, nullptr);
         if (!rc) /* the candidates are zero-length spans */
-            rc = zscrc_device_verify_commits_bounded(dimg, dq + 2 * m, dq + 3 * m, dprev, m, 0, dprev + m,
+            rc = zscrc_device_verify_commits_bounded(dimg, total, dq + 2 * m, dq + 3 * m, dprev, m, 0, dprev + m,
                                                      dprev + 2 * m, nullptr);
         if (!rc && hipMemcpy(st2.data(), dprev + 2 * m, m * 4, hipMemcpyDeviceToHost) != hipSuccess)
             rc = ZSCRC_EHIP;

@@ -40,6 +40,10 @@ struct BatchDesc {
      * write: the CRC is stored big-endian into the commit record. */
     uint32_t commit;
     uint32_t *status;     /* may be NULL */
+    /* commit mode: bytes of the image at base.  A span whose commit word
+     * (8 bytes, 24 for a long commit) does not lie inside the image gets
+     * status 2 and nothing outside the image is read or written. */
+    uint64_t img_size;
     /* variable batches: class-sorted record descriptors built on the device
      * by classify_kernel; this launch covers class `klass`, i.e. entries
      * [sum(class_count[<klass]), +class_count[klass]) */
@@ -82,7 +86,14 @@ struct Classify {
                              (BatchDesc::direct_max): no class-0 scatter, and
                              no scatter pass at all when every record is
                              class 0 */
+    int commit;           /* commit batch: spans outside img_size become
+                             empty no-commit descriptors (NO_COMMIT_OFF) */
+    uint64_t img_size;
 };
+
+/* Offset of a commit descriptor whose span or commit word lies outside the
+ * image (classify_kernel writes it with length 0; status 2). */
+constexpr uint64_t NO_COMMIT_OFF = ~0ull;
 
 /* How a length class is split (written by plan_kernel on the device). */
 struct SplitPlan {

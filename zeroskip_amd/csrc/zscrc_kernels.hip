@@ -171,6 +171,25 @@ struct Cursor {
 /* FIXED: record i = base + i*stride, fixed_len bytes (last_len for the last
  * one when set), fixed_seed -- no per-record metadata loads, so nothing here
  * waits on the vector-memory counter and the data prefetch ring survives. */
+/* Commit batches: do span [off, off+len) and the 8-byte commit word after it
+ * lie inside the image?  A record that does not is hashed as an empty span
+ * with no commit word (status 2): nothing outside the image is read. */
+__device__ __forceinline__ bool commit_fits(uint64_t size, uint64_t off, uint64_t len)
+{
+    return off <= size && len <= size - off && size - off - len >= 8;
+}
+
+/* (off, len) of a commit-batch record after the image bound: unchanged when
+ * it fits, else an empty span at the image start; returns whether it fits. */
+__device__ __forceinline__ bool commit_clamp(const BatchDesc &d, uint64_t &off, uint64_t &len)
+{
+    if (commit_fits(d.img_size, off, len))
+        return true;
+    off = 0;
+    len = 0;
+    return false;
+}
+
 /* The team's next record descriptor, loaded one record ahead. */
 struct Meta {
     uint64_t off, len;
@@ -221,6 +240,14 @@ __device__ __forceinline__ bool fetch_record(const BatchDesc &d, const RecDesc *
         off = m.off;
         seed = m.seed;
         rec = m.rec;
+        it.c0 = it.c1 = 0;
+        if (d.commit && !sp && commit_clamp(d, off, len)) {
+            /* the commit record's first word, fetched with the record so the
+             * check at the record end never waits on a late load */
+            const uintptr_t T = reinterpret_cast<uintptr_t>(d.base) + off + len;
+            it.c0 = ((g32p)T)[0];
+            it.c1 = ((g32p)T)[1];
+        }
         if (sp) {
             /* part p of the record: bytes [p * unit, +unit), the last one the rest */
             const uint64_t U = d.plan[d.klass].unit;
@@ -244,12 +271,6 @@ __device__ __forceinline__ bool fetch_record(const BatchDesc &d, const RecDesc *
     it.rec = rec;
     it.w = w;
     it.R0 = seed ^ d.xor_io;
-    if (!FIXED && d.commit && !sp) {
-        /* the commit record's first word, fetched with the record so the
-         * check at the record end never waits on a late load */
-        it.c0 = ((g32p)(A + len))[0];
-        it.c1 = ((g32p)(A + len))[1];
-    }
     return true;
 }
 
@@ -345,7 +366,8 @@ __device__ __forceinline__ void emit(const BatchDesc &d, const Item &it, uint32_
         stored = (uint32_t)w0;
         crc_at = end + 4;
         st = 0;
-    } else if (t == REC_LONG_COMMIT || t == REC_LONG_FINAL) {
+    } else if ((t == REC_LONG_COMMIT || t == REC_LONG_FINAL) &&
+               end + 24 <= reinterpret_cast<uintptr_t>(d.base) + d.img_size) {
         const uint64_t w1 = load_be64(end + 8), w2 = load_be64(end + 16);
         r = feed64(L, r, w0, c_lo, c_hi);
         r = feed64(L, r, w1, c_lo, c_hi);
@@ -827,11 +849,13 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
             seed = c.x;
             it.rec = c.y;
         }
+        it.c0 = it.c1 = 0;
+        const bool cfit = !FIXED && d.commit && commit_clamp(d, off, len);
         const uintptr_t A = reinterpret_cast<uintptr_t>(d.base) + off;
         it.A = A;
         it.len = len;
         it.R0 = seed ^ d.xor_io;
-        if (!FIXED && d.commit) {
+        if (cfit) {
             it.c0 = ((g32p)(A + len))[0];
             it.c1 = ((g32p)(A + len))[1];
         }
@@ -1018,6 +1042,14 @@ __device__ __forceinline__ void burst_meta(const BatchDesc &d, const RecDesc *li
         typedef const __attribute__((address_space(1))) uint64_t *g64p;
         len = ((g64p)d.len)[i];
         b.it.rec = i;
+        if (d.commit) {
+            /* an out-of-image commit is class 0 (empty): this kernel's */
+            off = ((g64p)d.off)[i];
+            if (!commit_fits(d.img_size, off, len)) {
+                off = NO_COMMIT_OFF;
+                len = 0;
+            }
+        }
         if (d.direct_max && len > d.direct_max) {
             b.skip = true;
             b.burst = false;
@@ -1026,7 +1058,8 @@ __device__ __forceinline__ void burst_meta(const BatchDesc &d, const RecDesc *li
             b.it.len = 0;
             return;
         }
-        off = ((g64p)d.off)[i];
+        if (!d.commit)
+            off = ((g64p)d.off)[i];
         seed = d.seed ? ((g32p)d.seed)[i] : 0u;
     } else {
         typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -1038,11 +1071,13 @@ __device__ __forceinline__ void burst_meta(const BatchDesc &d, const RecDesc *li
         seed = c.x;
         b.it.rec = c.y;
     }
+    b.it.c0 = b.it.c1 = 0;
+    const bool cfit = !FIXED && d.commit && commit_clamp(d, off, len);
     const uintptr_t A = reinterpret_cast<uintptr_t>(d.base) + off;
     b.it.A = A;
     b.it.len = len;
     b.it.R0 = seed ^ d.xor_io;
-    if (!FIXED && d.commit) {
+    if (cfit) {
         b.it.c0 = ((g32p)(A + len))[0];
         b.it.c1 = ((g32p)(A + len))[1];
     }
@@ -1364,6 +1399,7 @@ __global__ __launch_bounds__(CWG) void classify_kernel(Classify c)
     const uint64_t r1 = r0 + per < c.n ? r0 + per : c.n;
     const int lane = threadIdx.x & 63;
     const __attribute__((address_space(1))) uint64_t *lens = (const __attribute__((address_space(1))) uint64_t *)c.len;
+    const __attribute__((address_space(1))) uint64_t *offs = (const __attribute__((address_space(1))) uint64_t *)c.off;
     if (threadIdx.x < 4) {
         cnt[threadIdx.x] = 0;
         pos[threadIdx.x] = 0;
@@ -1377,6 +1413,12 @@ __global__ __launch_bounds__(CWG) void classify_kernel(Classify c)
 #pragma unroll
         for (int j = 0; j < CL; ++j)
             v[j] = rb + CWG * j < r1 ? lens[rb + CWG * j] : ~0ull;
+        if (c.commit) { /* out-of-image commits count as empty (class 0) */
+#pragma unroll
+            for (int j = 0; j < CL; ++j)
+                if (rb + CWG * j < r1 && !commit_fits(c.img_size, offs[rb + CWG * j], v[j]))
+                    v[j] = 0;
+        }
 #pragma unroll
         for (int j = 0; j < CL; ++j) {
             if (rb + CWG * j >= r1)
@@ -1424,9 +1466,14 @@ __global__ __launch_bounds__(CWG) void classify_kernel(Classify c)
     for (uint64_t b = r0 + (threadIdx.x & ~63u); b < r1; b += CWG) {
         const uint64_t rec = b + lane;
         int cls = -1;
-        uint64_t len = 0;
+        uint64_t len = 0, off = 0;
         if (rec < r1) {
             len = lens[rec];
+            off = offs[rec];
+            if (c.commit && !commit_fits(c.img_size, off, len)) {
+                off = NO_COMMIT_OFF;
+                len = 0;
+            }
             cls = class_of(c, len);
             if (cls == 0 && c.direct_ok)
                 cls = -1; /* the class-0 kernel reads the caller's arrays */
@@ -1443,7 +1490,7 @@ __global__ __launch_bounds__(CWG) void classify_kernel(Classify c)
             p = __shfl(p, leader);
             if (cls == k) {
                 RecDesc r;
-                r.off = ((const __attribute__((address_space(1))) uint64_t *)c.off)[rec];
+                r.off = off;
                 r.len = len;
                 r.seed = c.seed ? ((g32p)c.seed)[rec] : 0u;
                 r.rec = (uint32_t)rec;
@@ -1610,7 +1657,9 @@ __global__ __launch_bounds__(256) void part_fold_kernel(BatchDesc d, const uint3
             continue;
         }
         const uintptr_t end = reinterpret_cast<uintptr_t>(d.base) + r.off + len;
-        const uint64_t w0 = load_be64(end);
+        /* classify_kernel only lets commits inside the image through */
+        const uint64_t room = commit_fits(d.img_size, r.off, len) ? d.img_size - r.off - len : 0;
+        const uint64_t w0 = room >= 8 ? load_be64(end) : 0;
         const uint32_t ty = (uint32_t)(w0 >> 56);
         uint64_t tw[3];
         int nt = 0;
@@ -1620,7 +1669,7 @@ __global__ __launch_bounds__(256) void part_fold_kernel(BatchDesc d, const uint3
             tw[nt++] = w0 & 0xFFFFFFFF00000000ull;
             stored = (uint32_t)w0;
             crc_at = end + 4;
-        } else if (ty == REC_LONG_COMMIT || ty == REC_LONG_FINAL) {
+        } else if ((ty == REC_LONG_COMMIT || ty == REC_LONG_FINAL) && room >= 24) {
             const uint64_t w2 = load_be64(end + 16);
             tw[nt++] = w0;
             tw[nt++] = load_be64(end + 8);

@@ -29,10 +29,10 @@
 #include "../../include/zscrc.h"
 #include "zscrc_internal.h"
 
-extern "C" int zscrc_internal_verify_commits(const void *d_image, const uint64_t *d_off, const uint64_t *d_len,
-                                             const uint32_t *d_seed,
-                                             uint32_t *d_crc, uint32_t *d_status, size_t n, void *stream,
-                                             int write, uint64_t max_len);
+extern "C" int zscrc_internal_verify_commits(const void *d_image, uint64_t image_size, const uint64_t *d_off,
+                                             const uint64_t *d_len, const uint32_t *d_seed, uint32_t *d_crc,
+                                             uint32_t *d_status, size_t n, void *stream, int write,
+                                             uint64_t max_len);
 
 namespace {
 
@@ -92,8 +92,13 @@ int zscrc_zs_walk(const void *image, uint64_t size, uint64_t *span_off, uint64_t
     int rc = ZSCRC_ZS_END;
     if (!img || size < HDR)
         return ZSCRC_EINVAL;
+    /* Every length word comes from the file, which may be corrupt: each step
+     * is checked against the bytes left (`room`, never an add that can wrap),
+     * so the next offset is always past the current one and inside the image
+     * or the walk stops with TRUNCATED. */
     while (off < size) {
-        if (off + 8 > size) {
+        const uint64_t room = size - off;
+        if (room < 8) {
             rc = ZSCRC_ZS_TRUNCATED;
             break;
         }
@@ -104,22 +109,36 @@ int zscrc_zs_walk(const void *image, uint64_t size, uint64_t *span_off, uint64_t
             if (t == T_KEY) {
                 voff = w & 0xFFFFFFFFull;
             } else {
-                if (off + 24 > size) {
+                if (room < 24) {
                     rc = ZSCRC_ZS_TRUNCATED;
                     break;
                 }
                 voff = be64(img + off + 16);
             }
-            const uint64_t v = off + voff;
-            if (voff == 0 || v + 16 > size) {
+            /* the value record (16-byte header) starts voff bytes on */
+            if (voff == 0 || voff > room || room - voff < 16) {
                 rc = ZSCRC_ZS_TRUNCATED;
                 break;
             }
+            const uint64_t v = off + voff;
             const uint64_t vw = be64(img + v);
             const uint64_t vlen = (vw >> 56) == T_VALUE ? ((vw >> 32) & 0xFFFFFF) : be64(img + v + 8);
+            const uint64_t vroom = size - v - 16;
+            if (vlen > vroom || rup8(vlen) > vroom) { /* vlen <= vroom: rup8 cannot wrap */
+                rc = ZSCRC_ZS_TRUNCATED;
+                break;
+            }
             off = v + 16 + rup8(vlen);
         } else if (t == T_DELETED || t == T_LONG_DELETED_ALIAS) {
+            if (room < 24) {
+                rc = ZSCRC_ZS_TRUNCATED;
+                break;
+            }
             const uint64_t klen = t == T_DELETED ? ((w >> 40) & 0xFFFF) : be64(img + off + 8);
+            if (klen > room - 24 || rup8(klen) > room - 24) {
+                rc = ZSCRC_ZS_TRUNCATED;
+                break;
+            }
             off += 24 + rup8(klen);
         } else if (t == T_COMMIT || t == T_LONG_COMMIT) {
             uint64_t sl, rl;
@@ -217,41 +236,44 @@ int zscrc_zs_dotzsdb_crc(const void *image, uint64_t size, uint32_t *stored, uin
     return sig == SIGNATURE ? ZSCRC_OK : ZSCRC_ZS_BADSIG;
 }
 
-int zscrc_device_verify_commits(const void *d_image, const uint64_t *d_span_off, const uint64_t *d_span_len,
-                                size_t n, uint32_t *d_crc, uint32_t *d_status, void *stream)
+int zscrc_device_verify_commits(const void *d_image, uint64_t image_size, const uint64_t *d_span_off,
+                                const uint64_t *d_span_len, size_t n, uint32_t *d_crc, uint32_t *d_status,
+                                void *stream)
 {
-    return zscrc_internal_verify_commits(d_image, d_span_off, d_span_len, nullptr, d_crc, d_status, n, stream, 0,
-                                         ZSCRC_LEN_UNBOUNDED);
+    return zscrc_internal_verify_commits(d_image, image_size, d_span_off, d_span_len, nullptr, d_crc, d_status, n,
+                                         stream, 0, ZSCRC_LEN_UNBOUNDED);
 }
 
-int zscrc_device_verify_commits_seeded(const void *d_image, const uint64_t *d_span_off,
+int zscrc_device_verify_commits_seeded(const void *d_image, uint64_t image_size, const uint64_t *d_span_off,
                                        const uint64_t *d_span_len, const uint32_t *d_seed, size_t n,
                                        uint32_t *d_crc, uint32_t *d_status, void *stream)
 {
-    return zscrc_internal_verify_commits(d_image, d_span_off, d_span_len, d_seed, d_crc, d_status, n, stream, 0,
-                                         ZSCRC_LEN_UNBOUNDED);
+    return zscrc_internal_verify_commits(d_image, image_size, d_span_off, d_span_len, d_seed, d_crc, d_status, n,
+                                         stream, 0, ZSCRC_LEN_UNBOUNDED);
 }
 
-int zscrc_device_verify_commits_bounded(const void *d_image, const uint64_t *d_span_off,
+int zscrc_device_verify_commits_bounded(const void *d_image, uint64_t image_size, const uint64_t *d_span_off,
                                         const uint64_t *d_span_len, const uint32_t *d_seed, size_t n,
                                         uint64_t max_len, uint32_t *d_crc, uint32_t *d_status, void *stream)
 {
-    return zscrc_internal_verify_commits(d_image, d_span_off, d_span_len, d_seed, d_crc, d_status, n, stream, 0,
-                                         max_len);
+    return zscrc_internal_verify_commits(d_image, image_size, d_span_off, d_span_len, d_seed, d_crc, d_status, n,
+                                         stream, 0, max_len);
 }
 
-int zscrc_device_write_commits_bounded(void *d_image, const uint64_t *d_span_off, const uint64_t *d_span_len,
-                                       size_t n, uint64_t max_len, uint32_t *d_crc, void *stream)
+int zscrc_device_write_commits_bounded(void *d_image, uint64_t image_size, const uint64_t *d_span_off,
+                                       const uint64_t *d_span_len, size_t n, uint64_t max_len, uint32_t *d_crc,
+                                       uint32_t *d_status, void *stream)
 {
-    return zscrc_internal_verify_commits(d_image, d_span_off, d_span_len, nullptr, d_crc, nullptr, n, stream, 1,
-                                         max_len);
+    return zscrc_internal_verify_commits(d_image, image_size, d_span_off, d_span_len, nullptr, d_crc, d_status, n,
+                                         stream, 1, max_len);
 }
 
-int zscrc_device_write_commits(void *d_image, const uint64_t *d_span_off, const uint64_t *d_span_len, size_t n,
-                               uint32_t *d_crc, void *stream)
+int zscrc_device_write_commits(void *d_image, uint64_t image_size, const uint64_t *d_span_off,
+                               const uint64_t *d_span_len, size_t n, uint32_t *d_crc, uint32_t *d_status,
+                               void *stream)
 {
-    return zscrc_internal_verify_commits(d_image, d_span_off, d_span_len, nullptr, d_crc, nullptr, n, stream, 1,
-                                         ZSCRC_LEN_UNBOUNDED);
+    return zscrc_internal_verify_commits(d_image, image_size, d_span_off, d_span_len, nullptr, d_crc, d_status, n,
+                                         stream, 1, ZSCRC_LEN_UNBOUNDED);
 }
 
 int zscrc_zs_verify_image(const void *image, uint64_t size, int kind, zscrc_zs_report *rep)
@@ -310,7 +332,8 @@ int zscrc_zs_verify_image(const void *image, uint64_t size, int kind, zscrc_zs_r
             uint64_t max_len = 0;
             for (size_t i = 0; i < n; ++i)
                 max_len = len[i] > max_len ? len[i] : max_len;
-            rc = zscrc_device_verify_commits_bounded(dimg, doff, dlen, nullptr, n, max_len, dcrc, dst, nullptr);
+            rc = zscrc_device_verify_commits_bounded(dimg, size, doff, dlen, nullptr, n, max_len, dcrc, dst,
+                                                     nullptr);
             uint32_t *st = static_cast<uint32_t *>(malloc(n * 4));
             if (!rc && st && hipMemcpy(st, dst, n * 4, hipMemcpyDeviceToHost) == hipSuccess) {
                 for (size_t i = 0; i < n; ++i) {

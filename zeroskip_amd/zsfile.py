@@ -89,6 +89,7 @@ def verify_commits(d_image: torch.Tensor, span_off: torch.Tensor, span_len: torc
     max_len (optional): a known bound on the span lengths, e.g. from the host
     walk (zscrc_device_verify_commits_bounded); results never depend on it."""
     n = span_off.numel()
+    size = d_image.numel() * d_image.element_size()
     crc = torch.empty(n, dtype=torch.int32, device=d_image.device)
     st = torch.empty(n, dtype=torch.int32, device=d_image.device)
     with torch.cuda.device(d_image.device):
@@ -96,31 +97,36 @@ def verify_commits(d_image: torch.Tensor, span_off: torch.Tensor, span_len: torc
         if max_len is not None:
             assert seed is None or (seed.numel() == n and seed.dtype == torch.int32)
             check(lib().zscrc_device_verify_commits_bounded(
-                d_image.data_ptr(), span_off.data_ptr(), span_len.data_ptr(),
+                d_image.data_ptr(), size, span_off.data_ptr(), span_len.data_ptr(),
                 None if seed is None else seed.data_ptr(), n, max_len, crc.data_ptr(), st.data_ptr(),
                 stream), "zscrc_device_verify_commits_bounded")
         elif seed is None:
             check(lib().zscrc_device_verify_commits(
-                d_image.data_ptr(), span_off.data_ptr(), span_len.data_ptr(), n, crc.data_ptr(),
+                d_image.data_ptr(), size, span_off.data_ptr(), span_len.data_ptr(), n, crc.data_ptr(),
                 st.data_ptr(), stream), "zscrc_device_verify_commits")
         else:
             assert seed.numel() == n and seed.dtype == torch.int32 and seed.device == d_image.device
             check(lib().zscrc_device_verify_commits_seeded(
-                d_image.data_ptr(), span_off.data_ptr(), span_len.data_ptr(), seed.data_ptr(), n,
+                d_image.data_ptr(), size, span_off.data_ptr(), span_len.data_ptr(), seed.data_ptr(), n,
                 crc.data_ptr(), st.data_ptr(), stream), "zscrc_device_verify_commits_seeded")
     return crc, st
 
 
 def write_commits(d_image: torch.Tensor, span_off: torch.Tensor, span_len: torch.Tensor,
-                  max_len: int | None = None) -> torch.Tensor:
+                  max_len: int | None = None, status: bool = False):
     """Writer side on the GPU: compute every commit CRC and store it
     big-endian into its commit record in `d_image` (in place).  max_len: a
-    known bound on the span lengths (zscrc_device_write_commits_bounded)."""
+    known bound on the span lengths (zscrc_device_write_commits_bounded).
+    Returns the CRCs, or (crc, status) with status=True: 1 written, 2 no
+    commit record there (nothing written)."""
     n = span_off.numel()
+    size = d_image.numel() * d_image.element_size()
     crc = torch.empty(n, dtype=torch.int32, device=d_image.device)
+    st = torch.empty(n, dtype=torch.int32, device=d_image.device) if status else None
     with torch.cuda.device(d_image.device):
         check(lib().zscrc_device_write_commits_bounded(
-            d_image.data_ptr(), span_off.data_ptr(), span_len.data_ptr(), n,
+            d_image.data_ptr(), size, span_off.data_ptr(), span_len.data_ptr(), n,
             LEN_UNBOUNDED if max_len is None else max_len, crc.data_ptr(),
+            None if st is None else st.data_ptr(),
             torch.cuda.current_stream(d_image.device).cuda_stream), "zscrc_device_write_commits_bounded")
-    return crc
+    return (crc, st) if status else crc
