@@ -265,6 +265,39 @@ typedef struct zscrc_consistent_report {
 } zscrc_consistent_report;
 int zscrc_zs_consistent(const char *dbdir, zscrc_consistent_report *rep);
 
+/* Packed-file writer: the repack output path with its CRCs on the GPU.
+ * Same byte layout and CRC lifecycle as zs_packed_file_new_from_memtree
+ * (src/zeroskip-packed.c:384-473; from_packed_files :617-742):
+ *   header (CRC over host-order fields, zeroskip-header.c:30-94)
+ *   crc32_begin; records in caller order, pointer i = file offset of record i
+ *   records-region commit (short, or long above 16 MiB: zeroskip-file.c:253-350)
+ *   crc32_begin; count + pointers (big-endian); final commit.
+ * Records are serialised straight into pinned staging chunks; each full chunk
+ * is copied to the GPU and checksummed there while the host writes it to the
+ * file and serialises the next one -- the reference's one huge crc32_end over
+ * the records region (packed.c:442, mfile.c:534-546) never runs on the CPU.
+ * Keys must arrive in key order (the caller's merge, as memtree_walk_forward
+ * hands them over).  chunk_bytes 0 = 64 MiB. */
+typedef struct zscrc_packer zscrc_packer;
+#define ZSCRC_PACK_FSYNC 1u /* fsync the file on close (mfile_flush's msync) */
+int zscrc_pack_open(zscrc_packer **pk, const char *path, const uint8_t uuid[16], uint32_t startidx,
+                    uint32_t endidx, uint64_t chunk_bytes, unsigned flags);
+/* key/value record (zs_file_write_keyval_record, zeroskip-file.c:188-247), or
+ * a delete record when val is NULL (zs_file_write_delete_record, :352+) */
+int zscrc_pack_add(zscrc_packer *pk, const void *key, uint64_t keylen, const void *val, uint64_t vallen);
+typedef struct zscrc_pack_report {
+    uint64_t records;       /* pointers written                          */
+    uint64_t region_bytes;  /* records region (span of the first commit) */
+    uint64_t file_bytes;    /* size of the packed file                   */
+    uint32_t region_crc;    /* crc32c(0, records region)                 */
+    uint32_t pointers_crc;  /* crc32c(0, count + pointers)               */
+    uint32_t commit_crc;    /* stored CRC of the records-region commit   */
+    uint32_t final_crc;     /* stored CRC of the final commit            */
+} zscrc_pack_report;
+/* Writes the commits and the pointer section, closes the file and frees the
+ * writer (also on error, after which the file is removed). */
+int zscrc_pack_close(zscrc_packer *pk, zscrc_pack_report *rep);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,79 @@
+"""Link evidence for the drop-in boundary: the reference's
+own sources resolve their crc32c* calls in libzscrc.so.  CPU only; skipped
+where /root/reference is absent (the GPU box).
+
+* src/mfile.c (with util.c, log.c, cstring.c) needs no generated or missing
+  header: it is compiled UNMODIFIED (oracle/Makefile `ref`), linked against
+  libzscrc.so, and run -- crc32_begin / mfile_write / crc32_end
+  (src/mfile.c:526-546) over the drop-in crc32c_hw, checked by the oracle.
+* src/zeroskip-{file,record,header,packed,dotzsdb}.c include
+  zeroskip-priv.h -> <uuid/uuid.h>, which this image lacks (no libuuid
+  headers); a stand-in header would be a reference build with a stand-in, so
+  they are not compiled.  For them: every crc32c* identifier they call is an
+  exported symbol of libzscrc.so, and the reference's crc32c.h and
+  include/zscrc.h compile in one translation unit (a prototype that differs
+  in any parameter or return type is a hard "conflicting types" error).
+"""
+import json
+import os
+import re
+import subprocess
+
+import pytest
+
+from zeroskip_amd import LIB_PATH
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = "/root/reference"
+pytestmark = pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "src")), reason="no /root/reference here")
+CALLERS = ["mfile.c", "zeroskip-file.c", "zeroskip-record.c", "zeroskip-header.c", "zeroskip-packed.c",
+           "zeroskip-dotzsdb.c"]
+
+
+def _exports() -> set[str]:
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB_PATH], capture_output=True, text=True, check=True)
+    return {ln.split()[-1] for ln in out.stdout.splitlines() if ln.strip()}
+
+
+def test_mfile_links_unmodified_and_runs(tmp_path):
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "ref"])
+    obj = os.path.join(ROOT, "oracle", "_ref", "mfile.o")
+    und = subprocess.run(["nm", "-u", obj], capture_output=True, text=True, check=True).stdout.split()
+    needed = {s for s in und if s.startswith("crc32c")}
+    assert needed == {"crc32c", "crc32c_hw"}          # mfile.c:528, :538
+    assert needed <= _exports()
+    from oracle import oracle
+    f = tmp_path / "span"
+    out = subprocess.run([os.path.join(ROOT, "oracle", "_ref", "mfile_demo"), str(f), "100003", "37"],
+                         capture_output=True, text=True, timeout=120, env={**os.environ, "ZSCRC_GPU_MIN": "0"})
+    assert out.returncode == 0, out.stderr
+    rep = json.loads(out.stdout)
+    data = open(f, "rb").read()
+    assert rep["span"] == len(data) - 40 and rep["gpu_calls"] == 0
+    assert rep["crc"] == oracle.crc32c_hw(0, data[40:])
+
+
+def test_every_reference_caller_resolves():
+    exports = _exports()
+    called = set()
+    for name in CALLERS:
+        src = open(os.path.join(REF, "src", name)).read()
+        called |= set(re.findall(r"\b(crc32c\w*)\s*\(", src))
+    assert "crc32c_hw" in called
+    assert called <= exports, called - exports
+    # the reference's whole exported checksum API (src/libzeroskip.symbols:113-120)
+    syms = open(os.path.join(REF, "src", "libzeroskip.symbols")).read().split()
+    assert {s for s in syms if s.startswith("crc32c")} <= exports
+
+
+def test_reference_header_agrees_with_zscrc_h(tmp_path):
+    tu = tmp_path / "both.c"
+    tu.write_text("#include <libzeroskip/crc32c.h>\n#include \"zscrc.h\"\n"
+                  "uint32_t (*const fns[])(uint32_t, const void *, size_t) = {crc32c, crc32c_hw, crc32c_sw};\n"
+                  "uint32_t (*const fmap)(const char *, unsigned) = crc32c_map;\n"
+                  "uint32_t (*const fcs)(const cstring *) = crc32c_cstring;\n"
+                  "uint32_t (*const fbuf)(const char *) = crc32c_buf;\n"
+                  "uint32_t (*const fiov)(struct iovec *, int) = crc32c_iovec;\n"
+                  "void (*const finit)(void) = crc32c_init;\n")
+    subprocess.check_call(["gcc", "-fsyntax-only", "-Wall", "-Werror", "-I", os.path.join(REF, "include"),
+                           "-I", os.path.join(ROOT, "include"), str(tu)])

@@ -8,7 +8,13 @@ Times, over the same host bytes (anonymous memory and a file-backed mmap):
   nocopy   zscrc_stream NOCOPY (DMA straight from the caller's memory)
   scalar   crc32c_hw with ZSCRC_GPU_MIN set (the unchanged reference symbol)
 All results are checked equal.  Prints one JSON line per source.
-usage: python tools/repack_bench.py [--mib 4096] [--file /tmp/x]
+
+--pack N additionally writes a packed file of N records (16-byte keys, values
+of --value-bytes) through the packed-file writer (zscrc_pack_*, records and
+pointer CRCs on the GPU while the host writes the file), and times the CPU
+crc32_end the reference would run over the same records region afterwards
+(src/zeroskip-packed.c:442, one core).
+usage: python tools/repack_bench.py [--mib 4096] [--file /tmp/x] [--pack N --out /tmp/p]
 """
 from __future__ import annotations
 
@@ -60,12 +66,44 @@ def run(buf: np.ndarray, what: str, chunk: int) -> dict:
             "stream_nocopy_GBs": g(t_n), "scalar_offload_GBs": g(t_x), "crc": f"{c0:08x}"}
 
 
+def pack(nrec: int, vbytes: int, out: str, chunk: int) -> dict:
+    from zeroskip_amd import repack
+    rng = np.random.default_rng(7)
+    vals = rng.integers(0, 256, (64, vbytes), dtype=np.uint8)     # 64 distinct values, reused
+    keys = [b"%016d" % i for i in range(nrec)]
+    t0 = time.perf_counter()
+    with repack.Packer(out, bytes(range(16)), 1, 2, chunk_bytes=chunk) as p:
+        for i, k in enumerate(keys):
+            p.add(k, vals[i & 63])
+    t_pack = time.perf_counter() - t0
+    rep = p.report
+    mm = np.memmap(out, dtype=np.uint8, mode="r")
+    region = mm[40:40 + rep["region_bytes"]]
+    lib().zscrc_set_gpu_min(0)
+    t_crc, c = timed(lambda: zc.crc32c_hw(0, region), 2)
+    assert c == rep["region_crc"], (hex(c), hex(rep["region_crc"]))
+    del region, mm
+    os.unlink(out)
+    return {"source": "packed-file writer", "records": nrec, "value_bytes": vbytes,
+            "file_bytes": rep["file_bytes"], "pack_s": round(t_pack, 3),
+            "pack_GBs": round(rep["file_bytes"] / t_pack / 1e9, 2),
+            "cpu_region_crc_s": round(t_crc, 3), "cpu_region_crc_GBs": round(rep["region_bytes"] / t_crc / 1e9, 2),
+            "note": "pack_s includes serialising every record in Python->C calls, the GPU CRCs and the "
+                    "file writes; cpu_region_crc_s is the reference's extra one-core crc32_end over the "
+                    "written region (what the GPU pipeline removes)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mib", type=int, default=4096)
     ap.add_argument("--chunk-mib", type=int, default=64)
     ap.add_argument("--file", default=None)
+    ap.add_argument("--pack", type=int, default=0, help="records for the packed-file writer leg")
+    ap.add_argument("--value-bytes", type=int, default=16384)
+    ap.add_argument("--out", default="/tmp/zscrc_pack_bench")
     a = ap.parse_args()
+    if a.pack:
+        print(json.dumps(pack(a.pack, a.value_bytes, a.out, a.chunk_mib << 20)), flush=True)
     n = a.mib << 20
     buf = np.random.default_rng(3).integers(0, 256, n, dtype=np.uint8)
     print(json.dumps(run(buf, "anonymous", a.chunk_mib << 20)), flush=True)

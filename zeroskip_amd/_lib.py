@@ -55,6 +55,9 @@ SIGNATURES = {
     "zscrc_stream_update": (_int, [_vp, _vp, _sz]),
     "zscrc_stream_final": (_int, [_vp, _vp]),
     "zscrc_zs_consistent": (_int, [ctypes.c_char_p, _vp]),
+    "zscrc_pack_open": (_int, [_vp, ctypes.c_char_p, ctypes.c_char_p, _u32, _u32, _u64, ctypes.c_uint]),
+    "zscrc_pack_add": (_int, [_vp, _vp, _u64, _vp, _u64]),
+    "zscrc_pack_close": (_int, [_vp, _vp]),
 }
 
 ZSCRC_RAW = 1

@@ -1067,6 +1067,51 @@ int zscrc_stream_update(zscrc_stream *s, const void *buf, size_t len)
     return ZSCRC_OK;
 }
 
+/* Producer side without the update() copy (zscrc_pack.cpp): the caller
+ * serialises bytes straight into the stream's pinned staging.  stage()
+ * returns the free part of the current slot (waiting until the slot's
+ * previous copy has left); advance(n) marks n of them written and, when the
+ * slot is full (or on flush), submits it and hands it back in *done so the
+ * caller can also write it elsewhere (a file) before staging NSLOT more
+ * chunks.  Copy-mode streams only. */
+uint8_t *zscrc_internal_stream_stage(zscrc_stream *s, uint64_t *room)
+{
+    if (!s || s->err || (s->flags & ZSCRC_STREAM_NOCOPY))
+        return nullptr;
+    const int k = s->slot;
+    if (s->fill == 0 && s->used[k]) {
+        hipError_t e = hipEventSynchronize(s->copied[k]);
+        if (e != hipSuccess) {
+            stream_fail(s, "hipEventSynchronize", e);
+            return nullptr;
+        }
+    }
+    *room = s->chunk - s->fill;
+    return s->hpin[k] + s->fill;
+}
+
+int zscrc_internal_stream_advance(zscrc_stream *s, uint64_t n, int flush, const uint8_t **done, uint64_t *done_n)
+{
+    *done = nullptr;
+    *done_n = 0;
+    if (s->err)
+        return s->err;
+    if (n > s->chunk - s->fill)
+        return ZSCRC_EINVAL;
+    s->fill += n;
+    if (s->fill == s->chunk || (flush && s->fill)) {
+        const int k = s->slot;
+        const uint64_t m = s->fill;
+        s->fill = 0;
+        int rc = stream_submit(s, s->hpin[k], m);
+        if (rc)
+            return rc;
+        *done = s->hpin[k];
+        *done_n = m;
+    }
+    return ZSCRC_OK;
+}
+
 int zscrc_stream_final(zscrc_stream *s, uint32_t *crc)
 {
     if (!s)
