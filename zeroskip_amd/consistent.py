@@ -30,7 +30,8 @@ their midpoint; a packed records region crossing a cut is split there.  Every
 rank stages its ranges into one device buffer, walks its files on the host
 (threads; the ctypes calls release the GIL), verifies all its commits in ONE
 device launch and computes RAW registers of its split pieces in another.  The
-per-rank summaries are all-gathered (kilobytes); split regions are folded with
+per-rank digests are all-gathered as one fixed-shape int64 tensor per rank
+(tens of kilobytes; no pickling in the timed pass); split regions are folded with
 the zero-shift operator (``shard.fold``) and their commit trailers applied on
 the host.  Input bytes never cross xGMI.
 """
@@ -311,6 +312,8 @@ class Consistent:
         self.plan = make_plan(db, world)
         self.mine = [u for u in self.plan.units if u.rank == rank]
         self._names = None   # file names by id, for the bad / stale lists
+        self._pmax = 0
+        self._host_all = None
 
     # ---------------------------------------------------------------- prepare
     def prepare(self):
@@ -396,6 +399,19 @@ class Consistent:
         t1 = time.perf_counter()
         self.prepare_times = dict(stage_s=t_read - t0, walk_and_copy_s=t1 - t_read, total_s=t1 - t0,
                                   staged_bytes=pos)
+        # split pieces per rank are fixed by the plan: the exchange row's size
+        self._pmax = max([sum(1 for u in self.plan.units if u.rank == r and u.what == "piece")
+                          for r in range(self.world)] + [0])
+        # host-side findings do not change between runs: exchanged once, here
+        host = dict(files=self.local.files, bytes=self.local.bytes_checked,
+                    header_errors=self.local.header_errors, walk_errors=self.local.walk_errors,
+                    issues=self.local.issues)
+        if self.world == 1:
+            self._host_all = [host]
+        else:
+            import torch.distributed as dist
+            self._host_all = [None] * self.world
+            dist.all_gather_object(self._host_all, host, group=self.group)
         return self
 
     def _check_header(self, f: DbFile):
@@ -486,33 +502,72 @@ class Consistent:
                 stale_i = np.sort(np.concatenate([stale_i, ql[(st2 == 1).cpu().numpy()]]))
         bad_i = np.setdiff1d(bad_idx, stale_i, assume_unique=True)
 
-        if self._names is None:
-            self._names = np.array([f.name for f in self.db.files], dtype=object)
-
-        def listed(ix):
-            ix = ix[:self.MAX_LISTED]
-            return list(zip(self._names[self.c_file[ix]].tolist(), self.c_rec[ix].tolist()))
-
-        bad, stale = listed(bad_i), listed(stale_i)
-        summary = dict(rank=self.rank, commits=n, bad=bad, n_bad=len(bad_i),
-                       stale=stale, n_stale=len(stale_i),
-                       pieces=[(q[0], q[1], q[3] - q[2], r) for q, r in zip(self.pieces, raw_h)],
-                       files=loc.files, bytes=loc.bytes_checked, header_errors=loc.header_errors,
-                       walk_errors=loc.walk_errors, issues=loc.issues)
-        allsum = self._gather(summary)
+        L = self.MAX_LISTED
+        digest = dict(commits=n, n_bad=len(bad_i), n_stale=len(stale_i),
+                      bad=np.stack([self.c_file[bad_i[:L]], self.c_rec[bad_i[:L]]], 1),
+                      stale=np.stack([self.c_file[stale_i[:L]], self.c_rec[stale_i[:L]]], 1),
+                      pieces=np.array([(q[0], q[1], q[3] - q[2], r) for q, r in zip(self.pieces, raw_h)],
+                                      np.int64).reshape(-1, 4))
+        allsum = self._gather(digest)
         t_x = time.perf_counter()
         rep = self._merge(allsum)
         t1 = time.perf_counter()
         rep.timing = dict(device_s=t_dev - t0, exchange_s=t_x - t_dev, fold_s=t1 - t_x, total_s=t1 - t0)
         return rep
 
-    def _gather(self, summary):
+    # ------------------------------------------------------------- exchange
+    HEAD = 6   # commits, n_bad, n_stale, listed bad, listed stale, pieces
+
+    def _pack(self, d) -> np.ndarray:
+        """One rank's digest as a fixed-shape int64 row: the head, then
+        MAX_LISTED (file, offset) pairs of bad and of stale commits, then the
+        rank's split pieces (file, piece, length, raw register), padded to the
+        plan's largest per-rank piece count (the same on every rank)."""
+        L = self.MAX_LISTED
+        row = np.zeros(self.HEAD + 4 * L + 4 * self._pmax, np.int64)
+        row[:self.HEAD] = (d["commits"], d["n_bad"], d["n_stale"], len(d["bad"]), len(d["stale"]),
+                           len(d["pieces"]))
+        o = self.HEAD
+        row[o:o + 2 * len(d["bad"])] = d["bad"].reshape(-1)
+        o += 2 * L
+        row[o:o + 2 * len(d["stale"])] = d["stale"].reshape(-1)
+        o += 2 * L
+        row[o:o + 4 * len(d["pieces"])] = d["pieces"].reshape(-1)
+        return row
+
+    def _unpack(self, r: int, row: np.ndarray) -> dict:
+        L = self.MAX_LISTED
+        commits, n_bad, n_stale, nb, ns, npc = (int(v) for v in row[:self.HEAD])
+        o = self.HEAD
+        names = self._names
+        bad = [(names[f], int(x)) for f, x in row[o:o + 2 * nb].reshape(-1, 2)]
+        o += 2 * L
+        stale = [(names[f], int(x)) for f, x in row[o:o + 2 * ns].reshape(-1, 2)]
+        o += 2 * L
+        pieces = [tuple(int(v) for v in p) for p in row[o:o + 4 * npc].reshape(-1, 4)]
+        h = self._host_all[r]
+        return dict(rank=r, commits=commits, n_bad=n_bad, n_stale=n_stale, bad=bad, stale=stale, pieces=pieces,
+                    files=h["files"], bytes=h["bytes"], header_errors=h["header_errors"],
+                    walk_errors=h["walk_errors"], issues=h["issues"])
+
+    def _gather(self, digest):
+        """Per-rank digests to every rank: one fixed-shape all-gather of int64
+        rows (RCCL under nccl: a device tensor; gloo: host), no pickling.  The
+        host-side findings (headers, walks) were exchanged once in prepare()."""
+        if self._names is None:
+            self._names = np.array([f.name for f in self.db.files], dtype=object)
+        row = self._pack(digest)
         if self.world == 1:
-            return [summary]
+            return [self._unpack(0, row)]
         import torch.distributed as dist
-        out = [None] * self.world
-        dist.all_gather_object(out, summary, group=self.group)
-        return out
+        dev = torch.device("cpu")
+        if dist.get_backend(self.group) == "nccl":
+            dev = torch.device("cuda", torch.cuda.current_device())
+        mine = torch.from_numpy(row).to(dev)
+        out = torch.empty(self.world * row.size, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(out, mine, group=self.group)
+        rows = out.cpu().numpy().reshape(self.world, -1)
+        return [self._unpack(r, rows[r]) for r in range(self.world)]
 
     def _merge(self, allsum) -> Report:
         rep = Report()
