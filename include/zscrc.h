@@ -100,6 +100,17 @@ int zscrc_device_batch_bounded(const void *d_base, const uint64_t *d_off, const 
 int zscrc_device_fixed(const void *d_base, uint64_t stride, uint64_t len, uint32_t seed,
                        uint32_t *d_out, size_t n, unsigned flags, void *stream);
 
+/* K device-resident fixed-stride batches in one call: batch b is
+ * d_bases[b][i*stride .. +len) for i < n, results to d_outs[b][i] (as
+ * zscrc_device_fixed).  d_bases / d_outs are HOST arrays of k <= ZSCRC_MULTI_MAX
+ * device pointers.  Records of <= 64 bytes (BASELINE config 2) run as ONE
+ * persistent launch over all k batches: the launch, the operator-table fill
+ * and the HBM ramp are paid once instead of k times; longer records run one
+ * launch per batch. */
+#define ZSCRC_MULTI_MAX 64
+int zscrc_device_fixed_multi(const void *const *d_bases, uint32_t *const *d_outs, size_t k, uint64_t stride,
+                             uint64_t len, uint32_t seed, size_t n, unsigned flags, void *stream);
+
 /* One long device-resident span, split over every CU and folded on the GPU.
  * d_out (device, 1 word) receives crc32c(seed, span).  `scratch` may be NULL
  * (library-owned) or a device buffer of zscrc_span_scratch_bytes(len). */
@@ -264,6 +275,34 @@ typedef struct zscrc_consistent_report {
     char first_bad[512];          /* "file:offset: what" of the first problem    */
 } zscrc_consistent_report;
 int zscrc_zs_consistent(const char *dbdir, zscrc_consistent_report *rep);
+
+/* End to end from host memory: every CRC of n zeroskip file images (mmap'd
+ * files; kinds[i] = ZSCRC_ZS_ACTIVE / _FINALISED / _PACKED) -- header, record
+ * walk and every commit of active / finalised files, records-region and
+ * pointer-section commits of packed files.  `threads` host threads (0 = up to
+ * 16) walk the files and copy them into pinned staging; the copies to the
+ * current GPU, and the verification of every group of files whose bytes have
+ * arrived, overlap with that work.  Synchronous. */
+#define ZSCRC_FILES_BAD_HEADER 1
+#define ZSCRC_FILES_BAD_WALK 2
+#define ZSCRC_FILES_BAD_COMMIT 3
+typedef struct zscrc_files_report {
+    uint64_t files, commits, bytes;
+    uint64_t bad_commits;         /* stored CRC != recomputed                    */
+    uint64_t stale_empty_commits; /* zero-length commits hashed from the previous
+                                   * span's CRC (src/mfile.c:534-546 quirk)      */
+    uint64_t header_errors;       /* bad signature or header CRC                 */
+    uint64_t walk_errors;         /* walk stopped early / packed layout          */
+    uint64_t first_bad_file;      /* file index of the first problem, ~0 = none  */
+    uint64_t first_bad_off;       /* its offset: commit record / walk stop / 0   */
+    int32_t first_bad_what;       /* ZSCRC_FILES_BAD_*, 0 = none                 */
+    int32_t threads;              /* host threads used                           */
+    double copy_s;                /* start of the pipeline -> last byte on the GPU */
+    double verify_tail_s;         /* last byte on the GPU -> every verdict back  */
+    double total_s;               /* the whole call                              */
+} zscrc_files_report;
+int zscrc_zs_verify_files(const void *const *images, const uint64_t *sizes, const int *kinds, size_t n,
+                          int threads, zscrc_files_report *rep);
 
 /* Packed-file writer: the repack output path with its CRCs on the GPU.
  * Same byte layout and CRC lifecycle as zs_packed_file_new_from_memtree

@@ -1,0 +1,105 @@
+"""End to end from host memory (zscrc_zs_verify_files): threaded walks,
+pinned staging, overlapped H2D and per-group GPU verification, against the
+format oracle's verdicts -- clean DBs, corrupt commits / headers / walks,
+stale finalise commits, packed files with long commits, pieces smaller than
+a file and files smaller than a piece."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import zs_format as zf
+from tests.test_format_oracle import UUID, build_active
+from zeroskip_amd import zsfile
+
+pytestmark = pytest.mark.gpu
+
+
+def _db(seed, nfiles=40):
+    rng = np.random.default_rng(seed)
+    imgs, kinds = [], []
+    for i in range(nfiles):
+        w = zf.FileWriter(UUID, idx=i)
+        for t in range(int(rng.integers(1, 60))):
+            for _ in range(int(rng.integers(0, 4))):
+                w.add(b"%016d" % int(rng.integers(0, 10**9)),
+                      rng.integers(0, 256, int(rng.integers(0, 5000)), dtype=np.uint8).tobytes())
+            w.commit()
+        if i % 5 == 2:
+            w.finalise()          # a stale zero-length commit after a committed txn
+        imgs.append(np.frombuffer(w.image(), np.uint8).copy())
+        kinds.append(zsfile.FINALISED)
+    recs = sorted((b"%016d" % i, bytes(rng.integers(0, 256, int(rng.integers(0, 9000)), dtype=np.uint8)))
+                  for i in range(3000))
+    imgs.insert(7, np.frombuffer(zf.packed_file(recs, UUID, 0, 5), np.uint8).copy())   # > 16 MiB: long commit
+    kinds.insert(7, zsfile.PACKED)
+    return imgs, kinds
+
+
+def _expected(imgs, kinds):
+    commits = bad = stale = 0
+    for im, k in zip(imgs, kinds):
+        b = im.tobytes()
+        if k == zsfile.PACKED:
+            cs = zf.packed_check(b)
+            commits += 2
+            bad += sum(not c["ok"] for c in cs)
+            continue
+        cs, _, _ = zf.walk(b)
+        commits += len(cs)
+        prev = None
+        for c in cs:
+            if not c["ok"]:
+                if c["span_len"] == 0 and prev is not None and \
+                        zf._commit_check(b, c["commit_off"], prev)[4] == c["stored"]:
+                    stale += 1
+                else:
+                    bad += 1
+            prev = zf.oracle.crc32c_hw(0, b[c["span_off"]:c["span_off"] + c["span_len"]])
+    return commits, bad, stale
+
+
+@pytest.mark.parametrize("slot", [None, 1 << 20, 4 << 20])
+def test_clean_db_end_to_end(gpu, slot):
+    imgs, kinds = _db(1)
+    if slot:
+        os.environ["ZSCRC_FILES_SLOT"] = str(slot)
+    try:
+        rep = zsfile.verify_files(imgs, kinds, threads=6)
+    finally:
+        os.environ.pop("ZSCRC_FILES_SLOT", None)
+    commits, bad, stale = _expected(imgs, kinds)
+    assert bad == 0 and stale >= 3
+    assert rep["commits"] == commits and rep["bad_commits"] == 0 and rep["stale_empty_commits"] == stale
+    assert rep["header_errors"] == rep["walk_errors"] == 0 and rep["first_bad_what"] == 0
+    assert rep["bytes"] == sum(im.nbytes for im in imgs) and rep["files"] == len(imgs)
+
+
+def test_corruptions_located(gpu):
+    imgs, kinds = _db(2, nfiles=25)
+    # a payload byte of commit 3 of file 11, a header byte of file 4, a packed records byte
+    c = zf.walk(imgs[11].tobytes())[0][3]
+    imgs[11][c["span_off"] + 9] ^= 0x20
+    imgs[4][14] ^= 1
+    imgs[7][40 + 12345] ^= 0x80
+    os.environ["ZSCRC_FILES_SLOT"] = str(1 << 20)
+    try:
+        rep = zsfile.verify_files(imgs, kinds)
+    finally:
+        os.environ.pop("ZSCRC_FILES_SLOT", None)
+    commits, bad, stale = _expected(imgs, kinds)
+    assert bad == 2 and rep["bad_commits"] == 2 and rep["commits"] == commits
+    assert rep["header_errors"] == 1 and rep["first_bad_file"] == 4 and rep["first_bad_what"] == 1
+    # a truncated file: the walk stops
+    imgs2 = [imgs[0], imgs[1][:-3]]
+    rep2 = zsfile.verify_files(imgs2, kinds[:2])
+    assert rep2["walk_errors"] == 1 and rep2["first_bad_file"] == 1 and rep2["first_bad_what"] == 2
+
+
+def test_empty_and_tiny(gpu):
+    rep = zsfile.verify_files([])
+    assert rep["files"] == 0 and rep["commits"] == 0
+    img = np.frombuffer(build_active(3), np.uint8)
+    rep = zsfile.verify_files([np.zeros(0, np.uint8), img])
+    assert rep["header_errors"] == 1 and rep["walk_errors"] == 1 and rep["commits"] == 3
+    assert rep["first_bad_file"] == 0

@@ -411,3 +411,32 @@ def test_two_streams_share_scratch(gpu):
     for k, b, sp in outs:
         assert np.array_equal(b.cpu().numpy().view(np.uint32), cases[k][3])
         assert (sp.cpu().numpy().view(np.uint32)[0]) == cases[k][4]
+
+
+@pytest.mark.parametrize("stride,length,n,k", [
+    (64, 64, 1 << 20, 8),        # BASELINE config 2 records, 8 batches in one launch
+    (64, 64, 1000, 64),          # ZSCRC_MULTI_MAX batches, fewer records than threads
+    (48, 40, 30001, 5),          # front padding inside the piece, ragged count
+    (13, 11, 20000, 3),          # unaligned starts, tail bytes
+    (7, 5, 5000, 4),             # < 8 bytes: byte path
+    (4096, 1000, 300, 3),        # > 64 bytes: one launch per batch
+])
+def test_fixed_multi(gpu, stride, length, n, k):
+    """zscrc_device_fixed_multi (one persistent launch over k batches) equals
+    the oracle on every record of every batch, plain and raw."""
+    bufs, hosts = [], []
+    for b in range(k):
+        h = rand_bytes(stride * (n - 1) + length + b, 1000 * b + length)[b:]
+        hosts.append(h)
+        bufs.append(to_dev(h, gpu))
+    before = stats()
+    outs = zd.crc_fixed_multi(bufs, stride, length, n, seed=0x31337)
+    if length <= 64:
+        assert stats()[2] - before[2] == 1          # one launch for all k batches
+    for b in range(k):
+        assert np.array_equal(u32(outs[b]), _oracle_seeded(hosts[b], stride, length, n, 0x31337)), b
+    raws = zd.crc_fixed_multi(bufs[:2], stride, length, n, seed=7, raw=True)
+    for b in range(min(k, 2)):
+        ref = oracle.batch(hosts[b], n=n, stride=stride, fixed_len=length, impl="hw",
+                           seeds=np.full(n, ~7 & M32, np.uint32)) ^ np.uint32(M32)
+        assert np.array_equal(u32(raws[b]), ref)

@@ -28,6 +28,7 @@ SIGNATURES = {
     "zscrc_shift": (_u32, [_u32, _u64]),
     "zscrc_device_batch": (_int, [_vp, _vp, _vp, _vp, _vp, _sz, ctypes.c_uint, _vp]),
     "zscrc_device_fixed": (_int, [_vp, _u64, _u64, _u32, _vp, _sz, ctypes.c_uint, _vp]),
+    "zscrc_device_fixed_multi": (_int, [_vp, _vp, _sz, _u64, _u64, _u32, _sz, ctypes.c_uint, _vp]),
     "zscrc_span_scratch_bytes": (_sz, [_u64]),
     "zscrc_device_span": (_int, [_vp, _u64, _u32, _vp, _vp, ctypes.c_uint, _vp]),
     "zscrc_host_batch": (_int, [_vp, _vp, _vp, _vp, _vp, _sz]),
@@ -55,6 +56,7 @@ SIGNATURES = {
     "zscrc_stream_update": (_int, [_vp, _vp, _sz]),
     "zscrc_stream_final": (_int, [_vp, _vp]),
     "zscrc_zs_consistent": (_int, [ctypes.c_char_p, _vp]),
+    "zscrc_zs_verify_files": (_int, [_vp, _vp, _vp, _sz, _int, _vp]),
     "zscrc_pack_open": (_int, [_vp, ctypes.c_char_p, ctypes.c_char_p, _u32, _u32, _u64, ctypes.c_uint]),
     "zscrc_pack_add": (_int, [_vp, _vp, _u64, _vp, _u64]),
     "zscrc_pack_close": (_int, [_vp, _vp]),

@@ -37,6 +37,8 @@ int zs_launch_part_fold(const zs::BatchDesc *d, const uint32_t *gtab, hipStream_
 int zs_launch_plan(const zs::PlanArgs *a, hipStream_t stream);
 int zs_launch_burst(int fixed, int xp, int nb, const zs::BatchDesc *d, const uint32_t *gtab, int grid,
                     hipStream_t stream);
+int zs_launch_multi(const zs::BatchDesc *d, const zs::MultiBatch *m, const uint32_t *gtab, int grid,
+                    hipStream_t stream);
 }
 
 namespace {
@@ -667,6 +669,48 @@ int zscrc_device_fixed(const void *d_base, uint64_t stride, uint64_t len, uint32
     d.xor_io = (flags & ZSCRC_RAW) ? 0u : 0xffffffffu;
     return launch(c, team_for(len, n, c->ncu, stride, reinterpret_cast<uintptr_t>(d_base)), d,
                   static_cast<hipStream_t>(stream));
+}
+
+int zscrc_device_fixed_multi(const void *const *d_bases, uint32_t *const *d_outs, size_t k, uint64_t stride,
+                             uint64_t len, uint32_t seed, size_t n, unsigned flags, void *stream)
+{
+    if (n == 0 || k == 0)
+        return ZSCRC_OK;
+    if (!d_bases || !d_outs || k > ZSCRC_MULTI_MAX)
+        return ZSCRC_EINVAL;
+    for (size_t b = 0; b < k; ++b)
+        if (!d_bases[b] || !d_outs[b])
+            return ZSCRC_EINVAL;
+    DevCtx *c;
+    int rc = get_ctx(&c);
+    if (rc)
+        return rc;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (len > 64) {
+        /* multi-piece records: one launch per batch (each already long) */
+        for (size_t b = 0; b < k && !rc; ++b)
+            rc = zscrc_device_fixed(d_bases[b], stride, len, seed, d_outs[b], n, flags, stream);
+        return rc;
+    }
+    zs::BatchDesc d = make_desc();
+    d.stride = stride;
+    d.fixed_len = len;
+    d.fixed_seed = seed;
+    d.n = n;
+    d.xor_io = (flags & ZSCRC_RAW) ? 0u : 0xffffffffu;
+    zs::MultiBatch m;
+    memset(&m, 0, sizeof m);
+    m.nb = (uint32_t)k;
+    for (size_t b = 0; b < k; ++b) {
+        m.base[b] = static_cast<const uint8_t *>(d_bases[b]);
+        m.out[b] = d_outs[b];
+    }
+    if (zs_launch_multi(&d, &m, c->gtab, c->ncu, s)) {
+        set_err("multi kernel launch", hipGetLastError());
+        return ZSCRC_EHIP;
+    }
+    g_stat[2]++;
+    return ZSCRC_OK;
 }
 
 size_t zscrc_span_scratch_bytes(uint64_t len)

@@ -114,6 +114,15 @@ struct PlanArgs {
     uint32_t *part_rec;    /* per part: its record */
 };
 
+/* K fixed-stride batches of one launch (zscrc_device_fixed_multi): batch b
+ * is base[b] / out[b]; stride, length, seed and count come from BatchDesc. */
+constexpr int MULTI_MAX = 64;
+struct MultiBatch {
+    uint32_t nb;
+    const uint8_t *base[MULTI_MAX];
+    uint32_t *out[MULTI_MAX];
+};
+
 struct SpanFold {
     const uint32_t *part; /* W raw segment registers */
     uint32_t *out;

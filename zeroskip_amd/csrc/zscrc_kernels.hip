@@ -995,6 +995,110 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
 }
 
 /*
+ * multi_kernel: K fixed-stride batches of one-piece records (<= 64 bytes:
+ * BASELINE config 2's 1M x 64 B) in ONE persistent launch
+ * (zscrc_device_fixed_multi).  The launch, the 128 KiB table fill and the
+ * HBM ramp are paid once for all K batches instead of once per batch.  Item
+ * g of the launch is record g mod n of batch g / n; each thread keeps its next
+ * item's 64-byte piece in flight while it hashes the current one, across
+ * record and batch boundaries (two register buffers); a result is stored
+ * after the following item's loads are issued, so no load wait includes it.
+ */
+struct MItem {
+    uintptr_t A, V0, lo;
+    uint64_t i;
+    uint32_t b;
+    bool ok;
+};
+
+__device__ __forceinline__ void multi_fetch(const BatchDesc &d, const MultiBatch &m, uint32_t b, uint64_t i,
+                                            uintptr_t dummy, MItem &it, uint32_t (&w)[16])
+{
+    it.b = b;
+    it.i = i;
+    it.ok = b < m.nb;
+    uintptr_t P0 = dummy;
+    if (it.ok) {
+        const uintptr_t base = reinterpret_cast<uintptr_t>(m.base[b]);
+        it.A = base + i * d.stride;
+        const uintptr_t E = (it.A + d.fixed_len) & ~uintptr_t(3);
+        it.V0 = E - 64;
+        it.lo = base & ~uintptr_t(3);
+        if (d.fixed_len >= 8 && it.V0 >= it.lo)
+            P0 = it.V0;
+    }
+    issue_plain(P0, w);
+}
+
+__device__ __forceinline__ uint32_t multi_hash(const BatchDesc &d, const MItem &it, uint32_t (&w)[16],
+                                               const char *L, uint32_t c_lo, uint32_t c_hi)
+{
+    Item x;
+    x.A = it.A;
+    x.len = d.fixed_len;
+    x.R0 = d.fixed_seed ^ d.xor_io;
+    uint32_t r;
+    if (d.fixed_len < 8) {
+        r = x.R0;
+        for (uint64_t k = 0; k < d.fixed_len; ++k)
+            r = byte_step(L, r, ((g8p)it.A)[k], c_hi);
+        return r;
+    }
+    r = first_piece(L, x, it.V0, it.lo, w, c_lo, c_hi);
+    const uintptr_t E = it.V0 + 64;
+    const uint32_t tail = (uint32_t)((it.A + d.fixed_len) - E);
+    for (uint32_t k = 0; k < tail; ++k)
+        r = byte_step(L, r, ((g8p)E)[k], c_hi);
+    return r;
+}
+
+__global__ __launch_bounds__(WG) void multi_kernel(BatchDesc d, MultiBatch m, const uint32_t *__restrict__ gtab)
+{
+    __shared__ __attribute__((aligned(16))) char L[OFF_U];
+    const uint64_t n = d.n;
+    const uint64_t nthr = (uint64_t)gridDim.x * WG;
+    const uint64_t g0 = (uint64_t)blockIdx.x * WG + threadIdx.x;
+    if ((uint64_t)blockIdx.x * WG >= n * m.nb)
+        return;
+    fill_lds<1>(L, gtab);
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const uint32_t c_lo = (uint32_t)(lane & 31) << 2;
+    const uint32_t c_hi = c_lo | 0x10000u;
+    const uintptr_t dummy = reinterpret_cast<uintptr_t>(gtab);
+    /* cursor of the next item to fetch: batch b, record i */
+    uint32_t b = (uint32_t)(g0 / n);
+    uint64_t i = g0 - (uint64_t)b * n;
+    auto advance = [&]() {
+        i += nthr;
+        while (i >= n && b < m.nb) {
+            i -= n;
+            ++b;
+        }
+    };
+    MItem ia, ib;
+    uint32_t wa[16], wb[16];
+    multi_fetch(d, m, b, i, dummy, ia, wa);
+    advance();
+    for (;;) {
+        multi_fetch(d, m, b, i, dummy, ib, wb);
+        advance();
+        __builtin_amdgcn_sched_barrier(0);
+        if (!ia.ok)
+            break;
+        const uint32_t ra = multi_hash(d, ia, wa, L, c_lo, c_hi);
+        m.out[ia.b][ia.i] = ra ^ d.xor_io;
+        multi_fetch(d, m, b, i, dummy, ia, wa);
+        advance();
+        __builtin_amdgcn_sched_barrier(0);
+        if (!ib.ok)
+            break;
+        const uint32_t rb = multi_hash(d, ib, wb, L, c_lo, c_hi);
+        m.out[ib.b][ib.i] = rb ^ d.xor_io;
+    }
+}
+
+/*
  * burst_kernel: one lane per record of at most 5 pieces, all its pieces loaded
  * at once (a burst) and then hashed, so a line the record shares with the
  * neighbouring lane's record is requested by both lanes together and fetched
@@ -1820,6 +1924,13 @@ extern "C" int zs_launch_burst(int fixed, int xp, int nb, const zs::BatchDesc *d
     else
         ZS_BURST(false, false, 5);
 #undef ZS_BURST
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int zs_launch_multi(const zs::BatchDesc *d, const zs::MultiBatch *m, const uint32_t *gtab, int grid,
+                               hipStream_t stream)
+{
+    hipLaunchKernelGGL(zs::multi_kernel, dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

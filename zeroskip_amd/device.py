@@ -39,6 +39,27 @@ def crc_fixed(data: torch.Tensor, stride: int, length: int, n: int, seed: int = 
     return out
 
 
+def crc_fixed_multi(batches: list[torch.Tensor], stride: int, length: int, n: int, seed: int = 0,
+                    outs: list[torch.Tensor] | None = None, raw: bool = False) -> list[torch.Tensor]:
+    """crc_fixed over each of the device buffers in `batches` (same stride,
+    length and count), in one call (zscrc_device_fixed_multi): one persistent
+    launch for records of <= 64 bytes."""
+    import ctypes
+    k = len(batches)
+    dev = _dev(batches[0])
+    for b in batches:
+        if n and (n - 1) * stride + length > b.numel() * b.element_size():
+            raise ValueError("records extend past the end of a batch buffer")
+    if outs is None:
+        outs = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(k)]
+    bases = (ctypes.c_void_p * k)(*[b.data_ptr() for b in batches])
+    optrs = (ctypes.c_void_p * k)(*[o.data_ptr() for o in outs])
+    with torch.cuda.device(dev):
+        check(lib().zscrc_device_fixed_multi(bases, optrs, k, stride, length, seed & 0xFFFFFFFF, n,
+                                             ZSCRC_RAW if raw else 0, _stream(dev)), "zscrc_device_fixed_multi")
+    return outs
+
+
 def crc_batch(data: torch.Tensor, offs: torch.Tensor, lens: torch.Tensor,
               seeds: torch.Tensor | None = None, out: torch.Tensor | None = None,
               raw: bool = False, max_len: int | None = None) -> torch.Tensor:

@@ -130,3 +130,31 @@ def write_commits(d_image: torch.Tensor, span_off: torch.Tensor, span_len: torch
             None if st is None else st.data_ptr(),
             torch.cuda.current_stream(d_image.device).cuda_stream), "zscrc_device_write_commits_bounded")
     return (crc, st) if status else crc
+
+
+class FilesReport(ctypes.Structure):
+    """zscrc_files_report (include/zscrc.h)."""
+    _fields_ = [("files", ctypes.c_uint64), ("commits", ctypes.c_uint64), ("bytes", ctypes.c_uint64),
+                ("bad_commits", ctypes.c_uint64), ("stale_empty_commits", ctypes.c_uint64),
+                ("header_errors", ctypes.c_uint64), ("walk_errors", ctypes.c_uint64),
+                ("first_bad_file", ctypes.c_uint64), ("first_bad_off", ctypes.c_uint64),
+                ("first_bad_what", ctypes.c_int32), ("threads", ctypes.c_int32),
+                ("copy_s", ctypes.c_double), ("verify_tail_s", ctypes.c_double), ("total_s", ctypes.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+def verify_files(images, kinds=None, threads: int = 0) -> dict:
+    """End to end from host memory (zscrc_zs_verify_files): every header,
+    walk and commit CRC of the given file images (numpy uint8 arrays, bytes
+    or memmaps; kinds default ACTIVE), on the current GPU.  Synchronous."""
+    arrs = [_host(im)[0] for im in images]
+    n = len(arrs)
+    ptrs = (ctypes.c_void_p * max(n, 1))(*[a.ctypes.data if a.nbytes else None for a in arrs])
+    sizes = np.array([a.nbytes for a in arrs], np.uint64)
+    kk = np.array([ACTIVE] * n if kinds is None else list(kinds), np.int32)
+    rep = FilesReport()
+    check(lib().zscrc_zs_verify_files(ptrs, sizes.ctypes.data, kk.ctypes.data, n, threads, ctypes.byref(rep)),
+          "zscrc_zs_verify_files")
+    return rep.as_dict()
