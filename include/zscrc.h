@@ -148,8 +148,16 @@ void zscrc_set_prefetch(int g, int depth);
 /* team size the fixed-stride path picks for n packed records of len bytes
  * from a 128-byte-aligned base (1/2/16/64; 0 if no device) */
 int zscrc_team_for(uint64_t len, uint64_t n);
-/* Diagnostic: plain streaming read of len bytes (multiple of 8192) -- the
- * measured HBM read ceiling on this GPU.  d_scratch4: 4 writable device bytes. */
+/* tuning: coalesced non-temporal whole-wave teams (xteam_kernel) on
+ * fixed-stride records of at least min_len bytes (default 256 KiB): mode 0 =
+ * off, 1 = on (default; env ZSCRC_XTEAM, ZSCRC_XTEAM_MIN) */
+void zscrc_set_xteam(int mode, uint64_t min_len);
+/* the xteam mode the fixed-stride path uses for n packed records of len
+ * bytes (0 = another kernel, or no device) */
+int zscrc_xteam_for(uint64_t len, uint64_t n);
+/* Diagnostic: fully coalesced non-temporal streaming read of len bytes
+ * (multiple of 4096) -- the measured HBM read ceiling on this GPU (grid =
+ * grid_mult x CUs of 1024 threads).  d_scratch4: 4 writable device bytes. */
 int zscrc_diag_stream_read(const void *d_buf, uint64_t len, void *d_scratch4, int grid_mult,
                            void *stream);
 /* Number of gfx950 devices visible (0 if none / no HIP runtime). */

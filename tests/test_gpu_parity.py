@@ -274,25 +274,61 @@ def test_scalar_offload(gpu):
     assert after[0] - before[0] == 1   # the 37-byte call stayed on the CPU
 
 
-def test_config3_headline_dispatch(gpu):
+@pytest.mark.parametrize("xteam", [0, 1], ids=["team16", "xteam"])
+def test_config3_headline_dispatch(gpu, xteam):
     """BASELINE config 3 at full size through the exact call bench.py times:
     zscrc_device_fixed on 65,536 x 64 KiB chunks (4 GiB), seed 0, flags 0 --
-    the 16-lane team walk with xor_io = ~0 -- every CRC against the oracle."""
+    by default the 16-lane team walk (team_kernel<16>) with xor_io = ~0; also
+    the coalesced whole-wave teams (xteam_kernel) forced on -- every CRC
+    against the oracle."""
     n, L = 65536, 65536
-    assert lib().zscrc_team_for(L, n) == 16
-    g = torch.Generator(device=gpu)
-    g.manual_seed(0x9E3779B9)
-    d = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=gpu, generator=g)
-    out = torch.empty(n, dtype=torch.int32, device=gpu)
-    from zeroskip_amd._lib import check
-    check(lib().zscrc_device_fixed(d.data_ptr(), L, L, 0, out.data_ptr(), n, 0,
-                                   torch.cuda.current_stream(gpu).cuda_stream), "zscrc_device_fixed")
-    got = u32(out)
-    host = d.cpu().numpy()
-    del d
+    lib().zscrc_set_xteam(xteam, 32768 if xteam else 256 << 10)
+    try:
+        if xteam:
+            assert lib().zscrc_team_for(L, n) == 64 and lib().zscrc_xteam_for(L, n) == xteam
+        else:
+            assert lib().zscrc_team_for(L, n) == 16 and lib().zscrc_xteam_for(L, n) == 0
+        g = torch.Generator(device=gpu)
+        g.manual_seed(0x9E3779B9)
+        d = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=gpu, generator=g)
+        out = torch.empty(n, dtype=torch.int32, device=gpu)
+        from zeroskip_amd._lib import check
+        check(lib().zscrc_device_fixed(d.data_ptr(), L, L, 0, out.data_ptr(), n, 0,
+                                       torch.cuda.current_stream(gpu).cuda_stream), "zscrc_device_fixed")
+        got = u32(out)
+        host = d.cpu().numpy()
+        del d
+    finally:
+        lib().zscrc_set_xteam(1, 256 << 10)
     ref = oracle.batch(host, n=n, stride=L, fixed_len=L, impl="hw", threads=min(16, os.cpu_count() or 1))
     bad = np.nonzero(got != ref)[0]
     assert bad.size == 0, bad[:10]
+
+
+def test_xteam_shapes(gpu):
+    """xteam_kernel (coalesced whole-wave teams) on ragged shapes: unaligned
+    bases and strides, front-padded first steps at the buffer start, records
+    shorter than one step, < 8-byte records, gaps between records, fewer
+    records than waves -- forced on with a 1-byte threshold."""
+    lib().zscrc_set_xteam(1, 1)
+    lib().zscrc_set_teams(0, 1 << 20)   # no one-lane records: xteam down to 1 byte
+    try:
+        for stride, length, n, off in [(65536, 65536, 300, 0), (4096, 4096, 3000, 0), (100000, 99999, 300, 1),
+                                       (5200, 5199, 700, 3), (8192, 4096, 1000, 2), (4097, 4097, 333, 3),
+                                       (64, 64, 10000, 0), (320, 312, 5000, 1), (8, 8, 1000, 0),
+                                       (5, 5, 100, 1), (12345, 12000, 7, 1)]:
+            data = rand_bytes(stride * (n - 1) + length + off, stride + length + n)
+            assert lib().zscrc_xteam_for(length, n) == 1
+            out = u32(zd.crc_fixed(to_dev(data[off:], gpu), stride, length, n, seed=0xA5A5))
+            ref = _oracle_seeded(data[off:], stride, length, n, 0xA5A5)
+            bad = np.nonzero(out != ref)[0]
+            assert bad.size == 0, (stride, length, n, off, bad[:10])
+            raw = u32(zd.crc_fixed(to_dev(data[off:], gpu), stride, length, n, seed=0x1234, raw=True))
+            want = (~oracle.crc32c_hw(~0x1234 & M32, data[off:off + length])) & M32
+            assert raw[0] == want, (stride, length, "raw")
+    finally:
+        lib().zscrc_set_xteam(1, 256 << 10)
+        lib().zscrc_set_teams(*DEFAULT_TEAMS)
 
 
 def test_config2_full_size_vs_oracle(gpu):

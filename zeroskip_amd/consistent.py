@@ -284,17 +284,37 @@ class Report:
     commits: int = 0
     bytes_checked: int = 0
     dotzsdb: dict = field(default_factory=dict)
-    bad_commits: list = field(default_factory=list)         # (file, commit offset)
-    stale_empty_commits: list = field(default_factory=list)  # (file, commit offset)
     n_bad: int = 0            # counts (the lists hold at most MAX_LISTED per rank)
     n_stale: int = 0
     header_errors: list = field(default_factory=list)
     walk_errors: list = field(default_factory=list)
     issues: list = field(default_factory=list)
     timing: dict = field(default_factory=dict)
+    # (file id, commit offset) rows; named and sorted only when read, so the
+    # timed pass does no per-commit Python work
+    names: object = None
+    bad_rows: np.ndarray = field(default_factory=lambda: np.zeros((0, 2), np.int64))
+    stale_rows: np.ndarray = field(default_factory=lambda: np.zeros((0, 2), np.int64))
+    extra_bad: list = field(default_factory=list)           # (file name, commit offset)
+
+    def _named(self, rows) -> list:
+        return [(self.names[int(f)], int(x)) for f, x in rows]
+
+    @property
+    def bad_commits(self) -> list:
+        """(file, commit offset) of every listed bad commit, sorted."""
+        return sorted(self._named(self.bad_rows) + list(self.extra_bad))
+
+    @property
+    def stale_empty_commits(self) -> list:
+        """(file, commit offset) of every listed stale empty commit, sorted."""
+        return sorted(self._named(self.stale_rows))
 
     def as_dict(self):
-        return dict(self.__dict__)
+        d = {k: v for k, v in self.__dict__.items() if k not in ("names", "bad_rows", "stale_rows", "extra_bad")}
+        d["bad_commits"] = self.bad_commits
+        d["stale_empty_commits"] = self.stale_empty_commits
+        return d
 
 
 class Consistent:
@@ -539,10 +559,9 @@ class Consistent:
         L = self.MAX_LISTED
         commits, n_bad, n_stale, nb, ns, npc = (int(v) for v in row[:self.HEAD])
         o = self.HEAD
-        names = self._names
-        bad = [(names[f], int(x)) for f, x in row[o:o + 2 * nb].reshape(-1, 2)]
+        bad = row[o:o + 2 * nb].reshape(-1, 2)
         o += 2 * L
-        stale = [(names[f], int(x)) for f, x in row[o:o + 2 * ns].reshape(-1, 2)]
+        stale = row[o:o + 2 * ns].reshape(-1, 2)
         o += 2 * L
         pieces = [tuple(int(v) for v in p) for p in row[o:o + 4 * npc].reshape(-1, 4)]
         h = self._host_all[r]
@@ -554,11 +573,14 @@ class Consistent:
         """Per-rank digests to every rank: one fixed-shape all-gather of int64
         rows (RCCL under nccl: a device tensor; gloo: host), no pickling.  The
         host-side findings (headers, walks) were exchanged once in prepare()."""
-        if self._names is None:
-            self._names = np.array([f.name for f in self.db.files], dtype=object)
-        row = self._pack(digest)
         if self.world == 1:
-            return [self._unpack(0, row)]
+            h = self._host_all[0]
+            return [dict(rank=0, commits=digest["commits"], n_bad=digest["n_bad"], n_stale=digest["n_stale"],
+                         bad=digest["bad"], stale=digest["stale"],
+                         pieces=[tuple(int(v) for v in p) for p in digest["pieces"]],
+                         files=h["files"], bytes=h["bytes"], header_errors=h["header_errors"],
+                         walk_errors=h["walk_errors"], issues=h["issues"])]
+        row = self._pack(digest)
         import torch.distributed as dist
         dev = torch.device("cpu")
         if dist.get_backend(self.group) == "nccl":
@@ -570,15 +592,18 @@ class Consistent:
         return [self._unpack(r, rows[r]) for r in range(self.world)]
 
     def _merge(self, allsum) -> Report:
-        rep = Report()
+        if self._names is None:
+            self._names = [f.name for f in self.db.files]
+        rep = Report(names=self._names)
         rep.dotzsdb = self._check_dotzsdb()
         pieces = {}
+        bads, stales = [], []
         for s in allsum:
             rep.commits += s["commits"]
             rep.files += s["files"]
             rep.bytes_checked += s["bytes"]
-            rep.bad_commits += [tuple(b) for b in s["bad"]]
-            rep.stale_empty_commits += [tuple(b) for b in s["stale"]]
+            bads.append(s["bad"])
+            stales.append(s["stale"])
             rep.n_bad += s["n_bad"]
             rep.n_stale += s["n_stale"]
             rep.header_errors += [tuple(h) for h in s["header_errors"]]
@@ -597,10 +622,10 @@ class Consistent:
             at = lay["roff"] + lay["rlen"]
             _, _, _, stored, words = _commit_rec(f.image, at)
             if stored is None or _trailer_crc(span, words) != stored:
-                rep.bad_commits.append((f.name, at))
+                rep.extra_bad.append((f.name, at))
                 rep.n_bad += 1
-        rep.bad_commits.sort()
-        rep.stale_empty_commits.sort()
+        rep.bad_rows = np.concatenate(bads) if bads else rep.bad_rows
+        rep.stale_rows = np.concatenate(stales) if stales else rep.stale_rows
         dz = rep.dotzsdb
         if dz.get("present"):
             uu = {f.uuid for f in self.db.files}

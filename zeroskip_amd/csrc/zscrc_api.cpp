@@ -39,6 +39,7 @@ int zs_launch_burst(int fixed, int xp, int nb, const zs::BatchDesc *d, const uin
                     hipStream_t stream);
 int zs_launch_multi(const zs::BatchDesc *d, const zs::MultiBatch *m, const uint32_t *gtab, int grid,
                     hipStream_t stream);
+int zs_launch_xteam(int depth, const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
 }
 
 namespace {
@@ -56,6 +57,13 @@ std::atomic<int> g_split_team{64}; /* team size on split long records */
 /* 2-lane teams on fixed-stride records: 0 = automatic (128-byte-aligned
  * records of 128..1024 bytes), 1 = never, 2 = every record <= g1_max */
 std::atomic<int> g_small_team{0};
+/* coalesced non-temporal whole-wave teams (xteam_kernel) on fixed-stride
+ * records of at least g_xteam_min bytes: 0 = off, 1 = on (same-box
+ * interleaved A/B, profiles/r02/xteam_ab.jsonl: 1 MiB records 0.64-0.68 ms
+ * per 4 GiB against 0.73-0.77 for team<64>; on 64 KiB records (config 3)
+ * within -4..+8 % of team<16> from box to box, so team<16> keeps those) */
+std::atomic<int> g_xteam{1};
+std::atomic<uint64_t> g_xteam_min{256u << 10};
 std::atomic<int> g_span_team{16}; /* team size on span segments (16 or 64; 16: 3 GiB 5.56 -> 5.71 TB/s) */
 int g_strict = 0;
 /* record-walk override per team size (index 0/1/2 = G 1/16/64): -1 = automatic
@@ -113,6 +121,12 @@ void env_init()
     s = getenv("ZSCRC_G16_MAX");
     if (s)
         g_g16_max = strtoull(s, nullptr, 0);
+    s = getenv("ZSCRC_XTEAM");
+    if (s && atoi(s) >= 0 && atoi(s) <= 1)
+        g_xteam = atoi(s);
+    s = getenv("ZSCRC_XTEAM_MIN");
+    if (s)
+        g_xteam_min = strtoull(s, nullptr, 0);
 }
 
 bool is_gfx950(int dev)
@@ -263,6 +277,8 @@ int team_for(uint64_t len, uint64_t n, int ncu, uint64_t stride, uintptr_t base)
         return 2;
     if (len <= g_g1_max)
         return 1;
+    if (g_xteam && len >= g_xteam_min && len > g_g1_max)
+        return 64; /* xteam_kernel: coalesced non-temporal whole-wave teams */
     if (len <= g_g16_max && n >= (uint64_t)ncu * 16 * 4)
         return 16;
     return 64;
@@ -313,7 +329,10 @@ int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s, int depth_hi
     /* pieces per burst: a fixed-stride record spans at most ceil(len/64) */
     const int nb = fixed && d.fixed_len <= 64 && d.last_len == ~0ull ? 1
                    : fixed && d.fixed_len <= 128 && d.last_len == ~0ull ? 2 : 5;
-    int rc = depth >= 9  ? zs_launch_burst(fixed, depth == 10, nb, &dx, c->gtab, c->ncu, s)
+    const int xt = g_xteam;
+    const bool xteam = g == 64 && fixed && xt && g_depth[2] < 0 && depth_hint < 0 && d.fixed_len >= g_xteam_min;
+    int rc = xteam       ? zs_launch_xteam(xt, &d, c->gtab, c->ncu, s)
+             : depth >= 9 ? zs_launch_burst(fixed, depth == 10, nb, &dx, c->gtab, c->ncu, s)
              : depth >= 3 ? zs_launch_short(fixed, depth - 3, &dx, c->gtab, c->ncu, s)
                         : zs_launch_team(g, fixed, depth, &d, c->gtab, c->ncu, s);
     if (rc) {
@@ -507,7 +526,8 @@ int span_impl(DevCtx *c, const void *d_buf, uint64_t len, uint32_t seed, uint32_
     d.fixed_seed = 0;
     d.xor_io = 0;
     d.out = part;
-    int rc = launch(c, g, d, s);
+    /* segments of >= g_xteam_min bytes: the coalesced whole-wave teams */
+    int rc = launch(c, g_xteam && seg >= g_xteam_min ? 64 : g, d, s);
     if (rc)
         return rc;
     zs::SpanFold f;
@@ -888,6 +908,23 @@ void zscrc_set_small_team(int mode)
     std::call_once(g_env_once, env_init);
     if (mode >= 0 && mode <= 2)
         g_small_team = mode;
+}
+
+void zscrc_set_xteam(int mode, uint64_t min_len)
+{
+    std::call_once(g_env_once, env_init);
+    if (mode >= 0 && mode <= 1)
+        g_xteam = mode;
+    g_xteam_min = min_len;
+}
+
+int zscrc_xteam_for(uint64_t len, uint64_t n)
+{
+    DevCtx *c;
+    if (get_ctx(&c))
+        return 0;
+    return team_for(len, n, c->ncu, len, 0) == 64 && g_xteam && g_depth[2] < 0 && len >= g_xteam_min ? g_xteam.load()
+                                                                                                        : 0;
 }
 
 void zscrc_set_teams(uint64_t g1_max, uint64_t g16_max)

@@ -65,6 +65,19 @@ struct BatchDesc {
     const uint32_t *part_rec;
 };
 
+/* A fixed-stride batch for xteam_kernel (what it reads of a BatchDesc: few
+ * kernel arguments, few SGPRs).  last_len = fixed_len when there is none. */
+struct XDesc {
+    const uint8_t *base;
+    uint32_t *out;
+    uint64_t n;
+    uint64_t stride;
+    uint64_t fixed_len;
+    uint64_t last_len;
+    uint32_t seed;
+    uint32_t xor_io;
+};
+
 struct RecDesc {
     uint64_t off;
     uint64_t len;

@@ -700,6 +700,282 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d_in, const uint32_t
     }
 }
 
+/* ----------------------------------------- coalesced whole-wave teams */
+/*
+ * xteam_kernel: fixed-stride batches of long records (config 3's 64 KiB
+ * chunks), one record per wave at a time (G = 64, 4 KiB steps), hashed like
+ * team_kernel<64> -- lane j owns piece j of every step, the last word of a
+ * non-final piece jumps the lane's register over the rest of the step
+ * ("word then skip 63*64 bytes", U), the 64 lane registers are folded at the
+ * record end (Z) -- but loaded differently.  A step's four load instructions
+ * are fully coalesced non-temporal 1 KiB reads: in instruction i lane (g, c)
+ * reads bytes [16g, 16g+16) of piece 16i + c, so every cache line is consumed
+ * by the instruction that fetched it and the nt policy costs no L1 re-fetch;
+ * a row transpose (v_permlane32/16_swap: block i of lane (g, c) <-> block g
+ * of lane (i, c)) then hands lane 16g + c its whole piece.
+ * tools/ceiling_probe.hip: nt coalesced reads 6.9-7.2 TB/s against 6.4-6.6
+ * for per-lane 64-byte piece loads (team<16>), which lose half their rate
+ * with nt.  The next step's loads are in flight while a step is hashed (two
+ * register buffers; the loop is unrolled twice so that no buffer copy makes
+ * the compiler wait on them).  Each wave walks a contiguous block of records.
+ * Same-box interleaved A/B (tools/xteam_ab.py, profiles/r02/xteam_ab.jsonl,
+ * four boxes): 1 MiB x 4,096 records 0.635-0.676 ms against team<64>'s
+ * 0.726-0.771 (4 GiB: 6.4-6.8 TB/s); on 64 KiB x 65,536 (config 3) 0.646-0.72
+ * against team<16>'s 0.663-0.673, and slower on 4-16 KiB records: the
+ * per-record fold and only one 4 KiB step in flight per wave (a two-step
+ * ring measured slower: the register allocator reuses in-flight buffers)
+ * leave it short of the 7 TB/s its load shape reaches.  Used from 256 KiB.
+ */
+
+/* A record of the batch as the hashing walk sees it (wave-uniform). */
+struct XItem {
+    uintptr_t A;  /* first byte */
+    uintptr_t E;  /* last 4-aligned address <= A+len */
+    uintptr_t V0; /* step-grid start (<= A) */
+    uint64_t len;
+    uint64_t w;   /* record index */
+    uint32_t S;   /* steps; 0 = fewer than 8 bytes */
+    uint32_t R0;  /* initial register */
+};
+
+constexpr uint64_t XSTEP = 4096;
+
+__device__ __forceinline__ bool xitem(const XDesc &d, uint64_t w, uint64_t wend, XItem &it)
+{
+    if (w >= wend)
+        return false;
+    const uint64_t len = (w + 1 == d.n) ? d.last_len : d.fixed_len;
+    const uintptr_t A = reinterpret_cast<uintptr_t>(d.base) + w * d.stride;
+    const uintptr_t E = len < 8 ? A : ((A + len) & ~uintptr_t(3));
+    const uint32_t S = len < 8 ? 0u : (uint32_t)((E - A + XSTEP - 1) / XSTEP);
+    it.A = A;
+    it.E = E;
+    it.V0 = E - (uint64_t)S * XSTEP;
+    it.S = S;
+    it.len = len;
+    it.w = w;
+    it.R0 = d.seed ^ d.xor_io;
+    return true;
+}
+
+/* Issue the four coalesced nt loads of the step at `step` (wave-uniform):
+ * lane (g, c) gets bytes [16g, 16g+16) of pieces 16i + c, i < 4.  A step
+ * below the buffer's first aligned dword (front padding of a record at the
+ * buffer start) clamps its block addresses to lo (fix_piece re-aligns);
+ * no step: a cached dummy. */
+__device__ __forceinline__ void xissue(uintptr_t step, bool ok, uint32_t voff, uintptr_t dummy, uintptr_t lo,
+                                       uint32_t (&w)[16])
+{
+    const uintptr_t sb = uni64(ok ? step : dummy); /* scalar base + 32-bit lane offsets */
+    if (ok && step < lo) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            uintptr_t q = sb + voff + 1024u * (uint32_t)i;
+            q = q < lo ? lo : q;
+            const u32x4 v = __builtin_nontemporal_load((g4p)q);
+            w[4 * i + 0] = v.x;
+            w[4 * i + 1] = v.y;
+            w[4 * i + 2] = v.z;
+            w[4 * i + 3] = v.w;
+        }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const u32x4 v = __builtin_nontemporal_load((g4p)(sb + (voff + 1024u * (uint32_t)i)));
+        w[4 * i + 0] = v.x;
+        w[4 * i + 1] = v.y;
+        w[4 * i + 2] = v.z;
+        w[4 * i + 3] = v.w;
+    }
+}
+
+/* block i of lane (g, c) <-> block g of lane (i, c): v_permlane32_swap then
+ * v_permlane16_swap (xpose_burst's transpose). */
+__device__ __forceinline__ void xpose16(uint32_t (&w)[16])
+{
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const auto a = __builtin_amdgcn_permlane32_swap(w[k], w[8 + k], false, false);
+        const auto b = __builtin_amdgcn_permlane32_swap(w[4 + k], w[12 + k], false, false);
+        const auto e = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
+        const auto f = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
+        w[k] = e[0];
+        w[4 + k] = e[1];
+        w[8 + k] = f[0];
+        w[12 + k] = f[1];
+    }
+}
+
+/* Fix-ups of the 64-byte piece at p near the record start: undo the clamp
+ * of blocks below lo, zero every byte before A, XOR the initial register
+ * into bytes [A, A+4).  Pieces from A+4 on: nothing. */
+__device__ __forceinline__ void fix_piece(const XItem &it, uintptr_t p, uintptr_t lo, uint32_t (&w)[16])
+{
+    if (p >= it.A + 4)
+        return;
+    if (p < lo) { /* only records within 64 B of the buffer start */
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uintptr_t q = p + 16 * i;
+            const uint64_t m = q < lo ? (lo - q) >> 2 : 0;
+            const uint32_t b0 = w[4 * i], b1 = w[4 * i + 1], b2 = w[4 * i + 2];
+            w[4 * i + 3] = m == 0 ? w[4 * i + 3] : m == 1 ? b2 : m == 2 ? b1 : b0;
+            w[4 * i + 2] = m == 0 ? b2 : m == 1 ? b1 : b0;
+            w[4 * i + 1] = m == 0 ? b1 : b0;
+        }
+    }
+    const int32_t d0 = (int32_t)(int64_t)(it.A - p); /* > -4 */
+    if ((it.A & 3) == 0) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int32_t dk = d0 - 4 * k;
+            w[k] = dk > 0 ? 0u : (dk == 0 ? w[k] ^ it.R0 : w[k]);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int32_t dk = d0 - 4 * k;
+            uint32_t v = w[k];
+            if (dk >= 4)
+                v = 0;
+            else if (dk > 0)
+                v &= 0xffffffffu << (8 * dk);
+            if (dk >= 0 && dk < 4)
+                v ^= it.R0 << (8 * dk);
+            else if (dk < 0 && dk > -4)
+                v ^= it.R0 >> (8 * -dk);
+            w[k] = v;
+        }
+    }
+}
+
+/* The loads' walk over (record, step), one step ahead of the hashing: only
+ * what addresses a step (wave-uniform). */
+struct XLoad {
+    uint64_t w;    /* record */
+    uint64_t wend; /* end of the wave's block of records */
+    uintptr_t V;   /* address of the current step */
+    uint32_t left; /* steps of the record after this one */
+    bool ok;       /* a record with >= 8 bytes: loads */
+};
+
+__device__ __forceinline__ void xrec(const XDesc &d, XLoad &l)
+{
+    const uint64_t len = (l.w + 1 == d.n) ? d.last_len : d.fixed_len;
+    const uintptr_t A = reinterpret_cast<uintptr_t>(d.base) + l.w * d.stride;
+    const uintptr_t E = len < 8 ? A : ((A + len) & ~uintptr_t(3));
+    const uint64_t S = len < 8 ? 0 : (E - A + XSTEP - 1) / XSTEP;
+    l.V = E - S * XSTEP;
+    l.left = S ? (uint32_t)(S - 1) : 0u;
+    l.ok = l.w < l.wend && S; /* a record without loads: its one position reads the dummy */
+}
+
+__device__ __forceinline__ void xnext(const XDesc &d, XLoad &l)
+{
+    if (l.ok && l.left) {
+        --l.left;
+        l.V += XSTEP;
+        return;
+    }
+    if (l.w >= l.wend)
+        return;
+    l.w += 1;
+    xrec(d, l);
+}
+
+__global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, const uint32_t *__restrict__ gtab)
+{
+    __shared__ __attribute__((aligned(16))) char L[LDS_BYTES];
+    if ((uint64_t)blockIdx.x * WAVES >= d.n)
+        return;
+    fill_lds<64>(L, gtab);
+    __syncthreads();
+    const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+    const uint32_t c_lo = (uint32_t)(lane & 31) << 2;
+    const uint32_t c_hi = c_lo | 0x10000u;
+    /* each wave walks a contiguous block of records */
+    const uint64_t team = uni64((uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6));
+    const uint64_t nteams = (uint64_t)gridDim.x * WAVES;
+    const uint64_t per = (d.n + nteams - 1) / nteams;
+    const uint64_t wbeg = team * per < d.n ? team * per : d.n;
+    const uint64_t wend = wbeg + per < d.n ? wbeg + per : d.n;
+    const uintptr_t dummy = reinterpret_cast<uintptr_t>(gtab);
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(d.base) & ~uintptr_t(3);
+
+    XLoad ld;
+    ld.w = wbeg;
+    ld.wend = wend;
+    xrec(d, ld);
+    uint32_t b0[16], b1[16];
+    const uint32_t voff = 64u * (uint32_t)c + 16u * (uint32_t)g;
+    xissue(ld.V, ld.ok, voff, dummy, lo, b0);
+    XItem it;
+    bool ok = xitem(d, wbeg, wend, it);
+    uint32_t s = 0;
+    uint32_t acc = 0;
+    /* Results wait in a register (lane k: the k-th record of the current
+     * group of 64) and are stored 64 at a time. */
+    uint32_t stash = 0, nst = 0;
+    uint64_t first = wbeg;
+    auto stash_put = [&](uint32_t r) {
+        stash = lane == (int)nst ? r : stash;
+        if (++nst == 64) {
+            d.out[first + (uint64_t)lane] = stash;
+            first += 64;
+            nst = 0;
+        }
+    };
+    /* hash the step in w (the hashing walk's position it / s) */
+    auto hash = [&](uint32_t (&w)[16]) {
+        if (it.S == 0) { /* < 8 bytes: byte-serial (every lane, same result) */
+            uint32_t r = it.R0;
+            for (uint64_t i = 0; i < it.len; ++i)
+                r = byte_step(L, r, ((g8p)it.A)[i], c_hi);
+            stash_put(r ^ d.xor_io);
+            ok = xitem(d, it.w + 1, wend, it);
+            return;
+        }
+        xpose16(w);
+        const uintptr_t st = it.V0 + (uint64_t)s * XSTEP;
+        if (s <= 1 && st < it.A + 4) /* the record start is in this step */
+            fix_piece(it, st + 64 * (uintptr_t)lane, lo, w);
+        if (s + 1 < it.S) {
+            acc = piece<true>(L, acc, w, c_lo, c_hi);
+            ++s;
+            return;
+        }
+        acc = piece<false>(L, acc, w, c_lo, c_hi);
+        /* lane j's register sits (63-j)*64 bytes before E: fold the wave */
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const uint32_t sh = op4(L, OFF_Z + 4096u * k, acc);
+            const uint32_t other = __shfl_xor(sh, 1 << k);
+            acc ^= ((lane >> k) & 1) ? other : 0u;
+        }
+        const uint32_t tail = (uint32_t)((it.A + it.len) - it.E);
+        if (tail && lane == 63)
+            for (uint32_t i = 0; i < tail; ++i)
+                acc = byte_step(L, acc, ((g8p)it.E)[i], c_hi);
+        stash_put(__shfl(acc, 63) ^ d.xor_io);
+        acc = 0;
+        s = 0;
+        ok = xitem(d, it.w + 1, wend, it);
+    };
+    while (ok) {
+        xnext(d, ld);
+        xissue(ld.V, ld.ok, voff, dummy, lo, b1);
+        hash(b0);
+        if (!ok)
+            break;
+        xnext(d, ld);
+        xissue(ld.V, ld.ok, voff, dummy, lo, b0);
+        hash(b1);
+    }
+    if ((uint32_t)lane < nst)
+        d.out[first + (uint64_t)lane] = stash;
+}
+
 /* ------------------------------------------------------ short records */
 /*
  * One lane per record, records <= g1_max bytes (zsbench's 312-byte commit
@@ -1795,25 +2071,41 @@ __global__ __launch_bounds__(256) void part_fold_kernel(BatchDesc d, const uint3
 }
 
 /* ------------------------------------------------------ diagnostics */
-/* Plain coalesced streaming read (16 B per lane, 1 KiB per wave-instruction,
- * 8 instructions = 8 KiB in flight per wave) XOR-reduced into one word: the
- * measured HBM read ceiling the CRC kernels are judged against on the same
- * GPU (bench.py reports both). */
+/* The measured HBM read ceiling the CRC kernels are judged against on the
+ * same GPU (bench.py reports both): a fully coalesced non-temporal streaming
+ * read, each wave sweeping blocks of 4 x 1 KiB (lane l: 16 B at 16*l + 1024*i)
+ * with the next block's loads in flight while one is XOR-reduced -- the
+ * fastest read shape found (tools/ceiling_probe.hip: 6.9-7.2 TB/s, against
+ * 6.1-6.3 for plain loads and 6.4-6.6 for per-lane 64-byte pieces). */
 __global__ __launch_bounds__(1024) void stream_read_kernel(const uint8_t *buf, uint64_t n, uint32_t *out)
 {
+    constexpr uint64_t BLK = 4096;
     const uint64_t wave = (uint64_t)blockIdx.x * 16 + (threadIdx.x >> 6);
     const uint64_t nw = (uint64_t)gridDim.x * 16;
     const int lane = threadIdx.x & 63;
+    const uint64_t nb = n / BLK;
     uint32_t acc = 0;
-    for (uint64_t s = wave; (s + 1) * 8192 <= n; s += nw) {
-        const g4p q = (g4p)(buf + s * 8192 + 16 * (uint64_t)lane);
-        u32x4 v[8];
+    u32x4 a[4];
+    uint64_t s = wave;
+    if (s < nb) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
-            v[i] = q[64 * i];
+        for (int i = 0; i < 4; ++i)
+            a[i] = __builtin_nontemporal_load((g4p)(buf + s * BLK + 1024 * i + 16 * lane));
+    }
+    while (s < nb) {
+        const uint64_t t = s + nw;
+        u32x4 b[4];
+        if (t < nb) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
-            acc ^= v[i].x ^ v[i].y ^ v[i].z ^ v[i].w;
+            for (int i = 0; i < 4; ++i)
+                b[i] = __builtin_nontemporal_load((g4p)(buf + t * BLK + 1024 * i + 16 * lane));
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            acc ^= a[i].x ^ a[i].y ^ a[i].z ^ a[i].w;
+            a[i] = b[i];
+        }
+        s = t;
     }
     if (acc == 0x9E3779B9u)
         out[0] = acc; /* keeps the loads live; practically never taken */
@@ -1880,6 +2172,24 @@ extern "C" int zs_launch_team(int g, int fixed, int depth, const zs::BatchDesc *
     }
 #undef ZS_CASES
 #undef ZS_LAUNCH
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int zs_launch_xteam(int depth, const zs::BatchDesc *bd, const uint32_t *gtab, int grid,
+                               hipStream_t stream)
+{
+    zs::XDesc x;
+    x.base = bd->base;
+    x.out = bd->out;
+    x.n = bd->n;
+    x.stride = bd->stride;
+    x.fixed_len = bd->fixed_len;
+    x.last_len = bd->last_len == ~0ull ? bd->fixed_len : bd->last_len;
+    x.seed = bd->fixed_seed;
+    x.xor_io = bd->xor_io;
+    const zs::XDesc *d = &x;
+    (void)depth;
+    hipLaunchKernelGGL(zs::xteam_kernel, dim3(grid), dim3(zs::WG), 0, stream, *d, gtab);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
