@@ -527,8 +527,9 @@ def run_config5(args, world, rank, dev, stream):
     ncommit = len(job.c_off)
     local_bytes = job.local.bytes_checked
     nbytes = local_bytes + 24 * ncommit + 16 * len(job.pieces)
-    r = roof(nbytes, kern_ms, "verify_commits (classify + burst_kernel spans + team<64> split long "
-                              "regions + part_fold) + raw pieces, this rank",
+    r = roof(nbytes, kern_ms, "verify_commits_bounded (one burst_kernel over the short commit spans) + "
+                              "zscrc_device_span per records region / pointer section (xteam_kernel or "
+                              "team<16> segments + span_fold), this rank",
              traffic_for("config5_bytes_per_launch"), None)
     out_line = line(args, world, elapsed, job.plan.weight * args.steps,
                     {"workload": f"config5: consistent over a {job.plan.weight / GIB:.2f} GiB DB "
@@ -539,6 +540,8 @@ def run_config5(args, world, rank, dev, stream):
                     r, scaling="strong",
                     data="synthetic zeroskip DB generated on the GPU (tools/zsdb_gen.py), device-resident",
                     prepare={k: round(v, 4) if isinstance(v, float) else v for k, v in job.prepare_times.items()},
+                    device_pass={"verified_spans": len(job.c_off), "longest_verified_span": job.c_max,
+                                 "raw_spans": [q[3] - q[2] for q in job.pieces][:16]},
                     run_timing={k: round(v, 5) for k, v in rep.timing.items()},
                     gen_s=round(t_gen, 2), open_s=round(t_open, 2))
     if rank == 0 and world == 1 and not args.no_cpu:

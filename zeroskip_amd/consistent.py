@@ -145,7 +145,7 @@ def open_db(src) -> Db:
 @dataclass
 class Unit:
     fid: int
-    what: str                 # "file" | "tail" | "region" (whole records span) | "piece"
+    what: str                 # "file" | "tail" (packed: commit + pointers + final) | "piece" (of a records region)
     lo: int                   # byte range of the file this unit checksums
     hi: int
     rank: int = 0
@@ -191,7 +191,7 @@ def make_plan(db: Db, world: int) -> Plan:
     units, cur = [], 0
     for u, splittable in seq:
         w = u.hi - u.lo
-        if not splittable or world == 1:
+        if not splittable:
             u.rank = rank_of(cur + w // 2)
             units.append(u)
         else:
@@ -203,13 +203,12 @@ def make_plan(db: Db, world: int) -> Plan:
                     if cuts[-1] < c < u.hi:
                         cuts.append(c)
             cuts.append(u.hi)
-            if len(cuts) == 2:
-                u.rank = rank_of(cur + w // 2)
-                units.append(u)
-            else:
-                for i in range(len(cuts) - 1):
-                    a, b = cuts[i], cuts[i + 1]
-                    units.append(Unit(u.fid, "piece", a, b, rank_of(cur + (a - u.lo) + (b - a) // 2), i))
+            # a records region is always checksummed as raw pieces (one span
+            # each, zscrc_device_span) and its commit trailer checked on the
+            # host -- also whole, on one rank
+            for i in range(len(cuts) - 1):
+                a, b = cuts[i], cuts[i + 1]
+                units.append(Unit(u.fid, "piece", a, b, rank_of(cur + (a - u.lo) + (b - a) // 2), i))
         cur += w
     return Plan(world, units, packed, W)
 
@@ -230,6 +229,19 @@ class GpuBackend:
     def raw(self, buf, off, ln):
         from .device import crc_batch
         return crc_batch(buf, off, ln, raw=True)
+
+    def raw_spans(self, buf, off: list, ln: list, d_off, d_ln):
+        """raw registers of a few long spans (records-region pieces, pointer
+        sections; host offsets): one zscrc_device_span each -- segments over
+        every CU, the whole-wave coalesced teams on long ones; many: one
+        variable batch."""
+        from .device import crc_span
+        if len(off) > 64:
+            return self.raw(buf, d_off, d_ln)
+        out = torch.empty(len(off), dtype=torch.int32, device=buf.device)
+        for i, (o, n) in enumerate(zip(off, ln)):
+            crc_span(buf, offset=o, length=n, out=out[i:i + 1], raw=True)
+        return out
 
     def crc(self, buf, off, ln, max_len=None):
         from .device import crc_batch
@@ -342,10 +354,7 @@ class Consistent:
         # device layout: one slot per unit; a whole span also needs its commit record
         slots, pos = [], 0
         for u in self.mine:
-            f = db.files[u.fid]
             hi = u.hi
-            if u.what == "region":
-                hi = min(f.size, u.hi + 24)
             slots.append((u, u.lo, hi, pos))
             pos += -(-(hi - u.lo) // SLOT_ALIGN) * SLOT_ALIGN
         self.buf = be.empty(pos)
@@ -391,16 +400,9 @@ class Consistent:
                 c_file.append(np.full(len(so), u.fid, np.int64))
                 c_rec.append(so.astype(np.int64) + sl.astype(np.int64))
             elif u.what == "tail":
+                # the pointer section: a raw span, its commit checked on the host
                 lay = self.plan.packed[u.fid]
-                c_off += [np.array([lay["poff"] - lo + p], np.int64)]
-                c_len += [np.array([lay["plen"]], np.int64)]
-                c_file += [np.array([u.fid], np.int64)]
-                c_rec += [np.array([lay["poff"] + lay["plen"]], np.int64)]
-            elif u.what == "region":
-                c_off += [np.array([p], np.int64)]
-                c_len += [np.array([u.hi - u.lo], np.int64)]
-                c_file += [np.array([u.fid], np.int64)]
-                c_rec += [np.array([u.hi], np.int64)]
+                pieces.append((u.fid, -1, lay["poff"], lay["poff"] + lay["plen"], lay["poff"] - lo + p))
             else:
                 pieces.append((u.fid, u.piece, u.lo, u.hi, p))
         cat = (lambda xs: np.concatenate(xs) if xs else np.zeros(0, np.int64))
@@ -420,7 +422,7 @@ class Consistent:
         self.prepare_times = dict(stage_s=t_read - t0, walk_and_copy_s=t1 - t_read, total_s=t1 - t0,
                                   staged_bytes=pos)
         # split pieces per rank are fixed by the plan: the exchange row's size
-        self._pmax = max([sum(1 for u in self.plan.units if u.rank == r and u.what == "piece")
+        self._pmax = max([sum(1 for u in self.plan.units if u.rank == r and u.what in ("piece", "tail"))
                           for r in range(self.world)] + [0])
         # host-side findings do not change between runs: exchanged once, here
         host = dict(files=self.local.files, bytes=self.local.bytes_checked,
@@ -471,7 +473,13 @@ class Consistent:
             # the host walk knows the longest span: short-span batches skip
             # the device-side length classes (zscrc_device_verify_commits_bounded)
             crc, st = be.verify(self.buf, self.d_off, self.d_len, max_len=self.c_max)
-        raw = be.raw(self.buf, self.d_poff, self.d_plen) if self.pieces else None
+        raw = None
+        if self.pieces:
+            if hasattr(be, "raw_spans"):
+                raw = be.raw_spans(self.buf, [q[4] for q in self.pieces], [q[3] - q[2] for q in self.pieces],
+                                   self.d_poff, self.d_plen)
+            else:
+                raw = be.raw(self.buf, self.d_poff, self.d_plen)
         if events:
             events[1].record()
         pack = np.zeros((0, 18), np.int64)
@@ -610,16 +618,17 @@ class Consistent:
             rep.walk_errors += [tuple(w) for w in s["walk_errors"]]
             rep.issues += s["issues"]
             for fid, k, ln, r in s["pieces"]:
-                pieces.setdefault(fid, []).append((k, r, ln))
+                pieces.setdefault((fid, k < 0), []).append((k, r, ln))
             if s["n_bad"] > len(s["bad"]):
                 rep.issues.append(f"rank {s['rank']}: {s['n_bad'] - len(s['bad'])} more bad commits not listed")
-        # split records regions: fold the pieces, then the commit trailer
-        for fid, ps in sorted(pieces.items()):
+        # records regions (folded from their pieces) and pointer sections:
+        # the span register, then the commit trailer after it
+        for (fid, tail), ps in sorted(pieces.items()):
             ps.sort()
             f, lay = self.db.files[fid], self.plan.packed[fid]
             span = fold([(r, ln) for _, r, ln in ps])
             rep.commits += 1
-            at = lay["roff"] + lay["rlen"]
+            at = lay["poff"] + lay["plen"] if tail else lay["roff"] + lay["rlen"]
             _, _, _, stored, words = _commit_rec(f.image, at)
             if stored is None or _trailer_crc(span, words) != stored:
                 rep.extra_bad.append((f.name, at))

@@ -45,8 +45,11 @@ int zs_launch_xteam(int depth, const zs::BatchDesc *d, const uint32_t *gtab, int
 namespace {
 
 constexpr int MAX_DEV = 64;
-constexpr uint64_t SPAN_SPLIT_MIN = 1u << 20; /* below: one wavefront team */
-constexpr uint64_t SEG_MIN = 64u << 10;
+/* spans below SPAN_SPLIT_MIN: one whole-wave team; longer: segments of at
+ * least SEG_MIN over every CU (a lone 320 KB or 1.5 MB span ran as one wave's
+ * or 23 teams' serial walk: 0.1-0.25 ms) */
+constexpr uint64_t SPAN_SPLIT_MIN = 16u << 10;
+constexpr uint64_t SEG_MIN = 1u << 10;
 
 thread_local char t_err[256];
 std::atomic<uint64_t> g_stat[4];
@@ -504,10 +507,17 @@ int span_impl(DevCtx *c, const void *d_buf, uint64_t len, uint32_t seed, uint32_
         d.out = d_out;
         return launch(c, len <= g_g1_max ? 1 : 64, d, s);
     }
-    const int g = g_span_team;
-    const uint64_t nteams = (uint64_t)c->ncu * 16 * (64 / g);
+    int g = g_span_team;
+    uint64_t nteams = (uint64_t)c->ncu * 16 * (64 / g);
+    /* two segments per wave of >= g_xteam_min bytes: the coalesced
+     * whole-wave teams (xteam_kernel); else two per 16-lane team */
+    const uint64_t xseg = ((len + 2 * c->ncu * 16 - 1) / (2 * (uint64_t)c->ncu * 16) + 4095) & ~4095ull;
+    if (g_xteam && xseg >= g_xteam_min) {
+        g = 64;
+        nteams = (uint64_t)c->ncu * 16;
+    }
     uint64_t seg = (len + 2 * nteams - 1) / (2 * nteams);
-    seg = (seg + 4095) & ~4095ull;
+    seg = (seg + 1023) & ~1023ull;
     if (seg < SEG_MIN)
         seg = SEG_MIN;
     const uint64_t w = (len + seg - 1) / seg;
@@ -526,8 +536,7 @@ int span_impl(DevCtx *c, const void *d_buf, uint64_t len, uint32_t seed, uint32_
     d.fixed_seed = 0;
     d.xor_io = 0;
     d.out = part;
-    /* segments of >= g_xteam_min bytes: the coalesced whole-wave teams */
-    int rc = launch(c, g_xteam && seg >= g_xteam_min ? 64 : g, d, s);
+    int rc = launch(c, g, d, s);
     if (rc)
         return rc;
     zs::SpanFold f;
