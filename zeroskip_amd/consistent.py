@@ -413,6 +413,8 @@ class Consistent:
         dev = self.buf.device
         self.d_off = torch.from_numpy(self.c_off).to(dev)
         self.d_len = torch.from_numpy(self.c_len).to(dev)
+        self.d_end = self.d_off + self.d_len
+        self._ar8 = torch.arange(8, device=dev)
         self.d_poff = torch.tensor([q[4] for q in pieces], dtype=torch.int64, device=dev)
         self.d_plen = torch.tensor([q[3] - q[2] for q in pieces], dtype=torch.int64, device=dev)
         self.local.files = len(header_of)
@@ -483,19 +485,26 @@ class Consistent:
         if events:
             events[1].record()
         pack = np.zeros((0, 18), np.int64)
+        raw_h = []
         if n:
             # one round trip: the mismatches, their predecessors' computed
-            # commit CRCs, and the commit words after both spans
+            # commit CRCs, the commit words after both spans (and the raw
+            # registers of the long spans)
             bad = torch.nonzero(st != 1).reshape(-1)
-            prv = (bad - 1).clamp(min=0)
-            ar = torch.arange(8, device=bad.device)
-            lim = self.buf.numel() - 1
-            at = ((self.d_off[bad] + self.d_len[bad])[:, None] + ar).clamp(max=lim)
-            pat = ((self.d_off[prv] + self.d_len[prv])[:, None] + ar).clamp(max=lim)
-            pack = torch.cat([bad[:, None], crc[prv].to(torch.int64)[:, None] & M32,
-                              self.buf[at].to(torch.int64), self.buf[pat].to(torch.int64)], 1).cpu().numpy()
+            both = torch.stack([bad, (bad - 1).clamp(min=0)])
+            at = (self.d_end[both][:, :, None] + self._ar8).clamp(max=self.buf.numel() - 1)
+            w = self.buf[at].to(torch.int64)
+            cols = [bad[:, None], crc[both[1]].to(torch.int64)[:, None] & M32, w[0], w[1]]
+            pack = torch.cat(cols, 1)
+            if raw is not None:
+                flat = torch.cat([pack.reshape(-1), raw.to(torch.int64) & M32]).cpu().numpy()
+                raw_h = flat[pack.numel():].tolist()
+                pack = flat[:pack.numel()].reshape(-1, 18)
+            else:
+                pack = pack.cpu().numpy()
             bad_idx = pack[:, 0]
-        raw_h = [v & M32 for v in raw.cpu().tolist()] if raw is not None else []
+        elif raw is not None:
+            raw_h = [v & M32 for v in raw.cpu().tolist()]
         t_dev = time.perf_counter()
 
         # zero-length mismatches right after a span of the same file: the

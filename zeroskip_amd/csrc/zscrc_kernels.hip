@@ -1396,14 +1396,17 @@ struct BRec {
     bool ok;    /* a record */
     bool burst; /* <= 5 pieces, grid inside the buffer */
     bool skip;  /* another class's record (direct_max) */
+    bool cfit;  /* commit batch: the commit word is inside the image */
+    bool cnext; /* ... and is the first 8 bytes of the next lane's first piece */
 };
 
-template <bool FIXED>
+template <bool FIXED, bool XP>
 __device__ __forceinline__ void burst_meta(const BatchDesc &d, const RecDesc *list, bool direct, uint64_t count,
                                            uint64_t i, uintptr_t lo, BRec &b)
 {
     b.ok = i < count;
     b.skip = false;
+    b.cfit = b.cnext = false;
     if (!b.ok) {
         b.burst = false;
         b.np = 0;
@@ -1457,7 +1460,9 @@ __device__ __forceinline__ void burst_meta(const BatchDesc &d, const RecDesc *li
     b.it.A = A;
     b.it.len = len;
     b.it.R0 = seed ^ d.xor_io;
-    if (cfit) {
+    b.cfit = cfit;
+    b.cnext = false;
+    if (cfit && !XP) {
         b.it.c0 = ((g32p)(A + len))[0];
         b.it.c1 = ((g32p)(A + len))[1];
     }
@@ -1466,6 +1471,26 @@ __device__ __forceinline__ void burst_meta(const BatchDesc &d, const RecDesc *li
     b.np = len < 8 ? 0 : (E - A + 63) >> 6;
     b.V0 = E - b.np * 64;
     b.burst = b.np >= 1 && b.V0 >= lo;
+}
+
+/* Commit batches, quad-cooperative bursts: the commit word after lane l's
+ * span is the first 8 bytes of lane l+1's first piece whenever the next
+ * record's piece grid starts right there -- zsbench's BATCHED spans (312
+ * bytes, a 5-piece grid starting 8 bytes before the span) always do -- so
+ * it comes over a lane shuffle from the burst instead of two scattered
+ * dword loads per record (64 cache lines per load instruction).  Lanes
+ * without such a neighbour load it here, with the burst.  Every lane active. */
+__device__ __forceinline__ void commit_words(BRec &b, int lane)
+{
+    const uint32_t v_lo = (uint32_t)b.V0, v_hi = (uint32_t)((uint64_t)b.V0 >> 32);
+    const uint32_t n_lo = __shfl_down(v_lo, 1), n_hi = __shfl_down(v_hi, 1);
+    const int n_ok = __shfl_down((int)(b.ok && b.burst && !b.skip), 1);
+    const uintptr_t end = b.it.A + b.it.len;
+    b.cnext = b.cfit && lane < 63 && n_ok && ((((uintptr_t)n_hi << 32) | n_lo) == end) && (end & 3) == 0;
+    if (b.cfit && !b.cnext) {
+        b.it.c0 = ((g32p)end)[0];
+        b.it.c1 = ((g32p)end)[1];
+    }
 }
 
 template <int NB>
@@ -1528,6 +1553,17 @@ __device__ __forceinline__ void xpose_burst(uint32_t (&w)[NB][16])
             w[p][8 + k] = f[0];
             w[p][12 + k] = f[1];
         }
+}
+
+/* After the transpose, before any fix-up: the shared commit words. */
+template <int NB>
+__device__ __forceinline__ void commit_take(BRec &b, const uint32_t (&w)[NB][16])
+{
+    const uint32_t c0 = __shfl_down(w[0][0], 1), c1 = __shfl_down(w[0][1], 1);
+    if (b.cnext) {
+        b.it.c0 = c0;
+        b.it.c1 = c1;
+    }
 }
 
 template <int NB>
@@ -1645,41 +1681,52 @@ __global__ __launch_bounds__(NB == 1 ? 1024 : BWG) void burst_kernel(BatchDesc d
     uint32_t wa[NB][16], wb[NB][16];
     if (XP) {
         /* wave-uniform trip count: the transpose needs every lane */
-        burst_meta<FIXED>(d, list, direct, count, i, lo, ra);
+        const bool cm = !FIXED && d.commit;
+        burst_meta<FIXED, true>(d, list, direct, count, i, lo, ra);
+        if (cm)
+            commit_words(ra, lane);
         burst_issue_x(ra, dummy, wa, lane);
         for (;;) {
-            burst_meta<FIXED>(d, list, direct, count, i + nthr, lo, rb);
+            burst_meta<FIXED, true>(d, list, direct, count, i + nthr, lo, rb);
+            if (cm)
+                commit_words(rb, lane);
             burst_issue_x(rb, dummy, wb, lane);
             __builtin_amdgcn_sched_barrier(0);
             if (!__any(ra.ok))
                 break;
             xpose_burst(wa);
+            if (cm)
+                commit_take(ra, wa);
             if (ra.ok)
                 burst_hash(d, ra, wa, L, lo, c_lo, c_hi);
             i += nthr;
-            burst_meta<FIXED>(d, list, direct, count, i + nthr, lo, ra);
+            burst_meta<FIXED, true>(d, list, direct, count, i + nthr, lo, ra);
+            if (cm)
+                commit_words(ra, lane);
             burst_issue_x(ra, dummy, wa, lane);
             __builtin_amdgcn_sched_barrier(0);
             if (!__any(rb.ok))
                 break;
             xpose_burst(wb);
+            if (cm)
+                commit_take(rb, wb);
             if (rb.ok)
                 burst_hash(d, rb, wb, L, lo, c_lo, c_hi);
             i += nthr;
         }
         return;
     }
-    burst_meta<FIXED>(d, list, direct, count, i, lo, ra);
+    burst_meta<FIXED, false>(d, list, direct, count, i, lo, ra);
     burst_issue(ra, dummy, wa);
     for (;;) {
-        burst_meta<FIXED>(d, list, direct, count, i + nthr, lo, rb);
+        burst_meta<FIXED, false>(d, list, direct, count, i + nthr, lo, rb);
         burst_issue(rb, dummy, wb);
         __builtin_amdgcn_sched_barrier(0);
         if (!ra.ok)
             break;
         burst_hash(d, ra, wa, L, lo, c_lo, c_hi);
         i += nthr;
-        burst_meta<FIXED>(d, list, direct, count, i + nthr, lo, ra);
+        burst_meta<FIXED, false>(d, list, direct, count, i + nthr, lo, ra);
         burst_issue(ra, dummy, wa);
         __builtin_amdgcn_sched_barrier(0);
         if (!rb.ok)
