@@ -152,6 +152,11 @@ int zscrc_team_for(uint64_t len, uint64_t n);
  * fixed-stride records of at least min_len bytes (default 256 KiB): mode 0 =
  * off, 1 = on (default; env ZSCRC_XTEAM, ZSCRC_XTEAM_MIN) */
 void zscrc_set_xteam(int mode, uint64_t min_len);
+/* tuning bits (env ZSCRC_OPT), for A/B runs: 1 = hash five-piece record
+ * bursts as one chain instead of three; 2 = 64-byte record batches of
+ * zscrc_device_fixed_multi by the per-lane piece walk instead of coalesced
+ * chunks */
+void zscrc_set_opt(unsigned bits);
 /* the xteam mode the fixed-stride path uses for n packed records of len
  * bytes (0 = another kernel, or no device) */
 int zscrc_xteam_for(uint64_t len, uint64_t n);

@@ -476,3 +476,22 @@ def test_fixed_multi(gpu, stride, length, n, k):
         ref = oracle.batch(hosts[b], n=n, stride=stride, fixed_len=length, impl="hw",
                            seeds=np.full(n, ~7 & M32, np.uint32)) ^ np.uint32(M32)
         assert np.array_equal(u32(raws[b]), ref)
+
+
+@pytest.mark.parametrize("shift,n", [(0, 4099), (16, 1000), (48, 128), (3, 777), (0, 1)])
+def test_fixed_multi_64_offsets(gpu, shift, n):
+    """64-byte record batches at base offsets: 16-byte aligned bases take the
+    coalesced chunk kernel (multi64_kernel; ragged last chunks), others the
+    per-lane piece walk -- both against the oracle."""
+    k = 3
+    big = to_dev(rand_bytes(k * (64 * n + 64) + 64, n + shift), gpu)
+    bufs = [big[shift + b * (64 * n + 64):] for b in range(k)]
+    hosts = [b.cpu().numpy() for b in bufs]
+    for opt in (0, 2):
+        lib().zscrc_set_opt(opt)
+        try:
+            outs = zd.crc_fixed_multi(bufs, 64, 64, n, seed=0xC0C0)
+        finally:
+            lib().zscrc_set_opt(0)
+        for b in range(k):
+            assert np.array_equal(u32(outs[b]), _oracle_seeded(hosts[b], 64, 64, n, 0xC0C0)), (opt, b)

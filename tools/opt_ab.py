@@ -1,0 +1,61 @@
+"""Interleaved A/B of zscrc_set_opt bits on the config-4 verify and a
+fixed-stride 320-byte batch and config 2's 32 x 64 MiB multi-batch launch
+(median of 15 launches each, modes alternating
+launch by launch).  usage: python tools/opt_ab.py [bits ...] (default 0 1)"""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tools import zsdb_gen as zg  # noqa: E402
+from zeroskip_amd import device as zd  # noqa: E402
+from zeroskip_amd import zsfile  # noqa: E402
+from zeroskip_amd._lib import lib  # noqa: E402
+
+
+def main():
+    modes = [int(x) for x in sys.argv[1:]] or [0, 1]
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev)
+    g.manual_seed(7)
+    ppf = zg.pairs_per_file(True)
+    nfiles = -(-10_000_000 // ppf)
+    img = zg.log_files(bytes(range(16)), 0, nfiles, ppf, 0, True, g, dev).view(-1)
+    offs, lens = zg.log_spans(nfiles, ppf, True, True, dev)
+    mx = int(lens.max().item())
+    fx = torch.randint(0, 256, (320 * 10_000_000,), dtype=torch.uint8, device=dev, generator=g)
+    bufs = torch.randint(0, 256, (32, 64 << 20), dtype=torch.uint8, device=dev, generator=g)
+    blist = list(bufs)
+    cases = {"config4_verify": lambda: zsfile.verify_commits(img, offs, lens, max_len=mx),
+             "fixed_320x312": lambda: zd.crc_fixed(fx, 320, 312, 10_000_000),
+             "config2_multi32": lambda: torch.stack(zd.crc_fixed_multi(blist, 64, 64, 1 << 20))}
+    st = torch.cuda.current_stream()
+    for name, fn in cases.items():
+        ts = {m: [] for m in modes}
+        outs = {}
+        for i in range(17):
+            for m in modes:
+                lib().zscrc_set_opt(m)
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(st)
+                r = fn()
+                b.record(st)
+                torch.cuda.synchronize()
+                if i >= 2:
+                    ts[m].append(a.elapsed_time(b))
+                outs[m] = r
+        lib().zscrc_set_opt(0)
+        row = {"case": name}
+        for m in modes:
+            row[f"opt{m}_ms"] = round(sorted(ts[m])[len(ts[m]) // 2], 4)
+            o = outs[m] if isinstance(outs[m], torch.Tensor) else outs[m][0]
+            o0 = outs[modes[0]] if isinstance(outs[modes[0]], torch.Tensor) else outs[modes[0]][0]
+            if not torch.equal(o, o0):
+                row[f"opt{m}_MISMATCH"] = True
+        print(json.dumps(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()

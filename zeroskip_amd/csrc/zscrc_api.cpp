@@ -66,6 +66,8 @@ std::atomic<int> g_small_team{0};
  * per 4 GiB against 0.73-0.77 for team<64>; on 64 KiB records (config 3)
  * within -4..+8 % of team<16> from box to box, so team<16> keeps those) */
 std::atomic<int> g_xteam{1};
+/* tuning bits copied into every BatchDesc (zs::BatchDesc::opt; env ZSCRC_OPT) */
+std::atomic<uint32_t> g_opt{0};
 std::atomic<uint64_t> g_xteam_min{256u << 10};
 std::atomic<int> g_span_team{16}; /* team size on span segments (16 or 64; 16: 3 GiB 5.56 -> 5.71 TB/s) */
 int g_strict = 0;
@@ -127,6 +129,9 @@ void env_init()
     s = getenv("ZSCRC_XTEAM");
     if (s && atoi(s) >= 0 && atoi(s) <= 1)
         g_xteam = atoi(s);
+    s = getenv("ZSCRC_OPT");
+    if (s)
+        g_opt = (uint32_t)strtoul(s, nullptr, 0);
     s = getenv("ZSCRC_XTEAM_MIN");
     if (s)
         g_xteam_min = strtoull(s, nullptr, 0);
@@ -294,6 +299,7 @@ zs::BatchDesc make_desc()
     d.last_len = ~0ull;
     d.len_lo = 0;
     d.len_hi = ~0ull;
+    d.opt = g_opt;
     return d;
 }
 
@@ -934,6 +940,12 @@ int zscrc_xteam_for(uint64_t len, uint64_t n)
         return 0;
     return team_for(len, n, c->ncu, len, 0) == 64 && g_xteam && g_depth[2] < 0 && len >= g_xteam_min ? g_xteam.load()
                                                                                                         : 0;
+}
+
+void zscrc_set_opt(unsigned bits)
+{
+    std::call_once(g_env_once, env_init);
+    g_opt = bits;
 }
 
 void zscrc_set_teams(uint64_t g1_max, uint64_t g16_max)

@@ -59,6 +59,7 @@ struct BatchDesc {
      * record part_rec[p] covers bytes [(p - part_base[rec]) * unit, +unit);
      * raw part registers go to part_out[p], part_fold_kernel folds them */
     uint32_t split;
+    uint32_t opt;         /* tuning bits: 1 = no three-chain five-piece bursts, 2 = no multi64_kernel */
     uint32_t *part_out;
     const struct SplitPlan *plan;
     const uint32_t *part_base;

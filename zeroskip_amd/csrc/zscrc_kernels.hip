@@ -1375,6 +1375,90 @@ __global__ __launch_bounds__(WG) void multi_kernel(BatchDesc d, MultiBatch m, co
 }
 
 /*
+ * multi64_kernel: K batches of 64-byte records packed back to back (config
+ * 2), in chunks of 128 records (8 KiB) per wave.  A chunk's eight load
+ * instructions are fully coalesced non-temporal 1 KiB reads -- instruction i,
+ * lane (g, c): bytes [16g, 16g+16) of record 16i + c of the chunk -- and the
+ * row transpose of xteam_kernel (xpose16) hands lane j records j and 64 + j
+ * whole; the two records are hashed as two independent chains (every LDS
+ * lookup latency shared by two words).  The next chunk's loads are in
+ * flight while one is hashed (two register buffers, the loop unrolled twice).
+ * Loads past a batch's last record read its last 16 bytes (results not
+ * stored).
+ */
+__device__ __forceinline__ void m64_issue(const MultiBatch &m, uint64_t n, uint64_t cpb, uint64_t t, uint32_t voff,
+                                          uintptr_t dummy, uint32_t (&w)[32])
+{
+    const uint64_t b = t / cpb, k = t - b * cpb;
+    const bool ok = b < m.nb;
+    const uintptr_t base = ok ? reinterpret_cast<uintptr_t>(m.base[b < m.nb ? b : 0]) : dummy;
+    const uintptr_t sb = uni64(base + (ok ? k * 8192 : 0));
+    const uintptr_t last = uni64(base + (ok ? n * 64 - 16 : 0));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uintptr_t q = sb + (voff + 1024u * (uint32_t)i);
+        q = q > last ? last : q;
+        const u32x4 v = __builtin_nontemporal_load((g4p)q);
+        w[4 * i + 0] = v.x;
+        w[4 * i + 1] = v.y;
+        w[4 * i + 2] = v.z;
+        w[4 * i + 3] = v.w;
+    }
+}
+
+__global__ __launch_bounds__(WG) void multi64_kernel(BatchDesc d, MultiBatch m, const uint32_t *__restrict__ gtab)
+{
+    __shared__ __attribute__((aligned(16))) char L[OFF_U];
+    const uint64_t n = d.n;
+    const uint64_t cpb = (n + 127) / 128; /* chunks per batch */
+    const uint64_t items = cpb * m.nb;
+    const uint64_t wave = uni64((uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6));
+    const uint64_t nw = (uint64_t)gridDim.x * WAVES;
+    if ((uint64_t)blockIdx.x * WAVES >= items)
+        return;
+    fill_lds<1>(L, gtab);
+    __syncthreads();
+    const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+    const uint32_t c_lo = (uint32_t)(lane & 31) << 2;
+    const uint32_t c_hi = c_lo | 0x10000u;
+    const uint32_t voff = 64u * (uint32_t)c + 16u * (uint32_t)g;
+    const uintptr_t dummy = reinterpret_cast<uintptr_t>(gtab);
+    const uint32_t R0 = d.fixed_seed ^ d.xor_io;
+    uint32_t b0[32], b1[32];
+    uint64_t t = wave;
+    m64_issue(m, n, cpb, t, voff, dummy, b0);
+    auto hash = [&](uint32_t (&w)[32], uint64_t tt) {
+        xpose16(reinterpret_cast<uint32_t (&)[16]>(w[0]));
+        xpose16(reinterpret_cast<uint32_t (&)[16]>(w[16]));
+        w[0] ^= R0;
+        w[16] ^= R0;
+        uint32_t ra = 0, rb = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            ra = m4(L, ra ^ w[k], c_lo, c_hi);
+            rb = m4(L, rb ^ w[16 + k], c_lo, c_hi);
+        }
+        const uint64_t bb = tt / cpb, kk = tt - bb * cpb;
+        uint32_t *out = m.out[bb];
+        const uint64_t r = kk * 128 + (uint64_t)lane;
+        if (r < n)
+            out[r] = ra ^ d.xor_io;
+        if (r + 64 < n)
+            out[r + 64] = rb ^ d.xor_io;
+    };
+    while (t < items) {
+        m64_issue(m, n, cpb, t + nw, voff, dummy, b1);
+        hash(b0, t);
+        t += nw;
+        if (t >= items)
+            break;
+        m64_issue(m, n, cpb, t + nw, voff, dummy, b0);
+        hash(b1, t);
+        t += nw;
+    }
+}
+
+/*
  * burst_kernel: one lane per record of at most 5 pieces, all its pieces loaded
  * at once (a burst) and then hashed, so a line the record shares with the
  * neighbouring lane's record is requested by both lanes together and fetched
@@ -1584,7 +1668,53 @@ __device__ __forceinline__ void burst_hash(const BatchDesc &d, BRec &b, uint32_t
     }
     const uintptr_t V0 = b.V0;
     const uint32_t spill = A + 4 > V0 + 64 ? it.R0 >> (8 * (uint32_t)(V0 + 64 - A)) : 0u;
-    if (b.burst) {
+    if (NB == 5 && b.burst && b.np == 5 && !(d.opt & 1)) {
+        /* Five-piece records (zsbench's 312-byte spans): three independent
+         * chains -- pieces 0-1, 2-3 and 4 -- so every LDS lookup latency is
+         * shared by three words, joined by "shift 128 / 64 bytes" (Z1, Z0):
+         * shift(A, 192) ^ shift(B, 64) ^ C.  Piece 0's bytes before the record
+         * are zeroed in registers (leading zeros are free from a zero
+         * register), the initial register enters at A. */
+        constexpr int P1 = NB > 1 ? 1 : 0, P2 = NB > 2 ? 2 : 0, P3 = NB > 3 ? 3 : 0, P4 = NB > 4 ? 4 : 0;
+        w[P1][0] ^= spill;
+        const int32_t d0 = (int32_t)(A - V0); /* 0..63 */
+        if ((A & 3) == 0) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const int32_t dk = d0 - 4 * k;
+                w[0][k] = dk > 0 ? 0u : (dk == 0 ? w[0][k] ^ it.R0 : w[0][k]);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const int32_t dk = d0 - 4 * k;
+                uint32_t v = w[0][k];
+                if (dk >= 4)
+                    v = 0;
+                else if (dk > 0)
+                    v &= 0xffffffffu << (8 * dk);
+                if (dk >= 0 && dk < 4)
+                    v ^= it.R0 << (8 * dk);
+                else if (dk < 0 && dk > -4)
+                    v ^= it.R0 >> (8 * -dk);
+                w[0][k] = v;
+            }
+        }
+        uint32_t ra = 0, rb = 0, rc = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            ra = m4(L, ra ^ w[0][k], c_lo, c_hi);
+            rb = m4(L, rb ^ w[P2][k], c_lo, c_hi);
+            rc = m4(L, rc ^ w[P4][k], c_lo, c_hi);
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            ra = m4(L, ra ^ w[P1][k], c_lo, c_hi);
+            rb = m4(L, rb ^ w[P3][k], c_lo, c_hi);
+        }
+        r = op4(L, OFF_U + 4096, ra) ^ rb; /* shift 128 */
+        r = op4(L, OFF_U, r) ^ rc;         /* shift 64 */
+    } else if (b.burst) {
         if (NB > 1)
             w[NB > 1 ? 1 : 0][0] ^= b.np > 1 ? spill : 0u; /* NB = 1: below */
         r = first_piece(L, it, V0, 0, w[0], c_lo, c_hi); /* V0 >= lo here */
@@ -1643,7 +1773,8 @@ __device__ __forceinline__ void burst_hash(const BatchDesc &d, BRec &b, uint32_t
 template <bool FIXED, bool XP, int NB>
 __global__ __launch_bounds__(NB == 1 ? 1024 : BWG) void burst_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
 {
-    __shared__ __attribute__((aligned(16))) char L[OFF_U];
+    /* slice tables; five-piece bursts: + Z0, Z1 (compact, shift 64 / 128) */
+    __shared__ __attribute__((aligned(16))) char L[NB == 5 ? OFF_U + 8192 : OFF_U];
     uint64_t count = d.n;
     const RecDesc *list = nullptr;
     if (!FIXED && d.class_count) { /* no classes: every record, caller's arrays */
@@ -1667,6 +1798,11 @@ __global__ __launch_bounds__(NB == 1 ? 1024 : BWG) void burst_kernel(BatchDesc d
             const int tj = (dw >> 14) * 2 + ((dw >> 5) & 1);
             const uint32_t v = gtab[GT_S4 + tj * 256 + e];
             L4[i] = make_uint4(v, v, v, v);
+        }
+        if (NB == 5) {
+            uint32_t *Z = reinterpret_cast<uint32_t *>(L + OFF_U);
+            for (int i = threadIdx.x; i < 2048; i += T)
+                Z[i] = gtab[GT_Z + i];
         }
     }
     __syncthreads();
@@ -2287,7 +2423,15 @@ extern "C" int zs_launch_burst(int fixed, int xp, int nb, const zs::BatchDesc *d
 extern "C" int zs_launch_multi(const zs::BatchDesc *d, const zs::MultiBatch *m, const uint32_t *gtab, int grid,
                                hipStream_t stream)
 {
-    hipLaunchKernelGGL(zs::multi_kernel, dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
+    /* 64-byte records back to back from 16-byte aligned bases: coalesced
+     * chunks (multi64_kernel), unless tuning bit 2 asks for the piece walk */
+    bool packed64 = d->fixed_len == 64 && d->stride == 64 && !(d->opt & 2);
+    for (uint32_t b = 0; b < m->nb && packed64; ++b)
+        packed64 = (reinterpret_cast<uintptr_t>(m->base[b]) & 15) == 0;
+    if (packed64)
+        hipLaunchKernelGGL(zs::multi64_kernel, dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
+    else
+        hipLaunchKernelGGL(zs::multi_kernel, dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
