@@ -264,9 +264,7 @@ def run_config3(args, world, rank, dev, stream):
     if n_bad:
         raise SystemExit(f"config3: {n_bad} of {idx.size} sampled chunk CRCs differ from the oracle")
     read_peak = read_ceiling(data, NCHUNK * CHUNK, stream)
-    xt = lib().zscrc_xteam_for(CHUNK, NCHUNK)
-    kname = (f"zs::xteam_kernel<{xt}> (coalesced nt whole-wave teams)" if xt
-             else f"zs::team_kernel<{lib().zscrc_team_for(CHUNK, NCHUNK)}>")
+    kname = "zs::" + lib().zscrc_fixed_kernel(data.data_ptr(), CHUNK, CHUNK, NCHUNK).decode()
     r = roof(NCHUNK * CHUNK + NCHUNK * 4, kern_ms, kname,
              traffic_for("config3_bytes_per_launch"), read_peak)
     out_line = line(args, world, elapsed, NCHUNK * CHUNK * world * args.steps,

@@ -160,6 +160,9 @@ void zscrc_set_opt(unsigned bits);
 /* the xteam mode the fixed-stride path uses for n packed records of len
  * bytes (0 = another kernel, or no device) */
 int zscrc_xteam_for(uint64_t len, uint64_t n);
+/* name of the kernel zscrc_device_fixed launches for this batch shape
+ * (diagnostic; "none" if no device) */
+const char *zscrc_fixed_kernel(const void *d_base, uint64_t stride, uint64_t len, size_t n);
 /* Diagnostic: fully coalesced non-temporal streaming read of len bytes
  * (multiple of 4096) -- the measured HBM read ceiling on this GPU (grid =
  * grid_mult x CUs of 1024 threads).  d_scratch4: 4 writable device bytes. */
@@ -310,6 +313,8 @@ typedef struct zscrc_files_report {
     uint64_t first_bad_off;       /* its offset: commit record / walk stop / 0   */
     int32_t first_bad_what;       /* ZSCRC_FILES_BAD_*, 0 = none                 */
     int32_t threads;              /* host threads used                           */
+    int32_t staged;               /* 1: copies through pinned staging (ZSCRC_FILES_STAGE=1),
+                                   * 0: pageable H2D straight from the images    */
     double copy_s;                /* start of the pipeline -> last byte on the GPU */
     double verify_tail_s;         /* last byte on the GPU -> every verdict back  */
     double total_s;               /* the whole call                              */

@@ -274,23 +274,21 @@ def test_scalar_offload(gpu):
     assert after[0] - before[0] == 1   # the 37-byte call stayed on the CPU
 
 
-@pytest.mark.parametrize("xteam", [0, 1], ids=["team16", "xteam"])
-def test_config3_headline_dispatch(gpu, xteam):
+@pytest.mark.parametrize("mode", ["team16", "xteam"])
+def test_config3_headline_dispatch(gpu, mode):
     """BASELINE config 3 at full size through the exact call bench.py times:
     zscrc_device_fixed on 65,536 x 64 KiB chunks (4 GiB), seed 0, flags 0 --
     by default the 16-lane team walk (team_kernel<16>) with xor_io = ~0; also
     the coalesced whole-wave teams (xteam_kernel) forced on -- every CRC
     against the oracle."""
     n, L = 65536, 65536
-    lib().zscrc_set_xteam(xteam, 32768 if xteam else 256 << 10)
+    g = torch.Generator(device=gpu)
+    g.manual_seed(0x9E3779B9)
+    d = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=gpu, generator=g)
+    lib().zscrc_set_xteam(1, 32768 if mode == "xteam" else 256 << 10)
     try:
-        if xteam:
-            assert lib().zscrc_team_for(L, n) == 64 and lib().zscrc_xteam_for(L, n) == xteam
-        else:
-            assert lib().zscrc_team_for(L, n) == 16 and lib().zscrc_xteam_for(L, n) == 0
-        g = torch.Generator(device=gpu)
-        g.manual_seed(0x9E3779B9)
-        d = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=gpu, generator=g)
+        name = lib().zscrc_fixed_kernel(d.data_ptr(), L, L, n).decode()
+        assert name == {"team16": "team_kernel<16>", "xteam": "xteam_kernel"}[mode]
         out = torch.empty(n, dtype=torch.int32, device=gpu)
         from zeroskip_amd._lib import check
         check(lib().zscrc_device_fixed(d.data_ptr(), L, L, 0, out.data_ptr(), n, 0,

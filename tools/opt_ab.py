@@ -26,13 +26,21 @@ def main():
     offs, lens = zg.log_spans(nfiles, ppf, True, True, dev)
     mx = int(lens.max().item())
     fx = torch.randint(0, 256, (320 * 10_000_000,), dtype=torch.uint8, device=dev, generator=g)
+    only = os.environ.get("AB_CASES")
     bufs = torch.randint(0, 256, (32, 64 << 20), dtype=torch.uint8, device=dev, generator=g)
     blist = list(bufs)
-    cases = {"config4_verify": lambda: zsfile.verify_commits(img, offs, lens, max_len=mx),
+    c3 = torch.randint(0, 256, (4 << 30,), dtype=torch.uint8, device=dev, generator=g)
+    cases = {"config3": lambda: zd.crc_fixed(c3, 65536, 65536, 65536),
+             "fixed_16KiB": lambda: zd.crc_fixed(c3, 16384, 16384, 262144),
+             "fixed_4KiB": lambda: zd.crc_fixed(c3, 4096, 4096, 1 << 20),
+             "fixed_1MiB": lambda: zd.crc_fixed(c3, 1 << 20, 1 << 20, 4096),
+             "config4_verify": lambda: zsfile.verify_commits(img, offs, lens, max_len=mx),
              "fixed_320x312": lambda: zd.crc_fixed(fx, 320, 312, 10_000_000),
              "config2_multi32": lambda: torch.stack(zd.crc_fixed_multi(blist, 64, 64, 1 << 20))}
     st = torch.cuda.current_stream()
     for name, fn in cases.items():
+        if only and name not in only.split(","):
+            continue
         ts = {m: [] for m in modes}
         outs = {}
         for i in range(17):

@@ -41,6 +41,7 @@ SIGNATURES = {
     "zscrc_set_xteam": (None, [_int, _u64]),
     "zscrc_xteam_for": (_int, [_u64, _u64]),
     "zscrc_set_opt": (None, [ctypes.c_uint]),
+    "zscrc_fixed_kernel": (ctypes.c_char_p, [_vp, _u64, _u64, _sz]),
     "zscrc_set_prefetch": (None, [_int, _int]),
     "zscrc_diag_stream_read": (_int, [_vp, _u64, _vp, _int, _vp]),
     "zscrc_device_count": (_int, []),

@@ -933,6 +933,24 @@ void zscrc_set_xteam(int mode, uint64_t min_len)
     g_xteam_min = min_len;
 }
 
+const char *zscrc_fixed_kernel(const void *d_base, uint64_t stride, uint64_t len, size_t n)
+{
+    DevCtx *c;
+    if (get_ctx(&c))
+        return "none";
+    zs::BatchDesc d = make_desc();
+    d.base = static_cast<const uint8_t *>(d_base);
+    d.stride = stride;
+    d.fixed_len = len;
+    d.n = n;
+    const int g = team_for(len, n, c->ncu, stride, reinterpret_cast<uintptr_t>(d_base));
+    if (g == 64 && g_xteam && g_depth[2] < 0 && len >= g_xteam_min)
+        return "xteam_kernel";
+    static const char *names[] = {"team_kernel<1>/short_kernel/burst_kernel", "team_kernel<2>",
+                                  "team_kernel<16>", "team_kernel<64>"};
+    return names[g == 1 ? 0 : g == 2 ? 1 : g == 16 ? 2 : 3];
+}
+
 int zscrc_xteam_for(uint64_t len, uint64_t n)
 {
     DevCtx *c;

@@ -138,7 +138,7 @@ class FilesReport(ctypes.Structure):
                 ("bad_commits", ctypes.c_uint64), ("stale_empty_commits", ctypes.c_uint64),
                 ("header_errors", ctypes.c_uint64), ("walk_errors", ctypes.c_uint64),
                 ("first_bad_file", ctypes.c_uint64), ("first_bad_off", ctypes.c_uint64),
-                ("first_bad_what", ctypes.c_int32), ("threads", ctypes.c_int32),
+                ("first_bad_what", ctypes.c_int32), ("threads", ctypes.c_int32), ("staged", ctypes.c_int32),
                 ("copy_s", ctypes.c_double), ("verify_tail_s", ctypes.c_double), ("total_s", ctypes.c_double)]
 
     def as_dict(self):
