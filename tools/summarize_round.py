@@ -15,6 +15,7 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+UNITS = {"config2": 32}  # tools/prof_case.py config2: one pass = one 32-batch launch
 
 
 def newest(d, pat):
@@ -56,8 +57,10 @@ def main():
             k = r["Kernel_Name"].split("(")[0]
             per_kernel.setdefault(k, []).append(d)
         dom = max(per_kernel, key=lambda k: sum(per_kernel[k])) if per_kernel else None
+        units = UNITS.get(cfg, 1)  # bench.py steps per pass
         summ = {
             "passes": reps,
+            "bench_steps_per_pass": units,
             "kernel_ns_per_pass": sum(sum(v) for v in per_kernel.values()) / reps,
             "dominant_kernel": dom,
             "dominant_avg_ns": sum(per_kernel[dom]) / len(per_kernel[dom]) if dom else None,
@@ -72,7 +75,7 @@ def main():
         if "fetch_kb_per_pass" in summ and "write_kb_per_pass" in summ:
             summ["hbm_bytes_per_pass"] = int(summ["fetch_kb_per_pass"] * 1024 * 2
                                              + summ["write_kb_per_pass"] * 1024)
-            traffic[f"{cfg}_bytes_per_launch"] = summ["hbm_bytes_per_pass"]
+            traffic[f"{cfg}_bytes_per_launch"] = summ["hbm_bytes_per_pass"] // units
         out[cfg] = summ
     b = newest(os.path.join(src, "bench_trace"), "*kernel_stats.csv")
     if b:
