@@ -465,17 +465,23 @@ def run_config4(args, world, rank, dev, stream):
             img.copy_(src, non_blocking=True)
             torch.cuda.synchronize()
             e2e[f"h2d_{kind}_GBs"] = round(img.numel() / (time.perf_counter() - t0) / 1e9, 2)
-        hn = pinned.numpy()
-        from concurrent.futures import ThreadPoolExecutor
-        for threads in (1, 16):
+        # the real pipeline: zscrc_zs_verify_files over the host file images
+        # (threaded walks + pinned staging + overlapped H2D + one verify)
+        images = list(host.numpy().reshape(nfiles, -1))
+        kinds = [zsfile.FINALISED] * nfiles
+        zsfile.verify_files(images, kinds)                 # warm: pinned slots, device buffers
+        best = None
+        for _ in range(3):
             t0 = time.perf_counter()
-            with ThreadPoolExecutor(threads) as ex:
-                walked = sum(len(w[0]) for w in ex.map(zsfile.walk, list(hn)))
-            e2e[f"host_walk_{threads}t_s"] = round(time.perf_counter() - t0, 4)
-        assert walked == ncommit
-        total_s = img.numel() / (e2e["h2d_pinned_GBs"] * 1e9) + e2e["host_walk_16t_s"] + kern_ms * 1e-3
-        e2e["e2e_verify_pinned_walk16_GBs"] = round(img.numel() / total_s / 1e9, 2)
-        e2e["note"] = "the walk and the H2D copy can overlap per file; summed here"
+            rep = zsfile.verify_files(images, kinds)
+            dt = time.perf_counter() - t0
+            best = dt if best is None or dt < best else best
+        assert rep["commits"] == ncommit and rep["bad_commits"] == 0, rep
+        e2e["verify_files_s"] = round(best, 4)
+        e2e["verify_files_GBs"] = round(host.numel() / best / 1e9, 2)
+        e2e["note"] = ("host file images -> verdicts, walks included (zscrc_zs_verify_files, "
+                       f"{rep['threads']} host threads); PCIe-bound, never the line's value")
+        del images, pinned
 
     nbytes = span_bytes + 8 * ncommit + 16 * ncommit + 8 * ncommit   # spans + trailers + descriptors + crc/status
     r = roof(nbytes, kern_ms, "verify_commits, spans bounded by the walk: one zs::burst_kernel launch (312 B spans)",

@@ -59,15 +59,21 @@ def _expected(imgs, kinds):
     return commits, bad, stale
 
 
-@pytest.mark.parametrize("slot", [None, 1 << 20, 4 << 20])
-def test_clean_db_end_to_end(gpu, slot):
+@pytest.mark.parametrize("slot,stage", [(None, "1"), (1 << 20, "1"), (4 << 20, "1"), (None, "0")],
+                         ids=["staged-64M", "staged-1M", "staged-4M", "pageable"])
+def test_clean_db_end_to_end(gpu, slot, stage):
+    """staged (pinned slots, walks queued after each slot's copies) and
+    pageable direct copies"""
     imgs, kinds = _db(1)
     if slot:
         os.environ["ZSCRC_FILES_SLOT"] = str(slot)
+    os.environ["ZSCRC_FILES_STAGE"] = stage
     try:
         rep = zsfile.verify_files(imgs, kinds, threads=6)
     finally:
         os.environ.pop("ZSCRC_FILES_SLOT", None)
+        os.environ.pop("ZSCRC_FILES_STAGE", None)
+    assert rep["staged"] == int(stage)
     commits, bad, stale = _expected(imgs, kinds)
     assert bad == 0 and stale >= 3
     assert rep["commits"] == commits and rep["bad_commits"] == 0 and rep["stale_empty_commits"] == stale
@@ -75,8 +81,10 @@ def test_clean_db_end_to_end(gpu, slot):
     assert rep["bytes"] == sum(im.nbytes for im in imgs) and rep["files"] == len(imgs)
 
 
-def test_corruptions_located(gpu):
+@pytest.mark.parametrize("stage", ["1", "0"], ids=["staged", "pageable"])
+def test_corruptions_located(gpu, stage):
     imgs, kinds = _db(2, nfiles=25)
+    os.environ["ZSCRC_FILES_STAGE"] = stage
     # a payload byte of commit 3 of file 11, a header byte of file 4, a packed records byte
     c = zf.walk(imgs[11].tobytes())[0][3]
     imgs[11][c["span_off"] + 9] ^= 0x20
@@ -93,6 +101,7 @@ def test_corruptions_located(gpu):
     # a truncated file: the walk stops
     imgs2 = [imgs[0], imgs[1][:-3]]
     rep2 = zsfile.verify_files(imgs2, kinds[:2])
+    os.environ.pop("ZSCRC_FILES_STAGE", None)
     assert rep2["walk_errors"] == 1 and rep2["first_bad_file"] == 1 and rep2["first_bad_what"] == 2
 
 
