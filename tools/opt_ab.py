@@ -36,7 +36,8 @@ def main():
              "fixed_1MiB": lambda: zd.crc_fixed(c3, 1 << 20, 1 << 20, 4096),
              "config4_verify": lambda: zsfile.verify_commits(img, offs, lens, max_len=mx),
              "fixed_320x312": lambda: zd.crc_fixed(fx, 320, 312, 10_000_000),
-             "config2_multi32": lambda: torch.stack(zd.crc_fixed_multi(blist, 64, 64, 1 << 20))}
+             "config2_multi32": lambda: torch.stack(zd.crc_fixed_multi(blist, 64, 64, 1 << 20)),
+             "config2_warm32": lambda: torch.stack(zd.crc_fixed_multi([blist[0]] * 32, 64, 64, 1 << 20))}
     st = torch.cuda.current_stream()
     for name, fn in cases.items():
         if only and name not in only.split(","):

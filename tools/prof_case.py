@@ -25,11 +25,11 @@ def main():
         out = torch.empty(65536, dtype=torch.int32, device=dev)
         run = lambda k: zd.crc_fixed(data, 65536, 65536, 65536, out=out)  # noqa: E731
     elif cfg == "config2":
-        # one pass = one zscrc_device_fixed_multi launch over 32 batches of
-        # 1M x 64 B (bench.py's step unit is one batch: summarize divides by 32)
-        bufs = torch.randint(0, 256, (32, 64 << 20), dtype=torch.uint8, device=dev, generator=g)
+        # one pass = one zscrc_device_fixed_multi launch over 64 batches of
+        # 1M x 64 B (bench.py's step unit is one batch: summarize divides by 64)
+        bufs = torch.randint(0, 256, (64, 64 << 20), dtype=torch.uint8, device=dev, generator=g)
         blist = list(bufs)
-        outs = [torch.empty(1 << 20, dtype=torch.int32, device=dev) for _ in range(32)]
+        outs = [torch.empty(1 << 20, dtype=torch.int32, device=dev) for _ in range(64)]
         run = lambda k: zd.crc_fixed_multi(blist, 64, 64, 1 << 20, outs=outs)  # noqa: E731
     elif cfg == "config4":
         from tools import zsdb_gen as zg

@@ -15,7 +15,7 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-UNITS = {"config2": 32}  # tools/prof_case.py config2: one pass = one 32-batch launch
+UNITS = {"config2": 64}  # tools/prof_case.py config2: one pass = one 64-batch launch
 
 
 def newest(d, pat):

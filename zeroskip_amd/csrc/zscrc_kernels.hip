@@ -1386,16 +1386,18 @@ __global__ __launch_bounds__(WG) void multi_kernel(BatchDesc d, MultiBatch m, co
  * Loads past a batch's last record read its last 16 bytes (results not
  * stored).
  */
+template <int K>
 __device__ __forceinline__ void m64_issue(const MultiBatch &m, uint64_t n, uint64_t cpb, uint64_t t, uint32_t voff,
-                                          uintptr_t dummy, uint32_t (&w)[32])
+                                          uintptr_t dummy, uint32_t (&w)[16 * K])
 {
+    constexpr uint64_t CHUNK = 4096ull * K;
     const uint64_t b = t / cpb, k = t - b * cpb;
     const bool ok = b < m.nb;
     const uintptr_t base = ok ? reinterpret_cast<uintptr_t>(m.base[b < m.nb ? b : 0]) : dummy;
-    const uintptr_t sb = uni64(base + (ok ? k * 8192 : 0));
+    const uintptr_t sb = uni64(base + (ok ? k * CHUNK : 0));
     const uintptr_t last = uni64(base + (ok ? n * 64 - 16 : 0));
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < 4 * K; ++i) {
         uintptr_t q = sb + (voff + 1024u * (uint32_t)i);
         q = q > last ? last : q;
         const u32x4 v = __builtin_nontemporal_load((g4p)q);
@@ -1406,11 +1408,15 @@ __device__ __forceinline__ void m64_issue(const MultiBatch &m, uint64_t n, uint6
     }
 }
 
+/* K = records per lane per chunk (independent chains); K = 3 measured slower
+ * than 2 (128 VGPRs with spills, profiles/r02/opt_ab.jsonl) */
+template <int K>
 __global__ __launch_bounds__(WG) void multi64_kernel(BatchDesc d, MultiBatch m, const uint32_t *__restrict__ gtab)
 {
     __shared__ __attribute__((aligned(16))) char L[OFF_U];
+    constexpr uint64_t RPC = 64ull * K; /* records per chunk */
     const uint64_t n = d.n;
-    const uint64_t cpb = (n + 127) / 128; /* chunks per batch */
+    const uint64_t cpb = (n + RPC - 1) / RPC; /* chunks per batch */
     const uint64_t items = cpb * m.nb;
     const uint64_t wave = uni64((uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6));
     const uint64_t nw = (uint64_t)gridDim.x * WAVES;
@@ -1424,35 +1430,37 @@ __global__ __launch_bounds__(WG) void multi64_kernel(BatchDesc d, MultiBatch m, 
     const uint32_t voff = 64u * (uint32_t)c + 16u * (uint32_t)g;
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(gtab);
     const uint32_t R0 = d.fixed_seed ^ d.xor_io;
-    uint32_t b0[32], b1[32];
+    uint32_t b0[16 * K], b1[16 * K];
     uint64_t t = wave;
-    m64_issue(m, n, cpb, t, voff, dummy, b0);
-    auto hash = [&](uint32_t (&w)[32], uint64_t tt) {
-        xpose16(reinterpret_cast<uint32_t (&)[16]>(w[0]));
-        xpose16(reinterpret_cast<uint32_t (&)[16]>(w[16]));
-        w[0] ^= R0;
-        w[16] ^= R0;
-        uint32_t ra = 0, rb = 0;
+    m64_issue<K>(m, n, cpb, t, voff, dummy, b0);
+    auto hash = [&](uint32_t (&w)[16 * K], uint64_t tt) {
+        uint32_t r[K];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            ra = m4(L, ra ^ w[k], c_lo, c_hi);
-            rb = m4(L, rb ^ w[16 + k], c_lo, c_hi);
+        for (int q = 0; q < K; ++q) {
+            xpose16(reinterpret_cast<uint32_t (&)[16]>(w[16 * q]));
+            w[16 * q] ^= R0;
+            r[q] = 0;
         }
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+#pragma unroll
+            for (int q = 0; q < K; ++q)
+                r[q] = m4(L, r[q] ^ w[16 * q + k], c_lo, c_hi);
         const uint64_t bb = tt / cpb, kk = tt - bb * cpb;
         uint32_t *out = m.out[bb];
-        const uint64_t r = kk * 128 + (uint64_t)lane;
-        if (r < n)
-            out[r] = ra ^ d.xor_io;
-        if (r + 64 < n)
-            out[r + 64] = rb ^ d.xor_io;
+        const uint64_t r0 = kk * RPC + (uint64_t)lane;
+#pragma unroll
+        for (int q = 0; q < K; ++q)
+            if (r0 + 64 * q < n)
+                out[r0 + 64 * q] = r[q] ^ d.xor_io;
     };
     while (t < items) {
-        m64_issue(m, n, cpb, t + nw, voff, dummy, b1);
+        m64_issue<K>(m, n, cpb, t + nw, voff, dummy, b1);
         hash(b0, t);
         t += nw;
         if (t >= items)
             break;
-        m64_issue(m, n, cpb, t + nw, voff, dummy, b0);
+        m64_issue<K>(m, n, cpb, t + nw, voff, dummy, b0);
         hash(b1, t);
         t += nw;
     }
@@ -2428,8 +2436,8 @@ extern "C" int zs_launch_multi(const zs::BatchDesc *d, const zs::MultiBatch *m, 
     bool packed64 = d->fixed_len == 64 && d->stride == 64 && !(d->opt & 2);
     for (uint32_t b = 0; b < m->nb && packed64; ++b)
         packed64 = (reinterpret_cast<uintptr_t>(m->base[b]) & 15) == 0;
-    if (packed64)
-        hipLaunchKernelGGL(zs::multi64_kernel, dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
+    if (packed64) /* two chains per lane (three measured slower: VGPR spills) */
+        hipLaunchKernelGGL(zs::multi64_kernel<2>, dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
     else
         hipLaunchKernelGGL(zs::multi_kernel, dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
     return hipGetLastError() == hipSuccess ? 0 : -3;
