@@ -6,7 +6,8 @@ import os
 import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libzscrc.so")
+# ZSCRC_LIB_PATH: another build of the same ABI (A/B timing runs of two builds)
+LIB_PATH = os.environ.get("ZSCRC_LIB_PATH") or os.path.join(_HERE, "libzscrc.so")
 
 # library defaults of zscrc_set_teams(g1_max, g16_max) (zscrc_api.cpp g_g1_max, g_g16_max)
 DEFAULT_TEAMS = (640, 1 << 20)

@@ -69,6 +69,12 @@ __device__ __forceinline__ uint32_t lds32(const char *L, uint32_t addr)
 
 /* GF(2) product of two reflected residues mod P (bit 31 = x^0). */
 
+/* a ^ b ^ c in one VALU op: v_bitop3_b32 (gfx950) with the XOR truth table. */
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
 /* register x -> register after 4 zero bytes (= one slice-by-4 step on x). */
 __device__ __forceinline__ uint32_t m4(const char *L, uint32_t x, uint32_t c_lo, uint32_t c_hi)
 {
@@ -77,6 +83,24 @@ __device__ __forceinline__ uint32_t m4(const char *L, uint32_t x, uint32_t c_lo,
     const uint32_t a2 = __builtin_amdgcn_perm(x, c_hi, 0x0C020600u);
     const uint32_t a3 = __builtin_amdgcn_perm(x, c_hi, 0x0C020700u);
     return lds32(L, a0) ^ lds32(L, a1 + 128) ^ lds32(L, a2) ^ lds32(L, a3 + 128);
+}
+
+/* m4(x) ^ w.  B3: the four lookups and the data word folded by two
+ * v_bitop3_b32 (4 v_perm + 2 XOR ops per word instead of 4 + 4).  Same-box
+ * A/B of two builds (tools/lib_ab.sh, profiles/r02/bitop3_ab.jsonl):
+ * fixed-stride 312-byte bursts -5.5 %, config 2 chunks -2..-5 %, but the
+ * commit-batch bursts +3.5 % and team<16> +0.8 % (the chain then waits for
+ * two lookups at a time) -- so those keep the plain XOR chain. */
+template <bool B3>
+__device__ __forceinline__ uint32_t m4x(const char *L, uint32_t x, uint32_t w, uint32_t c_lo, uint32_t c_hi)
+{
+    if (!B3)
+        return m4(L, x, c_lo, c_hi) ^ w;
+    const uint32_t a0 = __builtin_amdgcn_perm(x, c_lo, 0x0C020400u);
+    const uint32_t a1 = __builtin_amdgcn_perm(x, c_lo, 0x0C020500u);
+    const uint32_t a2 = __builtin_amdgcn_perm(x, c_hi, 0x0C020600u);
+    const uint32_t a3 = __builtin_amdgcn_perm(x, c_hi, 0x0C020700u);
+    return xor3(xor3(lds32(L, a0), lds32(L, a1 + 128), w), lds32(L, a2), lds32(L, a3 + 128));
 }
 
 /* 4-lookup operator from a compact (non-replicated) 4 KiB table at `base`. */
@@ -1438,14 +1462,16 @@ __global__ __launch_bounds__(WG) void multi64_kernel(BatchDesc d, MultiBatch m, 
 #pragma unroll
         for (int q = 0; q < K; ++q) {
             xpose16(reinterpret_cast<uint32_t (&)[16]>(w[16 * q]));
-            w[16 * q] ^= R0;
-            r[q] = 0;
+            r[q] = w[16 * q] ^ R0; /* register before word k, XOR word k */
         }
 #pragma unroll
-        for (int k = 0; k < 16; ++k)
+        for (int k = 1; k < 16; ++k)
 #pragma unroll
             for (int q = 0; q < K; ++q)
-                r[q] = m4(L, r[q] ^ w[16 * q + k], c_lo, c_hi);
+                r[q] = m4x<true>(L, r[q], w[16 * q + k], c_lo, c_hi);
+#pragma unroll
+        for (int q = 0; q < K; ++q)
+            r[q] = m4(L, r[q], c_lo, c_hi);
         const uint64_t bb = tt / cpb, kk = tt - bb * cpb;
         uint32_t *out = m.out[bb];
         const uint64_t r0 = kk * RPC + (uint64_t)lane;
@@ -1658,7 +1684,8 @@ __device__ __forceinline__ void commit_take(BRec &b, const uint32_t (&w)[NB][16]
     }
 }
 
-template <int NB>
+/* FX: fixed-stride batch (the bitop3-folded chain measured faster there) */
+template <int NB, bool FX>
 __device__ __forceinline__ void burst_hash(const BatchDesc &d, BRec &b, uint32_t (&w)[NB][16], const char *L,
                                            uintptr_t lo, uint32_t c_lo, uint32_t c_hi)
 {
@@ -1708,18 +1735,23 @@ __device__ __forceinline__ void burst_hash(const BatchDesc &d, BRec &b, uint32_t
                 w[0][k] = v;
             }
         }
-        uint32_t ra = 0, rb = 0, rc = 0;
+        /* x = register before the word, XOR the word (m4x fuses the next one) */
+        uint32_t xa = w[0][0], xb = w[P2][0], xc = w[P4][0];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            ra = m4(L, ra ^ w[0][k], c_lo, c_hi);
-            rb = m4(L, rb ^ w[P2][k], c_lo, c_hi);
-            rc = m4(L, rc ^ w[P4][k], c_lo, c_hi);
+        for (int k = 1; k < 16; ++k) {
+            xa = m4x<FX>(L, xa, w[0][k], c_lo, c_hi);
+            xb = m4x<FX>(L, xb, w[P2][k], c_lo, c_hi);
+            xc = m4x<FX>(L, xc, w[P4][k], c_lo, c_hi);
         }
+        xa = m4x<FX>(L, xa, w[P1][0], c_lo, c_hi);
+        xb = m4x<FX>(L, xb, w[P3][0], c_lo, c_hi);
+        const uint32_t rc = m4(L, xc, c_lo, c_hi);
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            ra = m4(L, ra ^ w[P1][k], c_lo, c_hi);
-            rb = m4(L, rb ^ w[P3][k], c_lo, c_hi);
+        for (int k = 1; k < 16; ++k) {
+            xa = m4x<FX>(L, xa, w[P1][k], c_lo, c_hi);
+            xb = m4x<FX>(L, xb, w[P3][k], c_lo, c_hi);
         }
+        const uint32_t ra = m4(L, xa, c_lo, c_hi), rb = m4(L, xb, c_lo, c_hi);
         r = op4(L, OFF_U + 4096, ra) ^ rb; /* shift 128 */
         r = op4(L, OFF_U, r) ^ rc;         /* shift 64 */
     } else if (b.burst) {
@@ -1842,7 +1874,7 @@ __global__ __launch_bounds__(NB == 1 ? 1024 : BWG) void burst_kernel(BatchDesc d
             if (cm)
                 commit_take(ra, wa);
             if (ra.ok)
-                burst_hash(d, ra, wa, L, lo, c_lo, c_hi);
+                burst_hash<NB, FIXED>(d, ra, wa, L, lo, c_lo, c_hi);
             i += nthr;
             burst_meta<FIXED, true>(d, list, direct, count, i + nthr, lo, ra);
             if (cm)
@@ -1855,7 +1887,7 @@ __global__ __launch_bounds__(NB == 1 ? 1024 : BWG) void burst_kernel(BatchDesc d
             if (cm)
                 commit_take(rb, wb);
             if (rb.ok)
-                burst_hash(d, rb, wb, L, lo, c_lo, c_hi);
+                burst_hash<NB, FIXED>(d, rb, wb, L, lo, c_lo, c_hi);
             i += nthr;
         }
         return;
@@ -1868,14 +1900,14 @@ __global__ __launch_bounds__(NB == 1 ? 1024 : BWG) void burst_kernel(BatchDesc d
         __builtin_amdgcn_sched_barrier(0);
         if (!ra.ok)
             break;
-        burst_hash(d, ra, wa, L, lo, c_lo, c_hi);
+        burst_hash<NB, FIXED>(d, ra, wa, L, lo, c_lo, c_hi);
         i += nthr;
         burst_meta<FIXED, false>(d, list, direct, count, i + nthr, lo, ra);
         burst_issue(ra, dummy, wa);
         __builtin_amdgcn_sched_barrier(0);
         if (!rb.ok)
             break;
-        burst_hash(d, rb, wb, L, lo, c_lo, c_hi);
+        burst_hash<NB, FIXED>(d, rb, wb, L, lo, c_lo, c_hi);
         i += nthr;
     }
 }
