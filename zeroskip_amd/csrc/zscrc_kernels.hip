@@ -91,7 +91,20 @@ __device__ __forceinline__ uint32_t m4(const char *L, uint32_t x, uint32_t c_lo,
  * fixed-stride 312-byte bursts -5.5 %, config 2 chunks -2..-5 %, but the
  * commit-batch bursts +3.5 % and team<16> +0.8 % (the chain then waits for
  * two lookups at a time) -- so those keep the plain XOR chain. */
-template <bool B3>
+/* XOR3 grouping per kernel family (0 = plain chain, 1 = data word in the
+   first XOR3, 2 = data word in the last), each the fastest in interleaved
+   A/B (profiles/r02/bitop3_*.txt); piece() (team<G>, xteam, spans) keeps
+   the plain chain: both groupings measured level there. */
+#ifndef ZS_COMMIT_B3
+#define ZS_COMMIT_B3 2
+#endif
+#ifndef ZS_FIXED_B3
+#define ZS_FIXED_B3 1
+#endif
+#ifndef ZS_MULTI_B3
+#define ZS_MULTI_B3 1
+#endif
+template <int B3>
 __device__ __forceinline__ uint32_t m4x(const char *L, uint32_t x, uint32_t w, uint32_t c_lo, uint32_t c_hi)
 {
     if (!B3)
@@ -100,6 +113,8 @@ __device__ __forceinline__ uint32_t m4x(const char *L, uint32_t x, uint32_t w, u
     const uint32_t a1 = __builtin_amdgcn_perm(x, c_lo, 0x0C020500u);
     const uint32_t a2 = __builtin_amdgcn_perm(x, c_hi, 0x0C020600u);
     const uint32_t a3 = __builtin_amdgcn_perm(x, c_hi, 0x0C020700u);
+    if (B3 == 2) /* the last lookup and the data word in the final op */
+        return xor3(xor3(lds32(L, a0), lds32(L, a1 + 128), lds32(L, a2)), lds32(L, a3 + 128), w);
     return xor3(xor3(lds32(L, a0), lds32(L, a1 + 128), w), lds32(L, a2), lds32(L, a3 + 128));
 }
 
@@ -1468,7 +1483,7 @@ __global__ __launch_bounds__(WG) void multi64_kernel(BatchDesc d, MultiBatch m, 
         for (int k = 1; k < 16; ++k)
 #pragma unroll
             for (int q = 0; q < K; ++q)
-                r[q] = m4x<true>(L, r[q], w[16 * q + k], c_lo, c_hi);
+                r[q] = m4x<ZS_MULTI_B3>(L, r[q], w[16 * q + k], c_lo, c_hi);
 #pragma unroll
         for (int q = 0; q < K; ++q)
             r[q] = m4(L, r[q], c_lo, c_hi);
@@ -1739,17 +1754,17 @@ __device__ __forceinline__ void burst_hash(const BatchDesc &d, BRec &b, uint32_t
         uint32_t xa = w[0][0], xb = w[P2][0], xc = w[P4][0];
 #pragma unroll
         for (int k = 1; k < 16; ++k) {
-            xa = m4x<FX>(L, xa, w[0][k], c_lo, c_hi);
-            xb = m4x<FX>(L, xb, w[P2][k], c_lo, c_hi);
-            xc = m4x<FX>(L, xc, w[P4][k], c_lo, c_hi);
+            xa = m4x<FX ? ZS_FIXED_B3 : ZS_COMMIT_B3>(L, xa, w[0][k], c_lo, c_hi);
+            xb = m4x<FX ? ZS_FIXED_B3 : ZS_COMMIT_B3>(L, xb, w[P2][k], c_lo, c_hi);
+            xc = m4x<FX ? ZS_FIXED_B3 : ZS_COMMIT_B3>(L, xc, w[P4][k], c_lo, c_hi);
         }
-        xa = m4x<FX>(L, xa, w[P1][0], c_lo, c_hi);
-        xb = m4x<FX>(L, xb, w[P3][0], c_lo, c_hi);
+        xa = m4x<FX ? ZS_FIXED_B3 : ZS_COMMIT_B3>(L, xa, w[P1][0], c_lo, c_hi);
+        xb = m4x<FX ? ZS_FIXED_B3 : ZS_COMMIT_B3>(L, xb, w[P3][0], c_lo, c_hi);
         const uint32_t rc = m4(L, xc, c_lo, c_hi);
 #pragma unroll
         for (int k = 1; k < 16; ++k) {
-            xa = m4x<FX>(L, xa, w[P1][k], c_lo, c_hi);
-            xb = m4x<FX>(L, xb, w[P3][k], c_lo, c_hi);
+            xa = m4x<FX ? ZS_FIXED_B3 : ZS_COMMIT_B3>(L, xa, w[P1][k], c_lo, c_hi);
+            xb = m4x<FX ? ZS_FIXED_B3 : ZS_COMMIT_B3>(L, xb, w[P3][k], c_lo, c_hi);
         }
         const uint32_t ra = m4(L, xa, c_lo, c_hi), rb = m4(L, xb, c_lo, c_hi);
         r = op4(L, OFF_U + 4096, ra) ^ rb; /* shift 128 */
