@@ -13,7 +13,7 @@ from oracle import oracle
 from tests.golden.datagen import xorshift64_bytes
 from zeroskip_amd import device as zd
 from zeroskip_amd import crc32c as zc
-from zeroskip_amd._lib import DEFAULT_TEAMS, lib, stats
+from zeroskip_amd._lib import DEFAULT_TEAMS, QTEAM_DEFAULT, lib, stats
 
 pytestmark = pytest.mark.gpu
 
@@ -274,7 +274,7 @@ def test_scalar_offload(gpu):
     assert after[0] - before[0] == 1   # the 37-byte call stayed on the CPU
 
 
-@pytest.mark.parametrize("mode", ["team16", "xteam"])
+@pytest.mark.parametrize("mode", ["team16", "xteam", "qteam"])
 def test_config3_headline_dispatch(gpu, mode):
     """BASELINE config 3 at full size through the exact call bench.py times:
     zscrc_device_fixed on 65,536 x 64 KiB chunks (4 GiB), seed 0, flags 0 --
@@ -286,9 +286,10 @@ def test_config3_headline_dispatch(gpu, mode):
     g.manual_seed(0x9E3779B9)
     d = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=gpu, generator=g)
     lib().zscrc_set_xteam(1, 32768 if mode == "xteam" else 256 << 10)
+    lib().zscrc_set_qteam(1 if mode == "qteam" else 0)
     try:
         name = lib().zscrc_fixed_kernel(d.data_ptr(), L, L, n).decode()
-        assert name == {"team16": "team_kernel<16>", "xteam": "xteam_kernel"}[mode]
+        assert name == {"team16": "team_kernel<16>", "xteam": "xteam_kernel", "qteam": "qteam_kernel"}[mode]
         out = torch.empty(n, dtype=torch.int32, device=gpu)
         from zeroskip_amd._lib import check
         check(lib().zscrc_device_fixed(d.data_ptr(), L, L, 0, out.data_ptr(), n, 0,
@@ -298,6 +299,7 @@ def test_config3_headline_dispatch(gpu, mode):
         del d
     finally:
         lib().zscrc_set_xteam(1, 256 << 10)
+        lib().zscrc_set_qteam(QTEAM_DEFAULT)
     ref = oracle.batch(host, n=n, stride=L, fixed_len=L, impl="hw", threads=min(16, os.cpu_count() or 1))
     bad = np.nonzero(got != ref)[0]
     assert bad.size == 0, bad[:10]
@@ -327,6 +329,34 @@ def test_xteam_shapes(gpu):
     finally:
         lib().zscrc_set_xteam(1, 256 << 10)
         lib().zscrc_set_teams(*DEFAULT_TEAMS)
+
+
+def test_qteam_shapes(gpu):
+    """qteam_kernel (coalesced 16-lane column-quad teams) on ragged shapes of
+    equal-length records: a partial last group of four, unaligned bases (the
+    first record's front-padded step clamped at the buffer start), ragged
+    tails, gaps between records, seeds and raw registers -- every CRC against
+    the oracle; shapes it must not take (a different last length, stride
+    not a multiple of 4) go to team_kernel<16>."""
+    lib().zscrc_set_qteam(1)
+    try:
+        for stride, length, n, off in [(8192, 8192, 16385, 0), (8200, 8195, 16390, 1), (16384, 12000, 16387, 3),
+                                       (65540, 65537, 16385, 2), (12288, 9000, 16400, 0)]:
+            data = rand_bytes(stride * (n - 1) + length + off, stride + length + n)
+            dd = to_dev(data[off:], gpu)
+            assert lib().zscrc_fixed_kernel(dd.data_ptr(), stride, length, n).decode() == "qteam_kernel"
+            out = u32(zd.crc_fixed(dd, stride, length, n, seed=0xA5A5))
+            ref = _oracle_seeded(data[off:], stride, length, n, 0xA5A5)
+            bad = np.nonzero(out != ref)[0]
+            assert bad.size == 0, (stride, length, n, off, bad[:10])
+            raw = u32(zd.crc_fixed(dd, stride, length, n, seed=0x1234, raw=True))
+            want = (~oracle.crc32c_hw(~0x1234 & M32, data[off:off + length])) & M32
+            assert raw[0] == want, (stride, length, "raw")
+            del dd
+        d = torch.zeros(16, dtype=torch.uint8, device=gpu)
+        assert lib().zscrc_fixed_kernel(d.data_ptr(), 8194, 8192, 16384).decode() == "team_kernel<16>"
+    finally:
+        lib().zscrc_set_qteam(QTEAM_DEFAULT)
 
 
 def test_config2_full_size_vs_oracle(gpu):

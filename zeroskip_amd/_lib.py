@@ -11,6 +11,7 @@ LIB_PATH = os.environ.get("ZSCRC_LIB_PATH") or os.path.join(_HERE, "libzscrc.so"
 
 # library defaults of zscrc_set_teams(g1_max, g16_max) (zscrc_api.cpp g_g1_max, g_g16_max)
 DEFAULT_TEAMS = (640, 1 << 20)
+QTEAM_DEFAULT = 0  # zscrc_api.cpp g_qteam
 
 _u32, _u64, _vp, _sz, _int = (ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p,
                               ctypes.c_size_t, ctypes.c_int)
@@ -42,6 +43,7 @@ SIGNATURES = {
     "zscrc_set_xteam": (None, [_int, _u64]),
     "zscrc_xteam_for": (_int, [_u64, _u64]),
     "zscrc_set_opt": (None, [ctypes.c_uint]),
+    "zscrc_set_qteam": (None, [_int]),
     "zscrc_fixed_kernel": (ctypes.c_char_p, [_vp, _u64, _u64, _sz]),
     "zscrc_set_prefetch": (None, [_int, _int]),
     "zscrc_diag_stream_read": (_int, [_vp, _u64, _vp, _int, _vp]),

@@ -69,6 +69,10 @@ std::atomic<int> g_xteam{1};
 /* tuning bits copied into every BatchDesc (zs::BatchDesc::opt; env ZSCRC_OPT) */
 std::atomic<uint32_t> g_opt{0};
 std::atomic<uint64_t> g_xteam_min{256u << 10};
+/* coalesced non-temporal 16-lane teams (qteam_kernel) in place of
+ * team_kernel<16>'s two-level walk on equal-length fixed-stride records of
+ * >= 8 KiB: 0 = off, 1 = on */
+std::atomic<int> g_qteam{0};
 std::atomic<int> g_span_team{16}; /* team size on span segments (16 or 64; 16: 3 GiB 5.56 -> 5.71 TB/s) */
 int g_strict = 0;
 /* record-walk override per team size (index 0/1/2 = G 1/16/64): -1 = automatic
@@ -132,6 +136,9 @@ void env_init()
     s = getenv("ZSCRC_OPT");
     if (s)
         g_opt = (uint32_t)strtoul(s, nullptr, 0);
+    s = getenv("ZSCRC_QTEAM");
+    if (s && atoi(s) >= 0 && atoi(s) <= 1)
+        g_qteam = atoi(s);
     s = getenv("ZSCRC_XTEAM_MIN");
     if (s)
         g_xteam_min = strtoull(s, nullptr, 0);
@@ -322,6 +329,14 @@ int walk_for(int g, int fixed, uint64_t len)
     return (g == 16 && len > 2048) ? 1 : 2;
 }
 
+/* qteam_kernel's preconditions: every record the same length (>= 8 KiB, the
+ * two-level walk's range) and 4-byte phase, lane offsets within 32 bits */
+bool qteam_fits(const zs::BatchDesc &d)
+{
+    return d.fixed_len >= 8192 && (d.last_len == ~0ull || d.last_len == d.fixed_len) && (d.stride & 3) == 0 &&
+           d.stride <= (1ull << 30);
+}
+
 int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s, int depth_hint = -1)
 {
     /* fixed-stride form when no per-record arrays are involved */
@@ -340,7 +355,10 @@ int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s, int depth_hi
                    : fixed && d.fixed_len <= 128 && d.last_len == ~0ull ? 2 : 5;
     const int xt = g_xteam;
     const bool xteam = g == 64 && fixed && xt && g_depth[2] < 0 && depth_hint < 0 && d.fixed_len >= g_xteam_min;
-    int rc = xteam       ? zs_launch_xteam(xt, &d, c->gtab, c->ncu, s)
+    const bool qteam = g == 16 && fixed && depth == 0 && g_qteam && g_depth[1] < 0 && depth_hint < 0 &&
+                       qteam_fits(d);
+    int rc = qteam       ? zs_launch_xteam(16, &d, c->gtab, c->ncu, s)
+             : xteam     ? zs_launch_xteam(xt, &d, c->gtab, c->ncu, s)
              : depth >= 9 ? zs_launch_burst(fixed, depth == 10, nb, &dx, c->gtab, c->ncu, s)
              : depth >= 3 ? zs_launch_short(fixed, depth - 3, &dx, c->gtab, c->ncu, s)
                         : zs_launch_team(g, fixed, depth, &d, c->gtab, c->ncu, s);
@@ -946,6 +964,8 @@ const char *zscrc_fixed_kernel(const void *d_base, uint64_t stride, uint64_t len
     const int g = team_for(len, n, c->ncu, stride, reinterpret_cast<uintptr_t>(d_base));
     if (g == 64 && g_xteam && g_depth[2] < 0 && len >= g_xteam_min)
         return "xteam_kernel";
+    if (g == 16 && g_qteam && g_depth[1] < 0 && walk_for(16, 1, len) == 0 && qteam_fits(d))
+        return "qteam_kernel";
     static const char *names[] = {"team_kernel<1>/short_kernel/burst_kernel", "team_kernel<2>",
                                   "team_kernel<16>", "team_kernel<64>"};
     return names[g == 1 ? 0 : g == 2 ? 1 : g == 16 ? 2 : 3];
@@ -958,6 +978,13 @@ int zscrc_xteam_for(uint64_t len, uint64_t n)
         return 0;
     return team_for(len, n, c->ncu, len, 0) == 64 && g_xteam && g_depth[2] < 0 && len >= g_xteam_min ? g_xteam.load()
                                                                                                         : 0;
+}
+
+void zscrc_set_qteam(int mode)
+{
+    std::call_once(g_env_once, env_init);
+    if (mode >= 0 && mode <= 1)
+        g_qteam = mode;
 }
 
 void zscrc_set_opt(unsigned bits)

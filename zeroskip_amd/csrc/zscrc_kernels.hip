@@ -1015,6 +1015,153 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, const uint32_t *__re
         d.out[first + (uint64_t)lane] = stash;
 }
 
+/* ------------------------------------------- coalesced 16-lane teams */
+/*
+ * qteam_kernel: fixed-stride batches of equal-length records of 8 KiB ..
+ * 1 MiB with >= 64 records per CU (config 3's 65,536 x 64 KiB chunks).
+ * team_kernel<16>'s hashing -- four records per wave, a team of 16 lanes per
+ * record, 1 KiB steps, lane j owns piece j of every step, "word then skip
+ * 15*64 bytes" (U16) on non-final pieces, a 4-level Z fold at the record end
+ * -- with xteam_kernel's loads.  The team is not 16 adjacent lanes but a
+ * column quad: lanes (g, 4t+h), g = row 0..3, h = 0..3, own piece j = 4g+h
+ * of record t of the wave's group of four.  Load instruction i, lane (g, c =
+ * 4t+h): bytes [256i + 64h + 16g, +16) of team t's step -- every team reads
+ * one contiguous 256-byte segment per instruction, each cache line consumed
+ * by the instruction that fetched it, so the loads can be non-temporal --
+ * and the row transpose of xteam (v_permlane32/16_swap: block i of lane
+ * (g, c) <-> block g of lane (i, c)) hands lane (g, c) bytes
+ * [256g + 64h, +64) = piece 4g+h.  tools/ceiling_probe.hip: this load shape
+ * ("teamq S1 nt") reads at 6.77-6.88 TB/s against 6.44-6.57 for team<16>'s
+ * per-lane 64-byte piece loads, which cannot be non-temporal (4.4 TB/s:
+ * each 16-byte load re-fetches a line L1 no longer holds).
+ * Groups of four consecutive records are strided over the waves; every
+ * record has the same length and 4-byte phase (stride % 4 == 0), so the
+ * whole wave walks one (group, step) loop in SGPRs: scalar step base + a
+ * 32-bit lane offset, the next step in flight while one is hashed.  Teams
+ * past the last record (a partial last group) load a dummy line and store
+ * nothing.
+ */
+__global__ __launch_bounds__(WG) void qteam_kernel(XDesc d, const uint32_t *__restrict__ gtab)
+{
+    __shared__ __attribute__((aligned(16))) char L[LDS_BYTES];
+    const uint64_t ngroups = (d.n + 3) / 4;
+    if ((uint64_t)blockIdx.x * WAVES >= ngroups)
+        return;
+    fill_lds<16>(L, gtab);
+    __syncthreads();
+    const int lane = threadIdx.x & 63, g = lane >> 4, t = (lane >> 2) & 3, h = lane & 3;
+    const int j = 4 * g + h; /* piece of the team's step */
+    const uint32_t c_lo = (uint32_t)(lane & 31) << 2;
+    const uint32_t c_hi = c_lo | 0x10000u;
+    const uint64_t wave = uni64((uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6));
+    const uint64_t nwaves = (uint64_t)gridDim.x * WAVES;
+    /* record geometry, the same for every record: span = E - A, S steps of
+     * 1 KiB ending at E, the grid starting pad bytes before A */
+    const uintptr_t base = reinterpret_cast<uintptr_t>(d.base);
+    const uint64_t len = d.fixed_len;
+    const uint64_t ph = base & 3;
+    const uint64_t span = ((ph + len) & ~uint64_t(3)) - ph;
+    const uint32_t S = (uint32_t)((span + 1023) / 1024);
+    const uint64_t pad = (uint64_t)S * 1024 - span;
+    const uint32_t tail = (uint32_t)(len - span);
+    const uint32_t R0 = d.seed ^ d.xor_io;
+    const uintptr_t dummy = reinterpret_cast<uintptr_t>(gtab);
+    const uintptr_t lo = base & ~uintptr_t(3);
+    const uint64_t gstride = 4 * d.stride;
+    /* lane offset of its 16-byte block in instruction 0 */
+    const uint32_t voff = (uint32_t)((uint64_t)t * d.stride) + 64u * (uint32_t)h + 16u * (uint32_t)g;
+
+    /* issue the four loads of step s of group k (wave-uniform k, s) */
+    auto issue = [&](uint64_t k, uint32_t s, uint32_t (&w)[16]) {
+        const bool any = k < ngroups;
+        const uintptr_t sb = uni64(any ? base + k * gstride + (uint64_t)s * 1024 - pad : dummy);
+        if (any && (sb < lo || 4 * k + 4 > d.n)) {
+            /* the buffer's first group with front padding, or a partial last
+             * group: per-lane clamped / dummy addresses */
+            const bool live = 4 * k + (uint64_t)t < d.n;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                uintptr_t q = sb + voff + 256u * (uint32_t)i;
+                q = !live ? dummy : q < lo ? lo : q;
+                const u32x4 v = __builtin_nontemporal_load((g4p)q);
+                w[4 * i + 0] = v.x;
+                w[4 * i + 1] = v.y;
+                w[4 * i + 2] = v.z;
+                w[4 * i + 3] = v.w;
+            }
+            return;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const u32x4 v = __builtin_nontemporal_load((g4p)(sb + (any ? voff + 256u * (uint32_t)i : 0u)));
+            w[4 * i + 0] = v.x;
+            w[4 * i + 1] = v.y;
+            w[4 * i + 2] = v.z;
+            w[4 * i + 3] = v.w;
+        }
+    };
+
+    uint64_t kL = wave; /* load cursor: one step ahead of the hashing */
+    uint32_t sL = 0;
+    uint64_t kH = wave; /* hashing cursor */
+    uint32_t sH = 0;
+    uint32_t acc = 0;
+    uint32_t b0[16], b1[16];
+    issue(kL, sL, b0);
+    auto advance_load = [&]() {
+        if (++sL == S) {
+            sL = 0;
+            kL += nwaves;
+        }
+    };
+    auto hash = [&](uint32_t (&w)[16]) {
+        xpose16(w);
+        const uint64_t rec = 4 * kH + (uint64_t)t;
+        const uintptr_t A = base + rec * d.stride;
+        /* the record start lies in step 0, or its first 4 bytes reach step 1 */
+        if (sH == 0 || (sH == 1 && pad > 1020)) {
+            XItem it;
+            it.A = A;
+            it.R0 = R0;
+            fix_piece(it, A - pad + (uint64_t)sH * 1024 + 64 * (uintptr_t)j, lo, w);
+        }
+        if (sH + 1 < S) {
+            acc = piece<true>(L, acc, w, c_lo, c_hi);
+            ++sH;
+            return;
+        }
+        acc = piece<false>(L, acc, w, c_lo, c_hi);
+        /* lane j's register sits (15-j)*64 bytes before E: fold the team
+         * (pieces j and j - 2^k are lanes 2^k apart for k < 2, rows apart
+         * above) */
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t sh = op4(L, OFF_Z + 4096u * k, acc);
+            const uint32_t other = __shfl(sh, lane - (k < 2 ? (1 << k) : (16 << (k - 2))));
+            acc ^= (j & (1 << k)) ? other : 0u;
+        }
+        if (j == 15 && rec < d.n) {
+            const g8p e = (g8p)(A + span);
+            for (uint32_t i = 0; i < tail; ++i)
+                acc = byte_step(L, acc, e[i], c_hi);
+            d.out[rec] = acc ^ d.xor_io;
+        }
+        acc = 0;
+        sH = 0;
+        kH += nwaves;
+    };
+    while (kH < ngroups) {
+        advance_load();
+        issue(kL, sL, b1);
+        hash(b0);
+        if (kH >= ngroups)
+            break;
+        advance_load();
+        issue(kL, sL, b0);
+        hash(b1);
+    }
+}
+
 /* ------------------------------------------------------ short records */
 /*
  * One lane per record, records <= g1_max bytes (zsbench's 312-byte commit
@@ -2426,8 +2573,10 @@ extern "C" int zs_launch_xteam(int depth, const zs::BatchDesc *bd, const uint32_
     x.seed = bd->fixed_seed;
     x.xor_io = bd->xor_io;
     const zs::XDesc *d = &x;
-    (void)depth;
-    hipLaunchKernelGGL(zs::xteam_kernel, dim3(grid), dim3(zs::WG), 0, stream, *d, gtab);
+    if (depth == 16) /* equal-length records, stride % 4 == 0 (host checks) */
+        hipLaunchKernelGGL(zs::qteam_kernel, dim3(grid), dim3(zs::WG), 0, stream, *d, gtab);
+    else
+        hipLaunchKernelGGL(zs::xteam_kernel, dim3(grid), dim3(zs::WG), 0, stream, *d, gtab);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
