@@ -85,12 +85,24 @@ def main():
         lines = [ln for ln in open(bl) if ln.startswith("{")]
         if lines:
             open(os.path.join(dst, "bench_config3.json"), "w").write(lines[-1])
-    json.dump(out, open(os.path.join(dst, "summary.json"), "w"), indent=1)
+    # merge into an existing summary: a run that profiled some configs only
+    # updates those
+    prev_path = os.path.join(dst, "summary.json")
+    if os.path.exists(prev_path):
+        prev = json.load(open(prev_path))
+        prev.update(out)
+        out = prev
+    json.dump(out, open(prev_path, "w"), indent=1)
+    tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if traffic and os.path.exists(tpath):
+        old = json.load(open(tpath))
+        old.update(traffic)
+        traffic = old
     if traffic:
         traffic["source"] = (f"profiles/{tag}/summary.json: rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in "
                              "separate passes over tools/prof_case.py, zs:: dispatches per pass, "
                              "FETCH_SIZE x2 (gfx950 wide-read correction)")
-        json.dump(traffic, open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1)
+        json.dump(traffic, open(tpath, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
 

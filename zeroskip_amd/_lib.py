@@ -11,7 +11,7 @@ LIB_PATH = os.environ.get("ZSCRC_LIB_PATH") or os.path.join(_HERE, "libzscrc.so"
 
 # library defaults of zscrc_set_teams(g1_max, g16_max) (zscrc_api.cpp g_g1_max, g_g16_max)
 DEFAULT_TEAMS = (640, 1 << 20)
-QTEAM_DEFAULT = 0  # zscrc_api.cpp g_qteam
+QTEAM_DEFAULT = 1  # zscrc_api.cpp g_qteam
 
 _u32, _u64, _vp, _sz, _int = (ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p,
                               ctypes.c_size_t, ctypes.c_int)

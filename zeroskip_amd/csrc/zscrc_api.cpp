@@ -72,7 +72,7 @@ std::atomic<uint64_t> g_xteam_min{256u << 10};
 /* coalesced non-temporal 16-lane teams (qteam_kernel) in place of
  * team_kernel<16>'s two-level walk on equal-length fixed-stride records of
  * >= 8 KiB: 0 = off, 1 = on */
-std::atomic<int> g_qteam{0};
+std::atomic<int> g_qteam{1};
 std::atomic<int> g_span_team{16}; /* team size on span segments (16 or 64; 16: 3 GiB 5.56 -> 5.71 TB/s) */
 int g_strict = 0;
 /* record-walk override per team size (index 0/1/2 = G 1/16/64): -1 = automatic

@@ -59,7 +59,9 @@ struct BatchDesc {
      * record part_rec[p] covers bytes [(p - part_base[rec]) * unit, +unit);
      * raw part registers go to part_out[p], part_fold_kernel folds them */
     uint32_t split;
-    uint32_t opt;         /* tuning bits: 1 = no three-chain five-piece bursts, 2 = no multi64_kernel */
+    uint32_t opt;         /* tuning bits: 1 = no three-chain five-piece bursts, 2 = no multi64_kernel,
+                             4 / 8 = qteam_kernel with XOR3 grouping 1 / 2,
+                             16 = team_kernel<16>'s two-level walk with XOR3 grouping 2 */
     uint32_t *part_out;
     const struct SplitPlan *plan;
     const uint32_t *part_base;

@@ -101,6 +101,9 @@ __device__ __forceinline__ uint32_t m4(const char *L, uint32_t x, uint32_t c_lo,
 #ifndef ZS_FIXED_B3
 #define ZS_FIXED_B3 1
 #endif
+#ifndef ZS_QTEAM_B3
+#define ZS_QTEAM_B3 2
+#endif
 #ifndef ZS_MULTI_B3
 #define ZS_MULTI_B3 1
 #endif
@@ -173,11 +176,21 @@ __device__ __forceinline__ uint32_t byte_step(const char *L, uint32_t r, uint32_
     return lds32(L, __builtin_amdgcn_perm(x, c_hi, 0x0C020400u) + 128) ^ (r >> 8);
 }
 
-/* 16 words of one piece; the last one optionally fused with the skip. */
-template <bool SKIP>
+/* 16 words of one piece; the last one optionally fused with the skip.
+ * B3: the chain as y = m4(y) ^ w with the data word inside the XOR3s (m4x). */
+template <bool SKIP, int B3 = 0>
 __device__ __forceinline__ uint32_t piece(const char *L, uint32_t acc, const uint32_t (&w)[16],
                                           uint32_t c_lo, uint32_t c_hi)
 {
+    if (B3) {
+        uint32_t y = acc ^ w[0];
+#pragma unroll
+        for (int k = 1; k < 16; ++k)
+            y = m4x<B3>(L, y, w[k], c_lo, c_hi);
+        if (SKIP)
+            return op4(L, OFF_U, y);
+        return m4(L, y, c_lo, c_hi);
+    }
 #pragma unroll
     for (int k = 0; k < 15; ++k)
         acc = m4(L, acc ^ w[k], c_lo, c_hi);
@@ -571,7 +584,7 @@ __device__ __forceinline__ void compute(const BatchDesc &d, const Cursor &c, uin
     }
 }
 
-template <int G, bool FIXED, int DEPTH>
+template <int G, bool FIXED, int DEPTH, int B3 = 0>
 __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d_in, const uint32_t *__restrict__ gtab)
 {
     BatchDesc d = d_in;
@@ -660,9 +673,9 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d_in, const uint32_t
                 issue<G>(cn, j, dummy, lo, ba);
             fixup<G>(cur, 0, j, lo, w);
             if (G > 1 && cur.S > 1)
-                acc = piece<true>(L, acc, w, c_lo, c_hi);
+                acc = piece<true, B3>(L, acc, w, c_lo, c_hi);
             else
-                acc = piece<false>(L, acc, w, c_lo, c_hi);
+                acc = piece<false, B3>(L, acc, w, c_lo, c_hi);
             const bool spill = j == 0 && cur.A + 4 > cur.V0 + STEP;
             const uint32_t spill_v = cur.R0 >> (8 * (uint32_t)((cur.V0 + STEP - cur.A) & 3));
             for (uint64_t s = 1; s + 1 < cur.S; ++s) {
@@ -672,7 +685,7 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d_in, const uint32_t
                 issue_plain(p + STEP, ba);
                 if (s == 1 && spill)
                     w[0] ^= spill_v;
-                acc = piece<G != 1>(L, acc, w, c_lo, c_hi);
+                acc = piece<G != 1, B3>(L, acc, w, c_lo, c_hi);
                 p += STEP;
             }
             if (cur.S > 1) {
@@ -682,7 +695,7 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d_in, const uint32_t
                 issue<G>(cn, j, dummy, lo, ba);
                 if (cur.S == 2 && spill)
                     w[0] ^= spill_v;
-                acc = piece<false>(L, acc, w, c_lo, c_hi);
+                acc = piece<false, B3>(L, acc, w, c_lo, c_hi);
             }
             const uint32_t r = finish<G>(cur, acc, j, lane, L, c_hi);
             if (j == G - 1)
@@ -1041,6 +1054,7 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, const uint32_t *__re
  * past the last record (a partial last group) load a dummy line and store
  * nothing.
  */
+template <int B3>
 __global__ __launch_bounds__(WG) void qteam_kernel(XDesc d, const uint32_t *__restrict__ gtab)
 {
     __shared__ __attribute__((aligned(16))) char L[LDS_BYTES];
@@ -1126,11 +1140,11 @@ __global__ __launch_bounds__(WG) void qteam_kernel(XDesc d, const uint32_t *__re
             fix_piece(it, A - pad + (uint64_t)sH * 1024 + 64 * (uintptr_t)j, lo, w);
         }
         if (sH + 1 < S) {
-            acc = piece<true>(L, acc, w, c_lo, c_hi);
+            acc = piece<true, B3>(L, acc, w, c_lo, c_hi);
             ++sH;
             return;
         }
-        acc = piece<false>(L, acc, w, c_lo, c_hi);
+        acc = piece<false, B3>(L, acc, w, c_lo, c_hi);
         /* lane j's register sits (15-j)*64 bytes before E: fold the team
          * (pieces j and j - 2^k are lanes 2^k apart for k < 2, rows apart
          * above) */
@@ -2540,6 +2554,8 @@ extern "C" int zs_launch_team(int g, int fixed, int depth, const zs::BatchDesc *
             ZS_LAUNCH(G, false, 0);                   \
         else                                          \
             ZS_LAUNCH(G, false, 1);                   \
+    } else if (depth == 0 && G == 16 && (d->opt & 16)) { \
+        hipLaunchKernelGGL((zs::team_kernel<16, true, 0, 2>), dim3(grid), dim3(zs::WG), 0, stream, *d, gtab); \
     } else if (depth == 0) {                          \
         ZS_LAUNCH(G, true, 0);                        \
     } else if (depth == 1) {                          \
@@ -2573,8 +2589,14 @@ extern "C" int zs_launch_xteam(int depth, const zs::BatchDesc *bd, const uint32_
     x.seed = bd->fixed_seed;
     x.xor_io = bd->xor_io;
     const zs::XDesc *d = &x;
-    if (depth == 16) /* equal-length records, stride % 4 == 0 (host checks) */
-        hipLaunchKernelGGL(zs::qteam_kernel, dim3(grid), dim3(zs::WG), 0, stream, *d, gtab);
+    /* equal-length records, stride % 4 == 0 (host checks); tuning bits 4 / 8
+     * pick the XOR3 groupings for A/B runs */
+    if (depth == 16 && (bd->opt & 4))
+        hipLaunchKernelGGL(zs::qteam_kernel<1>, dim3(grid), dim3(zs::WG), 0, stream, *d, gtab);
+    else if (depth == 16 && (bd->opt & 8))
+        hipLaunchKernelGGL(zs::qteam_kernel<2>, dim3(grid), dim3(zs::WG), 0, stream, *d, gtab);
+    else if (depth == 16)
+        hipLaunchKernelGGL(zs::qteam_kernel<ZS_QTEAM_B3>, dim3(grid), dim3(zs::WG), 0, stream, *d, gtab);
     else
         hipLaunchKernelGGL(zs::xteam_kernel, dim3(grid), dim3(zs::WG), 0, stream, *d, gtab);
     return hipGetLastError() == hipSuccess ? 0 : -3;
