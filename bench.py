@@ -341,6 +341,7 @@ def run_config2(args, world, rank, dev, stream):
                 ev[1].record(stream)
         return step
 
+    read_peak = read_ceiling(bufs.view(-1), bufs.numel(), stream)   # also settles power (run_config3)
     tm = Timer(world, dev)
     warm_el = tm.run(multi(warm_bufs), replays, max(1, args.warmup // rot + 1))
     warm_ms = float(np.median(tm.kern_ms)) / rot
@@ -358,7 +359,7 @@ def run_config2(args, world, rank, dev, stream):
     graph_ms = float(np.mean(tm_g.kern_ms)) / rot
     nbytes = n * rl + n * 4
     r = roof(nbytes, cold_ms, f"zs::multi64_kernel, {rot} batches of 1M x 64 B per launch",
-             traffic_for("config2_bytes_per_launch"), None)
+             traffic_for("config2_bytes_per_launch"), read_peak)
     r["note"] = f"kernel_ms = launch time / {rot} batches (the algorithmic bytes are per batch)"
     out_line = line(a2, world, elapsed, n * rl * world * steps,
                     {"workload": f"config2: 1,048,576 x 64 B records per GPU (64 MiB) per step; cold: {rot} "
@@ -420,6 +421,7 @@ def run_config4(args, world, rank, dev, stream):
         if ev:
             ev[1].record(stream)
 
+    read_peak = read_ceiling(flat, flat.numel(), stream)   # also settles power (run_config3)
     tm = Timer(world, dev)
     elapsed = tm.run(step, args.steps, args.warmup)
     kern_ms = float(np.mean(tm.kern_ms))
@@ -493,7 +495,7 @@ def run_config4(args, world, rank, dev, stream):
 
     nbytes = span_bytes + 8 * ncommit + 16 * ncommit + 8 * ncommit   # spans + trailers + descriptors + crc/status
     r = roof(nbytes, kern_ms, "verify_commits, spans bounded by the walk: one zs::burst_kernel launch (312 B spans)",
-             traffic_for("config4_bytes_per_launch"), None)
+             traffic_for("config4_bytes_per_launch"), read_peak)
     out_line = line(args, world, elapsed, span_bytes * world * args.steps,
                     {"workload": f"config4: zsbench writeseqtxn replay, {pairs_total} pairs per GPU, "
                                  f"{nfiles} log files, {ncommit} commits (312 B spans + stale finalise "
@@ -531,6 +533,9 @@ def run_config5(args, world, rank, dev, stream):
         rep = job.run(events=ev)
         step.rep = rep
 
+    probe = torch.empty(4 << 30, dtype=torch.uint8, device=dev)
+    read_peak = read_ceiling(probe, probe.numel(), stream)   # also settles power (run_config3)
+    del probe
     tm = Timer(world, dev)
     elapsed = tm.run(step, args.steps, args.warmup)
     rep = step.rep
@@ -542,7 +547,7 @@ def run_config5(args, world, rank, dev, stream):
     r = roof(nbytes, kern_ms, "verify_commits_bounded (one burst_kernel over the short commit spans) + "
                               "zscrc_device_span per records region / pointer section (xteam_kernel or "
                               "team<16> segments + span_fold), this rank",
-             traffic_for("config5_bytes_per_launch"), None)
+             traffic_for("config5_bytes_per_launch"), read_peak)
     out_line = line(args, world, elapsed, job.plan.weight * args.steps,
                     {"workload": f"config5: consistent over a {job.plan.weight / GIB:.2f} GiB DB "
                                  f"(2 packed x {args.packed_mib} MiB, {args.finalised} finalised, 1 active, "

@@ -64,6 +64,19 @@ def main():
     scratch = torch.zeros(4096, dtype=torch.int32, device=dev)
     check(lib().zscrc_diag_stream_read(scratch.data_ptr(), 8192, scratch.data_ptr(), 1,
                                        torch.cuda.current_stream().cuda_stream), "marker")
+    if os.environ.get("PC_TIME"):  # sustained-rate probe: ms per pass per block of 50 passes
+        import json
+        import time
+        blocks = []
+        for k0 in range(0, reps, 50):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for k in range(k0, min(reps, k0 + 50)):
+                run(k)
+            torch.cuda.synchronize()
+            blocks.append(round((time.perf_counter() - t0) * 1e3 / (min(reps, k0 + 50) - k0), 4))
+        print(json.dumps({"case": cfg, "reps": reps, "ms_per_pass_by_block50": blocks}), flush=True)
+        return
     for k in range(reps):
         run(k)
     torch.cuda.synchronize()
