@@ -1586,21 +1586,31 @@ __global__ __launch_bounds__(WG) void multi_kernel(BatchDesc d, MultiBatch m, co
  * Loads past a batch's last record read its last 16 bytes (results not
  * stored).
  */
+/* A chunk of the multi-batch walk: batch b, chunk k of it (wave-uniform).
+ * The walk advances by the grid's wave count without a 64-bit division per
+ * chunk (the divisions and per-load clamps were ~20 % of the kernel's VALU
+ * and most of its scalar issue). */
+struct M64Pos {
+    uint64_t b, k;
+};
+
 template <int K>
-__device__ __forceinline__ void m64_issue(const MultiBatch &m, uint64_t n, uint64_t cpb, uint64_t t, uint32_t voff,
+__device__ __forceinline__ void m64_issue(const MultiBatch &m, uint64_t n, const M64Pos &p, uint32_t voff,
                                           uintptr_t dummy, uint32_t (&w)[16 * K])
 {
     constexpr uint64_t CHUNK = 4096ull * K;
-    const uint64_t b = t / cpb, k = t - b * cpb;
-    const bool ok = b < m.nb;
-    const uintptr_t base = ok ? reinterpret_cast<uintptr_t>(m.base[b < m.nb ? b : 0]) : dummy;
-    const uintptr_t sb = uni64(base + (ok ? k * CHUNK : 0));
-    const uintptr_t last = uni64(base + (ok ? n * 64 - 16 : 0));
+    const bool ok = p.b < m.nb;
+    const uintptr_t base = ok ? reinterpret_cast<uintptr_t>(m.base[ok ? p.b : 0]) : dummy;
+    const uintptr_t sb = uni64(base + (ok ? p.k * CHUNK : 0));
+    /* loads past the batch's last record read its last 16 bytes: a scalar
+     * bound on the 32-bit lane offset, no branch (a branchy clamp made the
+     * compiler wait for the next chunk's loads before hashing this one) */
+    const uint64_t room = ok ? base + n * 64 - 16 - sb : 0;
+    const uint32_t lim = __builtin_amdgcn_readfirstlane((uint32_t)(room < 0xffffffffull ? room : 0xffffffffull));
 #pragma unroll
     for (int i = 0; i < 4 * K; ++i) {
-        uintptr_t q = sb + (voff + 1024u * (uint32_t)i);
-        q = q > last ? last : q;
-        const u32x4 v = __builtin_nontemporal_load((g4p)q);
+        const uint32_t o = voff + 1024u * (uint32_t)i;
+        const u32x4 v = __builtin_nontemporal_load((g4p)(sb + (o < lim ? o : lim)));
         w[4 * i + 0] = v.x;
         w[4 * i + 1] = v.y;
         w[4 * i + 2] = v.z;
@@ -1609,7 +1619,10 @@ __device__ __forceinline__ void m64_issue(const MultiBatch &m, uint64_t n, uint6
 }
 
 /* K = records per lane per chunk (independent chains); K = 3 measured slower
- * than 2 (128 VGPRs with spills, profiles/r02/opt_ab.jsonl) */
+ * than 2 (128 VGPRs with spills, profiles/r02/opt_ab.jsonl); a three-chunk
+ * register ring (123 VGPRs) measured level with two (0.524 vs 0.522 ms per
+ * 32 batches): the kernel hashes at ~4.7 TB/s from L3 as well, so the loads
+ * are not what holds it back */
 template <int K>
 __global__ __launch_bounds__(WG) void multi64_kernel(BatchDesc d, MultiBatch m, const uint32_t *__restrict__ gtab)
 {
@@ -1630,10 +1643,23 @@ __global__ __launch_bounds__(WG) void multi64_kernel(BatchDesc d, MultiBatch m, 
     const uint32_t voff = 64u * (uint32_t)c + 16u * (uint32_t)g;
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(gtab);
     const uint32_t R0 = d.fixed_seed ^ d.xor_io;
+    /* the walk's step in (batch, chunk) form, once */
+    const uint64_t step_b = nw / cpb, step_k = nw - step_b * cpb;
+    auto advance = [&](M64Pos &p) {
+        p.k += step_k;
+        p.b += step_b;
+        if (p.k >= cpb) {
+            p.k -= cpb;
+            ++p.b;
+        }
+    };
     uint32_t b0[16 * K], b1[16 * K];
-    uint64_t t = wave;
-    m64_issue<K>(m, n, cpb, t, voff, dummy, b0);
-    auto hash = [&](uint32_t (&w)[16 * K], uint64_t tt) {
+    M64Pos ph, pl; /* hashing / loading position, the load one chunk ahead */
+    ph.b = wave / cpb;
+    ph.k = wave - ph.b * cpb;
+    pl = ph;
+    m64_issue<K>(m, n, pl, voff, dummy, b0);
+    auto hash = [&](uint32_t (&w)[16 * K], const M64Pos &p) {
         uint32_t r[K];
 #pragma unroll
         for (int q = 0; q < K; ++q) {
@@ -1648,23 +1674,24 @@ __global__ __launch_bounds__(WG) void multi64_kernel(BatchDesc d, MultiBatch m, 
 #pragma unroll
         for (int q = 0; q < K; ++q)
             r[q] = m4(L, r[q], c_lo, c_hi);
-        const uint64_t bb = tt / cpb, kk = tt - bb * cpb;
-        uint32_t *out = m.out[bb];
-        const uint64_t r0 = kk * RPC + (uint64_t)lane;
+        uint32_t *out = m.out[p.b];
+        const uint64_t r0 = p.k * RPC + (uint64_t)lane;
 #pragma unroll
         for (int q = 0; q < K; ++q)
             if (r0 + 64 * q < n)
                 out[r0 + 64 * q] = r[q] ^ d.xor_io;
     };
-    while (t < items) {
-        m64_issue<K>(m, n, cpb, t + nw, voff, dummy, b1);
-        hash(b0, t);
-        t += nw;
-        if (t >= items)
+    while (ph.b < m.nb) {
+        advance(pl);
+        m64_issue<K>(m, n, pl, voff, dummy, b1);
+        hash(b0, ph);
+        advance(ph);
+        if (ph.b >= m.nb)
             break;
-        m64_issue<K>(m, n, cpb, t + nw, voff, dummy, b0);
-        hash(b1, t);
-        t += nw;
+        advance(pl);
+        m64_issue<K>(m, n, pl, voff, dummy, b0);
+        hash(b1, ph);
+        advance(ph);
     }
 }
 
