@@ -592,10 +592,18 @@ def main() -> None:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world != 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # BENCH_SHARE_GPU=1: rehearsal of the N-rank path on a box with fewer GPUs
+    # (ranks share devices round-robin; RCCL, or gloo with BENCH_DIST=gloo)
+    if os.environ.get("BENCH_SHARE_GPU") == "1":
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("BENCH_DIST", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     if lib().zscrc_device_count() < 1:
         raise SystemExit("libzscrc: no gfx950 device")
     stream = torch.cuda.current_stream(dev)
