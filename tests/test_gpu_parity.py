@@ -359,6 +359,30 @@ def test_qteam_shapes(gpu):
         lib().zscrc_set_qteam(QTEAM_DEFAULT)
 
 
+@pytest.mark.parametrize("qteam,opt", [(1, 4), (1, 8), (0, 16)], ids=["qteam-xor3-1", "qteam-xor3-2", "team16-xor3"])
+def test_xor3_variants(gpu, qteam, opt):
+    """The A/B variants of the 16-lane walks (zscrc_set_opt bits 4 / 8: qteam
+    XOR3 groupings; 16: team_kernel<16>'s two-level walk with XOR3) on
+    16,384 equal 8 KiB records and an unaligned ragged shape, every CRC
+    against the oracle."""
+    lib().zscrc_set_qteam(qteam)
+    lib().zscrc_set_opt(opt)
+    try:
+        for stride, length, n, off in [(8192, 8192, 16384, 0), (12292, 12290, 16390, 3)]:
+            data = rand_bytes(stride * (n - 1) + length + off, stride + n + opt)
+            dd = to_dev(data[off:], gpu)
+            name = lib().zscrc_fixed_kernel(dd.data_ptr(), stride, length, n).decode()
+            assert name == ("qteam_kernel" if qteam else "team_kernel<16>")
+            out = u32(zd.crc_fixed(dd, stride, length, n, seed=0x5A5A))
+            ref = _oracle_seeded(data[off:], stride, length, n, 0x5A5A)
+            bad = np.nonzero(out != ref)[0]
+            assert bad.size == 0, (stride, length, n, off, bad[:10])
+            del dd
+    finally:
+        lib().zscrc_set_opt(0)
+        lib().zscrc_set_qteam(QTEAM_DEFAULT)
+
+
 def test_config2_full_size_vs_oracle(gpu):
     # BASELINE config 2 at full size: 1,048,576 x 64 B records, every CRC checked
     n = 1 << 20
