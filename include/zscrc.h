@@ -153,7 +153,7 @@ int zscrc_team_for(uint64_t len, uint64_t n);
  * off, 1 = on (default; env ZSCRC_XTEAM, ZSCRC_XTEAM_MIN) */
 void zscrc_set_xteam(int mode, uint64_t min_len);
 /* tuning: coalesced non-temporal 16-lane teams (qteam_kernel) in place of
- * team_kernel<16> on equal-length fixed-stride records of >= 8 KiB (stride a
+ * team_kernel<16> on equal-length fixed-stride records of >= 2 KiB (stride a
  * multiple of 4): mode 0 = off, 1 = on (env ZSCRC_QTEAM) */
 void zscrc_set_qteam(int mode);
 /* tuning bits (env ZSCRC_OPT), for A/B runs: 1 = hash five-piece record

@@ -71,8 +71,12 @@ std::atomic<uint32_t> g_opt{0};
 std::atomic<uint64_t> g_xteam_min{256u << 10};
 /* coalesced non-temporal 16-lane teams (qteam_kernel) in place of
  * team_kernel<16>'s two-level walk on equal-length fixed-stride records of
- * >= 8 KiB: 0 = off, 1 = on */
+ * >= g_qteam_min bytes: 0 = off, 1 = on */
 std::atomic<int> g_qteam{1};
+/* qteam from 2 KiB records (tools/qteam_ab.py, profiles/r02/qteam_ab_small.jsonl:
+ * 2 KiB 0.789 vs 0.824 ms per 4 GiB, 4 KiB 0.665 vs 0.756, 8 KiB 0.661 vs
+ * 0.736; ~1 KiB loses, 1.53 vs 1.32); env ZSCRC_QTEAM_MIN */
+std::atomic<uint64_t> g_qteam_min{2048};
 std::atomic<int> g_span_team{16}; /* team size on span segments (16 or 64; 16: 3 GiB 5.56 -> 5.71 TB/s) */
 int g_strict = 0;
 /* record-walk override per team size (index 0/1/2 = G 1/16/64): -1 = automatic
@@ -136,6 +140,9 @@ void env_init()
     s = getenv("ZSCRC_OPT");
     if (s)
         g_opt = (uint32_t)strtoul(s, nullptr, 0);
+    s = getenv("ZSCRC_QTEAM_MIN");
+    if (s)
+        g_qteam_min = strtoull(s, nullptr, 0);
     s = getenv("ZSCRC_QTEAM");
     if (s && atoi(s) >= 0 && atoi(s) <= 1)
         g_qteam = atoi(s);
@@ -329,11 +336,12 @@ int walk_for(int g, int fixed, uint64_t len)
     return (g == 16 && len > 2048) ? 1 : 2;
 }
 
-/* qteam_kernel's preconditions: every record the same length (>= 8 KiB, the
- * two-level walk's range) and 4-byte phase, lane offsets within 32 bits */
+/* qteam_kernel's preconditions: every record the same length (>= g_qteam_min)
+ * and 4-byte phase, lane offsets within 32 bits */
 bool qteam_fits(const zs::BatchDesc &d)
 {
-    return d.fixed_len >= 8192 && (d.last_len == ~0ull || d.last_len == d.fixed_len) && (d.stride & 3) == 0 &&
+    return d.fixed_len >= g_qteam_min && d.fixed_len >= 1024 && (d.last_len == ~0ull || d.last_len == d.fixed_len) &&
+           (d.stride & 3) == 0 &&
            d.stride <= (1ull << 30);
 }
 
@@ -355,8 +363,7 @@ int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s, int depth_hi
                    : fixed && d.fixed_len <= 128 && d.last_len == ~0ull ? 2 : 5;
     const int xt = g_xteam;
     const bool xteam = g == 64 && fixed && xt && g_depth[2] < 0 && depth_hint < 0 && d.fixed_len >= g_xteam_min;
-    const bool qteam = g == 16 && fixed && depth == 0 && g_qteam && g_depth[1] < 0 && depth_hint < 0 &&
-                       qteam_fits(d);
+    const bool qteam = g == 16 && fixed && g_qteam && g_depth[1] < 0 && depth_hint < 0 && qteam_fits(d);
     int rc = qteam       ? zs_launch_xteam(16, &d, c->gtab, c->ncu, s)
              : xteam     ? zs_launch_xteam(xt, &d, c->gtab, c->ncu, s)
              : depth >= 9 ? zs_launch_burst(fixed, depth == 10, nb, &dx, c->gtab, c->ncu, s)
@@ -964,7 +971,7 @@ const char *zscrc_fixed_kernel(const void *d_base, uint64_t stride, uint64_t len
     const int g = team_for(len, n, c->ncu, stride, reinterpret_cast<uintptr_t>(d_base));
     if (g == 64 && g_xteam && g_depth[2] < 0 && len >= g_xteam_min)
         return "xteam_kernel";
-    if (g == 16 && g_qteam && g_depth[1] < 0 && walk_for(16, 1, len) == 0 && qteam_fits(d))
+    if (g == 16 && g_qteam && g_depth[1] < 0 && qteam_fits(d))
         return "qteam_kernel";
     static const char *names[] = {"team_kernel<1>/short_kernel/burst_kernel", "team_kernel<2>",
                                   "team_kernel<16>", "team_kernel<64>"};
