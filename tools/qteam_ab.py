@@ -5,7 +5,8 @@ timed launches per mode, the modes alternating launch by launch; the outputs
 of the two modes compared record by record.
 
 usage: python tools/qteam_ab.py [> profiles/r02/qteam_ab.jsonl]
-env QT_CASES=stride:len:n,... to pick shapes"""
+env QT_CASES=stride:len:n,... to pick shapes; QT_VS_XTEAM=1: xteam_kernel (the
+default from 256 KiB) against qteam forced"""
 import json
 import os
 import sys
@@ -33,7 +34,12 @@ def main():
         names = {}
         for i in range(reps + 2):
             for m in (0, 1):
-                lib().zscrc_set_qteam(m)
+                if os.environ.get("QT_VS_XTEAM"):
+                    # mode 0: the default dispatch (xteam_kernel for >= 256 KiB); 1: qteam forced
+                    lib().zscrc_set_xteam(1, (1 << 40) if m else (256 << 10))
+                    lib().zscrc_set_qteam(1)
+                else:
+                    lib().zscrc_set_qteam(m)
                 names[m] = lib().zscrc_fixed_kernel(big.data_ptr(), stride, length, n).decode()
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record(st)
@@ -44,6 +50,7 @@ def main():
                 if i >= 2:
                     ts[m].append(a.elapsed_time(b))
         lib().zscrc_set_qteam(QTEAM_DEFAULT)
+        lib().zscrc_set_xteam(1, 256 << 10)
         row = {"stride": stride, "len": length, "n": n}
         for m in (0, 1):
             ms = sorted(ts[m])[len(ts[m]) // 2]
