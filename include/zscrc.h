@@ -346,6 +346,11 @@ int zscrc_pack_open(zscrc_packer **pk, const char *path, const uint8_t uuid[16],
 /* key/value record (zs_file_write_keyval_record, zeroskip-file.c:188-247), or
  * a delete record when val is NULL (zs_file_write_delete_record, :352+) */
 int zscrc_pack_add(zscrc_packer *pk, const void *key, uint64_t keylen, const void *val, uint64_t vallen);
+/* n records in one call (no per-record crossing of a language boundary):
+ * record i = key bytes keys + key_off[i] (key_len[i]) and value vals +
+ * val_off[i] (val_len[i]); vals NULL, or val_off[i] == ~0, writes a delete. */
+int zscrc_pack_add_batch(zscrc_packer *pk, const void *keys, const uint64_t *key_off, const uint64_t *key_len,
+                         const void *vals, const uint64_t *val_off, const uint64_t *val_len, size_t n);
 typedef struct zscrc_pack_report {
     uint64_t records;       /* pointers written                          */
     uint64_t region_bytes;  /* records region (span of the first commit) */

@@ -51,6 +51,31 @@ def test_pack_matches_oracle_short(gpu, tmp_path, chunk):
     assert r["walk_rc"] == 0 and r["n_commits"] == 2 and r["n_bad"] == 0
 
 
+def test_pack_batch_api(gpu, tmp_path):
+    """zscrc_pack_add_batch (Packer.add_many / add_arrays) writes the same
+    bytes as per-record adds: deletes, empty values, shared value bytes."""
+    recs = _records(3000, 6)
+    recs[10] = (recs[10][0], b"")
+    want = zf.packed_file(recs, UUID, 2, 9)
+    with repack.Packer(str(tmp_path / "m"), UUID, 2, 9, chunk_bytes=8192) as p:
+        p.add_many(recs[:1000])
+        p.add_many(recs[1000:])
+    assert open(tmp_path / "m", "rb").read() == want
+    # values sharing bytes: record i -> the same 40 bytes at offset 8 * (i % 5)
+    vals = np.arange(80, dtype=np.uint8)
+    keys = [b"k%07d" % i for i in range(500)]
+    kb = np.frombuffer(b"".join(keys), dtype=np.uint8)
+    koff = np.arange(500, dtype=np.uint64) * 8
+    klen = np.full(500, 8, np.uint64)
+    voff = (np.arange(500, dtype=np.uint64) % 5) * 8
+    voff[7] = ~np.uint64(0)
+    vlen = np.full(500, 40, np.uint64)
+    with repack.Packer(str(tmp_path / "a"), UUID, 2, 9) as p:
+        p.add_arrays(kb, koff, klen, vals, voff, vlen)
+    recs2 = [(k, None if i == 7 else vals[8 * (i % 5):8 * (i % 5) + 40].tobytes()) for i, k in enumerate(keys)]
+    assert open(tmp_path / "a", "rb").read() == zf.packed_file(recs2, UUID, 2, 9)
+
+
 @pytest.mark.parametrize("chunk", [0, 1 << 20])
 def test_pack_long_commit_long_records(gpu, tmp_path, chunk):
     """Records region above 16 MiB (long commit), a 17 MiB value (long value

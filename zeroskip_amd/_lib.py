@@ -66,6 +66,7 @@ SIGNATURES = {
     "zscrc_zs_verify_files": (_int, [_vp, _vp, _vp, _sz, _int, _vp]),
     "zscrc_pack_open": (_int, [_vp, ctypes.c_char_p, ctypes.c_char_p, _u32, _u32, _u64, ctypes.c_uint]),
     "zscrc_pack_add": (_int, [_vp, _vp, _u64, _vp, _u64]),
+    "zscrc_pack_add_batch": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz]),
     "zscrc_pack_close": (_int, [_vp, _vp]),
 }
 

@@ -238,6 +238,9 @@ int zscrc_pack_add(zscrc_packer *pk, const void *key, uint64_t keylen, const voi
 {
     if (!pk || (!key && keylen))
         return ZSCRC_EINVAL;
+    static const uint8_t empty = 0;
+    if (!key)
+        key = &empty;
     if (pk->err)
         return pk->err;
     pk->ptrs.push_back(pk->pos); /* zs_packed_file_write_memtree_record: vecu64_append(offset) */
@@ -278,6 +281,23 @@ int zscrc_pack_add(zscrc_packer *pk, const void *key, uint64_t keylen, const voi
     if (!rc)
         rc = put(pk, nullptr, rup8(vallen) - vallen);
     return rc;
+}
+
+int zscrc_pack_add_batch(zscrc_packer *pk, const void *keys, const uint64_t *key_off, const uint64_t *key_len,
+                         const void *vals, const uint64_t *val_off, const uint64_t *val_len, size_t n)
+{
+    if (!pk || (n && (!key_off || !key_len || (vals && (!val_off || !val_len)))))
+        return ZSCRC_EINVAL;
+    const uint8_t *kb = static_cast<const uint8_t *>(keys), *vb = static_cast<const uint8_t *>(vals);
+    for (size_t i = 0; i < n; ++i) {
+        /* NULL vals: every record a delete; else val_off[i] == ~0 marks one */
+        const bool del = !vb || val_off[i] == ~0ull;
+        int rc = zscrc_pack_add(pk, kb + key_off[i], key_len[i], del ? nullptr : vb + val_off[i],
+                                del ? 0 : val_len[i]);
+        if (rc)
+            return rc;
+    }
+    return ZSCRC_OK;
 }
 
 int zscrc_pack_close(zscrc_packer *pk, zscrc_pack_report *rep)

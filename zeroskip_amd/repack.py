@@ -57,6 +57,42 @@ class Packer:
         vp = v.ctypes.data if v.nbytes else ctypes.addressof(_EMPTY)
         check(lib().zscrc_pack_add(self._h, k.ctypes.data, k.nbytes, vp, v.nbytes), "zscrc_pack_add")
 
+    def add_many(self, records) -> None:
+        """(key, value-or-None) pairs in key order, one library call
+        (zscrc_pack_add_batch): keys and values packed into two blobs."""
+        records = list(records)
+        if not records:
+            return
+        klen = np.fromiter((len(k) for k, _ in records), dtype=np.uint64, count=len(records))
+        koff = np.zeros(len(records), dtype=np.uint64)
+        np.cumsum(klen[:-1], out=koff[1:])
+        kblob = np.frombuffer(b"".join(k for k, _ in records) or b"\0", dtype=np.uint8)
+        vlen = np.fromiter((0 if v is None else len(v) for _, v in records), dtype=np.uint64, count=len(records))
+        voff = np.zeros(len(records), dtype=np.uint64)
+        np.cumsum(vlen[:-1], out=voff[1:])
+        voff[[i for i, (_, v) in enumerate(records) if v is None]] = ~np.uint64(0)
+        vblob = np.frombuffer(b"".join(v for _, v in records if v is not None) or b"\0", dtype=np.uint8)
+        self.add_arrays(kblob, koff, klen, vblob, voff, vlen)
+
+    def add_arrays(self, kblob, koff, klen, vblob, voff, vlen) -> None:
+        """Records i = kblob[koff[i]:+klen[i]] -> vblob[voff[i]:+vlen[i]]
+        (voff[i] == 2**64-1: a delete; vblob None: all deletes), numpy arrays,
+        no copies (values may share bytes)."""
+        n = len(koff)
+        koff, klen = np.ascontiguousarray(koff, np.uint64), np.ascontiguousarray(klen, np.uint64)
+        kblob = np.ascontiguousarray(kblob).view(np.uint8)
+        assert len(klen) == n and (n == 0 or int((koff + klen).max()) <= kblob.nbytes)
+        vp = op = lp = None
+        if vblob is not None:
+            vblob = np.ascontiguousarray(vblob).view(np.uint8)
+            voff, vlen = np.ascontiguousarray(voff, np.uint64), np.ascontiguousarray(vlen, np.uint64)
+            live = voff != ~np.uint64(0)
+            assert len(voff) == n and len(vlen) == n
+            assert not live.any() or int((voff[live] + vlen[live]).max()) <= vblob.nbytes
+            vp, op, lp = vblob.ctypes.data, voff.ctypes.data, vlen.ctypes.data
+        check(lib().zscrc_pack_add_batch(self._h, kblob.ctypes.data, koff.ctypes.data, klen.ctypes.data,
+                                         vp, op, lp, n), "zscrc_pack_add_batch")
+
     def close(self) -> dict:
         if self._h:
             rep = PackReport()
@@ -121,7 +157,8 @@ def repack_dir(dbdir: str, out_path: str, uuid: bytes, startidx: int, endidx: in
         if f.kind == zsfile.FINALISED:
             for k, v in _records_of(f.image):
                 merged[k] = v
+    keys = sorted(merged)
     with Packer(out_path, uuid, startidx, endidx, chunk_bytes=chunk_bytes) as p:
-        for k in sorted(merged):
-            p.add(k, merged[k])
+        for i in range(0, len(keys), 65536):
+            p.add_many((k, merged[k]) for k in keys[i:i + 65536])
     return p.report
