@@ -342,7 +342,8 @@ def test_qteam_shapes(gpu):
     try:
         for stride, length, n, off in [(8192, 8192, 16385, 0), (8200, 8195, 16390, 1), (16384, 12000, 16387, 3),
                                        (65540, 65537, 16385, 2), (12288, 9000, 16400, 0), (2048, 2048, 16387, 0),
-                                       (4100, 4097, 16390, 1), (3000, 2050, 16384, 2)]:
+                                       (4100, 4097, 16390, 1), (3000, 2050, 16384, 2),
+                                       (4096, 8192, 16384, 0), (0, 9000, 16386, 1)]:   # overlapping, stride 0
             data = rand_bytes(stride * (n - 1) + length + off, stride + length + n)
             dd = to_dev(data[off:], gpu)
             assert lib().zscrc_fixed_kernel(dd.data_ptr(), stride, length, n).decode() == "qteam_kernel"
