@@ -118,6 +118,14 @@ size_t zscrc_span_scratch_bytes(uint64_t len);
 int zscrc_device_span(const void *d_buf, uint64_t len, uint32_t seed, uint32_t *d_out,
                       void *scratch, unsigned flags, void *stream);
 
+/* Device: k spans in one launch pair (segments of every span over every CU,
+ * then one fold launch for all): d_out[i] = crc32c(seeds[i], d_bufs[i],
+ * lens[i]) (seeds NULL = 0; ZSCRC_RAW: raw registers).  k <= 8 spans of
+ * >= 16 KiB each; otherwise one zscrc_device_span per span.  The library's
+ * scratch, like zscrc_device_span with scratch NULL. */
+int zscrc_device_spans(const void *const *d_bufs, const uint64_t *lens, const uint32_t *seeds, uint32_t *d_out,
+                       size_t k, unsigned flags, void *stream);
+
 /* Host-resident batch: copies [min off, max off+len) to the device, runs the
  * batch, copies results back.  Synchronous.  The PCIe-bound path. */
 int zscrc_host_batch(const void *base, const uint64_t *off, const uint64_t *len,

@@ -46,3 +46,34 @@ def test_default_chunk_large(gpu):
     with CrcStream(0, nocopy=True) as s:
         s.update(data)
     assert s.crc == oracle.crc32c_hw(0, data)
+
+
+@pytest.mark.parametrize("shape", ["mixed", "equal", "fallback_short", "fallback_many"])
+def test_device_spans(gpu, shape):
+    """zscrc_device_spans (one segment launch + one fold launch for up to 8
+    spans) against the oracle: spans of very different lengths, unaligned
+    offsets, seeds, standard and raw registers; short or many spans take
+    the per-span path."""
+    import torch
+    from oracle import oracle
+    from zeroskip_amd import device as zd
+    rng = np.random.default_rng(11)
+    host = rng.integers(0, 256, (300 << 20) + 4096, dtype=np.uint8)
+    d = torch.from_numpy(host).to(gpu)
+    if shape == "mixed":
+        spans = [(3, 200 << 20), (1, 16 << 10), ((200 << 20) + 17, 40 << 20), ((250 << 20) + 2, 1000003),
+                 ((260 << 20) + 5, 33 << 10)]
+    elif shape == "equal":
+        spans = [(i * (32 << 20), 32 << 20) for i in range(8)]
+    elif shape == "fallback_short":
+        spans = [(0, 100), (7, 64 << 20), (5, 1 << 10)]
+    else:
+        spans = [(i * (1 << 20) + i, (1 << 20) + 3 * i) for i in range(11)]
+    offs, lens = [o for o, _ in spans], [n for _, n in spans]
+    seeds = [int(v) for v in rng.integers(0, 2**32, len(spans), dtype=np.uint64)]
+    got = zd.crc_spans(d, offs, lens, seeds).cpu().numpy().view(np.uint32)
+    want = [oracle.crc32c_hw(s, host[o:o + n]) for (o, n), s in zip(spans, seeds)]
+    assert [int(v) for v in got] == want, shape
+    raw = zd.crc_spans(d, offs, lens, raw=True).cpu().numpy().view(np.uint32)
+    want_raw = [(~oracle.crc32c_hw(0xFFFFFFFF, host[o:o + n])) & 0xFFFFFFFF for o, n in spans]
+    assert [int(v) for v in raw] == want_raw, shape

@@ -232,12 +232,15 @@ class GpuBackend:
 
     def raw_spans(self, buf, off: list, ln: list, d_off, d_ln):
         """raw registers of a few long spans (records-region pieces, pointer
-        sections; host offsets): one zscrc_device_span each -- segments over
-        every CU, the whole-wave coalesced teams on long ones; many: one
-        variable batch."""
-        from .device import crc_span
+        sections; host offsets): up to 8 in one zscrc_device_spans call (one
+        segment launch of the coalesced whole-wave teams over every CU, one
+        fold launch), else one zscrc_device_span each; many: one variable
+        batch."""
+        from .device import crc_span, crc_spans
         if len(off) > 64:
             return self.raw(buf, d_off, d_ln)
+        if len(off) <= 8 and os.environ.get("ZS_SPANS_MULTI", "1") != "0":
+            return crc_spans(buf, off, ln, raw=True)
         out = torch.empty(len(off), dtype=torch.int32, device=buf.device)
         for i, (o, n) in enumerate(zip(off, ln)):
             crc_span(buf, offset=o, length=n, out=out[i:i + 1], raw=True)

@@ -40,6 +40,8 @@ int zs_launch_burst(int fixed, int xp, int nb, const zs::BatchDesc *d, const uin
 int zs_launch_multi(const zs::BatchDesc *d, const zs::MultiBatch *m, const uint32_t *gtab, int grid,
                     hipStream_t stream);
 int zs_launch_xteam(int depth, const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
+int zs_launch_spans(const zs::XDesc *x, const zs::XMulti *m, const zs::SpanFolds *fs, const uint32_t *gtab,
+                    int grid, hipStream_t stream);
 }
 
 namespace {
@@ -795,6 +797,101 @@ int zscrc_device_span(const void *d_buf, uint64_t len, uint32_t seed, uint32_t *
     rc = scratch_acquire(c, s);
     if (!rc)
         rc = span_impl(c, d_buf, len, seed, d_out, nullptr, flags, s);
+    const int rc2 = scratch_release(c, s);
+    return rc ? rc : rc2;
+}
+
+int zscrc_device_spans(const void *const *d_bufs, const uint64_t *lens, const uint32_t *seeds, uint32_t *d_out,
+                       size_t k, unsigned flags, void *stream)
+{
+    if (k == 0)
+        return ZSCRC_OK;
+    if (!d_bufs || !lens || !d_out)
+        return ZSCRC_EINVAL;
+    uint64_t total = 0;
+    bool multi = k <= (size_t)zs::SPANS_MAX && g_xteam;
+    for (size_t i = 0; i < k; ++i) {
+        if (!d_bufs[i] && lens[i])
+            return ZSCRC_EINVAL;
+        if (lens[i] < SPAN_SPLIT_MIN)
+            multi = false;
+        total += lens[i];
+    }
+    if (!multi) { /* short spans or many: one call each */
+        for (size_t i = 0; i < k; ++i) {
+            const int rc = zscrc_device_span(d_bufs[i], lens[i], seeds ? seeds[i] : 0u, d_out + i, nullptr, flags,
+                                             stream);
+            if (rc)
+                return rc;
+        }
+        return ZSCRC_OK;
+    }
+    DevCtx *c;
+    int rc = get_ctx(&c);
+    if (rc)
+        return rc;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const uint32_t xio = (flags & ZSCRC_RAW) ? 0u : 0xffffffffu;
+    /* one segment size for every span (two segments per wave in all), so a
+     * short span is as many segments as its length needs, not one wave's walk */
+    const uint64_t target = 2ull * (uint64_t)c->ncu * 16;
+    uint64_t seg = ((total + target - 1) / target + 1023) & ~1023ull;
+    if (seg < SEG_MIN)
+        seg = SEG_MIN;
+    zs::XMulti m;
+    memset(&m, 0, sizeof m);
+    zs::SpanFolds fs;
+    memset(&fs, 0, sizeof fs);
+    m.k = (uint32_t)k;
+    uint64_t w = 0;
+    for (size_t i = 0; i < k; ++i) {
+        const uint64_t W = (lens[i] + seg - 1) / seg;
+        m.base[i] = static_cast<const uint8_t *>(d_bufs[i]);
+        m.seg[i] = seg;
+        m.last[i] = lens[i] - (W - 1) * seg;
+        m.first[i] = w;
+        m.out[i] = d_out + i;
+        w += W;
+    }
+    m.first[k] = w;
+    if ((rc = scratch_acquire(c, s)))
+        return rc;
+    rc = grow(&c->scratch, &c->scratch_bytes, w * 4);
+    if (!rc) {
+        uint32_t *part = static_cast<uint32_t *>(c->scratch);
+        const uint32_t kseg = zs_gf2_xpow8n(seg);
+        for (size_t i = 0; i < k; ++i) {
+            zs::SpanFold &f = fs.f[i];
+            f.part = part + m.first[i];
+            f.out = d_out + i;
+            f.w = (uint32_t)(m.first[i + 1] - m.first[i]);
+            f.k = kseg;
+            f.kp2[0] = kseg;
+            for (int b = 1; b < 32; ++b)
+                f.kp2[b] = zs_gf2_mul(f.kp2[b - 1], f.kp2[b - 1]);
+            f.x_last = zs_gf2_xpow8n(m.last[i]);
+            f.x_total = zs_gf2_xpow8n(lens[i]);
+            f.r0 = (seeds ? seeds[i] : 0u) ^ xio;
+            f.xor_out = xio;
+            m.preset[i] = zs_gf2_mul(f.r0, f.x_total) ^ f.xor_out;
+        }
+        zs::XDesc x;
+        memset(&x, 0, sizeof x);
+        x.base = m.base[0];
+        x.out = part;
+        x.n = w;
+        x.stride = seg;
+        x.fixed_len = seg;
+        x.last_len = seg;
+        if (zs_launch_spans(&x, &m, &fs, c->gtab, c->ncu, s)) {
+            set_err("multi-span launch", hipGetLastError());
+            rc = ZSCRC_EHIP;
+        } else {
+            g_stat[2] += 2;
+            g_stat[3] += total;
+        }
+    }
     const int rc2 = scratch_release(c, s);
     return rc ? rc : rc2;
 }

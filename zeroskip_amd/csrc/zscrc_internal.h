@@ -81,6 +81,21 @@ struct XDesc {
     uint32_t xor_io;
 };
 
+/* Up to SPANS_MAX spans in one xteam_kernel launch (zscrc_device_spans):
+ * span s is segments [first[s], first[s+1]) of the launch, seg[s] bytes each
+ * from base[s], the last one last[s]; block 0 presets *out[s] = preset[s]
+ * (the constant terms the fold XORs into). */
+constexpr int SPANS_MAX = 8;
+struct XMulti {
+    uint32_t k;
+    uint32_t preset[SPANS_MAX];
+    const uint8_t *base[SPANS_MAX];
+    uint64_t seg[SPANS_MAX];
+    uint64_t last[SPANS_MAX];
+    uint64_t first[SPANS_MAX + 1];
+    uint32_t *out[SPANS_MAX];
+};
+
 struct RecDesc {
     uint64_t off;
     uint64_t len;
@@ -149,6 +164,11 @@ struct SpanFold {
     uint32_t x_total;     /* x^(8*span len) */
     uint32_t r0;          /* initial register */
     uint32_t xor_out;
+};
+
+/* The folds of the spans of one zscrc_device_spans launch (blockIdx.y = span). */
+struct SpanFolds {
+    SpanFold f[SPANS_MAX];
 };
 
 } /* namespace zs */

@@ -788,16 +788,41 @@ struct XItem {
     uint64_t w;   /* record index */
     uint32_t S;   /* steps; 0 = fewer than 8 bytes */
     uint32_t R0;  /* initial register */
+    uintptr_t lo; /* first aligned dword of the record's buffer (load clamp) */
 };
 
 constexpr uint64_t XSTEP = 4096;
 
-__device__ __forceinline__ bool xitem(const XDesc &d, uint64_t w, uint64_t wend, XItem &it)
+/* Record w's first byte, length and buffer clamp bound: a fixed-stride batch,
+ * or (MULTI) segment w of a multi-span launch (uniform w: a scalar scan of
+ * at most SPANS_MAX spans). */
+template <bool MULTI>
+__device__ __forceinline__ void xgeom(const XDesc &d, const XMulti &m, uint64_t w, uintptr_t &A, uint64_t &len,
+                                      uintptr_t &lo)
+{
+    if (!MULTI) {
+        len = (w + 1 == d.n) ? d.last_len : d.fixed_len;
+        A = reinterpret_cast<uintptr_t>(d.base) + w * d.stride;
+        lo = reinterpret_cast<uintptr_t>(d.base) & ~uintptr_t(3);
+        return;
+    }
+    uint32_t k = 0;
+    while (k + 1 < m.k && w >= m.first[k + 1])
+        ++k;
+    const uint64_t j = w - m.first[k];
+    len = w + 1 == m.first[k + 1] ? m.last[k] : m.seg[k];
+    A = reinterpret_cast<uintptr_t>(m.base[k]) + j * m.seg[k];
+    lo = reinterpret_cast<uintptr_t>(m.base[k]) & ~uintptr_t(3);
+}
+
+template <bool MULTI>
+__device__ __forceinline__ bool xitem(const XDesc &d, const XMulti &m, uint64_t w, uint64_t wend, XItem &it)
 {
     if (w >= wend)
         return false;
-    const uint64_t len = (w + 1 == d.n) ? d.last_len : d.fixed_len;
-    const uintptr_t A = reinterpret_cast<uintptr_t>(d.base) + w * d.stride;
+    uintptr_t A, lo;
+    uint64_t len;
+    xgeom<MULTI>(d, m, w, A, len, lo);
     const uintptr_t E = len < 8 ? A : ((A + len) & ~uintptr_t(3));
     const uint32_t S = len < 8 ? 0u : (uint32_t)((E - A + XSTEP - 1) / XSTEP);
     it.A = A;
@@ -807,6 +832,7 @@ __device__ __forceinline__ bool xitem(const XDesc &d, uint64_t w, uint64_t wend,
     it.len = len;
     it.w = w;
     it.R0 = d.seed ^ d.xor_io;
+    it.lo = lo;
     return true;
 }
 
@@ -910,12 +936,15 @@ struct XLoad {
     uintptr_t V;   /* address of the current step */
     uint32_t left; /* steps of the record after this one */
     bool ok;       /* a record with >= 8 bytes: loads */
+    uintptr_t lo;  /* the record's buffer clamp bound */
 };
 
-__device__ __forceinline__ void xrec(const XDesc &d, XLoad &l)
+template <bool MULTI>
+__device__ __forceinline__ void xrec(const XDesc &d, const XMulti &m, XLoad &l)
 {
-    const uint64_t len = (l.w + 1 == d.n) ? d.last_len : d.fixed_len;
-    const uintptr_t A = reinterpret_cast<uintptr_t>(d.base) + l.w * d.stride;
+    uintptr_t A;
+    uint64_t len;
+    xgeom<MULTI>(d, m, l.w < l.wend ? l.w : l.wend - 1, A, len, l.lo);
     const uintptr_t E = len < 8 ? A : ((A + len) & ~uintptr_t(3));
     const uint64_t S = len < 8 ? 0 : (E - A + XSTEP - 1) / XSTEP;
     l.V = E - S * XSTEP;
@@ -923,7 +952,8 @@ __device__ __forceinline__ void xrec(const XDesc &d, XLoad &l)
     l.ok = l.w < l.wend && S; /* a record without loads: its one position reads the dummy */
 }
 
-__device__ __forceinline__ void xnext(const XDesc &d, XLoad &l)
+template <bool MULTI>
+__device__ __forceinline__ void xnext(const XDesc &d, const XMulti &m, XLoad &l)
 {
     if (l.ok && l.left) {
         --l.left;
@@ -933,14 +963,17 @@ __device__ __forceinline__ void xnext(const XDesc &d, XLoad &l)
     if (l.w >= l.wend)
         return;
     l.w += 1;
-    xrec(d, l);
+    xrec<MULTI>(d, m, l);
 }
 
-__global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, const uint32_t *__restrict__ gtab)
+template <bool MULTI>
+__global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, const uint32_t *__restrict__ gtab)
 {
     __shared__ __attribute__((aligned(16))) char L[LDS_BYTES];
     if ((uint64_t)blockIdx.x * WAVES >= d.n)
         return;
+    if (MULTI && blockIdx.x == 0 && threadIdx.x < m.k)
+        m.out[threadIdx.x][0] = m.preset[threadIdx.x]; /* the fold kernel (next on the stream) XORs into it */
     fill_lds<64>(L, gtab);
     __syncthreads();
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
@@ -953,17 +986,16 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, const uint32_t *__re
     const uint64_t wbeg = team * per < d.n ? team * per : d.n;
     const uint64_t wend = wbeg + per < d.n ? wbeg + per : d.n;
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(gtab);
-    const uintptr_t lo = reinterpret_cast<uintptr_t>(d.base) & ~uintptr_t(3);
 
     XLoad ld;
     ld.w = wbeg;
     ld.wend = wend;
-    xrec(d, ld);
+    xrec<MULTI>(d, m, ld);
     uint32_t b0[16], b1[16];
     const uint32_t voff = 64u * (uint32_t)c + 16u * (uint32_t)g;
-    xissue(ld.V, ld.ok, voff, dummy, lo, b0);
+    xissue(ld.V, ld.ok, voff, dummy, ld.lo, b0);
     XItem it;
-    bool ok = xitem(d, wbeg, wend, it);
+    bool ok = xitem<MULTI>(d, m, wbeg, wend, it);
     uint32_t s = 0;
     uint32_t acc = 0;
     /* Results wait in a register (lane k: the k-th record of the current
@@ -985,13 +1017,13 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, const uint32_t *__re
             for (uint64_t i = 0; i < it.len; ++i)
                 r = byte_step(L, r, ((g8p)it.A)[i], c_hi);
             stash_put(r ^ d.xor_io);
-            ok = xitem(d, it.w + 1, wend, it);
+            ok = xitem<MULTI>(d, m, it.w + 1, wend, it);
             return;
         }
         xpose16(w);
         const uintptr_t st = it.V0 + (uint64_t)s * XSTEP;
         if (s <= 1 && st < it.A + 4) /* the record start is in this step */
-            fix_piece(it, st + 64 * (uintptr_t)lane, lo, w);
+            fix_piece(it, st + 64 * (uintptr_t)lane, it.lo, w);
         if (s + 1 < it.S) {
             acc = piece<true>(L, acc, w, c_lo, c_hi);
             ++s;
@@ -1012,16 +1044,16 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, const uint32_t *__re
         stash_put(__shfl(acc, 63) ^ d.xor_io);
         acc = 0;
         s = 0;
-        ok = xitem(d, it.w + 1, wend, it);
+        ok = xitem<MULTI>(d, m, it.w + 1, wend, it);
     };
     while (ok) {
-        xnext(d, ld);
-        xissue(ld.V, ld.ok, voff, dummy, lo, b1);
+        xnext<MULTI>(d, m, ld);
+        xissue(ld.V, ld.ok, voff, dummy, ld.lo, b1);
         hash(b0);
         if (!ok)
             break;
-        xnext(d, ld);
-        xissue(ld.V, ld.ok, voff, dummy, lo, b0);
+        xnext<MULTI>(d, m, ld);
+        xissue(ld.V, ld.ok, voff, dummy, ld.lo, b0);
         hash(b1);
     }
     if ((uint32_t)lane < nst)
@@ -2142,20 +2174,15 @@ __device__ __forceinline__ uint32_t kpow(const char *T, const uint32_t *kp2, uin
  */
 constexpr int FWG = 256; /* span fold: one wave per SIMD, the gmul chains are latency-bound */
 
-__global__ __launch_bounds__(FWG) void span_fold_kernel(SpanFold f, const uint32_t *__restrict__ gtab)
+/* One span's fold by block bid of nblk (tables already in LDS). */
+__device__ __forceinline__ void fold_blocks(const SpanFold &f, const char *T, const uint32_t *kp2, uint32_t *red,
+                                            uint32_t bid, uint32_t nblk)
 {
-    __shared__ uint32_t red[FWG / 64];
-    __shared__ __attribute__((aligned(16))) char T[4096];
-    __shared__ uint32_t kp2[32];
-    load_gmul_table(T, gtab);
-    if (threadIdx.x < 32)
-        kp2[threadIdx.x] = f.kp2[threadIdx.x];
-    __syncthreads();
     const uint32_t W = f.w;
     const uint32_t nh = W - 1; /* Horner terms */
-    const uint32_t nt = gridDim.x * (uint32_t)FWG;
+    const uint32_t nt = nblk * (uint32_t)FWG;
     const uint32_t per = (nh + nt - 1) / nt;
-    const uint32_t s = (blockIdx.x * (uint32_t)FWG + threadIdx.x) * per;
+    const uint32_t s = (bid * (uint32_t)FWG + threadIdx.x) * per;
     const uint32_t e = s + per < nh ? s + per : nh;
     uint32_t h = 0;
     for (uint32_t i = s; i < e; ++i)
@@ -2172,10 +2199,46 @@ __global__ __launch_bounds__(FWG) void span_fold_kernel(SpanFold f, const uint32
         for (int k = 0; k < FWG / 64; ++k)
             x ^= red[k];
         x = gmul_t(T, x, f.x_last);
-        if (blockIdx.x == 0)
+        if (bid == 0)
             x ^= f.part[W - 1];
         atomicXor(f.out, x);
     }
+}
+
+__global__ __launch_bounds__(FWG) void span_fold_kernel(SpanFold f, const uint32_t *__restrict__ gtab)
+{
+    __shared__ uint32_t red[FWG / 64];
+    __shared__ __attribute__((aligned(16))) char T[4096];
+    __shared__ uint32_t kp2[32];
+    load_gmul_table(T, gtab);
+    if (threadIdx.x < 32)
+        kp2[threadIdx.x] = f.kp2[threadIdx.x];
+    __syncthreads();
+    fold_blocks(f, T, kp2, red, blockIdx.x, gridDim.x);
+}
+
+/* The folds of a multi-span launch: blockIdx.y = span, each span over the
+ * first fold_nblk(W) blocks of its row. */
+__device__ __forceinline__ uint32_t fold_nblk(uint32_t w)
+{
+    const uint32_t b = (w + FWG - 1) / FWG;
+    return b < 1 ? 1 : b > 256 ? 256 : b;
+}
+
+__global__ __launch_bounds__(FWG) void span_folds_kernel(SpanFolds fs, const uint32_t *__restrict__ gtab)
+{
+    const SpanFold &f = fs.f[blockIdx.y];
+    const uint32_t nb = fold_nblk(f.w);
+    if (blockIdx.x >= nb)
+        return;
+    __shared__ uint32_t red[FWG / 64];
+    __shared__ __attribute__((aligned(16))) char T[4096];
+    __shared__ uint32_t kp2[32];
+    load_gmul_table(T, gtab);
+    if (threadIdx.x < 32)
+        kp2[threadIdx.x] = f.kp2[threadIdx.x];
+    __syncthreads();
+    fold_blocks(f, T, kp2, red, blockIdx.x, nb);
 }
 
 /* ------------------------------------------------- classes and parts */
@@ -2626,8 +2689,11 @@ extern "C" int zs_launch_xteam(int depth, const zs::BatchDesc *bd, const uint32_
         hipLaunchKernelGGL(zs::qteam_kernel<2>, dim3(grid), dim3(zs::WG), 0, stream, *d, gtab);
     else if (depth == 16)
         hipLaunchKernelGGL(zs::qteam_kernel<ZS_QTEAM_B3>, dim3(grid), dim3(zs::WG), 0, stream, *d, gtab);
-    else
-        hipLaunchKernelGGL(zs::xteam_kernel, dim3(grid), dim3(zs::WG), 0, stream, *d, gtab);
+    else {
+        zs::XMulti none;
+        none.k = 0;
+        hipLaunchKernelGGL(zs::xteam_kernel<false>, dim3(grid), dim3(zs::WG), 0, stream, *d, none, gtab);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -2687,6 +2753,22 @@ extern "C" int zs_launch_multi(const zs::BatchDesc *d, const zs::MultiBatch *m, 
         hipLaunchKernelGGL(zs::multi64_kernel<2>, dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
     else
         hipLaunchKernelGGL(zs::multi_kernel, dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int zs_launch_spans(const zs::XDesc *x, const zs::XMulti *m, const zs::SpanFolds *fs,
+                               const uint32_t *gtab, int grid, hipStream_t stream)
+{
+    hipLaunchKernelGGL(zs::xteam_kernel<true>, dim3(grid), dim3(zs::WG), 0, stream, *x, *m, gtab);
+    if (hipGetLastError() != hipSuccess)
+        return -3;
+    uint32_t bx = 1;
+    for (uint32_t k = 0; k < m->k; ++k) {
+        const uint32_t b = (fs->f[k].w + zs::FWG - 1) / zs::FWG;
+        bx = b > bx ? b : bx;
+    }
+    bx = bx > 256 ? 256 : bx;
+    hipLaunchKernelGGL(zs::span_folds_kernel, dim3(bx, m->k), dim3(zs::FWG), 0, stream, *fs, gtab);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

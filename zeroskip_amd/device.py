@@ -103,6 +103,30 @@ def crc_span(data: torch.Tensor, seed: int = 0, length: int | None = None,
     return out
 
 
+def crc_spans(data: torch.Tensor, offsets, lengths, seeds=None, out: torch.Tensor | None = None,
+              raw: bool = False) -> torch.Tensor:
+    """CRC of each span data[offsets[i] : +lengths[i]] in one call
+    (zscrc_device_spans: one segment launch and one fold launch for up to 8
+    spans of >= 16 KiB).  Returns an int32 device tensor."""
+    import ctypes
+    dev = _dev(data)
+    nbytes = data.numel() * data.element_size()
+    k = len(offsets)
+    assert len(lengths) == k
+    for o, n in zip(offsets, lengths):
+        if o < 0 or o + n > nbytes:
+            raise ValueError("span outside the buffer")
+    if out is None:
+        out = torch.empty(k, dtype=torch.int32, device=dev)
+    bufs = (ctypes.c_void_p * max(k, 1))(*[data.data_ptr() + int(o) for o in offsets])
+    lens = (ctypes.c_uint64 * max(k, 1))(*[int(n) for n in lengths])
+    sds = (ctypes.c_uint32 * max(k, 1))(*[int(v) & 0xFFFFFFFF for v in seeds]) if seeds is not None else None
+    with torch.cuda.device(dev):
+        check(lib().zscrc_device_spans(bufs, lens, sds, out.data_ptr(), k, ZSCRC_RAW if raw else 0,
+                                       _stream(dev)), "zscrc_device_spans")
+    return out
+
+
 def as_u32(t: torch.Tensor) -> list[int]:
     """int32 device tensor of CRCs -> python ints (unsigned)."""
     return [v & 0xFFFFFFFF for v in t.cpu().tolist()]
