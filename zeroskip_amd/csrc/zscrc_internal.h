@@ -61,7 +61,8 @@ struct BatchDesc {
     uint32_t split;
     uint32_t opt;         /* tuning bits: 1 = no three-chain five-piece bursts, 2 = no multi64_kernel,
                              4 / 8 = qteam_kernel with XOR3 grouping 1 / 2,
-                             16 = team_kernel<16>'s two-level walk with XOR3 grouping 2 */
+                             16 = team_kernel<16>'s two-level walk with XOR3 grouping 2,
+                             1024 = direct burst batches without the descriptor prefetch */
     uint32_t *part_out;
     const struct SplitPlan *plan;
     const uint32_t *part_base;

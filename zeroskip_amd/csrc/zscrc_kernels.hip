@@ -1755,9 +1755,27 @@ struct BRec {
     bool cnext; /* ... and is the first 8 bytes of the next lane's first piece */
 };
 
+/* A caller-array descriptor loaded a round ahead (direct batches): the next
+ * round's metadata is then already in registers when its loads are issued,
+ * instead of a dependent load latency per round. */
+struct BDesc {
+    uint64_t off, len;
+    uint32_t seed;
+};
+
+__device__ __forceinline__ void bdesc_load(const BatchDesc &d, uint64_t i, uint64_t count, BDesc &q)
+{
+    typedef const __attribute__((address_space(1))) uint64_t *g64p;
+    const uint64_t j = i < count ? i : count - 1; /* a valid address; unused past the end */
+    q.off = ((g64p)d.off)[j];
+    q.len = ((g64p)d.len)[j];
+    q.seed = d.seed ? ((g32p)d.seed)[j] : 0u;
+}
+
 template <bool FIXED, bool XP>
 __device__ __forceinline__ void burst_meta(const BatchDesc &d, const RecDesc *list, bool direct, uint64_t count,
-                                           uint64_t i, uintptr_t lo, BRec &b)
+                                           uint64_t i, uintptr_t lo, BRec &b, const BDesc &pq = BDesc(),
+                                           bool pre = false)
 {
     b.ok = i < count;
     b.skip = false;
@@ -1778,11 +1796,11 @@ __device__ __forceinline__ void burst_meta(const BatchDesc &d, const RecDesc *li
         b.it.rec = i;
     } else if (direct) {
         typedef const __attribute__((address_space(1))) uint64_t *g64p;
-        len = ((g64p)d.len)[i];
+        len = pre ? pq.len : ((g64p)d.len)[i];
         b.it.rec = i;
         if (d.commit) {
             /* an out-of-image commit is class 0 (empty): this kernel's */
-            off = ((g64p)d.off)[i];
+            off = pre ? pq.off : ((g64p)d.off)[i];
             if (!commit_fits(d.img_size, off, len)) {
                 off = NO_COMMIT_OFF;
                 len = 0;
@@ -1797,8 +1815,8 @@ __device__ __forceinline__ void burst_meta(const BatchDesc &d, const RecDesc *li
             return;
         }
         if (!d.commit)
-            off = ((g64p)d.off)[i];
-        seed = d.seed ? ((g32p)d.seed)[i] : 0u;
+            off = pre ? pq.off : ((g64p)d.off)[i];
+        seed = pre ? pq.seed : d.seed ? ((g32p)d.seed)[i] : 0u;
     } else {
         typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
         typedef const __attribute__((address_space(1))) u32x2 *g2p;
@@ -2095,12 +2113,19 @@ __global__ __launch_bounds__(NB == 1 ? 1024 : BWG) void burst_kernel(BatchDesc d
     if (XP) {
         /* wave-uniform trip count: the transpose needs every lane */
         const bool cm = !FIXED && d.commit;
+        /* direct batches: descriptors a round ahead (tuning bit 1024: off) */
+        const bool pf = !FIXED && direct && !(d.opt & 1024);
+        BDesc qn = {0, 0, 0};
         burst_meta<FIXED, true>(d, list, direct, count, i, lo, ra);
         if (cm)
             commit_words(ra, lane);
         burst_issue_x(ra, dummy, wa, lane);
+        if (pf)
+            bdesc_load(d, i + nthr, count, qn);
         for (;;) {
-            burst_meta<FIXED, true>(d, list, direct, count, i + nthr, lo, rb);
+            burst_meta<FIXED, true>(d, list, direct, count, i + nthr, lo, rb, qn, pf);
+            if (pf)
+                bdesc_load(d, i + 2 * nthr, count, qn);
             if (cm)
                 commit_words(rb, lane);
             burst_issue_x(rb, dummy, wb, lane);
@@ -2113,7 +2138,9 @@ __global__ __launch_bounds__(NB == 1 ? 1024 : BWG) void burst_kernel(BatchDesc d
             if (ra.ok)
                 burst_hash<NB, FIXED>(d, ra, wa, L, lo, c_lo, c_hi);
             i += nthr;
-            burst_meta<FIXED, true>(d, list, direct, count, i + nthr, lo, ra);
+            burst_meta<FIXED, true>(d, list, direct, count, i + nthr, lo, ra, qn, pf);
+            if (pf)
+                bdesc_load(d, i + 2 * nthr, count, qn);
             if (cm)
                 commit_words(ra, lane);
             burst_issue_x(ra, dummy, wa, lane);
