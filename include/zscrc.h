@@ -126,6 +126,15 @@ int zscrc_device_span(const void *d_buf, uint64_t len, uint32_t seed, uint32_t *
 int zscrc_device_spans(const void *const *d_bufs, const uint64_t *lens, const uint32_t *seeds, uint32_t *d_out,
                        size_t k, unsigned flags, void *stream);
 
+/* Device post-pass of a commit verification (consistent): for every commit
+ * i with d_status[i] != 1, one row of 18 int64 -- i, d_crc[i-1] (d_crc[0]
+ * for i = 0), the 8 image bytes at d_span_end[i] and the 8 at
+ * d_span_end[i-1] (each clamped to the image) -- in any order; *d_hdr = the
+ * number of such commits (rows past cap are counted, not written). */
+int zscrc_device_mismatch_rows(const uint32_t *d_status, const uint32_t *d_crc, const int64_t *d_span_end,
+                               const void *d_image, uint64_t image_size, size_t n, int64_t *d_hdr,
+                               int64_t *d_rows, uint32_t cap, void *stream);
+
 /* Host-resident batch: copies [min off, max off+len) to the device, runs the
  * batch, copies results back.  Synchronous.  The PCIe-bound path. */
 int zscrc_host_batch(const void *base, const uint64_t *off, const uint64_t *len,

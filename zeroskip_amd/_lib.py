@@ -34,6 +34,7 @@ SIGNATURES = {
     "zscrc_span_scratch_bytes": (_sz, [_u64]),
     "zscrc_device_span": (_int, [_vp, _u64, _u32, _vp, _vp, ctypes.c_uint, _vp]),
     "zscrc_device_spans": (_int, [_vp, _vp, _vp, _vp, _sz, ctypes.c_uint, _vp]),
+    "zscrc_device_mismatch_rows": (_int, [_vp, _vp, _vp, _vp, _u64, _sz, _vp, _vp, _u32, _vp]),
     "zscrc_host_batch": (_int, [_vp, _vp, _vp, _vp, _vp, _sz]),
     "zscrc_last_error": (ctypes.c_char_p, []),
     "zscrc_stats": (None, [_vp]),

@@ -250,6 +250,38 @@ class GpuBackend:
         from .device import crc_batch
         return crc_batch(buf, off, ln, max_len=max_len)
 
+    ROWS_CAP, RAW_CAP = 4096, 64
+
+    def mismatch_rows(self, st, crc, d_end, buf, raw):
+        """(rows, raw registers) of the commits with status != 1 in one
+        device->host copy (zscrc_device_mismatch_rows); None if they do not
+        fit the buffer."""
+        from ._lib import check, lib
+        if raw is not None and raw.numel() > self.RAW_CAP:
+            return None
+        dev = buf.device
+        key = (dev, self.ROWS_CAP)
+        if getattr(self, "_post_key", None) != key:
+            self._post = torch.empty(1 + self.RAW_CAP + 18 * self.ROWS_CAP, dtype=torch.int64, device=dev)
+            self._post_key = key
+        post = self._post
+        with torch.cuda.device(dev):
+            check(lib().zscrc_device_mismatch_rows(st.data_ptr(), crc.data_ptr(), d_end.data_ptr(), buf.data_ptr(),
+                                                   buf.numel(), st.numel(), post.data_ptr(),
+                                                   post[1 + self.RAW_CAP:].data_ptr(), self.ROWS_CAP,
+                                                   torch.cuda.current_stream(dev).cuda_stream),
+                  "zscrc_device_mismatch_rows")
+        k = 0 if raw is None else raw.numel()
+        if k:
+            post[1:1 + k] = raw.to(torch.int64) & M32
+        h = post.cpu().numpy()
+        cnt = int(h[0])
+        if cnt > self.ROWS_CAP:
+            return None
+        rows = h[1 + self.RAW_CAP:1 + self.RAW_CAP + 18 * cnt].reshape(-1, 18)
+        rows = rows[np.argsort(rows[:, 0], kind="stable")]
+        return rows, h[1:1 + k].tolist()
+
     def sync(self):
         torch.cuda.synchronize(self.device)
 
@@ -489,7 +521,17 @@ class Consistent:
             events[1].record()
         pack = np.zeros((0, 18), np.int64)
         raw_h = []
-        if n:
+        done = False
+        if n and hasattr(be, "mismatch_rows") and os.environ.get("ZS_POSTPASS", "native") == "native":
+            # one kernel writes the mismatch rows, one copy brings them (and
+            # the raw span registers) back; more mismatches than the buffer
+            # holds: the torch path below
+            got = be.mismatch_rows(st, crc, self.d_end, self.buf, raw)
+            if got is not None:
+                pack, raw_h = got
+                bad_idx = pack[:, 0]
+                done = True
+        if n and not done:
             # one round trip: the mismatches, their predecessors' computed
             # commit CRCs, the commit words after both spans (and the raw
             # registers of the long spans)
@@ -506,7 +548,7 @@ class Consistent:
             else:
                 pack = pack.cpu().numpy()
             bad_idx = pack[:, 0]
-        elif raw is not None:
+        elif raw is not None and not done:
             raw_h = [v & M32 for v in raw.cpu().tolist()]
         t_dev = time.perf_counter()
 

@@ -42,6 +42,9 @@ int zs_launch_multi(const zs::BatchDesc *d, const zs::MultiBatch *m, const uint3
 int zs_launch_xteam(int depth, const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
 int zs_launch_spans(const zs::XDesc *x, const zs::XMulti *m, const zs::SpanFolds *fs, const uint32_t *gtab,
                     int grid, hipStream_t stream);
+int zs_launch_mismatch_rows(const uint32_t *st, const uint32_t *crc, const int64_t *end, const uint8_t *img,
+                            uint64_t img_size, uint64_t n, int64_t *hdr, int64_t *rows, uint32_t cap,
+                            hipStream_t stream);
 }
 
 namespace {
@@ -894,6 +897,33 @@ int zscrc_device_spans(const void *const *d_bufs, const uint64_t *lens, const ui
     }
     const int rc2 = scratch_release(c, s);
     return rc ? rc : rc2;
+}
+
+int zscrc_device_mismatch_rows(const uint32_t *d_status, const uint32_t *d_crc, const int64_t *d_span_end,
+                               const void *d_image, uint64_t image_size, size_t n, int64_t *d_hdr,
+                               int64_t *d_rows, uint32_t cap, void *stream)
+{
+    if (!d_hdr || (n && (!d_status || !d_crc || !d_span_end || !d_image || !image_size || (cap && !d_rows))))
+        return ZSCRC_EINVAL;
+    DevCtx *c;
+    int rc = get_ctx(&c);
+    if (rc)
+        return rc;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipError_t e = hipMemsetAsync(d_hdr, 0, sizeof(int64_t), s);
+    if (e != hipSuccess) {
+        set_err("hipMemsetAsync(mismatch count)", e);
+        return ZSCRC_EHIP;
+    }
+    if (n == 0)
+        return ZSCRC_OK;
+    if (zs_launch_mismatch_rows(d_status, d_crc, d_span_end, static_cast<const uint8_t *>(d_image), image_size, n,
+                                d_hdr, d_rows, cap, s)) {
+        set_err("mismatch rows launch", hipGetLastError());
+        return ZSCRC_EHIP;
+    }
+    g_stat[2]++;
+    return ZSCRC_OK;
 }
 
 int zscrc_host_batch(const void *base, const uint64_t *off, const uint64_t *len,

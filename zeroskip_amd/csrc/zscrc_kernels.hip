@@ -2629,9 +2629,50 @@ __global__ __launch_bounds__(1024) void stream_read_kernel(const uint8_t *buf, u
         out[0] = acc; /* keeps the loads live; practically never taken */
 }
 
+/* consistent's post-pass: one row per commit whose status is not 1 --
+ * (index, computed CRC of the previous commit, the 8 bytes after this span,
+ * the 8 bytes after the previous span), bytes clamped to the image -- slots
+ * by one atomic counter in hdr[0]; rows past cap are counted, not written. */
+__global__ __launch_bounds__(256) void mismatch_rows_kernel(const uint32_t *st, const uint32_t *crc,
+                                                            const int64_t *end, const uint8_t *img,
+                                                            uint64_t img_size, uint64_t n, int64_t *hdr,
+                                                            int64_t *rows, uint32_t cap)
+{
+    const uint64_t nt = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += nt) {
+        if (st[i] == 1u)
+            continue;
+        const uint64_t slot = atomicAdd(reinterpret_cast<unsigned long long *>(hdr), 1ull);
+        if (slot >= cap)
+            continue;
+        int64_t *r = rows + slot * 18;
+        const uint64_t p = i ? i - 1 : 0;
+        r[0] = (int64_t)i;
+        r[1] = (int64_t)crc[p];
+        const uint64_t e0 = (uint64_t)end[i], e1 = (uint64_t)end[p];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint64_t a0 = e0 + k < img_size ? e0 + k : img_size - 1;
+            const uint64_t a1 = e1 + k < img_size ? e1 + k : img_size - 1;
+            r[2 + k] = img[a0];
+            r[10 + k] = img[a1];
+        }
+    }
+}
+
 } // namespace zs
 
 /* ------------------------------------------------------------ launchers */
+extern "C" int zs_launch_mismatch_rows(const uint32_t *st, const uint32_t *crc, const int64_t *end,
+                                       const uint8_t *img, uint64_t img_size, uint64_t n, int64_t *hdr,
+                                       int64_t *rows, uint32_t cap, hipStream_t stream)
+{
+    uint64_t blocks = (n + 255) / 256;
+    blocks = blocks < 1 ? 1 : blocks > 2048 ? 2048 : blocks;
+    hipLaunchKernelGGL(zs::mismatch_rows_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, st, crc, end, img,
+                       img_size, n, hdr, rows, cap);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
 extern "C" int zs_launch_classify(const zs::Classify *c, hipStream_t stream)
 {
     uint64_t blocks = (c->n + 8191) / 8192;
