@@ -65,6 +65,28 @@ def test_oracle_db_corruption(gpu, what):
         assert [h[0] for h in g.header_errors] == [f]
 
 
+@pytest.mark.parametrize("post", ["native", "native-overflow", "torch"])
+def test_post_pass_paths(gpu, monkeypatch, post):
+    """The mismatch post-pass: the native row kernel (one copy back), its
+    overflow fallback (more mismatches than the row buffer) and the torch
+    path give the oracle backend's report, with stale finalise commits and a
+    corrupted commit in the same DB."""
+    db = small_db(long_region=True)
+    f = name(7, 7)
+    img = bytearray(db[f])
+    c = zf.walk(img)[0][5]
+    img[c["span_off"] + 3] ^= 0x10
+    db[f] = bytes(img)
+    if post == "torch":
+        monkeypatch.setenv("ZS_POSTPASS", "torch")
+    elif post == "native-overflow":
+        monkeypatch.setattr(cs.GpuBackend, "ROWS_CAP", 2)
+    g = gpu_report(db)
+    o = cs.Consistent(cs.open_db(db), 0, 1, OracleBackend()).prepare().run()
+    assert not g.ok and same(g, o), (g.as_dict(), o.as_dict())
+    assert g.bad_commits == [(f, c["commit_off"])] and len(g.stale_empty_commits) == 3
+
+
 def _gen_small(gpu):
     from tools import zsdb_gen
     return zsdb_gen.make_db(device=gpu, packed=2, packed_region_bytes=20 << 20, packed_vlen=1000,
