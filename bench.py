@@ -290,7 +290,8 @@ def run_config3(args, world, rank, dev, stream):
     out_line = line(args, world, elapsed, NCHUNK * CHUNK * world * args.steps,
                     {"workload": "config3: 65536 x 64 KiB chunks per GPU (4 GiB), batched CRC-32C",
                      "records_per_gpu": NCHUNK, "record_bytes": CHUNK,
-                     "parallelism": f"shard{world}" + ("+rccl_allgather_digests" if world > 1 else "")}, r,
+                     "parallelism": f"shard{world}" + (("+rccl_allgather_digests" if os.environ.get("BENCH_DIST", "nccl") == "nccl"
+                                                        else "+gloo_allgather_digests") if world > 1 else "")}, r,
                     parity={"sampled_chunks": int(idx.size), "mismatches": n_bad, "checker": "oracle crc32c_hw"},
                     sustained=sustained)
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -589,6 +590,26 @@ def run_config5(args, world, rank, dev, stream):
     return out_line
 
 
+def torchrun_cmd(n: int) -> list:
+    """The launch the driver uses for N > 1 (one rank per GPU, 127.0.0.1)."""
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+
+
+def launch_ranks(n: int) -> int:
+    import subprocess
+    cmd = torchrun_cmd(n)
+    print("bench.py: --gpus %d without WORLD_SIZE: launching %s" % (n, " ".join(cmd)), file=sys.stderr, flush=True)
+    if os.environ.get("BENCH_LAUNCH_DRYRUN") == "1":
+        print(json.dumps({"launch": cmd}), flush=True)
+        return 0
+    return subprocess.call(cmd)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -602,11 +623,19 @@ def main() -> None:
     ap.add_argument("--finalised", type=int, default=1024, help="config5 finalised files")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # --gpus N without a launcher: one process per GPU is the contract, so
+        # start torchrun as a child (before anything touches the GPU) and
+        # exit with its status -- never a silent one-GPU measurement
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world != 1:
+    if args.gpus != world:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if world > 1:
+        # the file-image APIs of rank r use its own GPU only (zscrc_set_devices)
+        os.environ.setdefault("ZSCRC_DEVICES", str(local))
     # BENCH_SHARE_GPU=1: rehearsal of the N-rank path on a box with fewer GPUs
     # (ranks share devices round-robin; RCCL, or gloo with BENCH_DIST=gloo)
     if os.environ.get("BENCH_SHARE_GPU") == "1":

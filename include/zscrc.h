@@ -20,6 +20,14 @@
 extern "C" {
 #endif
 
+/* ABI version of this header.  3: round-3 ABI (zscrc_files_report.devices,
+ * the device-slot API); 2 added image_size / d_status to the commit entry
+ * points.  A caller built against this header checks at startup that
+ * zscrc_abi_version() == ZSCRC_ABI_VERSION: a library of another version
+ * has other struct layouts or argument lists. */
+#define ZSCRC_ABI_VERSION 3
+int zscrc_abi_version(void);
+
 /* zeroskip's string type (reference include/libzeroskip/cstring.h:23-29). */
 #ifndef _CSTRING_H_
 struct _cstring {
@@ -264,12 +272,26 @@ int zscrc_device_verify_commits_bounded(const void *d_image, uint64_t image_size
                                         const uint64_t *d_span_len, const uint32_t *d_seed, size_t n,
                                         uint64_t max_len, uint32_t *d_crc, uint32_t *d_status, void *stream);
 
+/* Device verdict of n commits (the verifier's question: is every commit
+ * good, and which are not?): as zscrc_device_verify_commits_bounded (d_seed
+ * may be NULL; max_len a bound on the span lengths, ZSCRC_LEN_UNBOUNDED if
+ * none is known), but no per-commit output -- *d_nbad (device) = the number
+ * of commits whose status would not be 1 (mismatch, or no commit record in
+ * the image), and d_bad (device, cap entries) receives the indices of the
+ * first cap of them found, in no particular order.  A clean batch writes
+ * nothing but the count. */
+int zscrc_device_verify_commits_verdict(const void *d_image, uint64_t image_size, const uint64_t *d_span_off,
+                                        const uint64_t *d_span_len, const uint32_t *d_seed, size_t n,
+                                        uint64_t max_len, uint64_t *d_nbad, uint64_t *d_bad, size_t cap,
+                                        void *stream);
+
 /* Device: compute n commit CRCs (the writer's side, zeroskip-file.c:253-350)
  * and store each one big-endian into its commit record; d_crc[i] receives it.
  * The commit record's header word (type, and for long commits the length
  * words) must already be in the image: only the CRC field is written.
  * d_status (may be NULL): 1 written, 2 not written (no commit record there,
- * or outside the image -- nothing outside the image is read or written). */
+ * or outside the image -- nothing outside the image is read or written).
+ * d_crc may be NULL (the CRCs only go into the image). */
 int zscrc_device_write_commits(void *d_image, uint64_t image_size, const uint64_t *d_span_off,
                                const uint64_t *d_span_len, size_t n, uint32_t *d_crc, uint32_t *d_status,
                                void *stream);
@@ -316,10 +338,14 @@ int zscrc_zs_consistent(const char *dbdir, zscrc_consistent_report *rep);
 /* End to end from host memory: every CRC of n zeroskip file images (mmap'd
  * files; kinds[i] = ZSCRC_ZS_ACTIVE / _FINALISED / _PACKED) -- header, record
  * walk and every commit of active / finalised files, records-region and
- * pointer-section commits of packed files.  `threads` host threads (0 = up to
- * 16) walk the files and copy them into pinned staging; the copies to the
- * current GPU, and the verification of every group of files whose bytes have
- * arrived, overlap with that work.  Synchronous. */
+ * pointer-section commits of packed files.  Multi-GPU in one process: the
+ * DB's bytes are cut into one equal share per device slot (records regions
+ * of packed files split across slots, their piece registers folded on the
+ * host with zscrc_shift); each slot checks its share in groups of at most
+ * ZSCRC_FILES_GROUP bytes (default 8 GiB, at most half the device's free
+ * memory).  `threads` host threads in all (0 = up to 16) walk the files and
+ * copy them into pinned staging; the H2D copies and the verification
+ * overlap with that work.  Synchronous. */
 #define ZSCRC_FILES_BAD_HEADER 1
 #define ZSCRC_FILES_BAD_WALK 2
 #define ZSCRC_FILES_BAD_COMMIT 3
@@ -339,9 +365,20 @@ typedef struct zscrc_files_report {
     double copy_s;                /* start of the pipeline -> last byte on the GPU */
     double verify_tail_s;         /* last byte on the GPU -> every verdict back  */
     double total_s;               /* the whole call                              */
+    int32_t devices;              /* device slots used (zscrc_set_devices)       */
 } zscrc_files_report;
 int zscrc_zs_verify_files(const void *const *images, const uint64_t *sizes, const int *kinds, size_t n,
                           int threads, zscrc_files_report *rep);
+/* Device slots of zscrc_zs_verify_files / zscrc_zs_consistent: n device ids
+ * (an id may repeat: two slots on one GPU); n = 0 restores the default --
+ * env ZSCRC_DEVICES ("0,1,2"), else every visible gfx950 device. */
+int zscrc_set_devices(const int *ids, int n);
+/* The slots a call would use now: writes up to cap ids, returns their count
+ * (or a negative status). */
+int zscrc_files_devices(int *ids, int cap);
+/* Frees the pinned staging and device buffers the file APIs keep between
+ * calls. */
+void zscrc_release_cache(void);
 
 /* Packed-file writer: the repack output path with its CRCs on the GPU.
  * Same byte layout and CRC lifecycle as zs_packed_file_new_from_memtree
@@ -380,6 +417,47 @@ typedef struct zscrc_pack_report {
 /* Writes the commits and the pointer section, closes the file and frees the
  * writer (also on error, after which the file is removed). */
 int zscrc_pack_close(zscrc_packer *pk, zscrc_pack_report *rep);
+/* Abandons a packing: frees the writer and removes the file without writing
+ * any commit (a partial repack never looks valid). */
+int zscrc_pack_abort(zscrc_packer *pk);
+
+/* Record lister: the key / value (or delete) records of a file image --
+ * active / finalised: the record walk (zeroskip-record.c:283-331), commits
+ * skipped; packed: the pointer section's order (zeroskip-packed.c:70-131).
+ * Offsets are into the image; val_off == ZSCRC_ZS_DELETED marks a delete.
+ * Returns ZSCRC_ZS_END (walked to the end; packed: ZSCRC_OK), STOPPED,
+ * TRUNCATED, or OVERFLOW with *n_records = all records when cap is short. */
+#define ZSCRC_ZS_DELETED UINT64_MAX
+typedef struct zscrc_zs_record {
+    uint64_t key_off, key_len, val_off, val_len;
+} zscrc_zs_record;
+int zscrc_zs_records(const void *image, uint64_t size, int kind, zscrc_zs_record *recs, size_t cap,
+                     size_t *n_records);
+/* The 61-byte .zsdb of zs_dotzsdb_update_end (zeroskip-dotzsdb.c:477-555),
+ * CRC over the host-order fields. */
+int zscrc_zs_dotzsdb_build(uint64_t offset, const char *uuidstr, uint32_t curidx, uint8_t out[61]);
+
+/* zsdb_repack (src/zeroskip.c:1419-1571) over a DB directory, in one call:
+ * finalised files present -> all of them merged (later record of a key
+ * wins, deletes kept) into one packed file; else two or more packed files
+ * -> the first two of the reference's pflist (the two newest; the older of
+ * the two wins a key present in both, a winning delete drops the key); the
+ * merged sources unlinked; .zsdb rewritten with its CRC.  Keys sorted on
+ * `threads` host threads (0 = up to 16); the packed file's records-region
+ * and pointer CRCs computed on the GPU (zscrc_pack_*).  flags:
+ * ZSCRC_PACK_FSYNC. */
+typedef struct zscrc_repack_report {
+    int32_t branch;             /* 0 nothing to pack, 1 finalised files, 2 packed files */
+    uint32_t startidx, endidx;  /* index range of the new packed file            */
+    uint64_t files_merged;
+    uint64_t records_in;        /* records listed from the sources               */
+    uint64_t records_out;       /* records written                               */
+    uint32_t dotzsdb_crc;       /* CRC of the rewritten .zsdb                     */
+    zscrc_pack_report pack;     /* the writer's report                           */
+    double list_s, merge_s, write_s, total_s;
+    char path[4096];            /* the new packed file                           */
+} zscrc_repack_report;
+int zscrc_zs_repack(const char *dbdir, unsigned flags, int threads, zscrc_repack_report *rep);
 
 #ifdef __cplusplus
 }

@@ -260,6 +260,75 @@ def packed_check(img) -> list[dict]:
     return out
 
 
+# ------------------------------------------------------------------ records (repack)
+def _record(img, off: int):
+    """(key, value-or-None, next offset) of the key / delete record at off
+    (zeroskip-record.c:38-181 read paths)."""
+    w0, = struct.unpack_from(">Q", img, off)
+    t = w0 >> 56
+    if t in (REC_KEY, REC_LONG_KEY):
+        if t == REC_KEY:
+            klen, voff = (w0 >> 40) & 0xFFFF, w0 & 0xFFFFFFFF
+        else:
+            klen, voff = struct.unpack_from(">QQ", img, off + 8)
+        v = off + voff
+        vw, = struct.unpack_from(">Q", img, v)
+        vlen = (vw >> 32) & 0xFFFFFF if (vw >> 56) == REC_VALUE else struct.unpack_from(">Q", img, v + 8)[0]
+        return bytes(img[off + 24:off + 24 + klen]), bytes(img[v + 16:v + 16 + vlen]), v + 16 + rup8(vlen)
+    if t in (REC_DELETED, REC_LONG_DELETED):
+        klen = (w0 >> 40) & 0xFFFF if t == REC_DELETED else struct.unpack_from(">Q", img, off + 8)[0]
+        return bytes(img[off + 24:off + 24 + klen]), None, off + 24 + rup8(klen)
+    return None
+
+
+def file_records(img) -> list:
+    """[(key, value-or-None)] of an active / finalised file in file order:
+    the record walk of zeroskip-record.c:283-331, commits skipped."""
+    out, off, n = [], HDR_SIZE, len(img)
+    while off + 8 <= n:
+        t = img[off]
+        if t in (REC_COMMIT, REC_LONG_COMMIT):
+            off += 8 if t == REC_COMMIT else 24
+            continue
+        r = _record(img, off)
+        if r is None:
+            break
+        out.append(r[:2])
+        off = r[2]
+    return out
+
+
+def packed_records(img) -> list:
+    """[(key, value-or-None)] of a packed file in pointer order
+    (zeroskip-packed.c:70-131: the pointer section after the records commit)."""
+    pc = packed_check(img)[0]
+    poff = pc["span_off"]
+    count, = struct.unpack_from(">Q", img, poff)
+    ptrs = struct.unpack_from(">%dQ" % count, img, poff + 8)
+    return [_record(img, p)[:2] for p in ptrs]
+
+
+def repack_finalised(images) -> list:
+    """Branch 1 of zsdb_repack (src/zeroskip.c:1460-1505): finalised files
+    loaded oldest first into the memtree (a later record of a key replaces an
+    earlier one, deletes kept), walked in key order."""
+    merged = {}
+    for img in images:
+        for k, v in file_records(img):
+            merged[k] = v
+    return sorted(merged.items())
+
+
+def repack_packed(older, newer) -> list:
+    """Branch 2 (src/zeroskip.c:1510-1565, zeroskip-packed.c:617-742) on the
+    two files it takes: on a key in both, the older file's record (its
+    iterator priority is the larger, zeroskip.c:520-526); a winning delete
+    drops the key."""
+    merged = dict(packed_records(newer))
+    merged.update(packed_records(older))
+    return sorted((k, v) for k, v in merged.items() if v is not None)
+
+
 # ------------------------------------------------------------------ bulk (zsbench replay)
 def zsbench_key(i: int) -> bytes:
     return b"%016d" % i  # benchmark/zsbench.c:183

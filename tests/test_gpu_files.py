@@ -112,3 +112,45 @@ def test_empty_and_tiny(gpu):
     rep = zsfile.verify_files([np.zeros(0, np.uint8), img])
     assert rep["header_errors"] == 1 and rep["walk_errors"] == 1 and rep["commits"] == 3
     assert rep["first_bad_file"] == 0
+
+
+def test_all_empty_files(gpu):
+    """zero-byte images only: no bytes to stage, every file still walked and
+    reported (header and walk errors)"""
+    rep = zsfile.verify_files([np.zeros(0, np.uint8)] * 3, [zsfile.FINALISED] * 3)
+    assert rep["files"] == 3 and rep["commits"] == 0
+    assert rep["header_errors"] == 3 and rep["walk_errors"] == 3 and rep["first_bad_file"] == 0
+
+
+@pytest.mark.parametrize("devs,group", [([0, 0], None), ([0, 0, 0], 4 << 20), ([0], 3 << 20)],
+                         ids=["2slots", "3slots-4MiB-groups", "1slot-3MiB-groups"])
+def test_device_slots_split_region(gpu, devs, group):
+    """Multi-GPU in one process (zscrc_set_devices; one GPU here, so the slots
+    share it): the DB's bytes cut into one share per slot, the packed file's
+    records region split across slots and into group-sized pieces whose raw
+    registers the host folds -- verdicts equal the format oracle's, with a
+    corrupt byte in the split region and one in a finalised file."""
+    imgs, kinds = _db(3, nfiles=30)
+    c = zf.walk(imgs[20].tobytes())[0][2]
+    imgs[20][c["span_off"] + 30] ^= 0x04          # a key payload byte
+    mid = imgs[7].nbytes // 2
+    imgs[7][mid] ^= 0x10                       # the middle of the packed records region
+    assert not zf.packed_check(imgs[7].tobytes())[1]["ok"]
+    commits, bad, stale = _expected(imgs, kinds)
+    assert bad == 2
+    zsfile.set_devices(devs)
+    if group:
+        os.environ["ZSCRC_FILES_GROUP"] = str(group)
+    try:
+        assert zsfile.devices() == devs
+        rep = zsfile.verify_files(imgs, kinds, threads=4)
+        imgs[7][mid] ^= 0x10
+        rep_ok7 = zsfile.verify_files(imgs, kinds, threads=4)
+    finally:
+        zsfile.set_devices(None)
+        os.environ.pop("ZSCRC_FILES_GROUP", None)
+    assert rep["devices"] == len(devs)
+    assert rep["commits"] == commits and rep["stale_empty_commits"] == stale
+    assert rep["bad_commits"] == 2 and rep["first_bad_file"] == 7 and rep["first_bad_what"] == 3
+    assert rep["header_errors"] == rep["walk_errors"] == 0
+    assert rep_ok7["bad_commits"] == 1 and rep_ok7["first_bad_file"] == 20

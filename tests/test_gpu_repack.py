@@ -100,28 +100,91 @@ def test_pack_empty(gpu, tmp_path):
     assert rep["records"] == 0 and rep["region_bytes"] == 0
 
 
+def _dotzsdb(path, curidx):
+    with open(path / ".zsdb", "wb") as fh:
+        fh.write(zf.dotzsdb_bytes(4096, UUIDSTR.encode() + b"\0", curidx))
+
+
 def test_repack_dir_finalised_files(gpu, tmp_path):
-    """zsdb_repack's CRC path over a DB directory: finalised files merged
-    (newest record of a key wins, deletes kept), one packed file out."""
+    """zsdb_repack branch 1 over a DB directory (zscrc_zs_repack): finalised
+    files merged (newest record of a key wins, deletes kept), one packed
+    file out, the sources unlinked, .zsdb rewritten -- byte for byte the
+    format oracle's."""
     rng = np.random.default_rng(3)
-    merged = {}
-    for idx in range(1, 6):
+    images = []
+    for idx in range(3, 8):
         w = zf.FileWriter(UUID, idx=idx)
         for t in range(200):
             k = b"%016d" % int(rng.integers(0, 500))
             if t % 17 == 3:
                 w.remove(k)
-                merged[k] = None
             else:
-                v = rng.integers(0, 256, int(rng.integers(0, 400)), dtype=np.uint8).tobytes()
-                w.add(k, v)
-                merged[k] = v
+                w.add(k, rng.integers(0, 256, int(rng.integers(0, 400)), dtype=np.uint8).tobytes())
             w.commit()
+        images.append(w.image())
         with open(tmp_path / f"zeroskip-{UUIDSTR}-{idx}-{idx}", "wb") as fh:
-            fh.write(w.image())
-    out = tmp_path / f"zeroskip-{UUIDSTR}-1-5"
-    rep = repack.repack_dir(str(tmp_path), str(out), UUID, 1, 5)
-    want = zf.packed_file(sorted(merged.items()), UUID, 1, 5)
+            fh.write(images[-1])
+    # an active file and an older packed file stay as they are
+    (tmp_path / f"zeroskip-{UUIDSTR}-8").write_bytes(zf.FileWriter(UUID, idx=8).image())
+    old = zf.packed_file(_records(50, 1), UUID, 0, 2)
+    (tmp_path / f"zeroskip-{UUIDSTR}-0-2").write_bytes(old)
+    _dotzsdb(tmp_path, 8)
+    before = stats()
+    rep = repack.repack_dir(str(tmp_path))
+    assert stats()[3] - before[3] >= rep["pack"]["region_bytes"]
+    want = zf.packed_file(zf.repack_finalised(images), UUID, 3, 7)
+    out = tmp_path / f"zeroskip-{UUIDSTR}-3-7"
+    assert rep["branch"] == 1 and rep["path"] == str(out) and (rep["startidx"], rep["endidx"]) == (3, 7)
     assert open(out, "rb").read() == want
-    assert rep["records"] == len(merged)
-    assert os.path.getsize(out) == rep["file_bytes"]
+    assert rep["records_out"] == len(zf.repack_finalised(images)) and rep["records_in"] == 1000
+    assert sorted(os.listdir(tmp_path)) == sorted([".zsdb", f"zeroskip-{UUIDSTR}-0-2", f"zeroskip-{UUIDSTR}-3-7",
+                                                   f"zeroskip-{UUIDSTR}-8"])
+    assert open(tmp_path / ".zsdb", "rb").read() == zf.dotzsdb_bytes(4096, UUIDSTR.encode() + b"\0", 8)
+
+
+def test_repack_dir_packed_files(gpu, tmp_path):
+    """zsdb_repack branch 2 (src/zeroskip.c:1510-1565): no finalised files,
+    three packed files -> the first two of the reference's pflist (the two
+    newest) merged by its packed-files iterator (the older of the two wins a
+    key in both; a winning delete drops the key), byte for byte against the
+    format oracle; a long records region (long commit) on the way."""
+    rng = np.random.default_rng(8)
+
+    def recs(n, lo, hi, vmax):
+        out = {}
+        for _ in range(n):
+            k = b"%016d" % int(rng.integers(lo, hi))
+            out[k] = None if rng.integers(0, 9) == 0 else rng.integers(0, 256, int(rng.integers(0, vmax)),
+                                                                     dtype=np.uint8).tobytes()
+        return sorted(out.items())
+    files = {(0, 3): recs(400, 0, 900, 300), (4, 7): recs(3000, 300, 40000, 14000), (8, 9): recs(600, 0, 5000, 500)}
+    imgs = {}
+    for (s_, e_), r in files.items():
+        imgs[(s_, e_)] = zf.packed_file(r, UUID, s_, e_)
+        (tmp_path / f"zeroskip-{UUIDSTR}-{s_}-{e_}").write_bytes(imgs[(s_, e_)])
+    _dotzsdb(tmp_path, 10)
+    rep = repack.repack_dir(str(tmp_path))
+    want = zf.packed_file(zf.repack_packed(imgs[(4, 7)], imgs[(8, 9)]), UUID, 4, 9)
+    out = tmp_path / f"zeroskip-{UUIDSTR}-4-9"
+    assert rep["branch"] == 2 and rep["files_merged"] == 2 and rep["path"] == str(out)
+    assert open(out, "rb").read() == want
+    assert rep["pack"]["region_bytes"] > zf.MAX_SHORT_VAL_LEN
+    assert sorted(os.listdir(tmp_path)) == sorted([".zsdb", f"zeroskip-{UUIDSTR}-0-3", f"zeroskip-{UUIDSTR}-4-9"])
+    r = zsfile.verify_image(open(out, "rb").read(), zsfile.PACKED)
+    assert r["n_bad"] == 0 and r["n_commits"] == 2
+    # nothing left to pack: branch 0, .zsdb still rewritten
+    rep2 = repack.repack_dir(str(tmp_path))
+    assert rep2["branch"] == 2            # 0-3 and 4-9 are two packed files
+    rep3 = repack.repack_dir(str(tmp_path))
+    assert rep3["branch"] == 0 and len([f for f in os.listdir(tmp_path) if f.startswith("zeroskip")]) == 1
+
+
+def test_packer_abort_removes_file(gpu, tmp_path):
+    """an exception inside the Packer context writes no commits and removes
+    the partial file (the reference xunlinks it, zeroskip-packed.c:465-466)"""
+    path = tmp_path / "partial"
+    with pytest.raises(RuntimeError):
+        with repack.Packer(str(path), UUID, 1, 2) as p:
+            p.add(b"a" * 16, b"x" * 100)
+            raise RuntimeError("interrupted")
+    assert not path.exists()

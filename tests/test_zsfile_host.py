@@ -83,3 +83,44 @@ def test_walk_survives_corrupt_lengths(case):
     off, ln, rc, end = zsfile.walk(img)
     assert rc == zsfile.TRUNCATED, (case, rc, end)
     assert zf.HDR_SIZE <= end <= len(img)
+
+
+def test_record_lister_matches_oracle():
+    """zscrc_zs_records (C) lists the same records as the format oracle's
+    walk (finalised files: adds, deletes, overwrites, empty values) and
+    pointer section (packed files, incl. a long value record); CPU only."""
+    import numpy as np
+    from oracle import zs_format as zf
+    from tests.test_format_oracle import UUID
+    from zeroskip_amd import repack, zsfile
+    rng = np.random.default_rng(31)
+    w = zf.FileWriter(UUID, idx=4)
+    for t in range(300):
+        k = b"%016d" % int(rng.integers(0, 90))
+        if t % 11 == 3:
+            w.remove(k)
+        else:
+            w.add(k, rng.integers(0, 256, int(rng.integers(0, 700)), dtype=np.uint8).tobytes())
+        if t % 3 == 0:
+            w.commit()
+    w.commit()
+    img = w.image()
+    (ko, kl, vo, vl), rc = repack.records(img, zsfile.FINALISED)
+    got = [(img[a:a + b], None if c == 2**64 - 1 else img[c:c + d]) for a, b, c, d in zip(ko, kl, vo, vl)]
+    assert rc == zsfile.END and got == zf.file_records(img)
+    recs = sorted({b"%08d" % i: (None if i % 7 == 1 else bytes([i % 256]) * (i % 50)) for i in range(400)}.items())
+    recs[5] = (recs[5][0], b"L" * ((16 << 20) + 9))
+    pimg = zf.packed_file(recs, UUID, 1, 9)
+    (ko, kl, vo, vl), rc = repack.records(pimg, zsfile.PACKED)
+    got = [(pimg[a:a + b], None if c == 2**64 - 1 else pimg[c:c + d]) for a, b, c, d in zip(ko, kl, vo, vl)]
+    assert rc == 0 and got == zf.packed_records(pimg) == recs
+
+
+def test_dotzsdb_build_matches_oracle():
+    import ctypes
+    from oracle import zs_format as zf
+    from zeroskip_amd._lib import lib
+    u = b"00010203-0405-0607-0809-0a0b0c0d0e0f"
+    out = (ctypes.c_uint8 * 61)()
+    assert lib().zscrc_zs_dotzsdb_build(123456789, u, 77, out) == 0
+    assert bytes(out) == zf.dotzsdb_bytes(123456789, u + b"\0", 77)

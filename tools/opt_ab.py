@@ -25,6 +25,9 @@ def main():
     img = zg.log_files(bytes(range(16)), 0, nfiles, ppf, 0, True, g, dev).view(-1)
     offs, lens = zg.log_spans(nfiles, ppf, True, True, dev)
     mx = int(lens.max().item())
+    live = lens > 0
+    vout = (torch.empty(1, dtype=torch.int64, device=dev), torch.empty(4096, dtype=torch.int64, device=dev))
+    ow, lw = offs[live].contiguous(), lens[live].contiguous()
     fx = torch.randint(0, 256, (320 * 10_000_000,), dtype=torch.uint8, device=dev, generator=g)
     only = os.environ.get("AB_CASES")
     bufs = torch.randint(0, 256, (32, 64 << 20), dtype=torch.uint8, device=dev, generator=g)
@@ -35,6 +38,9 @@ def main():
              "fixed_4KiB": lambda: zd.crc_fixed(c3, 4096, 4096, 1 << 20),
              "fixed_1MiB": lambda: zd.crc_fixed(c3, 1 << 20, 1 << 20, 4096),
              "config4_verify": lambda: zsfile.verify_commits(img, offs, lens, max_len=mx),
+             "config4_write": lambda: zsfile.write_commits(img, ow, lw, max_len=mx),
+             "config4_write_nocrc": lambda: zsfile.write_commits(img, ow, lw, max_len=mx, crc=False),
+             "config4_verdict": lambda: zsfile.verify_commits_verdict(img, offs, lens, max_len=mx, out=vout),
              "fixed_320x312": lambda: zd.crc_fixed(fx, 320, 312, 10_000_000),
              "config2_multi32": lambda: torch.stack(zd.crc_fixed_multi(blist, 64, 64, 1 << 20)),
              "config2_warm32": lambda: torch.stack(zd.crc_fixed_multi([blist[0]] * 32, 64, 64, 1 << 20))}
@@ -59,9 +65,9 @@ def main():
         row = {"case": name}
         for m in modes:
             row[f"opt{m}_ms"] = round(sorted(ts[m])[len(ts[m]) // 2], 4)
-            o = outs[m] if isinstance(outs[m], torch.Tensor) else outs[m][0]
-            o0 = outs[modes[0]] if isinstance(outs[modes[0]], torch.Tensor) else outs[modes[0]][0]
-            if not torch.equal(o, o0):
+            o = outs[m] if isinstance(outs[m], torch.Tensor) or outs[m] is None else outs[m][0]
+            o0 = outs[modes[0]] if isinstance(outs[modes[0]], torch.Tensor) or outs[modes[0]] is None else outs[modes[0]][0]
+            if o is not None and o0 is not None and not torch.equal(o, o0):
                 row[f"opt{m}_MISMATCH"] = True
         print(json.dumps(row), flush=True)
 

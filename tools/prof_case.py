@@ -39,6 +39,16 @@ def main():
         offs, lens = zg.log_spans(nfiles, ppf, True, True, dev)
         mx = int(lens.max().item())
         run = lambda k: zsfile.verify_commits(img.view(-1), offs, lens, max_len=mx)  # noqa: E731
+    elif cfg == "config4w":
+        # the writer side of config 4: every live commit's CRC recomputed and stored
+        from tools import zsdb_gen as zg
+        ppf = zg.pairs_per_file(True)
+        nfiles = -(-10_000_000 // ppf)
+        img = zg.log_files(bytes(range(16)), 0, nfiles, ppf, 0, True, g, dev)
+        offs, lens = zg.log_spans(nfiles, ppf, True, True, dev)
+        live = lens > 0
+        ow, lw = offs[live].contiguous(), lens[live].contiguous()
+        run = lambda k: zsfile.write_commits(img.view(-1), ow, lw, max_len=312)  # noqa: E731
     elif cfg == "config5":
         from tools import zsdb_gen as zg
         from zeroskip_amd import consistent as cs

@@ -70,7 +70,17 @@ SIGNATURES = {
     "zscrc_pack_add": (_int, [_vp, _vp, _u64, _vp, _u64]),
     "zscrc_pack_add_batch": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz]),
     "zscrc_pack_close": (_int, [_vp, _vp]),
+    "zscrc_abi_version": (_int, []),
+    "zscrc_device_verify_commits_verdict": (_int, [_vp, _u64, _vp, _vp, _vp, _sz, _u64, _vp, _vp, _sz, _vp]),
+    "zscrc_pack_abort": (_int, [_vp]),
+    "zscrc_zs_records": (_int, [_vp, _u64, _int, _vp, _sz, _vp]),
+    "zscrc_zs_dotzsdb_build": (_int, [_u64, ctypes.c_char_p, _u32, _vp]),
+    "zscrc_zs_repack": (_int, [ctypes.c_char_p, ctypes.c_uint, _int, _vp]),
+    "zscrc_set_devices": (_int, [_vp, _int]),
+    "zscrc_files_devices": (_int, [_vp, _int]),
+    "zscrc_release_cache": (None, []),
 }
+ABI_VERSION = 3  # include/zscrc.h ZSCRC_ABI_VERSION
 
 ZSCRC_RAW = 1
 LEN_UNBOUNDED = (1 << 64) - 1  # ZSCRC_LEN_UNBOUNDED
@@ -98,10 +108,17 @@ def lib() -> ctypes.CDLL:
                 f"{LIB_PATH} is missing: build it with `make -C {_HERE}` "
                 "(there is no CPU fallback for the GPU engine)")
         L = ctypes.CDLL(LIB_PATH)
+        # an older build under ZSCRC_LIB_PATH (A/B timing runs) may lack the
+        # newer entry points; the in-tree library must have them all
+        other = bool(os.environ.get("ZSCRC_LIB_PATH"))
         for name, (res, args) in SIGNATURES.items():
+            if other and not hasattr(L, name):
+                continue
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
+        if not other and L.zscrc_abi_version() != ABI_VERSION:
+            raise ImportError(f"{LIB_PATH}: ABI {L.zscrc_abi_version()}, this binding expects {ABI_VERSION}")
         _lib = L
     return _lib
 

@@ -40,6 +40,7 @@ int zs_launch_burst(int fixed, int xp, int nb, const zs::BatchDesc *d, const uin
 int zs_launch_multi(const zs::BatchDesc *d, const zs::MultiBatch *m, const uint32_t *gtab, int grid,
                     hipStream_t stream);
 int zs_launch_xteam(int depth, const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
+int zs_launch_commit(const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
 int zs_launch_spans(const zs::XDesc *x, const zs::XMulti *m, const zs::SpanFolds *fs, const uint32_t *gtab,
                     int grid, hipStream_t stream);
 int zs_launch_mismatch_rows(const uint32_t *st, const uint32_t *crc, const int64_t *end, const uint8_t *img,
@@ -174,6 +175,7 @@ void build_gtab(uint32_t *t)
     for (int k = 0; k < 64; ++k)
         t[GT_POW2 + k] = zs_gf2_xpow8n(1ull << k);
     zs_gf2_shift_table(t + GT_U2, 4 + 64);
+    zs_gf2_shift_table(t + GT_Z192, 192);
 }
 
 /* Context of the current device, initialised on first use. */
@@ -402,6 +404,15 @@ int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t max_len =
          * straight over the caller's arrays, no classify (it is correct for
          * any length, so a wrong bound costs only time) */
         const int w0 = g_depth[0];
+        if (max_len <= g1 && d.commit && !d.desc && !(d.opt & 32768) && w0 < 0) {
+            /* bounded commit batch: commit_kernel (run rounds, verdicts) */
+            if (zs_launch_commit(&d, c->gtab, c->ncu, s)) {
+                set_err("commit kernel launch", hipGetLastError());
+                return ZSCRC_EHIP;
+            }
+            g_stat[2]++;
+            return ZSCRC_OK;
+        }
         if (max_len <= g1 && (w0 < 0 || w0 >= 9))
             return launch(c, 1, d, s, walk_for(1, 0, 1));
     }
@@ -1016,7 +1027,7 @@ int zscrc_internal_verify_commits(const void *d_image, uint64_t image_size, cons
 {
     if (n == 0)
         return ZSCRC_OK;
-    if (!d_image || !d_off || !d_len || !d_crc || (!write && !d_status))
+    if (!d_image || !d_off || !d_len || (!write && !d_crc) || (!write && !d_status))
         return ZSCRC_EINVAL;
     DevCtx *c;
     int rc = get_ctx(&c);
@@ -1034,6 +1045,40 @@ int zscrc_internal_verify_commits(const void *d_image, uint64_t image_size, cons
     d.n = n;
     d.xor_io = 0xffffffffu;
     return launch_classes(c, d, static_cast<hipStream_t>(stream), max_len);
+}
+
+int zscrc_device_verify_commits_verdict(const void *d_image, uint64_t image_size, const uint64_t *d_span_off,
+                                        const uint64_t *d_span_len, const uint32_t *d_seed, size_t n,
+                                        uint64_t max_len, uint64_t *d_nbad, uint64_t *d_bad, size_t cap,
+                                        void *stream)
+{
+    if (!d_nbad || (cap && !d_bad) || (n && (!d_image || !d_span_off || !d_span_len)))
+        return ZSCRC_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipError_t e = hipMemsetAsync(d_nbad, 0, sizeof(uint64_t), s);
+    if (e != hipSuccess) {
+        set_err("hipMemsetAsync(verdict count)", e);
+        return ZSCRC_EHIP;
+    }
+    if (n == 0)
+        return ZSCRC_OK;
+    DevCtx *c;
+    int rc = get_ctx(&c);
+    if (rc)
+        return rc;
+    zs::BatchDesc d = make_desc();
+    d.base = static_cast<const uint8_t *>(d_image);
+    d.off = d_span_off;
+    d.len = d_span_len;
+    d.seed = d_seed;
+    d.commit = 1;
+    d.img_size = image_size;
+    d.n = n;
+    d.xor_io = 0xffffffffu;
+    d.bad_count = reinterpret_cast<unsigned long long *>(d_nbad);
+    d.bad_idx = d_bad;
+    d.bad_cap = cap;
+    return launch_classes(c, d, s, max_len);
 }
 
 const char *zscrc_last_error(void) { return t_err; }
@@ -1132,6 +1177,11 @@ void zscrc_set_teams(uint64_t g1_max, uint64_t g16_max)
     std::call_once(g_env_once, env_init);
     g_g1_max = g1_max;
     g_g16_max = g16_max;
+}
+
+int zscrc_abi_version(void)
+{
+    return ZSCRC_ABI_VERSION;
 }
 
 int zscrc_device_count(void)

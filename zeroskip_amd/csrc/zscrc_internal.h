@@ -12,7 +12,8 @@ enum {
     GT_Z = 3072,     /* GT_Z + k*1024: shift(b<<8j, 64<<k), k = 0..5          */
     GT_POW2 = 3072 + 6 * 1024, /* 64 words: x^(8*2^k) mod P, k = 0..63          */
     GT_U2 = 3072 + 6 * 1024 + 64, /* shift(b<<8j, 4 + 64): word then skip, 2-lane team */
-    GT_WORDS = 3072 + 6 * 1024 + 64 + 1024,
+    GT_Z192 = 3072 + 6 * 1024 + 64 + 1024, /* shift(b<<8j, 192): run rounds of burst_kernel */
+    GT_WORDS = 3072 + 6 * 1024 + 64 + 2 * 1024,
 };
 
 namespace zs {
@@ -62,8 +63,19 @@ struct BatchDesc {
     uint32_t opt;         /* tuning bits: 1 = no three-chain five-piece bursts, 2 = no multi64_kernel,
                              4 / 8 = qteam_kernel with XOR3 grouping 1 / 2,
                              16 = team_kernel<16>'s two-level walk with XOR3 grouping 2,
-                             1024 = direct burst batches without the descriptor prefetch */
+                             1024 = direct burst batches without the descriptor prefetch,
+                             2048 = no run rounds in commit bursts,
+                             4096 / 8192 = diagnostics of the run rounds (no chains / no
+                             trailer and result stores; results wrong),
+                             32768 = bounded commit batches on burst_kernel instead of
+                             commit_kernel */
     uint32_t *part_out;
+    /* commit verdict mode (bad_count != NULL): no per-record out / status;
+     * every commit whose status is not 1 is counted in *bad_count and its
+     * index stored in bad_idx[<bad_cap] (any order) */
+    unsigned long long *bad_count;
+    uint64_t *bad_idx;
+    uint64_t bad_cap;
     const struct SplitPlan *plan;
     const uint32_t *part_base;
     const uint32_t *part_rec;

@@ -300,6 +300,16 @@ int zscrc_pack_add_batch(zscrc_packer *pk, const void *keys, const uint64_t *key
     return ZSCRC_OK;
 }
 
+int zscrc_pack_abort(zscrc_packer *pk)
+{
+    /* a partial repack must never look valid: no commits, the file removed
+     * (the reference's fail path xunlinks it, src/zeroskip-packed.c:465-466) */
+    if (!pk)
+        return ZSCRC_EINVAL;
+    pk_free(pk, true);
+    return ZSCRC_OK;
+}
+
 int zscrc_pack_close(zscrc_packer *pk, zscrc_pack_report *rep)
 {
     if (!pk)

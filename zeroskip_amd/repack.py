@@ -6,17 +6,16 @@ The writer mirrors the reference's repack output path
 zs_packed_file_new_from_packed_files, :617-742): header, records in key order,
 records-region commit, pointer section, final commit.  Every byte of the
 records region and of the pointer section is checksummed on the GPU while the
-host writes the file.  ``repack_dir`` is the driver of zsdb_repack
-(src/zeroskip.c:1419-1571) for the checksum-relevant part: it merges the
-finalised files of a DB directory (newest record of a key wins, deletes kept
-as delete records, as the memtree of finalised records holds them) into one
-packed file.
+host writes the file.  ``repack_dir`` runs zsdb_repack (src/zeroskip.c:
+1419-1571) over a DB directory in ONE call into the library
+(zscrc_zs_repack, zeroskip_amd/csrc/zscrc_repack.cpp): record listing, the
+key merge (finalised files, or the reference's two packed files), the
+writer, the unlinks and the .zsdb rewrite are all C++.
 """
 from __future__ import annotations
 
 import ctypes
 import os
-import struct
 
 import numpy as np
 
@@ -108,57 +107,52 @@ class Packer:
         if et is None:
             self.close()
         elif self._h:
+            # an exception mid-packing: no commits, the partial file removed
             h, self._h = self._h, ctypes.c_void_p()
-            lib().zscrc_pack_close(h, None)   # frees the writer (file kept as written)
+            lib().zscrc_pack_abort(h)
 
 
 _EMPTY = ctypes.c_uint8(0)
 
 
-def _records_of(image) -> list[tuple[bytes, bytes | None]]:
-    """(key, value-or-None) of every record of an active/finalised file, in
-    file order, by the reference walk (src/zeroskip-record.c:283-331)."""
-    buf = memoryview(image)
-    out, off, n = [], 40, len(buf)
-    while off + 8 <= n:
-        w, = struct.unpack_from(">Q", buf, off)
-        t = w >> 56
-        if t in (1, 33):                              # KEY / LONG_KEY
-            if t == 1:
-                klen, voff = (w >> 40) & 0xFFFF, w & 0xFFFFFFFF
-            else:
-                klen, voff = struct.unpack_from(">QQ", buf, off + 8)
-            key = bytes(buf[off + 24:off + 24 + klen])
-            v = off + voff
-            vw, = struct.unpack_from(">Q", buf, v)
-            vlen = (vw >> 32) & 0xFFFFFF if (vw >> 56) == 2 else struct.unpack_from(">Q", buf, v + 8)[0]
-            out.append((key, bytes(buf[v + 16:v + 16 + vlen])))
-            off = v + 16 + ((vlen + 7) & ~7)
-        elif t in (64, 32):                           # DELETED / LONG_DELETED
-            klen = (w >> 40) & 0xFFFF if t == 64 else struct.unpack_from(">Q", buf, off + 8)[0]
-            out.append((bytes(buf[off + 24:off + 24 + klen]), None))
-            off += 24 + ((klen + 7) & ~7)
-        elif t in (4, 36):                            # COMMIT / LONG_COMMIT
-            off += 8 if t == 4 else 24
-        else:
-            break
-    return out
+class RepackReport(ctypes.Structure):
+    """zscrc_repack_report (include/zscrc.h)."""
+    _fields_ = [("branch", ctypes.c_int32), ("startidx", ctypes.c_uint32), ("endidx", ctypes.c_uint32),
+                ("files_merged", ctypes.c_uint64), ("records_in", ctypes.c_uint64),
+                ("records_out", ctypes.c_uint64), ("dotzsdb_crc", ctypes.c_uint32), ("pack", PackReport),
+                ("list_s", ctypes.c_double), ("merge_s", ctypes.c_double), ("write_s", ctypes.c_double),
+                ("total_s", ctypes.c_double), ("path", ctypes.c_char * 4096)]
+
+    def as_dict(self):
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("pack", "path")}
+        d["pack"] = self.pack.as_dict()
+        d["path"] = self.path.decode()
+        return d
 
 
-def repack_dir(dbdir: str, out_path: str, uuid: bytes, startidx: int, endidx: int,
-               chunk_bytes: int = 0) -> dict:
-    """Merge the finalised files `zeroskip-<uuid>-<idx>-<idx>` of dbdir (in
-    index order; the newest record of a key wins) into one packed file at
-    out_path, CRCs on the GPU.  Returns the writer's report."""
-    from . import consistent, zsfile
-    db = consistent.open_db(dbdir)
-    merged: dict[bytes, bytes | None] = {}
-    for f in db.files:                     # sorted by index: newer files last
-        if f.kind == zsfile.FINALISED:
-            for k, v in _records_of(f.image):
-                merged[k] = v
-    keys = sorted(merged)
-    with Packer(out_path, uuid, startidx, endidx, chunk_bytes=chunk_bytes) as p:
-        for i in range(0, len(keys), 65536):
-            p.add_many((k, merged[k]) for k in keys[i:i + 65536])
-    return p.report
+def repack_dir(dbdir: str, threads: int = 0, fsync: bool = False) -> dict:
+    """zsdb_repack over a DB directory (zscrc_zs_repack): branch 1 merges the
+    finalised files, branch 2 the reference's two packed files; returns the
+    report (branch 0: nothing to pack)."""
+    rep = RepackReport()
+    check(lib().zscrc_zs_repack(os.fsencode(dbdir), FSYNC if fsync else 0, threads, ctypes.byref(rep)),
+          "zscrc_zs_repack")
+    return rep.as_dict()
+
+
+def records(image, kind: int):
+    """(key_off, key_len, val_off, val_len) uint64 arrays of a file image's
+    records (zscrc_zs_records); val_off == 2**64-1 marks a delete."""
+    a = np.ascontiguousarray(np.frombuffer(image, dtype=np.uint8) if isinstance(image, (bytes, bytearray))
+                             else image)
+    cap = a.nbytes // 32 + 16
+    while True:
+        out = np.empty((cap, 4), np.uint64)
+        n = ctypes.c_size_t()
+        rc = lib().zscrc_zs_records(a.ctypes.data, a.nbytes, kind, out.ctypes.data, cap, ctypes.byref(n))
+        if rc == 3:                              # ZSCRC_ZS_OVERFLOW
+            cap = n.value
+            continue
+        if rc < 0:
+            check(rc, "zscrc_zs_records")
+        return out[:n.value].T.copy(), rc

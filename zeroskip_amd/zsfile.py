@@ -112,21 +112,46 @@ def verify_commits(d_image: torch.Tensor, span_off: torch.Tensor, span_len: torc
     return crc, st
 
 
+def verify_commits_verdict(d_image: torch.Tensor, span_off: torch.Tensor, span_len: torch.Tensor,
+                           seed: torch.Tensor | None = None, max_len: int | None = None, cap: int = 4096,
+                           out: tuple | None = None):
+    """Device verdict (zscrc_device_verify_commits_verdict): (nbad, bad)
+    int64 device tensors -- nbad[0] = commits that do not verify, bad[:min(
+    nbad, cap)] their indices in no particular order.  No per-commit output.
+    `out`: preallocated (nbad, bad) tensors to reuse."""
+    n = span_off.numel()
+    size = d_image.numel() * d_image.element_size()
+    dev = d_image.device
+    if out is None:
+        out = (torch.empty(1, dtype=torch.int64, device=dev), torch.empty(max(cap, 1), dtype=torch.int64, device=dev))
+    nbad, bad = out
+    assert seed is None or (seed.numel() == n and seed.dtype == torch.int32)
+    with torch.cuda.device(dev):
+        check(lib().zscrc_device_verify_commits_verdict(
+            d_image.data_ptr(), size, span_off.data_ptr(), span_len.data_ptr(),
+            None if seed is None else seed.data_ptr(), n, LEN_UNBOUNDED if max_len is None else max_len,
+            nbad.data_ptr(), bad.data_ptr(), min(cap, bad.numel()),
+            torch.cuda.current_stream(dev).cuda_stream), "zscrc_device_verify_commits_verdict")
+    return nbad, bad
+
+
 def write_commits(d_image: torch.Tensor, span_off: torch.Tensor, span_len: torch.Tensor,
-                  max_len: int | None = None, status: bool = False):
+                  max_len: int | None = None, status: bool = False, crc: bool = True):
     """Writer side on the GPU: compute every commit CRC and store it
     big-endian into its commit record in `d_image` (in place).  max_len: a
     known bound on the span lengths (zscrc_device_write_commits_bounded).
+    crc=False: the CRCs only go into the image (returns None).
     Returns the CRCs, or (crc, status) with status=True: 1 written, 2 no
     commit record there (nothing written)."""
     n = span_off.numel()
     size = d_image.numel() * d_image.element_size()
-    crc = torch.empty(n, dtype=torch.int32, device=d_image.device)
+    want_crc = crc
+    crc = torch.empty(n, dtype=torch.int32, device=d_image.device) if want_crc else None
     st = torch.empty(n, dtype=torch.int32, device=d_image.device) if status else None
     with torch.cuda.device(d_image.device):
         check(lib().zscrc_device_write_commits_bounded(
             d_image.data_ptr(), size, span_off.data_ptr(), span_len.data_ptr(), n,
-            LEN_UNBOUNDED if max_len is None else max_len, crc.data_ptr(),
+            LEN_UNBOUNDED if max_len is None else max_len, None if crc is None else crc.data_ptr(),
             None if st is None else st.data_ptr(),
             torch.cuda.current_stream(d_image.device).cuda_stream), "zscrc_device_write_commits_bounded")
     return (crc, st) if status else crc
@@ -139,10 +164,29 @@ class FilesReport(ctypes.Structure):
                 ("header_errors", ctypes.c_uint64), ("walk_errors", ctypes.c_uint64),
                 ("first_bad_file", ctypes.c_uint64), ("first_bad_off", ctypes.c_uint64),
                 ("first_bad_what", ctypes.c_int32), ("threads", ctypes.c_int32), ("staged", ctypes.c_int32),
-                ("copy_s", ctypes.c_double), ("verify_tail_s", ctypes.c_double), ("total_s", ctypes.c_double)]
+                ("copy_s", ctypes.c_double), ("verify_tail_s", ctypes.c_double), ("total_s", ctypes.c_double),
+                ("devices", ctypes.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+def set_devices(ids) -> None:
+    """Device slots of verify_files / consistent (zscrc_set_devices): a list
+    of device ids, repeats allowed; None or [] = the default (env
+    ZSCRC_DEVICES, else every visible gfx950 device)."""
+    ids = list(ids or [])
+    arr = (ctypes.c_int * max(1, len(ids)))(*ids)
+    check(lib().zscrc_set_devices(arr, len(ids)), "zscrc_set_devices")
+
+
+def devices() -> list:
+    """The device slots a verify_files call would use now."""
+    arr = (ctypes.c_int * 64)()
+    n = lib().zscrc_files_devices(arr, 64)
+    if n < 0:
+        check(n, "zscrc_files_devices")
+    return list(arr[:n])
 
 
 def verify_files(images, kinds=None, threads: int = 0) -> dict:
