@@ -15,8 +15,9 @@ Other BASELINE configs (parity/measurement runs, same JSON shape):
            rotating 64 MiB batches = 2 GiB, beyond the 256 MB L3); warm rate
            (one batch, L3-resident) alongside.
   config4  zsbench replay: 10 M pairs as byte-exact zeroskip log files
-           (1,526 files, 10 M commits of 312 B spans); one step = GPU verify of
-           every commit; GPU write, NOTBATCHED and end-to-end rates alongside.
+           (1,526 files, 10 M commits of 312 B spans); one step = the GPU
+           verdict of every commit; per-commit arrays, the GPU writer,
+           NOTBATCHED and end-to-end rates (both directions) alongside.
   config5  `consistent` full-DB re-checksum of an ~8 GiB DB (2 packed files of
            3 GiB with long commits, 1,024 finalised files, active file,
            .zsdb); strong scaling: the DB is split across ranks, digests
@@ -408,7 +409,26 @@ def run_config2(args, world, rank, dev, stream):
 
 
 # ------------------------------------------------------------------ config 4
+def _timed(fn, reps: int, stream) -> float:
+    """median ms of `reps` calls of fn (HIP events on `stream`), one warm call first"""
+    fn()
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        fn()
+        b.record(stream)
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b))
+    return float(np.median(ts))
+
+
 def run_config4(args, world, rank, dev, stream):
+    """zsbench writeseqtxn replay (10 M pairs as byte-exact log files).  One
+    step = the verdict of every commit on the GPU
+    (zscrc_device_verify_commits_verdict: commit_kernel, spans bounded by the
+    walk, no per-commit output); per-commit crc/status arrays, the writer, the
+    NOTBATCHED layout and the host-memory pipelines both ways alongside."""
     from tools import zsdb_gen as zg
     pairs_total = args.pairs
     ppf = zg.pairs_per_file(True)
@@ -425,15 +445,14 @@ def run_config4(args, world, rank, dev, stream):
     ncommit = offs.numel()
     span_bytes = int(lens.sum().item())
     # the longest span is known to the walk that found the commits (here: the
-    # replay's layout), as in consistent.py; it lets the library skip the
-    # device-side length classes (zscrc_device_verify_commits_bounded)
+    # replay's layout), as in consistent.py and zscrc_zs_verify_files
     max_span = int(lens.max().item())
-    res = {}
+    vout = (torch.empty(1, dtype=torch.int64, device=dev), torch.empty(4096, dtype=torch.int64, device=dev))
 
     def step(ev):
         if ev:
             ev[0].record(stream)
-        res["crc"], res["st"] = zsfile.verify_commits(flat, offs, lens, max_len=max_span)
+        zsfile.verify_commits_verdict(flat, offs, lens, max_len=max_span, out=vout)
         if ev:
             ev[1].record(stream)
 
@@ -441,45 +460,47 @@ def run_config4(args, world, rank, dev, stream):
     tm = Timer(world, dev)
     elapsed = tm.run(step, args.steps, args.warmup)
     kern_ms = float(np.mean(tm.kern_ms))
+    # the verdict: exactly the stale zero-length finalise commits (one per file)
+    nbad = int(vout[0].item())
+    stale = torch.nonzero(lens == 0).flatten()
+    bad = torch.sort(vout[1][:nbad]).values
+    assert nbad == nfiles and torch.equal(bad, stale), (nbad, nfiles)
+
+    # per-commit crc + status arrays (zscrc_device_verify_commits_bounded)
+    res = {}
+
+    def arrays():
+        res["crc"], res["st"] = zsfile.verify_commits(flat, offs, lens, max_len=max_span)
+    arrays_ms = _timed(arrays, 10, stream)
     st = res["st"]
     n_ok = int((st == 1).sum().item())
-    n_stale = int(((st == 0) & (lens == 0)).sum().item())
-    assert n_ok + n_stale == ncommit and n_stale == nfiles, (n_ok, n_stale, ncommit)
+    assert n_ok + nfiles == ncommit
 
     # writer side: recompute + store every commit CRC (the image is unchanged;
     # the stale finalise commits are not rewritten)
     offs_w, lens_w = offs[lens > 0].contiguous(), lens[lens > 0].contiguous()
-    ws = []
-    for i in range(6):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        zsfile.write_commits(flat, offs_w, lens_w, max_len=max_span)
-        b.record(stream)
-        torch.cuda.synchronize()
-        if i:
-            ws.append(a.elapsed_time(b))
-    write_ms = float(np.median(ws))
+    write_ms = _timed(lambda: zsfile.write_commits(flat, offs_w, lens_w, max_len=max_span, crc=False), 6, stream)
+    write_crc_ms = _timed(lambda: zsfile.write_commits(flat, offs_w, lens_w, max_len=max_span), 6, stream)
 
-    # NOTBATCHED (zsbench writeseq): one commit per ~2 MiB file
+    # NOTBATCHED (zsbench writeseq): one commit per ~2 MiB file, unbounded
+    # (device length classes; the spans go to xteam_kernel's parts mode)
     ppf_nb = zg.pairs_per_file(False)
     nf_nb = -(-pairs_total // ppf_nb)
     img_nb = zg.log_files(uuid, 0, nf_nb, ppf_nb, 0, False, gen, dev, batched=False)
     o_nb, l_nb = zg.log_spans(nf_nb, ppf_nb, False, False, dev)
-    nb = []
-    for i in range(6):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        _, st_nb = zsfile.verify_commits(img_nb.view(-1), o_nb, l_nb)
-        b.record(stream)
-        torch.cuda.synchronize()
-        if i:
-            nb.append(a.elapsed_time(b))
-    assert bool((st_nb == 1).all())
-    nb_ms = float(np.median(nb))
-    nb_bytes = int(l_nb.sum().item()) + 8 * nf_nb
+    nbo = (torch.empty(1, dtype=torch.int64, device=dev), torch.empty(64, dtype=torch.int64, device=dev))
+    nb_ms = _timed(lambda: zsfile.verify_commits_verdict(img_nb.view(-1), o_nb, l_nb, out=nbo), 6, stream)
+    assert int(nbo[0].item()) == 0
+    nb_arr = {}
+
+    def nb_arrays():
+        nb_arr["st"] = zsfile.verify_commits(img_nb.view(-1), o_nb, l_nb)[1]
+    nb_arrays_ms = _timed(nb_arrays, 6, stream)
+    assert bool((nb_arr["st"] == 1).all())
+    nb_bytes = int(l_nb.sum().item()) + 24 * nf_nb
     del img_nb
 
-    # end to end: host image -> H2D (pinned / pageable) -> host walk (threads) -> verify
+    # end to end from host memory, both directions
     e2e = {}
     if rank == 0 and not args.no_e2e:
         host = img.cpu()
@@ -491,8 +512,8 @@ def run_config4(args, world, rank, dev, stream):
             img.copy_(src, non_blocking=True)
             torch.cuda.synchronize()
             e2e[f"h2d_{kind}_GBs"] = round(img.numel() / (time.perf_counter() - t0) / 1e9, 2)
-        # the real pipeline: zscrc_zs_verify_files over the host file images
-        # (threaded walks + pinned staging + overlapped H2D + one verify)
+        # verify: zscrc_zs_verify_files over the host file images (threaded
+        # walks + pinned staging + overlapped H2D + one verify)
         images = list(host.numpy().reshape(nfiles, -1))
         kinds = [zsfile.FINALISED] * nfiles
         zsfile.verify_files(images, kinds)                 # warm: pinned slots, device buffers
@@ -505,23 +526,49 @@ def run_config4(args, world, rank, dev, stream):
         assert rep["commits"] == ncommit and rep["bad_commits"] == 0, rep
         e2e["verify_files_s"] = round(best, 4)
         e2e["verify_files_GBs"] = round(host.numel() / best / 1e9, 2)
-        e2e["note"] = ("host file images -> verdicts, walks included (zscrc_zs_verify_files, "
-                       f"{rep['threads']} host threads); PCIe-bound, never the line's value")
-        del images, pinned
+        # write: host images -> H2D -> write_commits -> D2H of the images
+        back = torch.empty(host.shape, dtype=torch.uint8, pin_memory=True)
+        for kind, src, dst in (("pinned", pinned, back), ("pageable", host, torch.empty_like(host))):
+            ts = []
+            for _ in range(3):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                img.copy_(src, non_blocking=True)
+                zsfile.write_commits(flat, offs_w, lens_w, max_len=max_span, crc=False)
+                dst.copy_(img, non_blocking=True)
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t0)
+            e2e[f"write_{kind}_s"] = round(min(ts), 4)
+            e2e[f"write_{kind}_GBs"] = round(host.numel() / min(ts) / 1e9, 2)
+        assert torch.equal(back, pinned)
+        e2e["note"] = ("verify: host file images -> verdicts, walks included (zscrc_zs_verify_files, "
+                       f"{rep['threads']} host threads); write: host images -> H2D -> GPU commit writer -> "
+                       "D2H of the images (image bytes / wall time); PCIe-bound, never the line's value")
+        del images, pinned, back
 
-    nbytes = span_bytes + 8 * ncommit + 16 * ncommit + 8 * ncommit   # spans + trailers + descriptors + crc/status
-    r = roof(nbytes, kern_ms, "verify_commits, spans bounded by the walk: one zs::burst_kernel launch (312 B spans)",
+    nbytes = span_bytes + 8 * ncommit + 16 * ncommit   # spans + commit trailers + descriptors
+    r = roof(nbytes, kern_ms, "zs::commit_kernel<false> (verdict: run rounds of 64 back-to-back spans as coalesced "
+                              "1 KiB loads, quad bursts elsewhere)",
              traffic_for("config4_bytes_per_launch"), read_peak)
     out_line = line(args, world, elapsed, span_bytes * world * args.steps,
                     {"workload": f"config4: zsbench writeseqtxn replay, {pairs_total} pairs per GPU, "
                                  f"{nfiles} log files, {ncommit} commits (312 B spans + stale finalise "
-                                 "commits), GPU verify of every commit", "pairs": pairs_total,
+                                 "commits), GPU verdict of every commit", "pairs": pairs_total,
                      "files": nfiles, "commits": ncommit, "parallelism": f"replica{world}"},
                     r, data="synthetic zsbench records (key %016d, 255 charset chars + NUL, fixed seed), "
                             "byte-exact zeroskip log images in HBM",
-                    write={"ms": round(write_ms, 4), "GBs": round((span_bytes + 8 * ncommit) / (write_ms * 1e-3) / 1e9, 1)},
+                    verdict={"bad_commits": nbad, "stale_finalise_commits": nfiles},
+                    per_commit_arrays={"ms": round(arrays_ms, 4),
+                                       "GBs": round((nbytes + 8 * ncommit) / (arrays_ms * 1e-3) / 1e9, 1),
+                                       "note": "zscrc_device_verify_commits_bounded: crc + status per commit "
+                                               "(8 B of HBM writes per commit)"},
+                    write={"ms": round(write_ms, 4), "GBs": round((span_bytes + 8 * ncommit) / (write_ms * 1e-3) / 1e9, 1),
+                           "ms_with_crc_array": round(write_crc_ms, 4),
+                           "note": "zscrc_device_write_commits_bounded, CRCs into the image (d_crc NULL)"},
                     notbatched={"files": nf_nb, "commits": nf_nb, "verify_ms": round(nb_ms, 4),
-                                "GBs": round(nb_bytes / (nb_ms * 1e-3) / 1e9, 1)},
+                                "GBs": round(nb_bytes / (nb_ms * 1e-3) / 1e9, 1),
+                                "frac": round(nb_bytes / (nb_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                "arrays_ms": round(nb_arrays_ms, 4)},
                     e2e=e2e, gen_s=round(t_gen, 2))
     if rank == 0 and world == 1 and not args.no_cpu:
         k = 200_000

@@ -335,6 +335,51 @@ typedef struct zscrc_consistent_report {
 } zscrc_consistent_report;
 int zscrc_zs_consistent(const char *dbdir, zscrc_consistent_report *rep);
 
+/* The device pass of `consistent` over a prepared, device-resident share of
+ * a DB (zeroskip_amd/consistent.py's inner loop, in C): the commits of
+ * active / finalised files as ONE verdict batch (no per-commit output), up
+ * to ZSCRC_CPASS_SPANS raw spans (records-region pieces, pointer sections),
+ * one post kernel -- zero-length finalise commits that chain from the
+ * previous span's CRC (src/zeroskip-active.c:122 + src/mfile.c:534-546)
+ * told from bad ones, the commit trailer after every span whose commit
+ * record is in the image checked (src/zeroskip-file.c:266-302) -- and ONE
+ * small device->host copy.  All pointers named d_* are device pointers. */
+#define ZSCRC_CPASS_SPANS 64
+#define ZSCRC_CPASS_LIST 1000
+typedef struct zscrc_cpass zscrc_cpass;
+typedef struct zscrc_cpass_spec {
+    const void *d_image;
+    uint64_t image_size;
+    size_t n;                     /* commits                                     */
+    const uint64_t *d_off;        /* commit spans: image offsets / lengths       */
+    const uint64_t *d_len;
+    const uint32_t *d_file;       /* file id of each commit                      */
+    uint64_t max_len;             /* bound on the span lengths (the host walk's) */
+    size_t nspans;                /* raw spans                                   */
+    const uint64_t *span_off;     /* host arrays: image offset, length, and the  */
+    const uint64_t *span_len;     /* image offset of the span's commit record   */
+    const int64_t *span_commit;   /* (-1: not in this image -- a split piece)    */
+} zscrc_cpass_spec;
+typedef struct zscrc_cpass_result {
+    uint64_t n_bad;               /* commits that do not verify (undecided incl.) */
+    uint64_t n_stale;             /* finalise-quirk commits                       */
+    uint64_t n_undecided;         /* zero-length commits after a long span or with a
+                                   * long trailer: the caller decides (indices below) */
+    int32_t complete;             /* 0: more mismatches than one pass lists       */
+    int32_t pad_;
+    uint64_t n_listed_bad, n_listed_stale;
+    uint64_t bad[ZSCRC_CPASS_LIST];        /* commit indices, ascending, undecided excl. */
+    uint64_t stale[ZSCRC_CPASS_LIST];
+    uint64_t undecided[ZSCRC_CPASS_SPANS];
+    uint32_t span_raw[ZSCRC_CPASS_SPANS];  /* raw register of each span (from 0)         */
+    int32_t span_status[ZSCRC_CPASS_SPANS]; /* 1 ok, 0 mismatch, 2 no commit record,
+                                             * -1 not checked (span_commit -1)            */
+} zscrc_cpass_result;
+int zscrc_cpass_create(zscrc_cpass **p, const zscrc_cpass_spec *spec);
+/* Synchronous on `stream` (NULL = default). */
+int zscrc_cpass_run(zscrc_cpass *p, void *stream, zscrc_cpass_result *res);
+void zscrc_cpass_destroy(zscrc_cpass *p);
+
 /* End to end from host memory: every CRC of n zeroskip file images (mmap'd
  * files; kinds[i] = ZSCRC_ZS_ACTIVE / _FINALISED / _PACKED) -- header, record
  * walk and every commit of active / finalised files, records-region and

@@ -65,18 +65,21 @@ def test_oracle_db_corruption(gpu, what):
         assert [h[0] for h in g.header_errors] == [f]
 
 
-@pytest.mark.parametrize("post", ["native", "native-overflow", "torch"])
+@pytest.mark.parametrize("post", ["cpass", "native", "native-overflow", "torch"])
 def test_post_pass_paths(gpu, monkeypatch, post):
-    """The mismatch post-pass: the native row kernel (one copy back), its
-    overflow fallback (more mismatches than the row buffer) and the torch
-    path give the oracle backend's report, with stale finalise commits and a
-    corrupted commit in the same DB."""
+    """The device pass: the one-call native pass (zscrc_cpass: verdict batch,
+    post kernel, one small copy), the per-commit arrays with the row kernel
+    (one copy back), its overflow fallback (more mismatches than the row
+    buffer) and the torch path give the oracle backend's report, with stale
+    finalise commits and a corrupted commit in the same DB."""
     db = small_db(long_region=True)
     f = name(7, 7)
     img = bytearray(db[f])
     c = zf.walk(img)[0][5]
     img[c["span_off"] + 3] ^= 0x10
     db[f] = bytes(img)
+    if post != "cpass":
+        monkeypatch.setattr(cs.GpuBackend, "native_pass", False)
     if post == "torch":
         monkeypatch.setenv("ZS_POSTPASS", "torch")
     elif post == "native-overflow":

@@ -8,7 +8,7 @@
  * "bytes" there is the SUM of the CRCs, a label bug recorded in SURVEY.md
  * Appendix A) and a corrected line with the byte count and GB/s, then one JSON
  * line.  Modes: hw = crc32c_hw (SSE4.2 3-way path), sw = crc32c_sw
- * (slice-by-4), default = crc32c() after crc32c_init (the dispatch), zlib =
+ * (libzscrc: slice-by-8; the reference: slice-by-4), default = crc32c() after crc32c_init (the dispatch), zlib =
  * zlib crc32 (CRC-32, another polynomial: timing context only).  Exit 1 if a
  * CRC differs from the golden value or the three CRC-32C modes disagree.
  *

@@ -28,6 +28,10 @@ def main():
     live = lens > 0
     vout = (torch.empty(1, dtype=torch.int64, device=dev), torch.empty(4096, dtype=torch.int64, device=dev))
     ow, lw = offs[live].contiguous(), lens[live].contiguous()
+    nb_files = -(-10_000_000 // zg.pairs_per_file(False))
+    img_nb = zg.log_files(bytes(range(16)), 0, nb_files, zg.pairs_per_file(False), 0, False, g, dev,
+                          batched=False).view(-1) if "config4_nb" in (os.environ.get("AB_CASES") or "") else None
+    o_nb, l_nb = zg.log_spans(nb_files, zg.pairs_per_file(False), False, False, dev)
     fx = torch.randint(0, 256, (320 * 10_000_000,), dtype=torch.uint8, device=dev, generator=g)
     only = os.environ.get("AB_CASES")
     bufs = torch.randint(0, 256, (32, 64 << 20), dtype=torch.uint8, device=dev, generator=g)
@@ -41,6 +45,7 @@ def main():
              "config4_write": lambda: zsfile.write_commits(img, ow, lw, max_len=mx),
              "config4_write_nocrc": lambda: zsfile.write_commits(img, ow, lw, max_len=mx, crc=False),
              "config4_verdict": lambda: zsfile.verify_commits_verdict(img, offs, lens, max_len=mx, out=vout),
+             "config4_nb": lambda: zsfile.verify_commits(img_nb, o_nb, l_nb)[1],
              "fixed_320x312": lambda: zd.crc_fixed(fx, 320, 312, 10_000_000),
              "config2_multi32": lambda: torch.stack(zd.crc_fixed_multi(blist, 64, 64, 1 << 20)),
              "config2_warm32": lambda: torch.stack(zd.crc_fixed_multi([blist[0]] * 32, 64, 64, 1 << 20))}

@@ -71,6 +71,9 @@ SIGNATURES = {
     "zscrc_pack_add_batch": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz]),
     "zscrc_pack_close": (_int, [_vp, _vp]),
     "zscrc_abi_version": (_int, []),
+    "zscrc_cpass_create": (_int, [_vp, _vp]),
+    "zscrc_cpass_run": (_int, [_vp, _vp, _vp]),
+    "zscrc_cpass_destroy": (None, [_vp]),
     "zscrc_device_verify_commits_verdict": (_int, [_vp, _u64, _vp, _vp, _vp, _sz, _u64, _vp, _vp, _sz, _vp]),
     "zscrc_pack_abort": (_int, [_vp]),
     "zscrc_zs_records": (_int, [_vp, _u64, _int, _vp, _sz, _vp]),

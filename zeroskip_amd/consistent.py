@@ -141,6 +141,34 @@ def open_db(src) -> Db:
     return Db(dot, files)
 
 
+# ------------------------------------------------------- the native pass
+CPASS_SPANS, CPASS_LIST = 64, 1000   # include/zscrc.h
+
+
+class CPassSpec(ctypes.Structure):
+    """zscrc_cpass_spec (include/zscrc.h)."""
+    _fields_ = [("d_image", ctypes.c_void_p), ("image_size", ctypes.c_uint64), ("n", ctypes.c_size_t),
+                ("d_off", ctypes.c_void_p), ("d_len", ctypes.c_void_p), ("d_file", ctypes.c_void_p),
+                ("max_len", ctypes.c_uint64), ("nspans", ctypes.c_size_t), ("span_off", ctypes.c_void_p),
+                ("span_len", ctypes.c_void_p), ("span_commit", ctypes.c_void_p)]
+
+
+class CPassResult(ctypes.Structure):
+    """zscrc_cpass_result (include/zscrc.h)."""
+    _fields_ = [("n_bad", ctypes.c_uint64), ("n_stale", ctypes.c_uint64), ("n_undecided", ctypes.c_uint64),
+                ("complete", ctypes.c_int32), ("pad_", ctypes.c_int32),
+                ("n_listed_bad", ctypes.c_uint64), ("n_listed_stale", ctypes.c_uint64),
+                ("bad", ctypes.c_uint64 * CPASS_LIST), ("stale", ctypes.c_uint64 * CPASS_LIST),
+                ("undecided", ctypes.c_uint64 * CPASS_SPANS), ("span_raw", ctypes.c_uint32 * CPASS_SPANS),
+                ("span_status", ctypes.c_int32 * CPASS_SPANS)]
+
+
+# span pieces checked on the device travel in the digest with these piece
+# indices (the host folds only the split ones: index >= 0, or -1 for a
+# pointer section whose commit is not in this rank's buffer)
+CHECKED_OK, CHECKED_BAD, CHECKED_TAIL_OK, CHECKED_TAIL_BAD = -2, -3, -4, -5
+
+
 # ------------------------------------------------------------------ the plan
 @dataclass
 class Unit:
@@ -216,6 +244,8 @@ def make_plan(db: Db, world: int) -> Plan:
 # ---------------------------------------------------------------- device side
 class GpuBackend:
     """The product path: libzscrc kernels on the staged device buffer."""
+
+    native_pass = True    # the whole device pass as one C call (zscrc_cpass)
 
     def __init__(self, device: torch.device):
         self.device = device
@@ -471,7 +501,51 @@ class Consistent:
             import torch.distributed as dist
             self._host_all = [None] * self.world
             dist.all_gather_object(self._host_all, host, group=self.group)
+        self._dotzsdb = self._check_dotzsdb()    # the .zsdb does not change between passes
+        self._cpass = None
+        if getattr(be, "native_pass", False) and os.environ.get("ZS_POSTPASS", "native") == "native" \
+                and len(pieces) <= CPASS_SPANS:
+            self._make_cpass(slots)
         return self
+
+    def _make_cpass(self, slots):
+        """The device pass as one C call (zscrc_cpass): verdict batch, raw
+        spans, post kernel, one small copy back."""
+        from ._lib import check, lib
+        dev = self.buf.device
+        self.d_file = torch.from_numpy(self.c_file.astype(np.int32)).to(dev)
+        tail_at = {u.fid: p for u, lo, hi, p in slots if u.what == "tail"}
+        so, sl, sc = [], [], []
+        for fid, k, lo, hi, p in self.pieces:
+            lay = self.plan.packed[fid]
+            so.append(p)
+            sl.append(hi - lo)
+            if k < 0:                                   # pointer section: its final commit follows
+                sc.append(p + (hi - lo))
+            elif lo == lay["roff"] and hi == lay["roff"] + lay["rlen"] and fid in tail_at:
+                sc.append(tail_at[fid])                 # whole region, its commit record staged here
+            else:
+                sc.append(-1)                           # a split piece: folded on the host
+        self._span_off = np.array(so, np.uint64)
+        self._span_len = np.array(sl, np.uint64)
+        self._span_commit = np.array(sc, np.int64)
+        spec = CPassSpec(self.buf.data_ptr(), self.buf.numel(), len(self.c_off), self.d_off.data_ptr(),
+                         self.d_len.data_ptr(), self.d_file.data_ptr(), self.c_max, len(so),
+                         self._span_off.ctypes.data, self._span_len.ctypes.data, self._span_commit.ctypes.data)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(dev):
+            check(lib().zscrc_cpass_create(ctypes.byref(h), ctypes.byref(spec)), "zscrc_cpass_create")
+        self._cpass = h
+        self._cres = CPassResult()
+
+    def __del__(self):
+        h = getattr(self, "_cpass", None)
+        if h:
+            try:
+                from ._lib import lib
+                lib().zscrc_cpass_destroy(h)
+            except Exception:
+                pass
 
     def _check_header(self, f: DbFile):
         rc, st, cp = zsfile.header_crc(f.image)
@@ -499,6 +573,55 @@ class Consistent:
     def run(self, events=None) -> Report:
         """events: optional (start, end) device events recorded around the
         device pass (bench.py's kernel timing)."""
+        if self._cpass is not None:
+            rep = self._run_native(events)
+            if rep is not None:
+                return rep
+        return self._run_torch(events)
+
+    def _run_native(self, events):
+        """One C call: the verdict batch, the raw spans, the post kernel and
+        one small copy back; the digest is built from that block alone.  None
+        (the torch path decides) when the pass left commits undecided or
+        listed only part of its mismatches."""
+        from ._lib import check, lib
+        t0 = time.perf_counter()
+        res = self._cres
+        dev = self.buf.device
+        stream = torch.cuda.current_stream(dev)
+        if events:
+            events[0].record(stream)
+        check(lib().zscrc_cpass_run(self._cpass, ctypes.c_void_p(stream.cuda_stream), ctypes.byref(res)),
+              "zscrc_cpass_run")
+        if events:
+            events[1].record(stream)
+        if res.n_undecided or not res.complete:
+            return None
+        t_dev = time.perf_counter()
+        L = self.MAX_LISTED
+        bad_i = np.ctypeslib.as_array(res.bad)[:res.n_listed_bad].astype(np.int64)
+        stale_i = np.ctypeslib.as_array(res.stale)[:res.n_listed_stale].astype(np.int64)
+        pieces = []
+        n_bad = int(res.n_bad)
+        for k, (fid, pc, lo, hi, p) in enumerate(self.pieces):
+            st = res.span_status[k]
+            if st < 0:
+                pieces.append((fid, pc, hi - lo, res.span_raw[k]))
+            else:
+                pieces.append((fid, (CHECKED_TAIL_OK if st == 1 else CHECKED_TAIL_BAD) if pc < 0 else
+                               (CHECKED_OK if st == 1 else CHECKED_BAD), hi - lo, 0))
+        digest = dict(commits=len(self.c_off), n_bad=n_bad, n_stale=int(res.n_stale),
+                      bad=np.stack([self.c_file[bad_i[:L]], self.c_rec[bad_i[:L]]], 1),
+                      stale=np.stack([self.c_file[stale_i[:L]], self.c_rec[stale_i[:L]]], 1),
+                      pieces=np.array(pieces, np.int64).reshape(-1, 4))
+        allsum = self._gather(digest)
+        t_x = time.perf_counter()
+        rep = self._merge(allsum)
+        t1 = time.perf_counter()
+        rep.timing = dict(device_s=t_dev - t0, exchange_s=t_x - t_dev, fold_s=t1 - t_x, total_s=t1 - t0)
+        return rep
+
+    def _run_torch(self, events=None) -> Report:
         be = self.backend
         t0 = time.perf_counter()
         n = len(self.c_off)
@@ -657,7 +780,7 @@ class Consistent:
         if self._names is None:
             self._names = [f.name for f in self.db.files]
         rep = Report(names=self._names)
-        rep.dotzsdb = self._check_dotzsdb()
+        rep.dotzsdb = getattr(self, "_dotzsdb", None) or self._check_dotzsdb()
         pieces = {}
         bads, stales = [], []
         for s in allsum:
@@ -672,6 +795,14 @@ class Consistent:
             rep.walk_errors += [tuple(w) for w in s["walk_errors"]]
             rep.issues += s["issues"]
             for fid, k, ln, r in s["pieces"]:
+                if k <= CHECKED_OK:             # checked on the device, trailer included
+                    rep.commits += 1
+                    if k in (CHECKED_BAD, CHECKED_TAIL_BAD):
+                        lay = self.plan.packed[fid]
+                        at = lay["poff"] + lay["plen"] if k == CHECKED_TAIL_BAD else lay["roff"] + lay["rlen"]
+                        rep.extra_bad.append((self.db.files[fid].name, at))
+                        rep.n_bad += 1
+                    continue
                 pieces.setdefault((fid, k < 0), []).append((k, r, ln))
             if s["n_bad"] > len(s["bad"]):
                 rep.issues.append(f"rank {s['rank']}: {s['n_bad'] - len(s['bad'])} more bad commits not listed")

@@ -41,6 +41,7 @@ int zs_launch_multi(const zs::BatchDesc *d, const zs::MultiBatch *m, const uint3
                     hipStream_t stream);
 int zs_launch_xteam(int depth, const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
 int zs_launch_commit(const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
+int zs_launch_xparts(const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
 int zs_launch_spans(const zs::XDesc *x, const zs::XMulti *m, const zs::SpanFolds *fs, const uint32_t *gtab,
                     int grid, hipStream_t stream);
 int zs_launch_mismatch_rows(const uint32_t *st, const uint32_t *crc, const int64_t *end, const uint8_t *img,
@@ -510,7 +511,13 @@ int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1
             pa.desc = desc;
             pa.klass = (uint32_t)k;
             pa.target = split_items(team[k]);
+            if (k == 3 && g_xteam && (d.opt & 131072))
+                pa.target *= 2; /* four parts per wave (A/B) */
             pa.unit_min = (uint64_t)team[k] * 64 * 16; /* 16 steps of the team */
+            /* class 3 (> g16_max): parts on xteam_kernel's coalesced whole-wave
+             * teams, every record through the part fold */
+            const bool xparts = k == 3 && g_xteam && !(d.opt & 65536);
+            pa.always_split = xparts ? 1u : 0u;
             pa.plan = plans;
             pa.part_base = part_base;
             pa.part_rec = part_rec;
@@ -525,7 +532,16 @@ int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1
             dk.part_rec = part_rec;
             dk.part_out = part_out;
         }
-        int rc = launch(c, team[k], dk, s, walk[k]);
+        int rc;
+        if (k == 3 && g_xteam && !(d.opt & 65536)) {
+            rc = zs_launch_xparts(&dk, c->gtab, c->ncu, s) ? ZSCRC_EHIP : ZSCRC_OK;
+            if (rc)
+                set_err("xparts launch", hipGetLastError());
+            else
+                g_stat[2]++;
+        } else {
+            rc = launch(c, team[k], dk, s, walk[k]);
+        }
         if (rc)
             return rc;
         if (k >= 2) {
@@ -1177,6 +1193,14 @@ void zscrc_set_teams(uint64_t g1_max, uint64_t g16_max)
     std::call_once(g_env_once, env_init);
     g_g1_max = g1_max;
     g_g16_max = g16_max;
+}
+
+/* The current device's operator tables (for the host objects in other
+ * translation units, e.g. zscrc_cpass.cpp); NULL without a device. */
+const uint32_t *zscrc_internal_gtab(void)
+{
+    DevCtx *c;
+    return get_ctx(&c) ? nullptr : c->gtab;
 }
 
 int zscrc_abi_version(void)

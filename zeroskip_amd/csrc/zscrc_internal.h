@@ -68,7 +68,10 @@ struct BatchDesc {
                              4096 / 8192 = diagnostics of the run rounds (no chains / no
                              trailer and result stores; results wrong),
                              32768 = bounded commit batches on burst_kernel instead of
-                             commit_kernel */
+                             commit_kernel, 65536 = split class 3 on team_kernel<64>
+                             instead of xteam_kernel's parts mode, 131072 = four parts
+                             per wave there instead of two, 262144 = diagnostic: multi64_kernel
+                             stores its results into one L2-resident window (wrong results) */
     uint32_t *part_out;
     /* commit verdict mode (bad_count != NULL): no per-record out / status;
      * every commit whose status is not 1 is counted in *bad_count and its
@@ -107,6 +110,43 @@ struct XMulti {
     uint64_t last[SPANS_MAX];
     uint64_t first[SPANS_MAX + 1];
     uint32_t *out[SPANS_MAX];
+};
+
+/* Parts of a split length class for xteam_kernel (MODE 2): part w of the
+ * class list's record part_rec[w] covers bytes [(w - part_base[rec]) * unit,
+ * +unit) (the last part the rest); raw registers to part_out[w] (folded by
+ * part_fold_kernel); the count of parts comes from plan[klass] on the device. */
+struct XParts {
+    const uint8_t *base;
+    const struct RecDesc *desc;
+    const uint32_t *class_count;
+    uint32_t klass;
+    uint32_t xor_io;
+    const struct SplitPlan *plan;
+    const uint32_t *part_base;
+    const uint32_t *part_rec;
+    uint32_t *part_out;
+};
+
+/* consistent's device post pass (zscrc_cpass, cpass_post_kernel): the
+ * verdict's bad list classified (stale finalise commit / bad / undecided),
+ * the whole raw spans' commit trailers checked. */
+constexpr uint32_t CPASS_SPANS = 64;
+struct CPassArgs {
+    const uint8_t *base;
+    uint64_t img_size;
+    const uint64_t *off, *len;   /* commits */
+    const uint32_t *file;        /* file id per commit */
+    const unsigned long long *nbad;
+    const uint64_t *bad;         /* the verdict's list (first `cap` of *nbad) */
+    uint64_t cap;
+    uint32_t *flags;             /* per listed entry: 0 bad, 1 stale, 2 undecided (host) */
+    unsigned long long *nstale;
+    uint32_t nspans;
+    const uint32_t *span_raw;    /* raw registers from 0 */
+    const int64_t *span_commit;  /* image offset of the span's commit record, -1 = none here */
+    const uint32_t *span_init;   /* shift(~0, span length): the register of ~0 after the span */
+    int32_t *span_status;        /* 1 ok, 0 mismatch, 2 no commit record, -1 not checked */
 };
 
 struct RecDesc {
@@ -153,6 +193,7 @@ struct PlanArgs {
     uint32_t klass;
     uint32_t target;       /* items wanted: two per team of the launch */
     uint64_t unit_min;     /* smallest part worth a team */
+    uint32_t always_split; /* never direct: every record one part at least (xteam parts) */
     SplitPlan *plan;
     uint32_t *part_base;   /* per record of the class: its first part */
     uint32_t *part_rec;    /* per part: its record */

@@ -33,6 +33,7 @@
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
 
 #include "zscrc_internal.h"
 
@@ -140,9 +141,8 @@ __device__ __forceinline__ uint32_t op4(const char *L, uint32_t base, uint32_t x
  * (high word x^0..x^31, low word x^32..x^63: 32 independent partial
  * products, two accumulators), then the low word reduced by one "shift by 4
  * bytes" lookup -- the compact slice-by-4 table at T (GT_S4, 4 KiB in LDS).
- * The span fold uses it (35 -> 18 us for 8192 parts).  part_fold_kernel
- * keeps the bit-serial gmul below: there the table form (with the part loads
- * hoisted) measured 55-69 us against ~44. */
+ * The span fold uses it (35 -> 18 us for 8192 parts), and so does
+ * part_fold_kernel since it folds one record per wave (round 3). */
 __device__ __forceinline__ uint32_t gmul_t(const char *T, uint32_t a, uint32_t b)
 {
     const uint64_t bb = (uint64_t)b << 32;
@@ -164,18 +164,6 @@ __device__ __forceinline__ void load_gmul_table(char *T, const uint32_t *gtab)
         t[i] = gtab[GT_S4 + i];
 }
 
-/* a * b mod P, bit-serial (reflected: bit 31 = x^0). */
-__device__ __forceinline__ uint32_t gmul(uint32_t a, uint32_t b)
-{
-    uint32_t acc = 0;
-#pragma unroll 4
-    for (int i = 0; i < 32; ++i) {
-        acc ^= (a & 0x80000000u) ? b : 0u;
-        a <<= 1;
-        b = (b >> 1) ^ ((b & 1u) ? 0x82F63B78u : 0u);
-    }
-    return acc;
-}
 
 /* One byte (Sarwate): table j=3 is shift(b<<24, 4) = shift(b, 1). */
 __device__ __forceinline__ uint32_t byte_step(const char *L, uint32_t r, uint32_t b, uint32_t c_hi)
@@ -815,16 +803,38 @@ constexpr uint64_t XSTEP = 4096;
 /* Record w's first byte, length and buffer clamp bound: a fixed-stride batch,
  * or (MULTI) segment w of a multi-span launch (uniform w: a scalar scan of
  * at most SPANS_MAX spans). */
-template <bool MULTI>
-__device__ __forceinline__ void xgeom(const XDesc &d, const XMulti &m, uint64_t w, uintptr_t &A, uint64_t &len,
-                                      uintptr_t &lo)
+/* MODE 0: fixed-stride records; 1: segments of a multi-span launch; 2: parts
+ * of a split length class (XParts).  R0: the item's initial register. */
+template <int MODE>
+__device__ __forceinline__ void xgeom(const XDesc &d, const XMulti &m, const XParts &xp, uint64_t w, uintptr_t &A,
+                                      uint64_t &len, uintptr_t &lo, uint32_t &R0)
 {
-    if (!MULTI) {
+    if (MODE == 0) {
         len = (w + 1 == d.n) ? d.last_len : d.fixed_len;
         A = reinterpret_cast<uintptr_t>(d.base) + w * d.stride;
         lo = reinterpret_cast<uintptr_t>(d.base) & ~uintptr_t(3);
+        R0 = d.seed ^ d.xor_io;
         return;
     }
+    if (MODE == 2) {
+        uint32_t first = 0;
+        for (uint32_t k = 0; k < xp.klass; ++k)
+            first += __builtin_amdgcn_readfirstlane(((g32p)xp.class_count)[k]);
+        const uint32_t idx = __builtin_amdgcn_readfirstlane(((g32p)xp.part_rec)[w]);
+        const RecDesc *r = xp.desc + first + idx;
+        typedef const __attribute__((address_space(1))) uint64_t *g64p;
+        const uint64_t off = uni64(((g64p)r)[0]), rlen = uni64(((g64p)r)[1]);
+        const uint32_t seed = __builtin_amdgcn_readfirstlane(((g32p)r)[4]);
+        const uint64_t U = uni64(((g64p)(xp.plan + xp.klass))[0]);
+        const uint64_t part = w - __builtin_amdgcn_readfirstlane(((g32p)xp.part_base)[idx]);
+        const uint64_t a = part * U < rlen ? part * U : rlen;
+        len = (a + U < rlen ? a + U : rlen) - a;
+        A = reinterpret_cast<uintptr_t>(xp.base) + off + a;
+        lo = reinterpret_cast<uintptr_t>(xp.base) & ~uintptr_t(3);
+        R0 = part ? 0u : seed ^ xp.xor_io; /* later parts start from a zero register */
+        return;
+    }
+    R0 = d.seed ^ d.xor_io;
     uint32_t k = 0;
     while (k + 1 < m.k && w >= m.first[k + 1])
         ++k;
@@ -834,14 +844,16 @@ __device__ __forceinline__ void xgeom(const XDesc &d, const XMulti &m, uint64_t 
     lo = reinterpret_cast<uintptr_t>(m.base[k]) & ~uintptr_t(3);
 }
 
-template <bool MULTI>
-__device__ __forceinline__ bool xitem(const XDesc &d, const XMulti &m, uint64_t w, uint64_t wend, XItem &it)
+template <int MODE>
+__device__ __forceinline__ bool xitem(const XDesc &d, const XMulti &m, const XParts &xp, uint64_t w, uint64_t wend,
+                                      XItem &it)
 {
     if (w >= wend)
         return false;
     uintptr_t A, lo;
     uint64_t len;
-    xgeom<MULTI>(d, m, w, A, len, lo);
+    uint32_t R0;
+    xgeom<MODE>(d, m, xp, w, A, len, lo, R0);
     const uintptr_t E = len < 8 ? A : ((A + len) & ~uintptr_t(3));
     const uint32_t S = len < 8 ? 0u : (uint32_t)((E - A + XSTEP - 1) / XSTEP);
     it.A = A;
@@ -850,7 +862,7 @@ __device__ __forceinline__ bool xitem(const XDesc &d, const XMulti &m, uint64_t 
     it.S = S;
     it.len = len;
     it.w = w;
-    it.R0 = d.seed ^ d.xor_io;
+    it.R0 = R0;
     it.lo = lo;
     return true;
 }
@@ -958,12 +970,13 @@ struct XLoad {
     uintptr_t lo;  /* the record's buffer clamp bound */
 };
 
-template <bool MULTI>
-__device__ __forceinline__ void xrec(const XDesc &d, const XMulti &m, XLoad &l)
+template <int MODE>
+__device__ __forceinline__ void xrec(const XDesc &d, const XMulti &m, const XParts &xp, XLoad &l)
 {
     uintptr_t A;
     uint64_t len;
-    xgeom<MULTI>(d, m, l.w < l.wend ? l.w : l.wend - 1, A, len, l.lo);
+    uint32_t R0;
+    xgeom<MODE>(d, m, xp, l.w < l.wend ? l.w : l.wend - 1, A, len, l.lo, R0);
     const uintptr_t E = len < 8 ? A : ((A + len) & ~uintptr_t(3));
     const uint64_t S = len < 8 ? 0 : (E - A + XSTEP - 1) / XSTEP;
     l.V = E - S * XSTEP;
@@ -971,8 +984,8 @@ __device__ __forceinline__ void xrec(const XDesc &d, const XMulti &m, XLoad &l)
     l.ok = l.w < l.wend && S; /* a record without loads: its one position reads the dummy */
 }
 
-template <bool MULTI>
-__device__ __forceinline__ void xnext(const XDesc &d, const XMulti &m, XLoad &l)
+template <int MODE>
+__device__ __forceinline__ void xnext(const XDesc &d, const XMulti &m, const XParts &xp, XLoad &l)
 {
     if (l.ok && l.left) {
         --l.left;
@@ -982,13 +995,19 @@ __device__ __forceinline__ void xnext(const XDesc &d, const XMulti &m, XLoad &l)
     if (l.w >= l.wend)
         return;
     l.w += 1;
-    xrec<MULTI>(d, m, l);
+    xrec<MODE>(d, m, xp, l);
 }
 
-template <bool MULTI>
-__global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, const uint32_t *__restrict__ gtab)
+template <int MODE>
+__global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp, const uint32_t *__restrict__ gtab)
 {
+    constexpr bool MULTI = MODE == 1;
     __shared__ __attribute__((aligned(16))) char L[LDS_BYTES];
+    if (MODE == 2) { /* parts of a split class: their count is on the device */
+        d.n = __builtin_amdgcn_readfirstlane(((const volatile uint32_t *)&xp.plan[xp.klass].parts)[0]);
+        d.out = xp.part_out;
+        d.xor_io = 0; /* raw part registers */
+    }
     if ((uint64_t)blockIdx.x * WAVES >= d.n)
         return;
     if (MULTI && blockIdx.x == 0 && threadIdx.x < m.k)
@@ -1009,12 +1028,12 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, const uint
     XLoad ld;
     ld.w = wbeg;
     ld.wend = wend;
-    xrec<MULTI>(d, m, ld);
+    xrec<MODE>(d, m, xp, ld);
     uint32_t b0[16], b1[16];
     const uint32_t voff = 64u * (uint32_t)c + 16u * (uint32_t)g;
     xissue(ld.V, ld.ok, voff, dummy, ld.lo, b0);
     XItem it;
-    bool ok = xitem<MULTI>(d, m, wbeg, wend, it);
+    bool ok = xitem<MODE>(d, m, xp, wbeg, wend, it);
     uint32_t s = 0;
     uint32_t acc = 0;
     /* Results wait in a register (lane k: the k-th record of the current
@@ -1036,7 +1055,7 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, const uint
             for (uint64_t i = 0; i < it.len; ++i)
                 r = byte_step(L, r, ((g8p)it.A)[i], c_hi);
             stash_put(r ^ d.xor_io);
-            ok = xitem<MULTI>(d, m, it.w + 1, wend, it);
+            ok = xitem<MODE>(d, m, xp, it.w + 1, wend, it);
             return;
         }
         xpose16(w);
@@ -1063,15 +1082,15 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, const uint
         stash_put(__shfl(acc, 63) ^ d.xor_io);
         acc = 0;
         s = 0;
-        ok = xitem<MULTI>(d, m, it.w + 1, wend, it);
+        ok = xitem<MODE>(d, m, xp, it.w + 1, wend, it);
     };
     while (ok) {
-        xnext<MULTI>(d, m, ld);
+        xnext<MODE>(d, m, xp, ld);
         xissue(ld.V, ld.ok, voff, dummy, ld.lo, b1);
         hash(b0);
         if (!ok)
             break;
-        xnext<MULTI>(d, m, ld);
+        xnext<MODE>(d, m, xp, ld);
         xissue(ld.V, ld.ok, voff, dummy, ld.lo, b0);
         hash(b1);
     }
@@ -1728,7 +1747,9 @@ __global__ __launch_bounds__(WG) void multi64_kernel(BatchDesc d, MultiBatch m, 
         for (int q = 0; q < K; ++q)
             r[q] = m4(L, r[q], c_lo, c_hi);
         uint32_t *out = m.out[p.b];
-        const uint64_t r0 = p.k * RPC + (uint64_t)lane;
+        uint64_t r0 = p.k * RPC + (uint64_t)lane;
+        if (d.opt & 262144) /* diagnostic: results into one L2-resident 64 KiB window (wrong results) */
+            r0 &= 16383;
 #pragma unroll
         for (int q = 0; q < K; ++q)
             if (r0 + 64 * q < n)
@@ -2453,6 +2474,106 @@ __global__ __launch_bounds__(BWG) void commit_kernel(BatchDesc d, const uint32_t
     }
 }
 
+/* ------------------------------------------------- consistent post pass */
+/* crc32c register r through the bytes [p, p + n) (any alignment): one
+ * thread, the compact slice-by-4 table T (GT_S4 in LDS). */
+__device__ __forceinline__ uint32_t crc_run(const char *T, uint32_t r, const uint8_t *p, uint64_t n)
+{
+    while (n && ((uintptr_t)p & 3)) {
+        r = lds32(T, 3072 + (((r ^ *(g8p)p) & 0xffu) << 2)) ^ (r >> 8);
+        ++p;
+        --n;
+    }
+    for (; n >= 4; n -= 4, p += 4)
+        r = op4(T, 0, r ^ *(g32p)p);
+    for (; n; --n, ++p)
+        r = lds32(T, 3072 + (((r ^ *(g8p)p) & 0xffu) << 2)) ^ (r >> 8);
+    return r;
+}
+
+/* register r through the host-order 64-bit word v */
+__device__ __forceinline__ uint32_t crc_word(const char *T, uint32_t r, uint64_t v)
+{
+    r = op4(T, 0, r ^ (uint32_t)v);
+    return op4(T, 0, r ^ (uint32_t)(v >> 32));
+}
+
+/*
+ * consistent's post pass, after the verdict batch and the raw spans
+ * (zscrc_cpass_run).  Thread per listed bad commit: a zero-length commit
+ * right after a span of the same file is the finalise quirk if its stored
+ * CRC continues from the previous span's CRC (zs_active_file_finalise,
+ * src/zeroskip-active.c:122 + src/mfile.c:534-546): that span is re-hashed
+ * here (<= 64 KiB; longer, or a long trailer: undecided, the host decides).
+ * Block 0 also checks the commit trailer of every whole raw span (records
+ * region or pointer section) with the writer's semantics
+ * (src/zeroskip-file.c:266-302).  Everything stays on the device: the host
+ * copies one small block back.
+ */
+__global__ __launch_bounds__(256) void cpass_post_kernel(CPassArgs a, const uint32_t *__restrict__ gtab)
+{
+    __shared__ __attribute__((aligned(16))) char T[4096];
+    load_gmul_table(T, gtab); /* GT_S4, compact: table j at 1024 j */
+    __syncthreads();
+    const uint64_t nbad = *a.nbad, nl = nbad < a.cap ? nbad : a.cap;
+    const uint64_t nt = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nl; k += nt) {
+        const uint64_t i = a.bad[k];
+        uint32_t flag = 0;
+        if (a.len[i] == 0 && i > 0 && a.file[i - 1] == a.file[i]) {
+            const uint64_t at = a.off[i]; /* the zero-length span's commit record */
+            const uint64_t pl = a.len[i - 1];
+            if (at + 8 <= a.img_size && pl <= 65536) {
+                const uint64_t w0 = load_be64(reinterpret_cast<uintptr_t>(a.base) + at);
+                const uint32_t t = (uint32_t)(w0 >> 56);
+                if (t == REC_COMMIT || t == REC_FINAL) {
+                    const uint32_t S = crc_run(T, 0xffffffffu, a.base + a.off[i - 1], pl) ^ 0xffffffffu;
+                    const uint32_t c = crc_word(T, S ^ 0xffffffffu, w0 & 0xFFFFFFFF00000000ull) ^ 0xffffffffu;
+                    flag = c == (uint32_t)w0 ? 1u : 0u;
+                } else {
+                    flag = 2;
+                }
+            } else {
+                flag = 2;
+            }
+        }
+        a.flags[k] = flag;
+        if (flag == 1)
+            atomicAdd(a.nstale, 1ull);
+    }
+    if (blockIdx.x == 0 && threadIdx.x < a.nspans) {
+        const uint32_t s = threadIdx.x;
+        int32_t st = -1;
+        const int64_t at = a.span_commit[s];
+        if (at >= 0) {
+            st = 2;
+            /* crc32c(0, span) = (shift(~0, len) ^ raw) ^ ~0: continue the register */
+            uint32_t r = a.span_init[s] ^ a.span_raw[s];
+            if ((uint64_t)at + 8 <= a.img_size) {
+                const uintptr_t e = reinterpret_cast<uintptr_t>(a.base) + (uint64_t)at;
+                const uint64_t w0 = load_be64(e);
+                const uint32_t t = (uint32_t)(w0 >> 56);
+                uint32_t stored = 0;
+                if (t == REC_COMMIT || t == REC_FINAL) {
+                    r = crc_word(T, r, w0 & 0xFFFFFFFF00000000ull);
+                    stored = (uint32_t)w0;
+                    st = 0;
+                } else if ((t == REC_LONG_COMMIT || t == REC_LONG_FINAL) && (uint64_t)at + 24 <= a.img_size) {
+                    const uint64_t w2 = load_be64(e + 16);
+                    r = crc_word(T, r, w0);
+                    r = crc_word(T, r, load_be64(e + 8));
+                    r = crc_word(T, r, w2 & 0xFF00000000000000ull);
+                    stored = (uint32_t)w2;
+                    st = 0;
+                }
+                if (st == 0)
+                    st = (r ^ 0xffffffffu) == stored ? 1 : 0;
+            }
+        }
+        a.span_status[s] = st;
+    }
+}
+
 /* ------------------------------------------------------------ span fold */
 /* K^m from the table K^(2^b). */
 __device__ __forceinline__ uint32_t kpow(const char *T, const uint32_t *kp2, uint32_t m)
@@ -2692,7 +2813,7 @@ __global__ __launch_bounds__(1024) void plan_kernel(PlanArgs a)
     const uint32_t count = a.count[a.klass];
     const RecDesc *list = a.desc + first;
     SplitPlan *pl = a.plan + a.klass;
-    if (count == 0 || count >= a.target) {
+    if (count == 0 || (count >= a.target && !a.always_split)) {
         if (t == 0) {
             pl->unit = 0;
             pl->parts = count;
@@ -2704,11 +2825,13 @@ __global__ __launch_bounds__(1024) void plan_kernel(PlanArgs a)
      * (target - count) the parts never exceed target, so no team gets one
      * item more than the others (a 2% overshoot of 2 items per team would
      * leave the kernel waiting on teams with 3) */
-    const uint64_t room = a.target - count;
+    const uint64_t room = a.target > count ? a.target - count : 1;
     uint64_t unit = (a.bytes[a.klass] + room - 1) / room;
     unit = (unit + 63) & ~63ull;
     if (unit < a.unit_min)
         unit = a.unit_min;
+    if (count >= a.target) /* always_split: one part per record */
+        unit = ~0ull >> 8;
     uint32_t running = 0;
     for (uint32_t c0 = 0; c0 < count; c0 += 1024) {
         const uint32_t r = c0 + t;
@@ -2755,35 +2878,28 @@ __global__ __launch_bounds__(1024) void plan_kernel(PlanArgs a)
     }
 }
 
-__device__ __forceinline__ uint32_t xpow8(const uint32_t *pow2, uint64_t n)
+
+/* x^(8n) mod P by square-and-multiply over the table x^(8*2^k) (table gmul). */
+__device__ __forceinline__ uint32_t xpow8_t(const char *T, const uint32_t *pow2, uint64_t n)
 {
     uint32_t r = 0x80000000u;
     for (int k = 0; n; ++k, n >>= 1)
         if (n & 1)
-            r = gmul(r, pow2[k]);
+            r = gmul_t(T, r, pow2[k]);
     return r;
 }
 
-/* Fold the part registers of every record of a split class (register after
- * part p = shift(register before, |part p|) ^ raw_p), then finish like
- * emit(): plain CRC, or the commit trailer + comparison in commit mode.  One
- * block per record: its m parts are m-1 parts of P = unit bytes and a last one
- * of Lm bytes, so  reg = (XOR_p<m-1 raw_p * XP^(m-2-p)) * x^(8 Lm) ^ raw_(m-1)
- * with XP = x^(8P).  Thread t Horner-folds a contiguous run of parts and
- * shifts its partial by XP^(parts after its run); the block XOR-reduces. */
-__device__ __forceinline__ uint32_t ppow(const uint32_t (&lad)[16], uint32_t e)
-{
-    uint32_t r = 0x80000000u;
-    for (int b = 0; e; ++b, e >>= 1)
-        if (e & 1)
-            r = gmul(r, lad[b]);
-    return r;
-}
-
+/* One wave per record of a split class: H = sum over the uniform parts p <
+ * nu of part[p] * K^(nu-1-p), K = x^(8*unit) (lane t takes part t of each
+ * chunk of 64, its power from the ladder K^(2^b); chunks joined by K^64),
+ * then reg = H * x^(8*last) ^ part[nu] and the record's output (a CRC, or a
+ * commit CRC continued over the commit trailer, compared or written).  The
+ * products are table GF(2) multiplies (gmul_t: the compact slice-by-4 table
+ * in LDS); the former block-per-record fold with bit-serial products took
+ * 41-45 us of the NOTBATCHED verify (1,488 records of ~2 MiB, 6 parts each). */
 __global__ __launch_bounds__(256) void part_fold_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
 {
-    __shared__ uint32_t red[4];
-    const uint32_t *pow2 = gtab + GT_POW2;
+    __shared__ __attribute__((aligned(16))) char T[4096];
     uint32_t base = 0;
     for (uint32_t k = 0; k < d.klass; ++k)
         base += d.class_count[k];
@@ -2791,42 +2907,48 @@ __global__ __launch_bounds__(256) void part_fold_kernel(BatchDesc d, const uint3
     const RecDesc *list = d.desc + base;
     if (((const volatile uint32_t *)&d.plan[d.klass].direct)[0])
         return; /* the team kernel emitted every record itself */
+    load_gmul_table(T, gtab);
+    __syncthreads();
+    const uint32_t *pow2 = gtab + GT_POW2;
     const uint64_t P = d.plan[d.klass].unit;
     const uint32_t nparts = ((const volatile uint32_t *)&d.plan[d.klass].parts)[0];
+    const int lane = threadIdx.x & 63;
+    /* K^(2^b), b = 0..6, once per wave (the same unit for every record) */
+    uint32_t lad[7];
+    lad[0] = P < (1ull << 56) ? xpow8_t(T, pow2, P) : 0x80000000u;
+#pragma unroll
+    for (int b = 1; b < 7; ++b)
+        lad[b] = gmul_t(T, lad[b - 1], lad[b - 1]);
     const uint32_t X4 = pow2[2]; /* x^32: one slice-by-4 step */
-    const int t = threadIdx.x;
-    for (uint64_t idx = blockIdx.x; idx < count; idx += gridDim.x) {
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t idx = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); idx < count; idx += nwaves) {
         const RecDesc r = list[idx];
         const uint64_t len = r.len;
         const uint32_t pb = d.part_base[idx];
         const uint32_t m = (idx + 1 < count ? d.part_base[idx + 1] : nparts) - pb; /* 1.. parts */
         const uint32_t *parts = d.part_out + pb;
-        const uint32_t nu = m - 1;                        /* uniform parts */
-        const uint32_t run = (nu + 255) / 256;
-        const uint32_t lo = t * run < nu ? t * run : nu;
-        const uint32_t hi = lo + run < nu ? lo + run : nu;
-        uint32_t part = 0;
-        if (lo < hi) {
-            uint32_t lad[16];
-            lad[0] = xpow8(pow2, P);
+        const uint32_t nu = m - 1;                                                /* uniform parts */
+        uint32_t H = 0;
+        for (uint32_t c0 = 0; c0 < nu; c0 += 64) {
+            const uint32_t cn = nu - c0 < 64 ? nu - c0 : 64;
+            uint32_t v = 0;
+            if ((uint32_t)lane < cn) {
+                v = parts[c0 + lane];
+                const uint32_t e = cn - 1 - (uint32_t)lane; /* K^e within the chunk */
 #pragma unroll
-            for (int b = 1; b < 16; ++b)
-                lad[b] = gmul(lad[b - 1], lad[b - 1]);
-            for (uint32_t p = lo; p < hi; ++p)
-                part = gmul(part, lad[0]) ^ parts[p];
-            part = gmul(part, ppow(lad, nu - hi));
+                for (int b = 0; b < 6; ++b)
+                    if ((e >> b) & 1)
+                        v = gmul_t(T, v, lad[b]);
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1)
+                v ^= __shfl_xor(v, o);
+            H = c0 ? (gmul_t(T, H, cn == 64 ? lad[6] : xpow8_t(T, pow2, P * cn)) ^ v) : v;
         }
-        for (int o = 32; o > 0; o >>= 1)
-            part ^= __shfl_xor(part, o);
-        if ((t & 63) == 0)
-            red[t >> 6] = part;
-        __syncthreads();
-        const uint32_t H = red[0] ^ red[1] ^ red[2] ^ red[3];
-        __syncthreads();
-        if (t != 0)
+        if (lane != 0)
             continue;
         const uint64_t Lm = len - (uint64_t)nu * P;
-        uint32_t reg = (nu ? gmul(H, xpow8(pow2, Lm)) : 0u) ^ parts[nu];
+        uint32_t reg = (nu ? gmul_t(T, H, xpow8_t(T, pow2, Lm)) : 0u) ^ parts[nu];
         if (!d.commit) {
             d.out[r.rec] = reg ^ d.xor_io;
             continue;
@@ -2853,8 +2975,8 @@ __global__ __launch_bounds__(256) void part_fold_kernel(BatchDesc d, const uint3
             crc_at = end + 20;
         }
         for (int i = 0; i < nt; ++i) {
-            reg = gmul(reg ^ (uint32_t)tw[i], X4);
-            reg = gmul(reg ^ (uint32_t)(tw[i] >> 32), X4);
+            reg = gmul_t(T, reg ^ (uint32_t)tw[i], X4);
+            reg = gmul_t(T, reg ^ (uint32_t)(tw[i] >> 32), X4);
         }
         const uint32_t crc = reg ^ 0xffffffffu;
         if (d.commit == 2 && nt)
@@ -3047,8 +3169,32 @@ extern "C" int zs_launch_xteam(int depth, const zs::BatchDesc *bd, const uint32_
     else {
         zs::XMulti none;
         none.k = 0;
-        hipLaunchKernelGGL(zs::xteam_kernel<false>, dim3(grid), dim3(zs::WG), 0, stream, *d, none, gtab);
+        zs::XParts np;
+        memset(&np, 0, sizeof np);
+        hipLaunchKernelGGL(zs::xteam_kernel<0>, dim3(grid), dim3(zs::WG), 0, stream, *d, none, np, gtab);
     }
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+/* the parts of a split length class on the coalesced whole-wave teams */
+extern "C" int zs_launch_xparts(const zs::BatchDesc *bd, const uint32_t *gtab, int grid, hipStream_t stream)
+{
+    zs::XDesc x;
+    memset(&x, 0, sizeof x);
+    x.base = bd->base;
+    zs::XMulti none;
+    none.k = 0;
+    zs::XParts p;
+    p.base = bd->base;
+    p.desc = bd->desc;
+    p.class_count = bd->class_count;
+    p.klass = bd->klass;
+    p.xor_io = bd->xor_io;
+    p.plan = bd->plan;
+    p.part_base = bd->part_base;
+    p.part_rec = bd->part_rec;
+    p.part_out = bd->part_out;
+    hipLaunchKernelGGL(zs::xteam_kernel<2>, dim3(grid), dim3(zs::WG), 0, stream, x, none, p, gtab);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -3098,6 +3244,12 @@ extern "C" int zs_launch_burst(int fixed, int xp, int nb, const zs::BatchDesc *d
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
+extern "C" int zs_launch_cpass_post(const zs::CPassArgs *a, const uint32_t *gtab, hipStream_t stream)
+{
+    hipLaunchKernelGGL(zs::cpass_post_kernel, dim3(64), dim3(256), 0, stream, *a, gtab);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
 extern "C" int zs_launch_commit(const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream)
 {
     if (d->commit == 2)
@@ -3125,7 +3277,9 @@ extern "C" int zs_launch_multi(const zs::BatchDesc *d, const zs::MultiBatch *m, 
 extern "C" int zs_launch_spans(const zs::XDesc *x, const zs::XMulti *m, const zs::SpanFolds *fs,
                                const uint32_t *gtab, int grid, hipStream_t stream)
 {
-    hipLaunchKernelGGL(zs::xteam_kernel<true>, dim3(grid), dim3(zs::WG), 0, stream, *x, *m, gtab);
+    zs::XParts np;
+    memset(&np, 0, sizeof np);
+    hipLaunchKernelGGL(zs::xteam_kernel<1>, dim3(grid), dim3(zs::WG), 0, stream, *x, *m, np, gtab);
     if (hipGetLastError() != hipSuccess)
         return -3;
     uint32_t bx = 1;
