@@ -606,10 +606,10 @@ def run_config5(args, world, rank, dev, stream):
     kern_ms = float(np.mean(tm.kern_ms))
     ncommit = len(job.c_off)
     local_bytes = job.local.bytes_checked
-    nbytes = local_bytes + 24 * ncommit + 16 * len(job.pieces)
-    r = roof(nbytes, kern_ms, "verify_commits_bounded (one burst_kernel over the short commit spans) + "
-                              "zscrc_device_span per records region / pointer section (xteam_kernel or "
-                              "team<16> segments + span_fold), this rank",
+    nbytes = local_bytes + 16 * ncommit + 16 * len(job.pieces)   # bytes + commit / span descriptors
+    r = roof(nbytes, kern_ms, "zscrc_cpass_run: commit_kernel verdict over the short commit spans + one "
+                              "xteam_kernel<1> launch over the records regions / pointer sections + span fold + "
+                              "post kernel + one small copy back, this rank",
              traffic_for("config5_bytes_per_launch"), read_peak)
     out_line = line(args, world, elapsed, job.plan.weight * args.steps,
                     {"workload": f"config5: consistent over a {job.plan.weight / GIB:.2f} GiB DB "

@@ -1,0 +1,5 @@
+bash tools/gpu_session.sh \
+ "t_cons:300:python -u -m pytest tests/test_gpu_consistent.py tests/test_gpu_files.py -x -q --timeout 120 --timeout-method thread" \
+ "bench5:300:python bench.py --workload config5 --no-cpu" \
+ "bench5_one:300:ZSCRC_CPASS_ONE_STREAM=1 python bench.py --workload config5 --no-cpu" \
+ "trace4:300:bash tools/trace_bench.sh config4"

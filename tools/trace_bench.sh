@@ -6,6 +6,6 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/trace_bench
 mkdir -p $O
 for c in "$@"; do
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/$c -o run -- \
+  timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d $O/$c -o run -- \
       python3 $R/bench.py --workload $c --no-cpu --no-e2e > $O/$c.json 2> $O/$c.err || exit $?
 done
