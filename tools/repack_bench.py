@@ -14,7 +14,12 @@ of --value-bytes) through the packed-file writer (zscrc_pack_*, records and
 pointer CRCs on the GPU while the host writes the file), and times the CPU
 crc32_end the reference would run over the same records region afterwards
 (src/zeroskip-packed.c:442, one core).
-usage: python tools/repack_bench.py [--mib 4096] [--file /tmp/x] [--pack N --out /tmp/p]
+--repack-dir N runs zsdb_repack (src/zeroskip.c:1419-1571) through
+zscrc_zs_repack over a generated DB directory, branch 1 (finalised zsbench
+log files holding N pairs) and branch 2 (two packed files of N/2 records
+each), and reports the library's own list / merge / write split against the
+wall time of the Python call (the Python share).
+usage: python tools/repack_bench.py [--mib 4096] [--file /tmp/x] [--pack N --out /tmp/p] [--repack-dir N]
 """
 from __future__ import annotations
 
@@ -105,6 +110,38 @@ def pack(nrec: int, vbytes: int, out: str, chunk: int) -> dict:
                     "written region (what the GPU pipeline removes)"}
 
 
+def repack_dirs(nrec: int, tmp: str) -> list:
+    import shutil
+    import tempfile
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import zsdb_gen
+    from zeroskip_amd import repack
+    out = []
+    per = zsdb_gen.pairs_per_file()
+    cases = (("finalised", dict(packed=0, finalised=-(-nrec // per), active_pairs=100)),
+             ("packed", dict(packed=2, packed_region_bytes=(nrec // 2) * 120, packed_vlen=64, finalised=0,
+                             active_pairs=100)))
+    for name, kw in cases:
+        d = tempfile.mkdtemp(prefix="zsrepack_", dir=tmp)
+        try:
+            db = zsdb_gen.make_db("cuda", **kw)
+            nbytes = zsdb_gen.write_dir(db, d)
+            del db
+            t0 = time.perf_counter()
+            rep = repack.repack_dir(d)
+            wall = time.perf_counter() - t0
+            out.append({"source": "zscrc_zs_repack", "branch": rep["branch"], "input": name,
+                        "db_bytes": nbytes, "records_in": rep["records_in"], "records_out": rep["records_out"],
+                        "files_merged": rep["files_merged"], "out_bytes": rep["pack"]["file_bytes"],
+                        "list_s": round(rep["list_s"], 3), "merge_s": round(rep["merge_s"], 3),
+                        "write_s": round(rep["write_s"], 3), "total_s": round(rep["total_s"], 3),
+                        "wall_s": round(wall, 3), "python_share": round(max(0.0, wall - rep["total_s"]) / wall, 4),
+                        "records_per_s": round(rep["records_in"] / wall), "note": "page-cache files, no fsync"})
+        finally:
+            shutil.rmtree(d, ignore_errors=True)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mib", type=int, default=4096)
@@ -113,7 +150,13 @@ def main():
     ap.add_argument("--pack", type=int, default=0, help="records for the packed-file writer leg")
     ap.add_argument("--value-bytes", type=int, default=16384)
     ap.add_argument("--out", default="/tmp/zscrc_pack_bench")
+    ap.add_argument("--repack-dir", type=int, default=0, help="pairs for the zscrc_zs_repack leg")
+    ap.add_argument("--tmp", default="/tmp")
     a = ap.parse_args()
+    if a.repack_dir:
+        for r in repack_dirs(a.repack_dir, a.tmp):
+            print(json.dumps(r), flush=True)
+        return
     if a.pack:
         print(json.dumps(pack(a.pack, a.value_bytes, a.out, a.chunk_mib << 20)), flush=True)
     n = a.mib << 20

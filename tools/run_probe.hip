@@ -145,7 +145,22 @@ __global__ __launch_bounds__(WG) void run_probe(const char *buf, unsigned *out)
             }
             issue(buf, r, voff, a);
             const unsigned h = consume<HASH>(L, a, c_lo, c_hi) ^ (unsigned)o ^ (unsigned)l;
-            if (X & 32) { /* stores to a 16 KiB region: L2-resident, no HBM writes */
+            if (X & (128 | 256 | 512)) { /* in place, at the record's own commit word */
+                typedef __attribute__((address_space(1))) u32x4 *gw4p;
+                char *R = (char *)buf + (r * 64 + lane) * GRID;
+                const u32x4 v = {h, h >> 1, h >> 2, h >> 3};
+                if (X & 128) /* one 4-byte CRC field: a partial 32 B sector */
+                    *(gw32p)(R + 316) = h;
+                else if (X & 256) { /* the whole 32 B sector holding it */
+                    *(gw4p)(R + 288) = v;
+                    *(gw4p)(R + 304) = v;
+                } else { /* the whole 64 B line holding it */
+                    *(gw4p)(R + 256) = v;
+                    *(gw4p)(R + 272) = v;
+                    *(gw4p)(R + 288) = v;
+                    *(gw4p)(R + 304) = v;
+                }
+            } else if (X & 32) { /* stores to a 16 KiB region: L2-resident, no HBM writes */
                 ((gw32p)out)[16 + (r & 63) * 64 + lane] = h;
             } else if (X & 4) { /* non-temporal result stores */
                 __builtin_nontemporal_store(h, (gw32p)out + 16 + r * 64 + lane);
@@ -221,6 +236,10 @@ int main()
         {"hash 8w sb +L2 stores", timeit(run_probe<512, 0, 1, 32>, cu, 512, d, o)},
         {"hash 8w sb blocked", timeit(run_probe<512, 0, 1, 64>, cu, 512, d, o)},
         {"hash 8w sb blocked +stores", timeit(run_probe<512, 0, 1, 66>, cu, 512, d, o)},
+        {"hash 8w sb +inplace 4B", timeit(run_probe<512, 0, 1, 128>, cu, 512, d, o)},
+        {"hash 8w sb +inplace 32B sector", timeit(run_probe<512, 0, 1, 256>, cu, 512, d, o)},
+        {"hash 8w sb +inplace 64B line", timeit(run_probe<512, 0, 1, 512>, cu, 512, d, o)},
+        {"hash 8w sb (end)", timeit(run_probe<512, 0, 1>, cu, 512, d, o)},
     };
     for (auto &x : r)
         printf("{\"case\": \"%s\", \"ms\": %.4f, \"GBs\": %.1f}\n", x.name, x.ms, (double)n / x.ms / 1e6);

@@ -51,11 +51,9 @@ struct zscrc_cpass {
     int64_t *dspan_commit = nullptr;
     uint32_t *dspan_init = nullptr;
     size_t head = 0;
-    /* the raw spans run on a second stream beside the verdict batch: the
-     * tail of one fills the CUs the other has left (both persistent,
-     * LDS-bound grids) */
-    hipStream_t side = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
+    /* one stream: the raw spans on a second stream beside the verdict batch
+     * measured slower (config 5: 1.659 vs 1.542 ms per pass,
+     * profiles/r03/cpass_streams.jsonl) */
 };
 
 namespace {
@@ -75,12 +73,6 @@ void cpass_free(zscrc_cpass *p)
         (void)hipFree(p->dflags_full);
     if (p->dspan_commit)
         (void)hipFree(p->dspan_commit);
-    if (p->fork)
-        (void)hipEventDestroy(p->fork);
-    if (p->join)
-        (void)hipEventDestroy(p->join);
-    if (p->side)
-        (void)hipStreamDestroy(p->side);
     delete p;
 }
 
@@ -121,12 +113,6 @@ extern "C" int zscrc_cpass_create(zscrc_cpass **out, const zscrc_cpass_spec *spe
         e = hipMalloc(&p->dflags_full, 4 * p->cap);
     if (e == hipSuccess)
         e = hipMalloc(&p->dspan_commit, (8 + 4) * zs::CPASS_SPANS);
-    if (e == hipSuccess)
-        e = hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking);
-    if (e == hipSuccess)
-        e = hipEventCreateWithFlags(&p->fork, hipEventDisableTiming);
-    if (e == hipSuccess)
-        e = hipEventCreateWithFlags(&p->join, hipEventDisableTiming);
     if (e != hipSuccess) {
         cpass_free(p);
         return ZSCRC_ENOMEM;
@@ -150,18 +136,12 @@ extern "C" int zscrc_cpass_run(zscrc_cpass *p, void *stream, zscrc_cpass_result 
     const zscrc_cpass_spec &sp = p->spec;
     uint64_t *d_nbad = reinterpret_cast<uint64_t *>(p->dblk);
     uint32_t *d_raw = reinterpret_cast<uint32_t *>(p->dblk + OFF_RAW);
-    const bool two = sp.nspans && !getenv("ZSCRC_CPASS_ONE_STREAM");
-    int rc = ZSCRC_OK;
-    if (two && (hipEventRecord(p->fork, s) != hipSuccess || hipStreamWaitEvent(p->side, p->fork, 0) != hipSuccess))
-        rc = ZSCRC_EHIP;
-    if (!rc)
-        rc = zscrc_device_verify_commits_verdict(sp.d_image, sp.image_size, sp.d_off, sp.d_len, nullptr, sp.n,
+    int rc = zscrc_device_verify_commits_verdict(sp.d_image, sp.image_size, sp.d_off, sp.d_len, nullptr, sp.n,
                                                  sp.max_len, d_nbad, p->dbad_full, p->cap, s);
     if (!rc && hipMemsetAsync(p->dblk + 8, 0, 8, s) != hipSuccess)
         rc = ZSCRC_EHIP;
     /* raw spans: up to 8 of >= 16 KiB per launch pair, else one by one */
     const uint8_t *img = static_cast<const uint8_t *>(sp.d_image);
-    hipStream_t ss = two ? p->side : s;
     for (size_t i = 0; !rc && i < sp.nspans;) {
         const void *bufs[8];
         uint64_t lens[8];
@@ -172,15 +152,13 @@ extern "C" int zscrc_cpass_run(zscrc_cpass *p, void *stream, zscrc_cpass_result 
             ++k;
         }
         if (k >= 2) {
-            rc = zscrc_device_spans(bufs, lens, nullptr, d_raw + i, k, ZSCRC_RAW, ss);
+            rc = zscrc_device_spans(bufs, lens, nullptr, d_raw + i, k, ZSCRC_RAW, s);
             i += k;
         } else {
-            rc = zscrc_device_span(img + p->span_off[i], p->span_len[i], 0, d_raw + i, nullptr, ZSCRC_RAW, ss);
+            rc = zscrc_device_span(img + p->span_off[i], p->span_len[i], 0, d_raw + i, nullptr, ZSCRC_RAW, s);
             ++i;
         }
     }
-    if (!rc && two && (hipEventRecord(p->join, p->side) != hipSuccess || hipStreamWaitEvent(s, p->join, 0) != hipSuccess))
-        rc = ZSCRC_EHIP;
     if (!rc) {
         zs::CPassArgs a;
         memset(&a, 0, sizeof a);
