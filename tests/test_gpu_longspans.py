@@ -1,0 +1,150 @@
+"""Long commit spans through the unbounded commit route: zsbench NOTBATCHED
+layouts (benchmark/zsbench.c:159-217 writeseq: one commit per ~2 MiB file,
+spans as written by src/zeroskip-file.c:253-350) and longer -- a span past the
+short commit's 24-bit length takes the long commit trailer (writer
+semantics, zeroskip-file.c:266-302).  Without a caller bound the batch goes
+classify -> plan -> parts (xteam_kernel's parts mode for class 3, team<16>
+parts for class 2) -> part fold; every CRC, status, verdict and written CRC
+against the format oracle, on both class-3 routes (xteam parts and team<64>
+parts, tuning bit 65536) and both classify forms (one single-block launch
+with the plans, or two passes and plan launches: bit 524288), with corruptions at a record's first byte, its
+last span byte, its stored CRC and bytes either side of a part boundary."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import zs_format as zf
+from tests.test_format_oracle import UUID
+from zeroskip_amd import zsfile
+from zeroskip_amd._lib import lib
+
+pytestmark = pytest.mark.gpu
+
+TEAM64_PARTS = 65536  # zs::BatchDesc::opt: class 3 on team<64> parts instead of xteam parts
+MULTI_CLASSIFY = 524288  # opt: two multi-block classify passes + plan launches (not the single-block one)
+OPTS = [0, TEAM64_PARTS, MULTI_CLASSIFY]
+IDS = ["xteam-parts", "team64-parts", "multi-classify"]
+
+# transaction sizes in bytes of value payload: class 3 (> g16_max) records
+# of 0.3-3 MiB, one past 16 MiB (long commit), class 2 and short ones beside
+SIZES = [[2_100_000, 312, 3_000_000], [1_100_000, 20_000, 300_000, 17_000_000], [9_000, 2_200_000, 5_000, 64]]
+
+
+def _db(seed=11):
+    rng = np.random.default_rng(seed)
+    parts, commits, base = [], [], 0
+    for f, sizes in enumerate(SIZES):
+        w = zf.FileWriter(UUID, idx=f)
+        for t, size in enumerate(sizes):
+            left = size
+            k = 0
+            while left > 0:               # values of up to 1 MiB per key
+                v = min(left, 1 << 20)
+                w.add(b"%08d-%07d" % (f * 100 + t, k), rng.integers(0, 256, v, dtype=np.uint8).tobytes())
+                left -= v
+                k += 1
+            w.commit()
+        img = w.image()
+        cs, _, _ = zf.walk(img)
+        for c in cs:
+            c = dict(c)
+            c["span_off"] += base
+            c["commit_off"] += base
+            commits.append(c)
+        parts.append(img)
+        base += len(img)
+    host = np.frombuffer(b"".join(parts), np.uint8).copy()
+    offs = np.array([c["span_off"] for c in commits], np.int64)
+    lens = np.array([c["span_len"] for c in commits], np.int64)
+    return host, offs, lens, commits
+
+
+@pytest.fixture(scope="module")
+def db():
+    return _db()
+
+
+def _with_opt(opt, fn):
+    lib().zscrc_set_opt(opt)
+    try:
+        r = fn()
+        torch.cuda.synchronize()
+    finally:
+        lib().zscrc_set_opt(0)
+    return r
+
+
+def test_layout(db):
+    host, offs, lens, commits = db
+    assert len(commits) == sum(len(s) for s in SIZES)
+    assert lens.max() > (1 << 24)             # one long commit trailer
+    assert all(c["ok"] for c in commits)
+
+
+@pytest.mark.parametrize("opt", OPTS, ids=IDS)
+def test_long_spans_match_oracle(gpu, db, opt):
+    host, offs, lens, commits = db
+    d = torch.from_numpy(host).cuda()
+    o, ln = torch.from_numpy(offs).cuda(), torch.from_numpy(lens).cuda()
+    crc, st = _with_opt(opt, lambda: zsfile.verify_commits(d, o, ln))
+    crc = crc.cpu().numpy().view(np.uint32)
+    assert (crc == np.array([c["computed"] for c in commits], np.uint32)).all()
+    assert (st.cpu().numpy() == 1).all()
+    nbad, _ = _with_opt(opt, lambda: zsfile.verify_commits_verdict(d, o, ln))
+    assert int(nbad.item()) == 0
+
+
+@pytest.mark.parametrize("opt", OPTS, ids=IDS)
+def test_long_spans_corruptions(gpu, db, opt):
+    host, offs, lens, commits = db
+    h = host.copy()
+    big = [i for i in range(len(commits)) if lens[i] > 1_000_000]
+    hit = {}
+    i0, i1, i2, i3 = big[:4]
+    h[offs[i0]] ^= 0x01                              # first span byte (the short first part)
+    h[offs[i1] + lens[i1] - 1] ^= 0x80               # last span byte
+    e = commits[i2]["commit_off"] + (20 if lens[i2] > (1 << 24) else 4)
+    h[e] ^= 0x10                                     # the stored CRC
+    h[offs[i3] + lens[i3] // 2] ^= 0x02              # mid-span, near a part boundary
+    h[offs[i3] + lens[i3] // 2 + 1] ^= 0x02          # (two flips in one record)
+    hit = {i0, i1, i2, i3}
+    d = torch.from_numpy(h).cuda()
+    o, ln = torch.from_numpy(offs).cuda(), torch.from_numpy(lens).cuda()
+    crc, st = _with_opt(opt, lambda: zsfile.verify_commits(d, o, ln))
+    crc = crc.cpu().numpy().view(np.uint32)
+    hb = h.tobytes()
+    for i, c in enumerate(commits):
+        assert crc[i] == zf._commit_check(hb, c["commit_off"])[4], i
+    assert set(np.nonzero(st.cpu().numpy() != 1)[0].tolist()) == hit
+    nbad, bad = _with_opt(opt, lambda: zsfile.verify_commits_verdict(d, o, ln))
+    assert int(nbad.item()) == len(hit) and set(bad[:len(hit)].cpu().tolist()) == hit
+
+
+@pytest.mark.parametrize("opt", OPTS, ids=IDS)
+def test_long_spans_writer(gpu, db, opt):
+    """write_commits over blanked CRC fields: the image byte for byte"""
+    host, offs, lens, commits = db
+    blank = host.copy()
+    for c in commits:
+        at = c["commit_off"] + (20 if c["span_len"] > (1 << 24) else 4)
+        blank[at:at + 4] = 0
+    d = torch.from_numpy(blank).cuda()
+    o, ln = torch.from_numpy(offs).cuda(), torch.from_numpy(lens).cuda()
+    _with_opt(opt, lambda: zsfile.write_commits(d, o, ln, crc=False))
+    assert np.array_equal(d.cpu().numpy(), host)
+
+
+def test_long_spans_seeded_crc_batch(gpu, db):
+    """the same spans as a plain CRC batch with per-record seeds (the fold's
+    non-commit output)"""
+    from oracle import oracle
+    from zeroskip_amd import device
+    host, offs, lens, _ = db
+    rng = np.random.default_rng(3)
+    seeds = rng.integers(0, 2**32, len(offs), dtype=np.uint64).astype(np.uint32)
+    d = torch.from_numpy(host).cuda()
+    out = device.crc_batch(d, torch.from_numpy(offs).cuda(), torch.from_numpy(lens).cuda(),
+                           seeds=torch.from_numpy(seeds.view(np.int32)).cuda())
+    got = out.cpu().numpy().view(np.uint32)
+    for i in range(len(offs)):
+        assert got[i] == oracle.crc32c_hw(int(seeds[i]), host[offs[i]:offs[i] + lens[i]]), i

@@ -425,6 +425,9 @@ int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t max_len =
     return rc ? rc : rc2;
 }
 
+/* batches up to this many records classify in one single-block launch */
+constexpr uint64_t SMALL_CLASSIFY = 16384;
+
 int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1, uint64_t g16)
 {
     const uint64_t n = d.n;
@@ -433,15 +436,16 @@ int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1
         b1 = g1;
     const uint64_t b2 = g16 > b1 ? g16 : b1;
     /* classes buffer: [0,32) class sizes + scatter cursors, [32,64) class
-     * byte totals, [64,128) split plans, [256, ...) class-sorted descriptors */
+     * byte totals, [64,160) split plans, [256, ...) class-sorted descriptors */
     constexpr size_t HEAD = 256;
     const size_t list_bytes = HEAD + n * sizeof(zs::RecDesc);
     const int gs = g_split_team;
     /* split target per class: two items per team of the launch */
     auto split_items = [&](int g) { return 2u * (uint32_t)c->ncu * 16u * (uint32_t)(64 / g); };
     const size_t T = split_items(16) > split_items(gs) ? split_items(16) : split_items(gs);
-    /* parts buffer: part registers (< 2T), part_rec (< 2T), part_base (< T) */
-    const size_t part_bytes = 5 * T * sizeof(uint32_t);
+    /* parts buffer, one half per split class (2, 3): part registers (< 2T),
+     * part_rec (< 2T), part_base (< T) */
+    const size_t part_bytes = 2 * 5 * T * sizeof(uint32_t);
     {
         int rc = grow(&c->classes, &c->classes_bytes, list_bytes);
         if (!rc)
@@ -453,13 +457,34 @@ int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1
     uint64_t *cbytes = reinterpret_cast<uint64_t *>(static_cast<char *>(c->classes) + 32);
     zs::SplitPlan *plans = reinterpret_cast<zs::SplitPlan *>(static_cast<char *>(c->classes) + 64);
     zs::RecDesc *desc = reinterpret_cast<zs::RecDesc *>(static_cast<char *>(c->classes) + HEAD);
-    uint32_t *part_out = static_cast<uint32_t *>(c->parts);
-    uint32_t *part_rec = part_out + 2 * T;
-    uint32_t *part_base = part_rec + 2 * T;
-    hipError_t e = hipMemsetAsync(cnt, 0, HEAD, s);
-    if (e != hipSuccess) {
-        set_err("hipMemsetAsync(class counters)", e);
-        return ZSCRC_EHIP;
+    const int team[4] = {1, 16, 16, gs};
+    const int walk[4] = {-1, 1, 0, 0};
+    /* classes 2-3 with fewer records than two per team are cut into equal
+     * parts (a lone 1 MiB record would otherwise be one team's serial walk; a
+     * few 3 GiB regions beside small records would leave most teams idle),
+     * folded per record afterwards.  Class 3 (> g16_max): parts on
+     * xteam_kernel's coalesced whole-wave teams, every record through the
+     * part fold. */
+    const bool xparts = g_xteam && !(d.opt & 65536);
+    zs::PlanArgs pa[2];
+    uint32_t *part_out[2];
+    for (int k = 2; k < 4; ++k) {
+        zs::PlanArgs &p = pa[k - 2];
+        memset(&p, 0, sizeof p);
+        p.count = cnt;
+        p.bytes = cbytes;
+        p.desc = desc;
+        p.klass = (uint32_t)k;
+        p.target = split_items(team[k]);
+        if (k == 3 && g_xteam && (d.opt & 131072))
+            p.target *= 2; /* four parts per wave (A/B) */
+        p.unit_min = (uint64_t)team[k] * 64 * 16; /* 16 steps of the team */
+        p.always_split = k == 3 && xparts ? 1u : 0u;
+        p.gtab = c->gtab;
+        p.plan = plans;
+        part_out[k - 2] = static_cast<uint32_t *>(c->parts) + (k == 3 ? 5 * T : 0);
+        p.part_rec = part_out[k - 2] + 2 * T;
+        p.part_base = p.part_rec + 2 * T;
     }
     zs::Classify cl;
     memset(&cl, 0, sizeof cl);
@@ -481,7 +506,20 @@ int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1
         const int w0 = g_depth[0];
         cl.direct_ok = g1 > 0 && (w0 < 0 || w0 >= 9);
     }
-    for (int pass = 0; pass < 2; ++pass) {
+    /* small batches: one single-block classify launch that also writes the
+     * counters and both plans (no memset, no second pass, no plan launches) */
+    cl.single = n <= SMALL_CLASSIFY && !(d.opt & 524288) ? 1 : 0;
+    if (cl.single) {
+        cl.plan[0] = pa[0];
+        cl.plan[1] = pa[1];
+    } else {
+        hipError_t e = hipMemsetAsync(cnt, 0, HEAD, s);
+        if (e != hipSuccess) {
+            set_err("hipMemsetAsync(class counters)", e);
+            return ZSCRC_EHIP;
+        }
+    }
+    for (int pass = 0; pass < (cl.single ? 1 : 2); ++pass) {
         cl.pass = pass;
         if (zs_launch_classify(&cl, s)) {
             set_err("classify launch", hipGetLastError());
@@ -489,51 +527,36 @@ int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1
         }
         g_stat[2]++;
     }
-    const int team[4] = {1, 16, 16, gs};
-    const int walk[4] = {-1, 1, 0, 0};
     d.len_lo = 0;
     d.len_hi = ~0ull;
     d.desc = desc;
     d.class_count = cnt;
-    for (int k = 0; k < 4; ++k) {
+    /* class 3 first: its long launch is queued while the host still submits
+     * the small ones, which then run back to back behind it (the parts
+     * buffers are per class); the folds last */
+    zs::BatchDesc fold[2];
+    int nfold = 0;
+    for (const int k : {3, 0, 1, 2}) {
         zs::BatchDesc dk = d;
         dk.klass = (uint32_t)k;
         if (k == 0 && cl.direct_ok)
             dk.direct_max = g1;
         if (k >= 2) {
-            /* classes 2-3 with fewer records than two per team are cut into
-             * equal parts (a lone 1 MiB record would otherwise be one team's
-             * serial walk; a few 3 GiB regions beside small records would
-             * leave most teams idle), folded per record afterwards */
-            zs::PlanArgs pa;
-            pa.count = cnt;
-            pa.bytes = cbytes;
-            pa.desc = desc;
-            pa.klass = (uint32_t)k;
-            pa.target = split_items(team[k]);
-            if (k == 3 && g_xteam && (d.opt & 131072))
-                pa.target *= 2; /* four parts per wave (A/B) */
-            pa.unit_min = (uint64_t)team[k] * 64 * 16; /* 16 steps of the team */
-            /* class 3 (> g16_max): parts on xteam_kernel's coalesced whole-wave
-             * teams, every record through the part fold */
-            const bool xparts = k == 3 && g_xteam && !(d.opt & 65536);
-            pa.always_split = xparts ? 1u : 0u;
-            pa.plan = plans;
-            pa.part_base = part_base;
-            pa.part_rec = part_rec;
-            if (zs_launch_plan(&pa, s)) {
-                set_err("split plan launch", hipGetLastError());
-                return ZSCRC_EHIP;
+            if (!cl.single) {
+                if (zs_launch_plan(&pa[k - 2], s)) {
+                    set_err("split plan launch", hipGetLastError());
+                    return ZSCRC_EHIP;
+                }
+                g_stat[2]++;
             }
-            g_stat[2]++;
             dk.split = 1;
             dk.plan = plans;
-            dk.part_base = part_base;
-            dk.part_rec = part_rec;
-            dk.part_out = part_out;
+            dk.part_base = pa[k - 2].part_base;
+            dk.part_rec = pa[k - 2].part_rec;
+            dk.part_out = part_out[k - 2];
         }
         int rc;
-        if (k == 3 && g_xteam && !(d.opt & 65536)) {
+        if (k == 3 && xparts) {
             rc = zs_launch_xparts(&dk, c->gtab, c->ncu, s) ? ZSCRC_EHIP : ZSCRC_OK;
             if (rc)
                 set_err("xparts launch", hipGetLastError());
@@ -544,13 +567,15 @@ int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1
         }
         if (rc)
             return rc;
-        if (k >= 2) {
-            if (zs_launch_part_fold(&dk, c->gtab, s)) {
-                set_err("part fold launch", hipGetLastError());
-                return ZSCRC_EHIP;
-            }
-            g_stat[2]++;
+        if (k >= 2)
+            fold[nfold++] = dk;
+    }
+    for (int i = 0; i < nfold; ++i) {
+        if (zs_launch_part_fold(&fold[i], c->gtab, s)) {
+            set_err("part fold launch", hipGetLastError());
+            return ZSCRC_EHIP;
         }
+        g_stat[2]++;
     }
     return ZSCRC_OK;
 }

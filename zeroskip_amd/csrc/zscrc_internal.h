@@ -57,7 +57,8 @@ struct BatchDesc {
     uint64_t direct_max;
     /* split != 0: this class may be split into parts (plan_kernel decides
      * from the class's record count and bytes, plan[klass]); part p of
-     * record part_rec[p] covers bytes [(p - part_base[rec]) * unit, +unit);
+     * record part_rec[p] covers part p - part_base[rec] of it (split_part:
+     * the first part the rest of len / unit, then unit bytes each);
      * raw part registers go to part_out[p], part_fold_kernel folds them */
     uint32_t split;
     uint32_t opt;         /* tuning bits: 1 = no three-chain five-piece bursts, 2 = no multi64_kernel,
@@ -71,7 +72,9 @@ struct BatchDesc {
                              commit_kernel, 65536 = split class 3 on team_kernel<64>
                              instead of xteam_kernel's parts mode, 131072 = four parts
                              per wave there instead of two, 262144 = diagnostic: multi64_kernel
-                             stores its results into one L2-resident window (wrong results) */
+                             stores its results into one L2-resident window (wrong results),
+                             524288 = small variable batches classify in two multi-block
+                             passes and plan launches instead of one single-block launch */
     uint32_t *part_out;
     /* commit verdict mode (bad_count != NULL): no per-record out / status;
      * every commit whose status is not 1 is counted in *bad_count and its
@@ -156,6 +159,35 @@ struct RecDesc {
     uint32_t rec;         /* index in the caller's batch */
 };
 
+
+/* Offset of a commit descriptor whose span or commit word lies outside the
+ * image (classify_kernel writes it with length 0; status 2). */
+constexpr uint64_t NO_COMMIT_OFF = ~0ull;
+
+/* How a length class is split (written by plan_kernel on the device). */
+struct SplitPlan {
+    uint64_t unit;   /* bytes per part (the FIRST part of a record: the rest,
+                      * 1..unit bytes, so every later part is exactly unit) */
+    uint32_t parts;  /* work items: parts in all, or records when direct     */
+    uint32_t direct; /* 1 = enough records: no split                          */
+    uint32_t K;      /* x^(8 unit) mod P: the part fold's Horner multiplier   */
+    uint32_t pad;
+};
+
+struct PlanArgs {
+    const uint32_t *count; /* class sizes */
+    const uint64_t *bytes; /* class byte totals */
+    const struct RecDesc *desc;
+    uint32_t klass;
+    uint32_t target;       /* items wanted: two per team of the launch */
+    uint64_t unit_min;     /* smallest part worth a team */
+    uint32_t always_split; /* never direct: every record one part at least (xteam parts) */
+    SplitPlan *plan;
+    uint32_t *part_base;   /* per record of the class: its first part */
+    uint32_t *part_rec;    /* per part: its record */
+    const uint32_t *gtab;  /* operator tables (x^(8 2^k) for K) */
+};
+
 struct Classify {
     const uint64_t *off;
     const uint64_t *len;
@@ -173,30 +205,13 @@ struct Classify {
     int commit;           /* commit batch: spans outside img_size become
                              empty no-commit descriptors (NO_COMMIT_OFF) */
     uint64_t img_size;
-};
-
-/* Offset of a commit descriptor whose span or commit word lies outside the
- * image (classify_kernel writes it with length 0; status 2). */
-constexpr uint64_t NO_COMMIT_OFF = ~0ull;
-
-/* How a length class is split (written by plan_kernel on the device). */
-struct SplitPlan {
-    uint64_t unit;   /* bytes per part (the last part of a record: the rest) */
-    uint32_t parts;  /* work items: parts in all, or records when direct     */
-    uint32_t direct; /* 1 = enough records: no split                          */
-};
-
-struct PlanArgs {
-    const uint32_t *count; /* class sizes */
-    const uint64_t *bytes; /* class byte totals */
-    const struct RecDesc *desc;
-    uint32_t klass;
-    uint32_t target;       /* items wanted: two per team of the launch */
-    uint64_t unit_min;     /* smallest part worth a team */
-    uint32_t always_split; /* never direct: every record one part at least (xteam parts) */
-    SplitPlan *plan;
-    uint32_t *part_base;   /* per record of the class: its first part */
-    uint32_t *part_rec;    /* per part: its record */
+    /* single = 1 (small batches, one block): both passes in one launch, the
+     * counters written rather than accumulated (no zeroing needed), then the
+     * split plans of classes 2 and 3 (plan[0], plan[1]; target 0 = none)
+     * from the block's own counts -- one launch instead of two classify
+     * passes and two plan launches */
+    int single;
+    PlanArgs plan[2];
 };
 
 /* K fixed-stride batches of one launch (zscrc_device_fixed_multi): batch b

@@ -143,6 +143,17 @@ __device__ __forceinline__ uint32_t op4(const char *L, uint32_t base, uint32_t x
  * bytes" lookup -- the compact slice-by-4 table at T (GT_S4, 4 KiB in LDS).
  * The span fold uses it (35 -> 18 us for 8192 parts), and so does
  * part_fold_kernel since it folds one record per wave (round 3). */
+/* Part p of a split record of len bytes cut at unit U (plan_kernel: ceil(len
+ * / U) parts): part 0 holds the first len - (parts - 1) U bytes (1..U), every
+ * later part exactly U -- so the fold is a Horner pass by one multiplier,
+ * x^(8U), with no per-record power (part_fold_kernel). */
+__device__ __forceinline__ void split_part(uint64_t len, uint64_t U, uint64_t part, uint64_t &lo, uint64_t &plen)
+{
+    const uint64_t first = len - ((len + U - 1) / U - 1) * U;
+    lo = part ? first + (part - 1) * U : 0;
+    plen = part ? U : first;
+}
+
 __device__ __forceinline__ uint32_t gmul_t(const char *T, uint32_t a, uint32_t b)
 {
     const uint64_t bb = (uint64_t)b << 32;
@@ -297,12 +308,11 @@ __device__ __forceinline__ bool fetch_record(const BatchDesc &d, const RecDesc *
             it.c1 = ((g32p)T)[1];
         }
         if (sp) {
-            /* part p of the record: bytes [p * unit, +unit), the last one the rest */
+            /* part p of the record (split_part): the first one the rest, then
+             * unit bytes each */
             const uint64_t U = d.plan[d.klass].unit;
             const uint64_t part = w - ((g32p)d.part_base)[idx];
-            lo = part * U < len ? part * U : len;
-            const uint64_t hi = lo + U < len ? lo + U : len;
-            len = hi - lo;
+            split_part(len, U, part, lo, len);
             if (part)
                 seed = d.xor_io; /* parts after the first start from a zero register */
             rec = w;             /* part_out index */
@@ -827,8 +837,8 @@ __device__ __forceinline__ void xgeom(const XDesc &d, const XMulti &m, const XPa
         const uint32_t seed = __builtin_amdgcn_readfirstlane(((g32p)r)[4]);
         const uint64_t U = uni64(((g64p)(xp.plan + xp.klass))[0]);
         const uint64_t part = w - __builtin_amdgcn_readfirstlane(((g32p)xp.part_base)[idx]);
-        const uint64_t a = part * U < rlen ? part * U : rlen;
-        len = (a + U < rlen ? a + U : rlen) - a;
+        uint64_t a;
+        split_part(rlen, U, part, a, len);
         A = reinterpret_cast<uintptr_t>(xp.base) + off + a;
         lo = reinterpret_cast<uintptr_t>(xp.base) & ~uintptr_t(3);
         R0 = part ? 0u : seed ^ xp.xor_io; /* later parts start from a zero register */
@@ -2685,6 +2695,85 @@ __device__ __forceinline__ int class_of(const Classify &c, uint64_t len)
     return len <= c.bound[0] ? 0 : len <= c.bound[1] ? 1 : len <= c.bound[2] ? 2 : 3;
 }
 
+/* The scatter pass of classify_kernel over records [r0, r1): class k's
+ * records go to desc[slot[k] + ...] (LDS cursors pos[k]). */
+__device__ __forceinline__ void classify_scatter(const Classify &c, const uint32_t *slot, uint32_t *pos, uint64_t r0,
+                                                 uint64_t r1)
+{
+    const int lane = threadIdx.x & 63;
+    const __attribute__((address_space(1))) uint64_t *lens = (const __attribute__((address_space(1))) uint64_t *)c.len;
+    const __attribute__((address_space(1))) uint64_t *offs = (const __attribute__((address_space(1))) uint64_t *)c.off;
+    for (uint64_t b = r0 + (threadIdx.x & ~63u); b < r1; b += CWG) {
+        const uint64_t rec = b + lane;
+        int cls = -1;
+        uint64_t len = 0, off = 0;
+        if (rec < r1) {
+            len = lens[rec];
+            off = offs[rec];
+            if (c.commit && !commit_fits(c.img_size, off, len)) {
+                off = NO_COMMIT_OFF;
+                len = 0;
+            }
+            cls = class_of(c, len);
+            if (cls == 0 && c.direct_ok)
+                cls = -1; /* the class-0 kernel reads the caller's arrays */
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint64_t m = __ballot(cls == k);
+            if (!m)
+                continue;
+            const int leader = __ffsll((unsigned long long)m) - 1;
+            uint32_t p = 0;
+            if (lane == leader)
+                p = atomicAdd(&pos[k], (uint32_t)__popcll(m));
+            p = __shfl(p, leader);
+            if (cls == k) {
+                RecDesc r;
+                r.off = off;
+                r.len = len;
+                r.seed = c.seed ? ((g32p)c.seed)[rec] : 0u;
+                r.rec = (uint32_t)rec;
+                c.desc[slot[k] + p + __popcll(m & ((1ull << lane) - 1))] = r;
+            }
+        }
+    }
+}
+
+__device__ void plan_block(const PlanArgs &a, uint32_t first, uint32_t count, uint64_t bytes, uint32_t *sbase,
+                           uint32_t *wsum, char *T);
+
+/* classify_kernel with one block (Classify::single): the counts are the
+ * block's own, so the counters, byte totals and class offsets are written,
+ * the scatter follows in the same launch, then the split plans of classes 2
+ * and 3 from the same counts. */
+__device__ void classify_single(const Classify &c, uint32_t *cnt, const unsigned long long *bsum, uint64_t r0,
+                                uint64_t r1)
+{
+    __shared__ uint32_t slot[4], pos[4];
+    __shared__ uint32_t sbase[1025];
+    __shared__ uint32_t wsum[16];
+    __shared__ __attribute__((aligned(16))) char T[4096];
+    if (threadIdx.x < 4) {
+        uint32_t base = 0;
+        for (uint32_t k = 0; k < threadIdx.x; ++k)
+            base += cnt[k];
+        slot[threadIdx.x] = base;
+        pos[threadIdx.x] = 0;
+        c.count[threadIdx.x] = cnt[threadIdx.x];
+        c.count[4 + threadIdx.x] = cnt[threadIdx.x];
+        c.bytes[threadIdx.x] = bsum[threadIdx.x];
+    }
+    __syncthreads();
+    if (!(c.direct_ok && cnt[0] == c.n))
+        classify_scatter(c, slot, pos, r0, r1);
+    __threadfence();
+    __syncthreads();
+    for (int k = 2; k < 4; ++k)
+        if (c.plan[k - 2].target)
+            plan_block(c.plan[k - 2], slot[k], cnt[k], bsum[k], sbase, wsum, T);
+}
+
 __global__ __launch_bounds__(CWG) void classify_kernel(Classify c)
 {
     __shared__ uint32_t cnt[4], slot[4], pos[4];
@@ -2745,6 +2834,10 @@ __global__ __launch_bounds__(CWG) void classify_kernel(Classify c)
         }
     }
     __syncthreads();
+    if (c.single) {
+        classify_single(c, cnt, bsum, r0, r1);
+        return;
+    }
     if (c.pass == 0) {
         if (threadIdx.x < 4 && cnt[threadIdx.x]) {
             atomicAdd(&c.count[threadIdx.x], cnt[threadIdx.x]);
@@ -2759,58 +2852,23 @@ __global__ __launch_bounds__(CWG) void classify_kernel(Classify c)
         slot[threadIdx.x] = base + (cnt[threadIdx.x] ? atomicAdd(&c.count[4 + threadIdx.x], cnt[threadIdx.x]) : 0);
     }
     __syncthreads();
-    for (uint64_t b = r0 + (threadIdx.x & ~63u); b < r1; b += CWG) {
-        const uint64_t rec = b + lane;
-        int cls = -1;
-        uint64_t len = 0, off = 0;
-        if (rec < r1) {
-            len = lens[rec];
-            off = offs[rec];
-            if (c.commit && !commit_fits(c.img_size, off, len)) {
-                off = NO_COMMIT_OFF;
-                len = 0;
-            }
-            cls = class_of(c, len);
-            if (cls == 0 && c.direct_ok)
-                cls = -1; /* the class-0 kernel reads the caller's arrays */
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint64_t m = __ballot(cls == k);
-            if (!m)
-                continue;
-            const int leader = __ffsll((unsigned long long)m) - 1;
-            uint32_t p = 0;
-            if (lane == leader)
-                p = atomicAdd(&pos[k], (uint32_t)__popcll(m));
-            p = __shfl(p, leader);
-            if (cls == k) {
-                RecDesc r;
-                r.off = off;
-                r.len = len;
-                r.seed = c.seed ? ((g32p)c.seed)[rec] : 0u;
-                r.rec = (uint32_t)rec;
-                c.desc[slot[k] + p + __popcll(m & ((1ull << lane) - 1))] = r;
-            }
-        }
-    }
+    classify_scatter(c, slot, pos, r0, r1);
 }
 
 /* Split plan of one length class (one block; runs after the scatter): with
  * fewer records than `target`, every record is cut into ceil(len / unit)
  * parts, unit ~ class bytes / target -- parts of equal size whatever the mix
  * of record lengths, so the work items balance over the chip.  Writes
- * part_base (first part of each record, a block-wide scan) and part_rec
- * (record of each part, a search in the chunk's bases in LDS). */
-__global__ __launch_bounds__(1024) void plan_kernel(PlanArgs a)
+ * part_base (first part of each record, a block-wide scan), part_rec (record
+ * of each part, a search in the chunk's bases in LDS) and the plan with K =
+ * x^(8 unit).  first / count / bytes: the class's offset in the class-sorted
+ * list and its size.  Run by plan_kernel, or by the single-block classify of
+ * a small batch right after its scatter (the list read with device-coherent
+ * loads). */
+__device__ void plan_block(const PlanArgs &a, uint32_t first, uint32_t count, uint64_t bytes, uint32_t *sbase,
+                           uint32_t *wsum, char *T)
 {
-    __shared__ uint32_t sbase[1025];
-    __shared__ uint32_t wsum[16];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    uint32_t first = 0;
-    for (uint32_t k = 0; k < a.klass; ++k)
-        first += a.count[k];
-    const uint32_t count = a.count[a.klass];
     const RecDesc *list = a.desc + first;
     SplitPlan *pl = a.plan + a.klass;
     if (count == 0 || (count >= a.target && !a.always_split)) {
@@ -2818,6 +2876,7 @@ __global__ __launch_bounds__(1024) void plan_kernel(PlanArgs a)
             pl->unit = 0;
             pl->parts = count;
             pl->direct = 1;
+            pl->K = 0x80000000u;
         }
         return;
     }
@@ -2826,16 +2885,18 @@ __global__ __launch_bounds__(1024) void plan_kernel(PlanArgs a)
      * item more than the others (a 2% overshoot of 2 items per team would
      * leave the kernel waiting on teams with 3) */
     const uint64_t room = a.target > count ? a.target - count : 1;
-    uint64_t unit = (a.bytes[a.klass] + room - 1) / room;
+    uint64_t unit = (bytes + room - 1) / room;
     unit = (unit + 63) & ~63ull;
     if (unit < a.unit_min)
         unit = a.unit_min;
     if (count >= a.target) /* always_split: one part per record */
         unit = ~0ull >> 8;
+    load_gmul_table(T, a.gtab);
+    __syncthreads();
     uint32_t running = 0;
     for (uint32_t c0 = 0; c0 < count; c0 += 1024) {
         const uint32_t r = c0 + t;
-        const uint32_t np = r < count ? (uint32_t)((list[r].len + unit - 1) / unit) : 0u;
+        const uint32_t np = r < count ? (uint32_t)((((const volatile uint64_t *)&list[r].len)[0] + unit - 1) / unit) : 0u;
         uint32_t v = np;
         for (int o = 1; o < 64; o <<= 1) {
             const uint32_t u = __shfl_up(v, o);
@@ -2871,84 +2932,86 @@ __global__ __launch_bounds__(1024) void plan_kernel(PlanArgs a)
         running = hi;
         __syncthreads();
     }
-    if (t == 0) {
-        pl->unit = unit;
-        pl->parts = running;
-        pl->direct = 0;
+    if (wv == 0) {
+        /* K = x^(8 unit): the product of x^(8 2^k) over unit's set bits, a
+         * six-level tree across the wave (gmul commutes) */
+        const uint32_t *pow2 = a.gtab + GT_POW2;
+        uint32_t v = (lane < 56 && ((unit >> lane) & 1)) ? pow2[lane] : 0x80000000u;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1)
+            v = gmul_t(T, v, __shfl_xor(v, o));
+        if (lane == 0) {
+            pl->unit = unit;
+            pl->parts = running;
+            pl->direct = 0;
+            pl->K = v;
+        }
     }
 }
 
-
-/* x^(8n) mod P by square-and-multiply over the table x^(8*2^k) (table gmul). */
-__device__ __forceinline__ uint32_t xpow8_t(const char *T, const uint32_t *pow2, uint64_t n)
+__global__ __launch_bounds__(1024) void plan_kernel(PlanArgs a)
 {
-    uint32_t r = 0x80000000u;
-    for (int k = 0; n; ++k, n >>= 1)
-        if (n & 1)
-            r = gmul_t(T, r, pow2[k]);
-    return r;
+    __shared__ uint32_t sbase[1025];
+    __shared__ uint32_t wsum[16];
+    __shared__ __attribute__((aligned(16))) char T[4096];
+    uint32_t first = 0;
+    for (uint32_t k = 0; k < a.klass; ++k)
+        first += a.count[k];
+    plan_block(a, first, a.count[a.klass], a.bytes[a.klass], sbase, wsum, T);
 }
 
-/* One wave per record of a split class: H = sum over the uniform parts p <
- * nu of part[p] * K^(nu-1-p), K = x^(8*unit) (lane t takes part t of each
- * chunk of 64, its power from the ladder K^(2^b); chunks joined by K^64),
- * then reg = H * x^(8*last) ^ part[nu] and the record's output (a CRC, or a
- * commit CRC continued over the commit trailer, compared or written).  The
- * products are table GF(2) multiplies (gmul_t: the compact slice-by-4 table
- * in LDS); the former block-per-record fold with bit-serial products took
- * 41-45 us of the NOTBATCHED verify (1,488 records of ~2 MiB, 6 parts each). */
+
+/* One lane per record of a split class (parts cut by split_part: the first
+ * one short, the rest exactly unit bytes): reg = Horner over the part
+ * registers by K = x^(8 unit), reg = reg * K ^ part[p], where * K is four
+ * lookups in a per-block table of K's products with every byte position
+ * (built from 32 basis products, one gmul per lane); then the record's output
+ * (a CRC, or a commit CRC continued over the commit trailer, compared or
+ * written).  The round-2/3 wave-per-record fold, which raised every part to
+ * its own power of x^(8 unit) and each record to x^(8 last) by
+ * square-and-multiply, took 36-40 us of the NOTBATCHED verify (1,488 records
+ * of ~2 MiB, ~6 parts each) -- bit-serial products in one lane. */
 __global__ __launch_bounds__(256) void part_fold_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
 {
     __shared__ __attribute__((aligned(16))) char T[4096];
+    __shared__ uint32_t TK[1024];
+    __shared__ uint32_t basis[32];
     uint32_t base = 0;
     for (uint32_t k = 0; k < d.klass; ++k)
         base += d.class_count[k];
     const uint64_t count = d.class_count[d.klass];
     const RecDesc *list = d.desc + base;
-    if (((const volatile uint32_t *)&d.plan[d.klass].direct)[0])
-        return; /* the team kernel emitted every record itself */
+    if (((const volatile uint32_t *)&d.plan[d.klass].direct)[0] || (uint64_t)blockIdx.x * blockDim.x >= count)
+        return; /* the team kernel emitted every record itself / no records here */
     load_gmul_table(T, gtab);
-    __syncthreads();
-    const uint32_t *pow2 = gtab + GT_POW2;
-    const uint64_t P = d.plan[d.klass].unit;
+    const uint32_t K = ((const volatile uint32_t *)&d.plan[d.klass].K)[0];
     const uint32_t nparts = ((const volatile uint32_t *)&d.plan[d.klass].parts)[0];
-    const int lane = threadIdx.x & 63;
-    /* K^(2^b), b = 0..6, once per wave (the same unit for every record) */
-    uint32_t lad[7];
-    lad[0] = P < (1ull << 56) ? xpow8_t(T, pow2, P) : 0x80000000u;
+    __syncthreads();
+    if (threadIdx.x < 32) /* a * K is linear in a's bits: K * x^(31 - i) */
+        basis[threadIdx.x] = gmul_t(T, 1u << threadIdx.x, K);
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < 1024; e += blockDim.x) {
+        const uint32_t j = e >> 8, b = e & 255;
+        uint32_t v = 0;
 #pragma unroll
-    for (int b = 1; b < 7; ++b)
-        lad[b] = gmul_t(T, lad[b - 1], lad[b - 1]);
-    const uint32_t X4 = pow2[2]; /* x^32: one slice-by-4 step */
-    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    for (uint64_t idx = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); idx < count; idx += nwaves) {
+        for (int t = 0; t < 8; ++t)
+            if ((b >> t) & 1)
+                v ^= basis[8 * j + t];
+        TK[e] = v;
+    }
+    __syncthreads();
+    const uint32_t X4 = gtab[GT_POW2 + 2]; /* x^32: one slice-by-4 step */
+    const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < count; idx += nthr) {
         const RecDesc r = list[idx];
         const uint64_t len = r.len;
         const uint32_t pb = d.part_base[idx];
         const uint32_t m = (idx + 1 < count ? d.part_base[idx + 1] : nparts) - pb; /* 1.. parts */
         const uint32_t *parts = d.part_out + pb;
-        const uint32_t nu = m - 1;                                                /* uniform parts */
-        uint32_t H = 0;
-        for (uint32_t c0 = 0; c0 < nu; c0 += 64) {
-            const uint32_t cn = nu - c0 < 64 ? nu - c0 : 64;
-            uint32_t v = 0;
-            if ((uint32_t)lane < cn) {
-                v = parts[c0 + lane];
-                const uint32_t e = cn - 1 - (uint32_t)lane; /* K^e within the chunk */
-#pragma unroll
-                for (int b = 0; b < 6; ++b)
-                    if ((e >> b) & 1)
-                        v = gmul_t(T, v, lad[b]);
-            }
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1)
-                v ^= __shfl_xor(v, o);
-            H = c0 ? (gmul_t(T, H, cn == 64 ? lad[6] : xpow8_t(T, pow2, P * cn)) ^ v) : v;
-        }
-        if (lane != 0)
-            continue;
-        const uint64_t Lm = len - (uint64_t)nu * P;
-        uint32_t reg = (nu ? gmul_t(T, H, xpow8_t(T, pow2, Lm)) : 0u) ^ parts[nu];
+        uint32_t reg = parts[0];
+        for (uint32_t q = 1; q < m; ++q)
+            reg = TK[reg & 255] ^ TK[256 + ((reg >> 8) & 255)] ^ TK[512 + ((reg >> 16) & 255)] ^ TK[768 + (reg >> 24)] ^
+                  parts[q];
         if (!d.commit) {
             d.out[r.rec] = reg ^ d.xor_io;
             continue;
@@ -3087,7 +3150,7 @@ extern "C" int zs_launch_classify(const zs::Classify *c, hipStream_t stream)
     uint64_t blocks = (c->n + 8191) / 8192;
     if (blocks > 256)
         blocks = 256;
-    if (blocks == 0)
+    if (blocks == 0 || c->single)
         blocks = 1;
     hipLaunchKernelGGL(zs::classify_kernel, dim3((uint32_t)blocks), dim3(zs::CWG), 0, stream, *c);
     return hipGetLastError() == hipSuccess ? 0 : -3;
@@ -3101,7 +3164,7 @@ extern "C" int zs_launch_plan(const zs::PlanArgs *a, hipStream_t stream)
 
 extern "C" int zs_launch_part_fold(const zs::BatchDesc *d, const uint32_t *gtab, hipStream_t stream)
 {
-    hipLaunchKernelGGL(zs::part_fold_kernel, dim3(2048), dim3(256), 0, stream, *d, gtab);
+    hipLaunchKernelGGL(zs::part_fold_kernel, dim3(256), dim3(256), 0, stream, *d, gtab);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
