@@ -410,16 +410,22 @@ def run_config2(args, world, rank, dev, stream):
 
 # ------------------------------------------------------------------ config 4
 def _timed(fn, reps: int, stream) -> float:
-    """median ms of `reps` calls of fn (HIP events on `stream`), one warm call first"""
+    """ms per call of fn: `reps` calls back to back between two HIP events on
+    `stream` (as the timed steps of a line run), the median of three such
+    blocks, one warm call first.  Back to back, the host's submission of a
+    call (Python, ctypes, several launches) overlaps the previous call's
+    kernels instead of being counted as idle GPU time."""
     fn()
+    torch.cuda.synchronize()
     ts = []
-    for _ in range(reps):
+    for _ in range(3):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(stream)
-        fn()
+        for _ in range(reps):
+            fn()
         b.record(stream)
         torch.cuda.synchronize()
-        ts.append(a.elapsed_time(b))
+        ts.append(a.elapsed_time(b) / reps)
     return float(np.median(ts))
 
 

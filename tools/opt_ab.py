@@ -41,6 +41,7 @@ def main():
              "fixed_16KiB": lambda: zd.crc_fixed(c3, 16384, 16384, 262144),
              "fixed_4KiB": lambda: zd.crc_fixed(c3, 4096, 4096, 1 << 20),
              "fixed_1MiB": lambda: zd.crc_fixed(c3, 1 << 20, 1 << 20, 4096),
+             "span_3GiB": lambda: zd.crc_span(c3[:3 << 30]),
              "config4_verify": lambda: zsfile.verify_commits(img, offs, lens, max_len=mx),
              "config4_write": lambda: zsfile.write_commits(img, ow, lw, max_len=mx),
              "config4_write_nocrc": lambda: zsfile.write_commits(img, ow, lw, max_len=mx, crc=False),

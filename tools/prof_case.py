@@ -43,6 +43,15 @@ def main():
             run = lambda k: zsfile.verify_commits(img.view(-1), offs, lens, max_len=mx)  # noqa: E731
         else:                               # the bench line's verdict
             run = lambda k: zsfile.verify_commits_verdict(img.view(-1), offs, lens, max_len=mx, out=vout)  # noqa: E731
+    elif cfg == "config4nb":
+        # NOTBATCHED: one ~2 MiB commit per log file, unbounded verdict (bench.py's notbatched leg)
+        from tools import zsdb_gen as zg
+        ppf = zg.pairs_per_file(False)
+        nfiles = -(-10_000_000 // ppf)
+        img = zg.log_files(bytes(range(16)), 0, nfiles, ppf, 0, False, g, dev, batched=False)
+        offs, lens = zg.log_spans(nfiles, ppf, False, False, dev)
+        vout = (torch.empty(1, dtype=torch.int64, device=dev), torch.empty(64, dtype=torch.int64, device=dev))
+        run = lambda k: zsfile.verify_commits_verdict(img.view(-1), offs, lens, out=vout)  # noqa: E731
     elif cfg == "config4w":
         # the writer side of config 4: every live commit's CRC recomputed and stored
         from tools import zsdb_gen as zg

@@ -28,6 +28,7 @@ __device__ __forceinline__ unsigned m4(const char *L, unsigned x, unsigned c_lo,
                                        lds32(L, a3 + 128), 0u, 0x96);
 }
 
+template <bool NT = true>
 __device__ __forceinline__ void issue(const char *buf, size_t round, unsigned voff, unsigned (&w)[5][16])
 {
     const char *V = buf + round * 64 * GRID;
@@ -35,7 +36,8 @@ __device__ __forceinline__ void issue(const char *buf, size_t round, unsigned vo
     for (int p = 0; p < 5; ++p)
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-            const u32x4 v = __builtin_nontemporal_load((g4p)(V + 4096 * p + 1024 * t + voff));
+            const g4p a = (g4p)(V + 4096 * p + 1024 * t + voff);
+            const u32x4 v = NT ? __builtin_nontemporal_load(a) : *a;
             w[p][4 * t] = v.x;
             w[p][4 * t + 1] = v.y;
             w[p][4 * t + 2] = v.z;
@@ -143,9 +145,17 @@ __global__ __launch_bounds__(WG) void run_probe(const char *buf, unsigned *out)
                 o = desc[r * 64 + lane];
                 l = desc[NREC + r * 64 + lane];
             }
-            issue(buf, r, voff, a);
+            issue<!(X & 8192)>(buf, r, voff, a);
             const unsigned h = consume<HASH>(L, a, c_lo, c_hi) ^ (unsigned)o ^ (unsigned)l;
-            if (X & (128 | 256 | 512)) { /* in place, at the record's own commit word */
+            if (X & 1024) { /* the whole 128 B L2 line holding the record's CRC field */
+                typedef __attribute__((address_space(1))) u32x4 *gw4p;
+                char *R = (char *)buf + (r * 64 + lane) * GRID;
+                char *C = (char *)((uintptr_t)(R + 316) & ~(uintptr_t)127);
+                const u32x4 v = {h, h >> 1, h >> 2, h >> 3};
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    *(gw4p)(C + 16 * k) = v;
+            } else if (X & (128 | 256 | 512)) { /* in place, at the record's own commit word */
                 typedef __attribute__((address_space(1))) u32x4 *gw4p;
                 char *R = (char *)buf + (r * 64 + lane) * GRID;
                 const u32x4 v = {h, h >> 1, h >> 2, h >> 3};
@@ -239,6 +249,10 @@ int main()
         {"hash 8w sb +inplace 4B", timeit(run_probe<512, 0, 1, 128>, cu, 512, d, o)},
         {"hash 8w sb +inplace 32B sector", timeit(run_probe<512, 0, 1, 256>, cu, 512, d, o)},
         {"hash 8w sb +inplace 64B line", timeit(run_probe<512, 0, 1, 512>, cu, 512, d, o)},
+        {"hash 8w sb +inplace 128B line", timeit(run_probe<512, 0, 1, 1024>, cu, 512, d, o)},
+        {"hash 8w sb plain loads", timeit(run_probe<512, 0, 1, 8192>, cu, 512, d, o)},
+        {"hash 8w sb plain loads +inplace 4B", timeit(run_probe<512, 0, 1, 8192 | 128>, cu, 512, d, o)},
+        {"hash 8w sb plain loads +inplace 128B line", timeit(run_probe<512, 0, 1, 8192 | 1024>, cu, 512, d, o)},
         {"hash 8w sb (end)", timeit(run_probe<512, 0, 1>, cu, 512, d, o)},
     };
     for (auto &x : r)

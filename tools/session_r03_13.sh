@@ -1,0 +1,5 @@
+bash tools/gpu_session.sh \
+ "tests:600:python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread" \
+ "smoke:180:python -c 'import __graft_entry__ as g; g.smoke()'" \
+ "bench3:300:python bench.py" \
+ "bench4:300:python bench.py --workload config4 --no-cpu"

@@ -821,21 +821,32 @@ class Consistent:
         rep.bad_rows = np.concatenate(bads) if bads else rep.bad_rows
         rep.stale_rows = np.concatenate(stales) if stales else rep.stale_rows
         dz = rep.dotzsdb
-        if dz.get("present"):
-            uu = {f.uuid for f in self.db.files}
-            if uu - {dz["uuid"]}:
-                rep.issues.append(f"files with a uuid other than .zsdb's: {sorted(uu - {dz['uuid']})}")
-            act = [f for f in self.db.files if f.kind == zsfile.ACTIVE]
-            if len(act) > 1:
-                rep.issues.append(f"{len(act)} active files")
-            for f in act:
-                if f.startidx != dz["curidx"]:
-                    rep.issues.append(f"{f.name}: active index {f.startidx} != .zsdb curidx {dz['curidx']}")
-                elif f.size != dz["offset"]:
-                    rep.issues.append(f"{f.name}: size {f.size} != .zsdb offset {dz['offset']}")
+        rep.issues += self._dotzsdb_issues(dz)
         rep.ok = (not rep.n_bad and not rep.header_errors and not rep.walk_errors
                   and dz.get("ok", False))
         return rep
+
+    def _dotzsdb_issues(self, dz) -> list:
+        """.zsdb against the file set (uuids, the active file's index and
+        size): host metadata only, fixed for an opened DB, so built once (a
+        walk over every file object per run was most of a run's host tail)."""
+        if getattr(self, "_dz_issues", None) is not None and self._dz_key is dz:
+            return self._dz_issues
+        out = []
+        if dz.get("present"):
+            uu = {f.uuid for f in self.db.files}
+            if uu - {dz["uuid"]}:
+                out.append(f"files with a uuid other than .zsdb's: {sorted(uu - {dz['uuid']})}")
+            act = [f for f in self.db.files if f.kind == zsfile.ACTIVE]
+            if len(act) > 1:
+                out.append(f"{len(act)} active files")
+            for f in act:
+                if f.startidx != dz["curidx"]:
+                    out.append(f"{f.name}: active index {f.startidx} != .zsdb curidx {dz['curidx']}")
+                elif f.size != dz["offset"]:
+                    out.append(f"{f.name}: size {f.size} != .zsdb offset {dz['offset']}")
+        self._dz_issues, self._dz_key = out, dz
+        return out
 
     def _check_dotzsdb(self) -> dict:
         d = self.db.dotzsdb
