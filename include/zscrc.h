@@ -197,6 +197,11 @@ const char *zscrc_fixed_kernel(const void *d_base, uint64_t stride, uint64_t len
  * grid_mult x CUs of 1024 threads).  d_scratch4: 4 writable device bytes. */
 int zscrc_diag_stream_read(const void *d_buf, uint64_t len, void *d_scratch4, int grid_mult,
                            void *stream);
+/* Diagnostic: per-wave timestamps of xteam_kernel launches on the current
+ * device -- d_buf (device, 32 bytes per wave of the grid: entry, after the
+ * LDS table fill, end, in s_memrealtime ticks of 100 MHz, and the wave's
+ * record / part count) or NULL to stop. */
+int zscrc_diag_wave_times(void *d_buf);
 /* Number of gfx950 devices visible (0 if none / no HIP runtime). */
 int zscrc_device_count(void);
 

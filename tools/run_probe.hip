@@ -189,6 +189,30 @@ __global__ __launch_bounds__(WG) void run_probe(const char *buf, unsigned *out)
         out[0] = acc;
 }
 
+/* the writer's stores alone: 10 M in-place stores into the records' CRC
+ * fields (W = 4: the 4-byte field; 128: the whole 128 B line holding it), no
+ * reads -- what a separate scatter launch after a read-only pass would cost */
+template <int W>
+__global__ __launch_bounds__(1024) void scatter_probe(const char *buf, unsigned *o)
+{
+    typedef __attribute__((address_space(1))) u32x4 *gw4p;
+    typedef __attribute__((address_space(1))) unsigned *gw32p;
+    const size_t nt = (size_t)gridDim.x * blockDim.x;
+    for (size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x; r < NREC; r += nt) {
+        char *R = (char *)buf + r * GRID;
+        const unsigned h = (unsigned)r * 2654435761u;
+        if (W == 4) {
+            *(gw32p)(R + 316) = h;
+        } else {
+            char *C = (char *)((uintptr_t)(R + 316) & ~(uintptr_t)127);
+            const u32x4 v = {h, h >> 1, h >> 2, h >> 3};
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                *(gw4p)(C + 16 * k) = v;
+        }
+    }
+}
+
 template <typename F>
 float timeit(F kern, int grid, int wg, const char *d, unsigned *o)
 {
@@ -253,6 +277,8 @@ int main()
         {"hash 8w sb plain loads", timeit(run_probe<512, 0, 1, 8192>, cu, 512, d, o)},
         {"hash 8w sb plain loads +inplace 4B", timeit(run_probe<512, 0, 1, 8192 | 128>, cu, 512, d, o)},
         {"hash 8w sb plain loads +inplace 128B line", timeit(run_probe<512, 0, 1, 8192 | 1024>, cu, 512, d, o)},
+        {"scatter only: 4 B CRC fields", timeit(scatter_probe<4>, 4 * cu, 1024, d, o)},
+        {"scatter only: 128 B lines", timeit(scatter_probe<128>, 4 * cu, 1024, d, o)},
         {"hash 8w sb (end)", timeit(run_probe<512, 0, 1>, cu, 512, d, o)},
     };
     for (auto &x : r)

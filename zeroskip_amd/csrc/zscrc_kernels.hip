@@ -1008,9 +1008,16 @@ __device__ __forceinline__ void xnext(const XDesc &d, const XMulti &m, const XPa
     xrec<MODE>(d, m, xp, l);
 }
 
+/* Diagnostic (zscrc_diag_wave_times): when set, every wave of xteam_kernel
+ * records [entry, after the table fill, end] (s_memrealtime, 100 MHz) and
+ * its record / part count at zs_wave_times + 4 * wave.  Null in production:
+ * one scalar load per wave. */
+__device__ uint64_t *zs_wave_times = nullptr;
+
 template <int MODE>
 __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp, const uint32_t *__restrict__ gtab)
 {
+    const uint64_t t_entry = __builtin_amdgcn_s_memrealtime();
     constexpr bool MULTI = MODE == 1;
     __shared__ __attribute__((aligned(16))) char L[LDS_BYTES];
     if (MODE == 2) { /* parts of a split class: their count is on the device */
@@ -1024,6 +1031,7 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp,
         m.out[threadIdx.x][0] = m.preset[threadIdx.x]; /* the fold kernel (next on the stream) XORs into it */
     fill_lds<64>(L, gtab);
     __syncthreads();
+    const uint64_t t_fill = __builtin_amdgcn_s_memrealtime();
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
     const uint32_t c_lo = (uint32_t)(lane & 31) << 2;
     const uint32_t c_hi = c_lo | 0x10000u;
@@ -1106,6 +1114,19 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp,
     }
     if ((uint32_t)lane < nst)
         d.out[first + (uint64_t)lane] = stash;
+    uint64_t *wt = zs_wave_times;
+    if (wt && lane == 0) {
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        wt[4 * team + 0] = t_entry;
+        wt[4 * team + 1] = t_fill;
+        wt[4 * team + 2] = t_end;
+        wt[4 * team + 3] = wend - wbeg;
+    }
+}
+
+extern "C" int zs_set_wave_times(uint64_t *p)
+{
+    return hipMemcpyToSymbol(HIP_SYMBOL(zs_wave_times), &p, sizeof p) == hipSuccess ? 0 : -3;
 }
 
 /* ------------------------------------------- coalesced 16-lane teams */
