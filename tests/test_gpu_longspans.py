@@ -6,7 +6,8 @@ semantics, zeroskip-file.c:266-302).  Without a caller bound the batch goes
 classify -> plan -> parts (xteam_kernel's parts mode for class 3, team<16>
 parts for class 2) -> part fold; every CRC, status, verdict and written CRC
 against the format oracle, on both class-3 routes (xteam parts and team<64>
-parts, tuning bit 65536) and both classify forms (one single-block launch
+parts, tuning bit 65536; the segment plan -- the class's bytes end to end
+cut into one equal segment per wave -- and per-record parts, bit 256) and both classify forms (one single-block launch
 with the plans, or two passes and plan launches: bit 524288), with corruptions at a record's first byte, its
 last span byte, its stored CRC and bytes either side of a part boundary."""
 import numpy as np
@@ -22,8 +23,9 @@ pytestmark = pytest.mark.gpu
 
 TEAM64_PARTS = 65536  # zs::BatchDesc::opt: class 3 on team<64> parts instead of xteam parts
 MULTI_CLASSIFY = 524288  # opt: two multi-block classify passes + plan launches (not the single-block one)
-OPTS = [0, TEAM64_PARTS, MULTI_CLASSIFY]
-IDS = ["xteam-parts", "team64-parts", "multi-classify"]
+RECORD_PARTS = 256  # opt: class 3 parts cut per record instead of the segment plan
+OPTS = [0, TEAM64_PARTS, MULTI_CLASSIFY, RECORD_PARTS]
+IDS = ["xteam-segments", "team64-parts", "multi-classify", "xteam-record-parts"]
 
 # transaction sizes in bytes of value payload: class 3 (> g16_max) records
 # of 0.3-3 MiB, one past 16 MiB (long commit), class 2 and short ones beside
@@ -148,3 +150,40 @@ def test_long_spans_seeded_crc_batch(gpu, db):
     got = out.cpu().numpy().view(np.uint32)
     for i in range(len(offs)):
         assert got[i] == oracle.crc32c_hw(int(seeds[i]), host[offs[i]:offs[i] + lens[i]]), i
+
+
+@pytest.mark.parametrize("nseg", [1, 3, 7, 50, 400])
+def test_segment_plans(gpu, db, nseg, monkeypatch):
+    """Segment plans with fewer segments than waves (ZSCRC_XSEGS): segments
+    holding several records, records over many segments, a single segment
+    -- every CRC, status and a corruption next to a segment boundary"""
+    host, offs, lens, commits = db
+    monkeypatch.setenv("ZSCRC_XSEGS", str(nseg))
+    d = torch.from_numpy(host).cuda()
+    o, ln = torch.from_numpy(offs).cuda(), torch.from_numpy(lens).cuda()
+    crc, st = _with_opt(0, lambda: zsfile.verify_commits(d, o, ln))
+    assert (crc.cpu().numpy().view(np.uint32) == np.array([c["computed"] for c in commits], np.uint32)).all()
+    assert (st.cpu().numpy() == 1).all()
+    big = [i for i in range(len(commits)) if lens[i] > 1_000_000]
+    # the byte at a segment boundary of the class-3 records laid end to end
+    klass3 = [i for i in range(len(commits)) if lens[i] > (1 << 20)]   # g16_max
+    total = int(sum(lens[i] for i in klass3))
+    G = max(-(-total // nseg) + 63 & ~63, 1 << 16)
+    start, at = 0, None
+    for i in klass3:
+        j = -(-start // G) * G
+        if j < start + lens[i] and j > start:
+            at = (i, j - start)
+            break
+        start += int(lens[i])
+    h = host.copy()
+    hit = {big[0]}
+    h[offs[big[0]] + lens[big[0]] // 3] ^= 0x40
+    if at is not None:
+        i, k = at
+        h[offs[i] + k] ^= 0x08
+        h[offs[i] + k - 1] ^= 0x01
+        hit.add(i)
+    d = torch.from_numpy(h).cuda()
+    nbad, bad = _with_opt(0, lambda: zsfile.verify_commits_verdict(d, o, ln))
+    assert int(nbad.item()) == len(hit) and set(bad[:len(hit)].cpu().tolist()) == hit

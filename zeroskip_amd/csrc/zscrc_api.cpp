@@ -34,7 +34,7 @@ int zs_launch_short(int fixed, int pf, const zs::BatchDesc *d, const uint32_t *g
 int zs_launch_stream_read(const void *buf, uint64_t n, uint32_t *out, int grid, hipStream_t stream);
 int zs_set_wave_times(uint64_t *p);
 int zs_launch_classify(const zs::Classify *c, hipStream_t stream);
-int zs_launch_part_fold(const zs::BatchDesc *d, const uint32_t *gtab, hipStream_t stream);
+int zs_launch_part_fold(const zs::BatchDesc *d, int nd, const uint32_t *gtab, hipStream_t stream);
 int zs_launch_plan(const zs::PlanArgs *a, hipStream_t stream);
 int zs_launch_burst(int fixed, int xp, int nb, const zs::BatchDesc *d, const uint32_t *gtab, int grid,
                     hipStream_t stream);
@@ -406,6 +406,16 @@ int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t max_len =
          * straight over the caller's arrays, no classify (it is correct for
          * any length, so a wrong bound costs only time) */
         const int w0 = g_depth[0];
+        const bool direct = max_len <= g1 && (w0 < 0 || w0 >= 9);
+        if (d.bad_count && direct) {
+            /* verdict batch without classify: zero its counter here (the
+             * classify launch does it otherwise) */
+            hipError_t e = hipMemsetAsync(d.bad_count, 0, sizeof(uint64_t), s);
+            if (e != hipSuccess) {
+                set_err("hipMemsetAsync(verdict count)", e);
+                return ZSCRC_EHIP;
+            }
+        }
         if (max_len <= g1 && d.commit && !d.desc && !(d.opt & 32768) && w0 < 0) {
             /* bounded commit batch: commit_kernel (run rounds, verdicts) */
             if (zs_launch_commit(&d, c->gtab, c->ncu, s)) {
@@ -446,7 +456,9 @@ int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1
     const size_t T = split_items(16) > split_items(gs) ? split_items(16) : split_items(gs);
     /* parts buffer, one half per split class (2, 3): part registers (< 2T),
      * part_rec (< 2T), part_base (< T) */
-    const size_t part_bytes = 2 * 5 * T * sizeof(uint32_t);
+    /* + class 3's segment plan: rec_start (< T records, 64-bit) and
+     * seg_first (one per wave + 1) */
+    const size_t part_bytes = (2 * 5 * T + 2 * T + T + 64) * sizeof(uint32_t);
     {
         int rc = grow(&c->classes, &c->classes_bytes, list_bytes);
         if (!rc)
@@ -486,6 +498,21 @@ int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1
         part_out[k - 2] = static_cast<uint32_t *>(c->parts) + (k == 3 ? 5 * T : 0);
         p.part_rec = part_out[k - 2] + 2 * T;
         p.part_base = p.part_rec + 2 * T;
+        if (k == 3 && xparts && !(d.opt & (256 | 131072))) {
+            /* class 3 on xteam_kernel: one segment per wave of its grid */
+            uint32_t *ext = static_cast<uint32_t *>(c->parts) + 10 * T;
+            p.nseg = (uint32_t)c->ncu * 16u;
+            /* test hook: fewer segments than waves (several records per
+             * segment at small sizes) */
+            if (const char *e = getenv("ZSCRC_XSEGS")) {
+                const unsigned long v = strtoul(e, nullptr, 0);
+                if (v >= 1 && v < p.nseg)
+                    p.nseg = (uint32_t)v;
+            }
+            p.max_parts = (uint32_t)T; /* part_base / rec_start hold T records */
+            p.rec_start = reinterpret_cast<uint64_t *>(ext);
+            p.seg_first = ext + 2 * T;
+        }
     }
     zs::Classify cl;
     memset(&cl, 0, sizeof cl);
@@ -501,6 +528,7 @@ int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1
     cl.desc = desc;
     cl.commit = d.commit != 0;
     cl.img_size = d.img_size;
+    cl.zero_count = d.bad_count;
     {
         /* class 0 goes to burst_kernel (walk 9, the default), which walks
          * the caller's arrays and skips longer records: no class-0 list */
@@ -554,6 +582,8 @@ int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1
             dk.plan = plans;
             dk.part_base = pa[k - 2].part_base;
             dk.part_rec = pa[k - 2].part_rec;
+            dk.rec_start = pa[k - 2].rec_start;
+            dk.seg_first = pa[k - 2].seg_first;
             dk.part_out = part_out[k - 2];
         }
         int rc;
@@ -571,8 +601,9 @@ int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1
         if (k >= 2)
             fold[nfold++] = dk;
     }
-    for (int i = 0; i < nfold; ++i) {
-        if (zs_launch_part_fold(&fold[i], c->gtab, s)) {
+    /* both split classes' folds in one launch */
+    if (nfold) {
+        if (zs_launch_part_fold(fold, nfold, c->gtab, s)) {
             set_err("part fold launch", hipGetLastError());
             return ZSCRC_EHIP;
         }
@@ -1110,13 +1141,16 @@ int zscrc_device_verify_commits_verdict(const void *d_image, uint64_t image_size
     if (!d_nbad || (cap && !d_bad) || (n && (!d_image || !d_span_off || !d_span_len)))
         return ZSCRC_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    hipError_t e = hipMemsetAsync(d_nbad, 0, sizeof(uint64_t), s);
-    if (e != hipSuccess) {
-        set_err("hipMemsetAsync(verdict count)", e);
-        return ZSCRC_EHIP;
-    }
-    if (n == 0)
+    if (n == 0) {
+        hipError_t e = hipMemsetAsync(d_nbad, 0, sizeof(uint64_t), s);
+        if (e != hipSuccess) {
+            set_err("hipMemsetAsync(verdict count)", e);
+            return ZSCRC_EHIP;
+        }
         return ZSCRC_OK;
+    }
+    /* *d_nbad is zeroed on the stream by launch_classes (a memset before a
+     * direct launch, or the first classify launch) */
     DevCtx *c;
     int rc = get_ctx(&c);
     if (rc)

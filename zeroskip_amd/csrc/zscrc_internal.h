@@ -71,7 +71,9 @@ struct BatchDesc {
                              32768 = bounded commit batches on burst_kernel instead of
                              commit_kernel, 65536 = split class 3 on team_kernel<64>
                              instead of xteam_kernel's parts mode, 131072 = four parts
-                             per wave there instead of two, 262144 = diagnostic: multi64_kernel
+                             per wave there instead of two (no segment plan), 256 = class 3
+                             parts cut per record instead of the segment plan
+                             (SplitPlan::seg), 262144 = diagnostic: multi64_kernel
                              stores its results into one L2-resident window (wrong results),
                              524288 = small variable batches classify in two multi-block
                              passes and plan launches instead of one single-block launch */
@@ -85,6 +87,10 @@ struct BatchDesc {
     const struct SplitPlan *plan;
     const uint32_t *part_base;
     const uint32_t *part_rec;
+    /* segment plans (SplitPlan::seg): each record's first byte in the
+     * class's bytes laid end to end (part_fold_kernel's last-part shift) */
+    const uint64_t *rec_start;
+    const uint32_t *seg_first; /* segment plans: first part of segment w */
 };
 
 /* A fixed-stride batch for xteam_kernel (what it reads of a BatchDesc: few
@@ -129,6 +135,9 @@ struct XParts {
     const uint32_t *part_base;
     const uint32_t *part_rec;
     uint32_t *part_out;
+    const uint64_t *rec_start; /* segment plans: see SplitPlan::seg */
+    const uint32_t *seg_first; /* segment plans: first part of segment w */
+    uint32_t seg;              /* the plan's seg (read on the device)     */
 };
 
 /* consistent's device post pass (zscrc_cpass, cpass_post_kernel): the
@@ -171,7 +180,13 @@ struct SplitPlan {
     uint32_t parts;  /* work items: parts in all, or records when direct     */
     uint32_t direct; /* 1 = enough records: no split                          */
     uint32_t K;      /* x^(8 unit) mod P: the part fold's Horner multiplier   */
-    uint32_t pad;
+    /* seg = 1 (class 3 on xteam_kernel): the class's bytes laid end to end
+     * are cut into `nseg` segments of `unit` bytes, one per wave, and a part
+     * is a segment's piece of one record -- every wave gets the same bytes
+     * whatever the record lengths.  A record's parts: a partial first one,
+     * full segments, a partial last one (part_fold_kernel shifts the Horner
+     * sum by x^(8 |last part|)).  seg = nseg, 0 = parts cut per record. */
+    uint32_t seg;
 };
 
 struct PlanArgs {
@@ -186,6 +201,12 @@ struct PlanArgs {
     uint32_t *part_base;   /* per record of the class: its first part */
     uint32_t *part_rec;    /* per part: its record */
     const uint32_t *gtab;  /* operator tables (x^(8 2^k) for K) */
+    /* segment plan (SplitPlan::seg) when nseg != 0 and the class's records
+     * + nseg parts fit the part arrays (max_parts) */
+    uint32_t nseg;
+    uint32_t max_parts;
+    uint64_t *rec_start;   /* per record: first byte in the class laid end to end */
+    uint32_t *seg_first;   /* nseg + 1 entries: first part of each segment */
 };
 
 struct Classify {
@@ -212,6 +233,9 @@ struct Classify {
      * passes and two plan launches */
     int single;
     PlanArgs plan[2];
+    /* commit verdict batches: the bad-commit counter, zeroed by the first
+     * classify launch (the class kernels run after it on the stream) */
+    unsigned long long *zero_count;
 };
 
 /* K fixed-stride batches of one launch (zscrc_device_fixed_multi): batch b

@@ -838,10 +838,18 @@ __device__ __forceinline__ void xgeom(const XDesc &d, const XMulti &m, const XPa
         const uint64_t U = uni64(((g64p)(xp.plan + xp.klass))[0]);
         const uint64_t part = w - __builtin_amdgcn_readfirstlane(((g32p)xp.part_base)[idx]);
         uint64_t a;
-        split_part(rlen, U, part, a, len);
+        if (xp.seg) { /* the part is segment j0 + part's piece of the record */
+            const uint64_t S = uni64(((g64p)xp.rec_start)[idx]);
+            const uint64_t j = S / U + part;
+            const uint64_t b0 = j * U > S ? j * U : S, b1 = (j + 1) * U < S + rlen ? (j + 1) * U : S + rlen;
+            a = b0 - S;
+            len = b1 - b0;
+        } else {
+            split_part(rlen, U, part, a, len);
+        }
         A = reinterpret_cast<uintptr_t>(xp.base) + off + a;
         lo = reinterpret_cast<uintptr_t>(xp.base) & ~uintptr_t(3);
-        R0 = part ? 0u : seed ^ xp.xor_io; /* later parts start from a zero register */
+        R0 = a ? 0u : seed ^ xp.xor_io; /* later parts start from a zero register */
         return;
     }
     R0 = d.seed ^ d.xor_io;
@@ -1022,10 +1030,12 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp,
     __shared__ __attribute__((aligned(16))) char L[LDS_BYTES];
     if (MODE == 2) { /* parts of a split class: their count is on the device */
         d.n = __builtin_amdgcn_readfirstlane(((const volatile uint32_t *)&xp.plan[xp.klass].parts)[0]);
+        xp.seg = __builtin_amdgcn_readfirstlane(((const volatile uint32_t *)&xp.plan[xp.klass].seg)[0]);
         d.out = xp.part_out;
         d.xor_io = 0; /* raw part registers */
     }
-    if ((uint64_t)blockIdx.x * WAVES >= d.n)
+    /* segment plans: wave w takes segment w's parts (every block works) */
+    if ((MODE != 2 || !xp.seg) && (uint64_t)blockIdx.x * WAVES >= d.n)
         return;
     if (MULTI && blockIdx.x == 0 && threadIdx.x < m.k)
         m.out[threadIdx.x][0] = m.preset[threadIdx.x]; /* the fold kernel (next on the stream) XORs into it */
@@ -1039,8 +1049,15 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp,
     const uint64_t team = uni64((uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6));
     const uint64_t nteams = (uint64_t)gridDim.x * WAVES;
     const uint64_t per = (d.n + nteams - 1) / nteams;
-    const uint64_t wbeg = team * per < d.n ? team * per : d.n;
-    const uint64_t wend = wbeg + per < d.n ? wbeg + per : d.n;
+    uint64_t wbeg = team * per < d.n ? team * per : d.n;
+    uint64_t wend = wbeg + per < d.n ? wbeg + per : d.n;
+    if (MODE == 2 && xp.seg) { /* segment w (of xp.seg) for wave w of this grid */
+        wbeg = wend = 0;
+        if (team < xp.seg) {
+            wbeg = __builtin_amdgcn_readfirstlane(((g32p)xp.seg_first)[team]);
+            wend = __builtin_amdgcn_readfirstlane(((g32p)xp.seg_first)[team + 1]);
+        }
+    }
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(gtab);
 
     XLoad ld;
@@ -2816,6 +2833,8 @@ __device__ void classify_single(const Classify &c, uint32_t *cnt, const unsigned
 __global__ __launch_bounds__(CWG) void classify_kernel(Classify c)
 {
     __shared__ uint32_t cnt[4], slot[4], pos[4];
+    if (c.zero_count && c.pass == 0 && blockIdx.x == 0 && threadIdx.x == 0)
+        *c.zero_count = 0ull;
     if (c.pass == 1 && c.direct_ok && ((const volatile uint32_t *)c.count)[0] == c.n)
         return; /* one class: its kernel reads the caller's arrays directly */
     const uint64_t per = (c.n + gridDim.x - 1) / gridDim.x;
@@ -2894,6 +2913,126 @@ __global__ __launch_bounds__(CWG) void classify_kernel(Classify c)
     classify_scatter(c, slot, pos, r0, r1);
 }
 
+/* x^(8 n) mod P from the table x^(8 2^k) (gtab GT_POW2), one lane. */
+__device__ __forceinline__ uint32_t xpow8(const char *T, const uint32_t *gtab, uint64_t n)
+{
+    uint32_t r = 0x80000000u;
+    for (int k = 0; n; ++k, n >>= 1)
+        if (n & 1)
+            r = gmul_t(T, r, gtab[GT_POW2 + k]);
+    return r;
+}
+
+/* K = x^(8 unit) as a six-level product tree across wave 0; lane 0 writes
+ * the plan. */
+__device__ __forceinline__ void plan_write(const PlanArgs &a, SplitPlan *pl, const char *T, uint64_t unit,
+                                           uint32_t parts, uint32_t seg)
+{
+    const int lane = threadIdx.x & 63;
+    if (threadIdx.x >= 64)
+        return;
+    const uint32_t *pow2 = a.gtab + GT_POW2;
+    uint32_t v = (lane < 56 && ((unit >> lane) & 1)) ? pow2[lane] : 0x80000000u;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1)
+        v = gmul_t(T, v, __shfl_xor(v, o));
+    if (lane == 0) {
+        pl->unit = unit;
+        pl->parts = parts;
+        pl->direct = 0;
+        pl->K = v;
+        pl->seg = seg;
+    }
+}
+
+/* Segment plan (SplitPlan::seg): the class's bytes end to end cut into
+ * nseg segments of G bytes (G >= bytes / nseg, a multiple of 64), segment
+ * w for wave w of the xteam_kernel launch; record r (its first byte at S_r
+ * in that order) gets one part per segment it meets.  Writes rec_start
+ * (S_r, a block-wide 64-bit scan), part_base (scan of the part counts),
+ * part_rec, and seg_first[j] = the part holding byte j G (every segment
+ * starts inside exactly one record), seg_first[j >= used] = all parts. */
+__device__ void plan_segments(const PlanArgs &a, const RecDesc *list, SplitPlan *pl, uint32_t count,
+                              uint64_t bytes, uint32_t *sbase, uint32_t *wsum, char *T)
+{
+    __shared__ unsigned long long wsum64[16];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    uint64_t G = (bytes + a.nseg - 1) / a.nseg;
+    G = (G + 63) & ~63ull;
+    if (G < a.unit_min)
+        G = a.unit_min;
+    const uint64_t used = (bytes + G - 1) / G;
+    load_gmul_table(T, a.gtab);
+    __syncthreads();
+    uint32_t running = 0;
+    uint64_t run_bytes = 0;
+    for (uint32_t c0 = 0; c0 < count; c0 += 1024) {
+        const uint32_t r = c0 + t;
+        const uint64_t len = r < count ? ((const volatile uint64_t *)&list[r].len)[0] : 0ull;
+        /* exclusive 64-bit scan of the lengths: S_r */
+        uint64_t v = len;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint64_t u = __shfl_up(v, o);
+            if (lane >= o)
+                v += u;
+        }
+        if (lane == 63)
+            wsum64[wv] = v;
+        __syncthreads();
+        uint64_t woff = 0, ctot = 0;
+        for (int i = 0; i < 16; ++i) {
+            woff += i < wv ? wsum64[i] : 0ull;
+            ctot += wsum64[i];
+        }
+        const uint64_t S = run_bytes + woff + v - len;
+        const uint64_t j0 = S / G;
+        const uint32_t np = len ? (uint32_t)((S + len - 1) / G - j0 + 1) : 0u;
+        /* exclusive scan of the part counts: part_base */
+        uint32_t x = np;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t u = __shfl_up(x, o);
+            if (lane >= o)
+                x += u;
+        }
+        if (lane == 63)
+            wsum[wv] = x;
+        __syncthreads();
+        uint32_t poff = 0;
+        for (int i = 0; i < wv; ++i)
+            poff += wsum[i];
+        const uint32_t pbase = running + poff + x - np;
+        sbase[t] = pbase;
+        if (t == 1023)
+            sbase[1024] = pbase + np;
+        if (r < count) {
+            a.part_base[r] = pbase;
+            a.rec_start[r] = S;
+            /* the segments that start inside this record */
+            for (uint64_t j = (S + G - 1) / G; j * G < S + len; ++j)
+                a.seg_first[j] = pbase + (uint32_t)(j - j0);
+        }
+        __syncthreads();
+        const uint32_t lo = sbase[0], hi = sbase[1024];
+        for (uint32_t q = lo + t; q < hi; q += 1024) {
+            uint32_t a0 = 0, a1 = 1024;
+            while (a1 - a0 > 1) {
+                const uint32_t mid = (a0 + a1) >> 1;
+                if (sbase[mid] <= q)
+                    a0 = mid;
+                else
+                    a1 = mid;
+            }
+            a.part_rec[q] = c0 + a0;
+        }
+        running = hi;
+        run_bytes += ctot;
+        __syncthreads();
+    }
+    for (uint64_t j = used + t; j <= a.nseg; j += 1024)
+        a.seg_first[j] = running;
+    plan_write(a, pl, T, G, running, a.nseg);
+}
+
 /* Split plan of one length class (one block; runs after the scatter): with
  * fewer records than `target`, every record is cut into ceil(len / unit)
  * parts, unit ~ class bytes / target -- parts of equal size whatever the mix
@@ -2916,7 +3055,12 @@ __device__ void plan_block(const PlanArgs &a, uint32_t first, uint32_t count, ui
             pl->parts = count;
             pl->direct = 1;
             pl->K = 0x80000000u;
+            pl->seg = 0;
         }
+        return;
+    }
+    if (a.nseg && (uint64_t)count + a.nseg <= a.max_parts) {
+        plan_segments(a, list, pl, count, bytes, sbase, wsum, T);
         return;
     }
     /* each record adds at most one partial part: with unit >= bytes /
@@ -2971,21 +3115,9 @@ __device__ void plan_block(const PlanArgs &a, uint32_t first, uint32_t count, ui
         running = hi;
         __syncthreads();
     }
-    if (wv == 0) {
-        /* K = x^(8 unit): the product of x^(8 2^k) over unit's set bits, a
-         * six-level tree across the wave (gmul commutes) */
-        const uint32_t *pow2 = a.gtab + GT_POW2;
-        uint32_t v = (lane < 56 && ((unit >> lane) & 1)) ? pow2[lane] : 0x80000000u;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1)
-            v = gmul_t(T, v, __shfl_xor(v, o));
-        if (lane == 0) {
-            pl->unit = unit;
-            pl->parts = running;
-            pl->direct = 0;
-            pl->K = v;
-        }
-    }
+    /* K = x^(8 unit): the product of x^(8 2^k) over unit's set bits, a
+     * six-level tree across wave 0 (gmul commutes) */
+    plan_write(a, pl, T, unit, running, 0u);
 }
 
 __global__ __launch_bounds__(1024) void plan_kernel(PlanArgs a)
@@ -3010,8 +3142,14 @@ __global__ __launch_bounds__(1024) void plan_kernel(PlanArgs a)
  * its own power of x^(8 unit) and each record to x^(8 last) by
  * square-and-multiply, took 36-40 us of the NOTBATCHED verify (1,488 records
  * of ~2 MiB, ~6 parts each) -- bit-serial products in one lane. */
-__global__ __launch_bounds__(256) void part_fold_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
+/* the folds of both split classes in one launch: blockIdx.y picks one */
+struct FoldPair {
+    BatchDesc d[2];
+};
+
+__global__ __launch_bounds__(256) void part_fold_kernel(FoldPair fp, const uint32_t *__restrict__ gtab)
 {
+    const BatchDesc &d = fp.d[blockIdx.y];
     __shared__ __attribute__((aligned(16))) char T[4096];
     __shared__ uint32_t TK[1024];
     __shared__ uint32_t basis[32];
@@ -3025,6 +3163,8 @@ __global__ __launch_bounds__(256) void part_fold_kernel(BatchDesc d, const uint3
     load_gmul_table(T, gtab);
     const uint32_t K = ((const volatile uint32_t *)&d.plan[d.klass].K)[0];
     const uint32_t nparts = ((const volatile uint32_t *)&d.plan[d.klass].parts)[0];
+    const uint32_t seg = ((const volatile uint32_t *)&d.plan[d.klass].seg)[0];
+    const uint64_t U = ((const volatile uint64_t *)&d.plan[d.klass].unit)[0];
     __syncthreads();
     if (threadIdx.x < 32) /* a * K is linear in a's bits: K * x^(31 - i) */
         basis[threadIdx.x] = gmul_t(T, 1u << threadIdx.x, K);
@@ -3048,9 +3188,17 @@ __global__ __launch_bounds__(256) void part_fold_kernel(BatchDesc d, const uint3
         const uint32_t m = (idx + 1 < count ? d.part_base[idx + 1] : nparts) - pb; /* 1.. parts */
         const uint32_t *parts = d.part_out + pb;
         uint32_t reg = parts[0];
-        for (uint32_t q = 1; q < m; ++q)
+        /* segment plans: the last part is partial (shifted by its own
+         * length below), the ones between are whole segments */
+        const uint32_t mh = seg && m > 1 ? m - 1 : m;
+        for (uint32_t q = 1; q < mh; ++q)
             reg = TK[reg & 255] ^ TK[256 + ((reg >> 8) & 255)] ^ TK[512 + ((reg >> 16) & 255)] ^ TK[768 + (reg >> 24)] ^
                   parts[q];
+        if (mh < m) {
+            const uint64_t e = d.rec_start[idx] + len;
+            const uint64_t blast = e - ((e - 1) / U) * U; /* bytes of the last part */
+            reg = gmul_t(T, reg, xpow8(T, gtab, blast)) ^ parts[m - 1];
+        }
         if (!d.commit) {
             d.out[r.rec] = reg ^ d.xor_io;
             continue;
@@ -3201,9 +3349,12 @@ extern "C" int zs_launch_plan(const zs::PlanArgs *a, hipStream_t stream)
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
-extern "C" int zs_launch_part_fold(const zs::BatchDesc *d, const uint32_t *gtab, hipStream_t stream)
+extern "C" int zs_launch_part_fold(const zs::BatchDesc *d, int nd, const uint32_t *gtab, hipStream_t stream)
 {
-    hipLaunchKernelGGL(zs::part_fold_kernel, dim3(256), dim3(256), 0, stream, *d, gtab);
+    zs::FoldPair fp;
+    fp.d[0] = d[0];
+    fp.d[1] = nd > 1 ? d[1] : d[0];
+    hipLaunchKernelGGL(zs::part_fold_kernel, dim3(256, nd > 1 ? 2 : 1), dim3(256), 0, stream, fp, gtab);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -3296,6 +3447,9 @@ extern "C" int zs_launch_xparts(const zs::BatchDesc *bd, const uint32_t *gtab, i
     p.part_base = bd->part_base;
     p.part_rec = bd->part_rec;
     p.part_out = bd->part_out;
+    p.rec_start = bd->rec_start;
+    p.seg_first = bd->seg_first;
+    p.seg = 0; /* read from the plan on the device */
     hipLaunchKernelGGL(zs::xteam_kernel<2>, dim3(grid), dim3(zs::WG), 0, stream, x, none, p, gtab);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
