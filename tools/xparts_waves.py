@@ -32,7 +32,10 @@ def waves(name, fn, nwaves):
     t0 = a[:, 0].min()
     ent, fill, end, cnt = (a[:, 0] - t0) / 100.0, (a[:, 1] - t0) / 100.0, (a[:, 2] - t0) / 100.0, a[:, 3]
     work = end - fill
-    row = {"case": name, "waves_recorded": int(live.sum()), "kernel_us": round(float(end.max()), 1),
+    wave_id = np.nonzero(live)[0]
+    xcd = (wave_id // 16) % 8                      # blockIdx.x % 8: the XCD a block lands on
+    by_xcd = [round(float(np.median(end[xcd == x])), 1) for x in range(8)]
+    row = {"case": name, "end_us_median_by_xcd": by_xcd, "waves_recorded": int(live.sum()), "kernel_us": round(float(end.max()), 1),
            "entry_us_max": round(float(ent.max()), 1), "fill_done_us_p50": round(float(np.median(fill)), 1),
            "end_us_p10_p50_p90_max": [round(float(np.percentile(end, q)), 1) for q in (10, 50, 90, 100)],
            "waves_by_items": {int(k): int((cnt == k).sum()) for k in np.unique(cnt)},
@@ -57,6 +60,11 @@ def main():
     waves("span 3 GiB (xteam segments)", lambda: zd.crc_span(c3), nw)
     per = 762 * 1024
     waves("4096 x 762 KiB records (xteam, one per wave)", lambda: zd.crc_fixed(c3, per, per, 4096), nw)
+    if os.environ.get("WAVES_C3"):  # config 3's qteam has no wave timing; its xteam form for comparison
+        del c3
+        c4 = torch.randint(0, 256, (4 << 30,), dtype=torch.uint8, device=dev, generator=g)
+        waves("4 GiB span (xteam segments)", lambda: zd.crc_span(c4), nw)
+        waves("config 3: 65,536 x 64 KiB (qteam_kernel)", lambda: zd.crc_fixed(c4, 65536, 65536, 65536), nw)
 
 
 if __name__ == "__main__":

@@ -1178,11 +1178,13 @@ template <int B3>
 __global__ __launch_bounds__(WG) void qteam_kernel(XDesc d, const uint32_t *__restrict__ gtab)
 {
     __shared__ __attribute__((aligned(16))) char L[LDS_BYTES];
+    const uint64_t t_entry = __builtin_amdgcn_s_memrealtime();
     const uint64_t ngroups = (d.n + 3) / 4;
     if ((uint64_t)blockIdx.x * WAVES >= ngroups)
         return;
     fill_lds<16>(L, gtab);
     __syncthreads();
+    const uint64_t t_fill = __builtin_amdgcn_s_memrealtime();
     const int lane = threadIdx.x & 63, g = lane >> 4, t = (lane >> 2) & 3, h = lane & 3;
     const int j = 4 * g + h; /* piece of the team's step */
     const uint32_t c_lo = (uint32_t)(lane & 31) << 2;
@@ -1293,6 +1295,13 @@ __global__ __launch_bounds__(WG) void qteam_kernel(XDesc d, const uint32_t *__re
         advance_load();
         issue(kL, sL, b0);
         hash(b1);
+    }
+    uint64_t *wt = zs_wave_times; /* diagnostic (zscrc_diag_wave_times) */
+    if (wt && lane == 0) {
+        wt[4 * wave + 0] = t_entry;
+        wt[4 * wave + 1] = t_fill;
+        wt[4 * wave + 2] = __builtin_amdgcn_s_memrealtime();
+        wt[4 * wave + 3] = wave < ngroups ? (ngroups - wave + nwaves - 1) / nwaves : 0;
     }
 }
 
@@ -2913,16 +2922,6 @@ __global__ __launch_bounds__(CWG) void classify_kernel(Classify c)
     classify_scatter(c, slot, pos, r0, r1);
 }
 
-/* x^(8 n) mod P from the table x^(8 2^k) (gtab GT_POW2), one lane. */
-__device__ __forceinline__ uint32_t xpow8(const char *T, const uint32_t *gtab, uint64_t n)
-{
-    uint32_t r = 0x80000000u;
-    for (int k = 0; n; ++k, n >>= 1)
-        if (n & 1)
-            r = gmul_t(T, r, gtab[GT_POW2 + k]);
-    return r;
-}
-
 /* K = x^(8 unit) as a six-level product tree across wave 0; lane 0 writes
  * the plan. */
 __device__ __forceinline__ void plan_write(const PlanArgs &a, SplitPlan *pl, const char *T, uint64_t unit,
@@ -3158,12 +3157,16 @@ __global__ __launch_bounds__(256) void part_fold_kernel(FoldPair fp, const uint3
         base += d.class_count[k];
     const uint64_t count = d.class_count[d.klass];
     const RecDesc *list = d.desc + base;
-    if (((const volatile uint32_t *)&d.plan[d.klass].direct)[0] || (uint64_t)blockIdx.x * blockDim.x >= count)
+    const uint32_t seg = ((const volatile uint32_t *)&d.plan[d.klass].seg)[0];
+    /* segment plans: 16 lanes per record -- the last part's shift x^(8 b)
+     * is a product over b's bits spread over the group (depth 3 + 4
+     * multiplies instead of ~21 in one lane); otherwise a lane per record */
+    const uint32_t gsz = seg ? 16u : 1u;
+    if (((const volatile uint32_t *)&d.plan[d.klass].direct)[0] || (uint64_t)blockIdx.x * blockDim.x / gsz >= count)
         return; /* the team kernel emitted every record itself / no records here */
     load_gmul_table(T, gtab);
     const uint32_t K = ((const volatile uint32_t *)&d.plan[d.klass].K)[0];
     const uint32_t nparts = ((const volatile uint32_t *)&d.plan[d.klass].parts)[0];
-    const uint32_t seg = ((const volatile uint32_t *)&d.plan[d.klass].seg)[0];
     const uint64_t U = ((const volatile uint64_t *)&d.plan[d.klass].unit)[0];
     __syncthreads();
     if (threadIdx.x < 32) /* a * K is linear in a's bits: K * x^(31 - i) */
@@ -3179,9 +3182,26 @@ __global__ __launch_bounds__(256) void part_fold_kernel(FoldPair fp, const uint3
         TK[e] = v;
     }
     __syncthreads();
-    const uint32_t X4 = gtab[GT_POW2 + 2]; /* x^32: one slice-by-4 step */
-    const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < count; idx += nthr) {
+    const uint32_t sub = threadIdx.x & (gsz - 1);
+    const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x / gsz;
+    for (uint64_t idx = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / gsz; __any(idx < count); idx += nthr) {
+        const bool ok = idx < count;
+        uint32_t pw = 0x80000000u;
+        if (seg) {
+            uint64_t blast = 0; /* bytes of the record's last part */
+            if (ok) {
+                const uint64_t e = d.rec_start[idx] + list[idx].len;
+                blast = e - ((e - 1) / U) * U;
+            }
+            for (uint32_t t = sub; t < 48; t += 16)
+                if ((blast >> t) & 1)
+                    pw = gmul_t(T, pw, gtab[GT_POW2 + t]);
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1)
+                pw = gmul_t(T, pw, __shfl_xor(pw, o));
+        }
+        if (!ok || sub)
+            continue;
         const RecDesc r = list[idx];
         const uint64_t len = r.len;
         const uint32_t pb = d.part_base[idx];
@@ -3189,16 +3209,13 @@ __global__ __launch_bounds__(256) void part_fold_kernel(FoldPair fp, const uint3
         const uint32_t *parts = d.part_out + pb;
         uint32_t reg = parts[0];
         /* segment plans: the last part is partial (shifted by its own
-         * length below), the ones between are whole segments */
+         * length), the ones between are whole segments */
         const uint32_t mh = seg && m > 1 ? m - 1 : m;
         for (uint32_t q = 1; q < mh; ++q)
             reg = TK[reg & 255] ^ TK[256 + ((reg >> 8) & 255)] ^ TK[512 + ((reg >> 16) & 255)] ^ TK[768 + (reg >> 24)] ^
                   parts[q];
-        if (mh < m) {
-            const uint64_t e = d.rec_start[idx] + len;
-            const uint64_t blast = e - ((e - 1) / U) * U; /* bytes of the last part */
-            reg = gmul_t(T, reg, xpow8(T, gtab, blast)) ^ parts[m - 1];
-        }
+        if (mh < m)
+            reg = gmul_t(T, reg, pw) ^ parts[m - 1];
         if (!d.commit) {
             d.out[r.rec] = reg ^ d.xor_io;
             continue;
@@ -3224,9 +3241,9 @@ __global__ __launch_bounds__(256) void part_fold_kernel(FoldPair fp, const uint3
             stored = (uint32_t)w2;
             crc_at = end + 20;
         }
-        for (int i = 0; i < nt; ++i) {
-            reg = gmul_t(T, reg ^ (uint32_t)tw[i], X4);
-            reg = gmul_t(T, reg ^ (uint32_t)(tw[i] >> 32), X4);
+        for (int i = 0; i < nt; ++i) { /* the trailer words: slice-by-4 steps */
+            reg = op4(T, 0, reg ^ (uint32_t)tw[i]);
+            reg = op4(T, 0, reg ^ (uint32_t)(tw[i] >> 32));
         }
         const uint32_t crc = reg ^ 0xffffffffu;
         if (d.commit == 2 && nt)
