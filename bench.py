@@ -390,7 +390,10 @@ def run_config2(args, world, rank, dev, stream):
                                        "kernel_ms": round(graph_ms, 4),
                                        "achieved_GBs": round(nbytes / (graph_ms * 1e-3) / 1e9, 1),
                                        "note": f"round-1 form: {rot} single-batch short_kernel launches per "
-                                               "hipGraph"})
+                                               "hipGraph"},
+                    amortized=(f"value is amortized over {rot} batches per zscrc_device_fixed_multi launch (launch "
+                               "cost, LDS table fill and HBM ramp paid once per launch); the per-batch launch "
+                               "form is graph_of_launches"))
     if rank == 0 and world == 1 and not args.no_cpu:
         h = bufs[0, :n * rl // 8].cpu().numpy()
         from oracle import oracle
