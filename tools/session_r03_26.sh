@@ -1,0 +1,8 @@
+# final-build check: full GPU suite, smoke, the default bench line (config 3) and its bench-protocol trace
+O=gpurun_out/trace_bench
+bash tools/gpu_session.sh \
+ "tail:200:./tools/tail_probe" \
+ "tests:600:python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread" \
+ "smoke:180:python -c 'import __graft_entry__ as g; g.smoke()'" \
+ "bench3:300:python bench.py" \
+ "trace3:300:bash tools/trace_bench.sh config3 && python tools/trace_summary.py $O/config3 > $O/config3_summary.json && cat $O/config3_summary.json"

@@ -1,0 +1,176 @@
+// tail_probe: is the last ~10 % of a persistent streaming launch (waves
+// ending between p10 and max) recoverable by handing the work
+// out dynamically?  4 GiB of non-temporal coalesced reads (stream_read_kernel's
+// shape: 4 KiB blocks, a wave's next block in flight), one 1024-thread block
+// per CU; static = blocks strided over the waves (the product's walk),
+// dynamic = units of U bytes taken from a global counter (the next unit's
+// index fetched one unit ahead).  Prints kernel time (median of 15) and the
+// waves' end-time spread.  Measurement tooling, not product code.
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u32x4 *g4p;
+constexpr size_t N = 4ull << 30, BLK = 4096;
+
+__device__ __forceinline__ void load4(const char *buf, size_t blk, int lane, u32x4 (&a)[4])
+{
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        a[i] = __builtin_nontemporal_load((g4p)(buf + blk * BLK + 1024 * i + 16 * lane));
+}
+
+__device__ __forceinline__ void stamp(unsigned long long *t, size_t wave, int lane, unsigned long long t0)
+{
+    if (t && lane == 0) {
+        t[2 * wave] = t0;
+        t[2 * wave + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
+__global__ __launch_bounds__(1024) void static_read(const char *buf, unsigned *out, unsigned long long *t)
+{
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    const size_t wave = (size_t)blockIdx.x * 16 + (threadIdx.x >> 6), nw = (size_t)gridDim.x * 16;
+    const int lane = threadIdx.x & 63;
+    const size_t nb = N / BLK;
+    unsigned acc = 0;
+    u32x4 a[4], b[4];
+    size_t s = wave;
+    if (s < nb)
+        load4(buf, s, lane, a);
+    while (s < nb) {
+        const size_t n2 = s + nw;
+        if (n2 < nb)
+            load4(buf, n2, lane, b);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            acc ^= a[i].x ^ a[i].y ^ a[i].z ^ a[i].w;
+            a[i] = b[i];
+        }
+        s = n2;
+    }
+    if (acc == 0x9E3779B9u)
+        out[0] = acc;
+    stamp(t, wave, lane, t0);
+}
+
+/* units of UB blocks: unit u = blocks [u*UB, (u+1)*UB) */
+template <int UB>
+__global__ __launch_bounds__(1024) void dynamic_read(const char *buf, unsigned *out, unsigned *ctr,
+                                                     unsigned long long *t)
+{
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    const size_t wave = (size_t)blockIdx.x * 16 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const unsigned nu = (unsigned)(N / BLK / UB);
+    unsigned acc = 0;
+    auto grab = [&]() {
+        unsigned u = 0;
+        if (lane == 0)
+            u = atomicAdd(ctr, 1u);
+        return __builtin_amdgcn_readfirstlane(u);
+    };
+    unsigned u = grab(), un = u < nu ? grab() : nu;
+    u32x4 a[4], b[4];
+    size_t s = (size_t)u * UB, e = s + UB;
+    if (u < nu)
+        load4(buf, s, lane, a);
+    while (u < nu) {
+        /* next block: within the unit, or the first block of the next one */
+        size_t n2 = s + 1;
+        bool more = true;
+        if (n2 == e) {
+            u = un;
+            if (u < nu) {
+                un = grab();
+                n2 = (size_t)u * UB;
+                e = n2 + UB;
+            } else {
+                more = false;
+            }
+        }
+        if (more)
+            load4(buf, n2, lane, b);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            acc ^= a[i].x ^ a[i].y ^ a[i].z ^ a[i].w;
+            a[i] = b[i];
+        }
+        s = n2;
+        if (!more)
+            break;
+    }
+    if (acc == 0x9E3779B9u)
+        out[0] = acc;
+    stamp(t, wave, lane, t0);
+}
+
+template <typename F>
+void run(const char *name, F launch, unsigned long long *t, int nwaves)
+{
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    for (int i = 0; i < 5; ++i)
+        launch(nullptr);
+    std::vector<float> ms;
+    for (int r = 0; r < 15; ++r) {
+        (void)hipEventRecord(a);
+        launch(nullptr);
+        (void)hipEventRecord(b);
+        (void)hipEventSynchronize(b);
+        float x;
+        (void)hipEventElapsedTime(&x, a, b);
+        ms.push_back(x);
+    }
+    std::sort(ms.begin(), ms.end());
+    launch(t);
+    (void)hipDeviceSynchronize();
+    std::vector<unsigned long long> h(2 * nwaves);
+    (void)hipMemcpy(h.data(), t, h.size() * 8, hipMemcpyDeviceToHost);
+    unsigned long long t0 = ~0ull;
+    for (int w = 0; w < nwaves; ++w)
+        t0 = std::min(t0, h[2 * w]);
+    std::vector<double> end(nwaves);
+    for (int w = 0; w < nwaves; ++w)
+        end[w] = (h[2 * w + 1] - t0) / 100.0;
+    std::sort(end.begin(), end.end());
+    printf("{\"case\": \"%s\", \"ms\": %.4f, \"TBs\": %.3f, \"end_us_p10_p50_p90_max\": [%.1f, %.1f, %.1f, %.1f]}\n",
+           name, ms[ms.size() / 2], N / (ms[ms.size() / 2] * 1e-3) / 1e12, end[nwaves / 10], end[nwaves / 2],
+           end[nwaves * 9 / 10], end[nwaves - 1]);
+}
+
+int main()
+{
+    char *d;
+    unsigned *o, *ctr;
+    unsigned long long *t;
+    int cu = 0;
+    (void)hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, 0);
+    const int nw = cu * 16;
+    if (hipMalloc(&d, N) != hipSuccess || hipMalloc(&o, 64) != hipSuccess || hipMalloc(&ctr, 4096) != hipSuccess ||
+        hipMalloc(&t, 16ull * nw) != hipSuccess)
+        return 1;
+    (void)hipMemset(d, 7, N);
+    (void)hipMemset(ctr, 0, 4096); /* one counter per dynamic launch, zeroed up front */
+    int k = 0;
+    (void)hipDeviceSynchronize();
+    for (int rep = 0; rep < 2; ++rep) {
+        run("static (strided 4 KiB blocks)", [&](unsigned long long *tt) {
+            hipLaunchKernelGGL(static_read, dim3(cu), dim3(1024), 0, 0, d, o, tt);
+        }, t, nw);
+        run("dynamic 64 KiB units", [&](unsigned long long *tt) {
+            hipLaunchKernelGGL(dynamic_read<16>, dim3(cu), dim3(1024), 0, 0, d, o, ctr + (k++ % 1024), tt);
+        }, t, nw);
+        run("dynamic 16 KiB units", [&](unsigned long long *tt) {
+            hipLaunchKernelGGL(dynamic_read<4>, dim3(cu), dim3(1024), 0, 0, d, o, ctr + (k++ % 1024), tt);
+        }, t, nw);
+        run("dynamic 256 KiB units", [&](unsigned long long *tt) {
+            hipLaunchKernelGGL(dynamic_read<64>, dim3(cu), dim3(1024), 0, 0, d, o, ctr + (k++ % 1024), tt);
+        }, t, nw);
+    }
+    return 0;
+}
