@@ -274,10 +274,7 @@ def test_scalar_offload(gpu):
     assert after[0] - before[0] == 1   # the 37-byte call stayed on the CPU
 
 
-QDYN = 32  # zscrc_set_opt: qteam with dynamic units (qteam_dyn_kernel + qfold_kernel)
-
-
-@pytest.mark.parametrize("mode", ["team16", "xteam", "qteam", "qdyn"])
+@pytest.mark.parametrize("mode", ["team16", "xteam", "qteam"])
 def test_config3_headline_dispatch(gpu, mode):
     """BASELINE config 3 at full size through the exact call bench.py times:
     zscrc_device_fixed on 65,536 x 64 KiB chunks (4 GiB), seed 0, flags 0 --
@@ -289,12 +286,10 @@ def test_config3_headline_dispatch(gpu, mode):
     g.manual_seed(0x9E3779B9)
     d = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=gpu, generator=g)
     lib().zscrc_set_xteam(1, 32768 if mode == "xteam" else 256 << 10)
-    lib().zscrc_set_qteam(1 if mode in ("qteam", "qdyn") else 0)
-    lib().zscrc_set_opt(QDYN if mode == "qdyn" else 0)
+    lib().zscrc_set_qteam(1 if mode == "qteam" else 0)
     try:
         name = lib().zscrc_fixed_kernel(d.data_ptr(), L, L, n).decode()
-        assert name == {"team16": "team_kernel<16>", "xteam": "xteam_kernel", "qteam": "qteam_kernel",
-                        "qdyn": "qteam_dyn_kernel"}[mode]
+        assert name == {"team16": "team_kernel<16>", "xteam": "xteam_kernel", "qteam": "qteam_kernel"}[mode]
         out = torch.empty(n, dtype=torch.int32, device=gpu)
         from zeroskip_amd._lib import check
         check(lib().zscrc_device_fixed(d.data_ptr(), L, L, 0, out.data_ptr(), n, 0,
@@ -303,7 +298,6 @@ def test_config3_headline_dispatch(gpu, mode):
         host = d.cpu().numpy()
         del d
     finally:
-        lib().zscrc_set_opt(0)
         lib().zscrc_set_xteam(1, 256 << 10)
         lib().zscrc_set_qteam(QTEAM_DEFAULT)
     ref = oracle.batch(host, n=n, stride=L, fixed_len=L, impl="hw", threads=min(16, os.cpu_count() or 1))
@@ -337,21 +331,14 @@ def test_xteam_shapes(gpu):
         lib().zscrc_set_teams(*DEFAULT_TEAMS)
 
 
-@pytest.mark.parametrize("opt,parts", [(0, None), (QDYN, None), (QDYN, "1"), (QDYN, "3"), (QDYN, "4096")],
-                         ids=["qteam", "qdyn-P16", "qdyn-P1", "qdyn-P3", "qdyn-one-part"])
-def test_qteam_shapes(gpu, opt, parts, monkeypatch):
+def test_qteam_shapes(gpu):
     """qteam_kernel (coalesced 16-lane column-quad teams) on ragged shapes of
     equal-length records: a partial last group of four, unaligned bases (the
     first record's front-padded step clamped at the buffer start), ragged
     tails, gaps between records, seeds and raw registers -- every CRC against
     the oracle; shapes it must not take (a different last length, stride
-    not a multiple of 4) go to team_kernel<16>.  Also with dynamic units
-    (qteam_dyn_kernel, parts of P steps: 16, 1, 3 and one part per record)."""
-    if parts:
-        monkeypatch.setenv("ZSCRC_QDYN_P", parts)
+    not a multiple of 4) go to team_kernel<16>."""
     lib().zscrc_set_qteam(1)
-    lib().zscrc_set_opt(opt)
-    kname = "qteam_dyn_kernel" if opt == QDYN else "qteam_kernel"
     try:
         for stride, length, n, off in [(8192, 8192, 16385, 0), (8200, 8195, 16390, 1), (16384, 12000, 16387, 3),
                                        (65540, 65537, 16385, 2), (12288, 9000, 16400, 0), (2048, 2048, 16387, 0),
@@ -359,7 +346,7 @@ def test_qteam_shapes(gpu, opt, parts, monkeypatch):
                                        (4096, 8192, 16384, 0), (0, 9000, 16386, 1)]:   # overlapping, stride 0
             data = rand_bytes(stride * (n - 1) + length + off, stride + length + n)
             dd = to_dev(data[off:], gpu)
-            assert lib().zscrc_fixed_kernel(dd.data_ptr(), stride, length, n).decode() == kname
+            assert lib().zscrc_fixed_kernel(dd.data_ptr(), stride, length, n).decode() == "qteam_kernel"
             out = u32(zd.crc_fixed(dd, stride, length, n, seed=0xA5A5))
             ref = _oracle_seeded(data[off:], stride, length, n, 0xA5A5)
             bad = np.nonzero(out != ref)[0]
@@ -371,7 +358,6 @@ def test_qteam_shapes(gpu, opt, parts, monkeypatch):
         d = torch.zeros(16, dtype=torch.uint8, device=gpu)
         assert lib().zscrc_fixed_kernel(d.data_ptr(), 8194, 8192, 16384).decode() == "team_kernel<16>"
     finally:
-        lib().zscrc_set_opt(0)
         lib().zscrc_set_qteam(QTEAM_DEFAULT)
 
 

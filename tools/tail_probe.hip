@@ -108,6 +108,62 @@ __global__ __launch_bounds__(1024) void dynamic_read(const char *buf, unsigned *
     stamp(t, wave, lane, t0);
 }
 
+/* the same with the next unit's index fetched asynchronously: the atomic is
+ * issued when a unit starts and its answer read when the unit ends (an
+ * address the compiler cannot prove uniform, so its atomic optimizer does
+ * not turn the add into a wave-wide one read back at once) */
+template <int UB>
+__global__ __launch_bounds__(1024) void dynamic_async(const char *buf, unsigned *out, unsigned *ctr,
+                                                      unsigned long long *t)
+{
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    const size_t wave = (size_t)blockIdx.x * 16 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const unsigned nu = (unsigned)(N / BLK / UB);
+    unsigned acc = 0;
+    auto fetch = [&]() {
+        unsigned zero = 0;
+        asm volatile("" : "+v"(zero));
+        unsigned u = 0;
+        if (lane == 0)
+            u = atomicAdd(ctr + zero, 1u);
+        return u;
+    };
+    unsigned u = __builtin_amdgcn_readlane(fetch(), 0);
+    unsigned pend = fetch();
+    u32x4 a[4], b[4];
+    size_t s = (size_t)u * UB, e = s + UB;
+    if (u < nu)
+        load4(buf, s, lane, a);
+    while (u < nu) {
+        size_t n2 = s + 1;
+        bool more = true;
+        if (n2 == e) {
+            u = __builtin_amdgcn_readlane(pend, 0);
+            if (u < nu) {
+                pend = fetch();
+                n2 = (size_t)u * UB;
+                e = n2 + UB;
+            } else {
+                more = false;
+            }
+        }
+        if (more)
+            load4(buf, n2, lane, b);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            acc ^= a[i].x ^ a[i].y ^ a[i].z ^ a[i].w;
+            a[i] = b[i];
+        }
+        s = n2;
+        if (!more)
+            break;
+    }
+    if (acc == 0x9E3779B9u)
+        out[0] = acc;
+    stamp(t, wave, lane, t0);
+}
+
 template <typename F>
 void run(const char *name, F launch, unsigned long long *t, int nwaves)
 {
@@ -159,6 +215,15 @@ int main()
     int k = 0;
     (void)hipDeviceSynchronize();
     for (int rep = 0; rep < 2; ++rep) {
+        run("async 64 KiB units", [&](unsigned long long *tt) {
+            hipLaunchKernelGGL(dynamic_async<16>, dim3(cu), dim3(1024), 0, 0, d, o, ctr + (k++ % 1024), tt);
+        }, t, nw);
+        run("async 256 KiB units", [&](unsigned long long *tt) {
+            hipLaunchKernelGGL(dynamic_async<64>, dim3(cu), dim3(1024), 0, 0, d, o, ctr + (k++ % 1024), tt);
+        }, t, nw);
+        run("async 128 KiB units", [&](unsigned long long *tt) {
+            hipLaunchKernelGGL(dynamic_async<32>, dim3(cu), dim3(1024), 0, 0, d, o, ctr + (k++ % 1024), tt);
+        }, t, nw);
         run("static (strided 4 KiB blocks)", [&](unsigned long long *tt) {
             hipLaunchKernelGGL(static_read, dim3(cu), dim3(1024), 0, 0, d, o, tt);
         }, t, nw);

@@ -65,10 +65,6 @@ def main():
         c4 = torch.randint(0, 256, (4 << 30,), dtype=torch.uint8, device=dev, generator=g)
         waves("4 GiB span (xteam segments)", lambda: zd.crc_span(c4), nw)
         waves("config 3: 65,536 x 64 KiB (qteam_kernel)", lambda: zd.crc_fixed(c4, 65536, 65536, 65536), nw)
-        lib().zscrc_set_opt(32)
-        waves("config 3: 65,536 x 64 KiB (qteam_dyn_kernel, dynamic units)",
-              lambda: zd.crc_fixed(c4, 65536, 65536, 65536), nw)
-        lib().zscrc_set_opt(0)
 
 
 if __name__ == "__main__":

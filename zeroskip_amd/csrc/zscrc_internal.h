@@ -64,7 +64,6 @@ struct BatchDesc {
     uint32_t opt;         /* tuning bits: 1 = no three-chain five-piece bursts, 2 = no multi64_kernel,
                              4 / 8 = qteam_kernel with XOR3 grouping 1 / 2,
                              16 = team_kernel<16>'s two-level walk with XOR3 grouping 2,
-                             32 = qteam with dynamic units (qteam_dyn_kernel + qfold_kernel),
                              1024 = direct burst batches without the descriptor prefetch,
                              2048 = no run rounds in commit bursts,
                              4096 / 8192 = diagnostics of the run rounds (no chains / no
@@ -105,16 +104,6 @@ struct XDesc {
     uint64_t last_len;
     uint32_t seed;
     uint32_t xor_io;
-};
-
-/* qteam_dyn_kernel's dynamic units (a part of P steps of a group of four
- * records, taken from a global counter) and the part registers qfold_kernel
- * folds per record. */
-struct QDyn {
-    unsigned *ctr;      /* unit counter: 0 on entry, re-zeroed by qfold_kernel */
-    uint32_t *part_out; /* raw register of part p of record r at r * np + p */
-    uint32_t P;         /* 1 KiB steps per part (part 0: the rest)          */
-    uint32_t np;        /* parts per record                                */
 };
 
 /* Up to SPANS_MAX spans in one xteam_kernel launch (zscrc_device_spans):
