@@ -41,12 +41,12 @@ struct zscrc_cpass {
     std::vector<uint64_t> span_off, span_len;
     std::vector<int64_t> span_commit;
     /* device block: [0] nbad, [1] nstale, then span_raw[64] (u32),
-     * span_status[64] (i32), flags[LIST_CAP] (u32), bad[LIST_CAP] (u64) --
-     * the first `head` bytes go back to the host every pass */
+     * span_status[64] (i32), flags[LIST_CAP] (u32), bad[LIST_CAP] (u64)
+     * (written by the post kernel) -- the block goes back to the host every
+     * pass */
     uint8_t *dblk = nullptr;
     uint8_t *hblk = nullptr;
     uint64_t *dbad_full = nullptr; /* the verdict's list (cap entries) */
-    uint32_t *dflags_full = nullptr;
     uint64_t cap = 0;
     int64_t *dspan_commit = nullptr;
     uint32_t *dspan_init = nullptr;
@@ -69,8 +69,6 @@ void cpass_free(zscrc_cpass *p)
         (void)hipHostFree(p->hblk);
     if (p->dbad_full)
         (void)hipFree(p->dbad_full);
-    if (p->dflags_full)
-        (void)hipFree(p->dflags_full);
     if (p->dspan_commit)
         (void)hipFree(p->dspan_commit);
     delete p;
@@ -109,8 +107,6 @@ extern "C" int zscrc_cpass_create(zscrc_cpass **out, const zscrc_cpass_spec *spe
         e = hipHostMalloc(reinterpret_cast<void **>(&p->hblk), BLK, hipHostMallocDefault);
     if (e == hipSuccess)
         e = hipMalloc(&p->dbad_full, 8 * p->cap);
-    if (e == hipSuccess)
-        e = hipMalloc(&p->dflags_full, 4 * p->cap);
     if (e == hipSuccess)
         e = hipMalloc(&p->dspan_commit, (8 + 4) * zs::CPASS_SPANS);
     if (e != hipSuccess) {
@@ -170,7 +166,9 @@ extern "C" int zscrc_cpass_run(zscrc_cpass *p, void *stream, zscrc_cpass_result 
         a.nbad = reinterpret_cast<const unsigned long long *>(d_nbad);
         a.bad = p->dbad_full;
         a.cap = p->cap;
-        a.flags = p->dflags_full;
+        a.flags = reinterpret_cast<uint32_t *>(p->dblk + OFF_FLAGS);
+        a.bad_out = reinterpret_cast<uint64_t *>(p->dblk + OFF_BAD);
+        a.out_cap = LIST_CAP;
         a.nstale = reinterpret_cast<unsigned long long *>(p->dblk + 8);
         a.nspans = (uint32_t)sp.nspans;
         a.span_raw = d_raw;
@@ -180,12 +178,10 @@ extern "C" int zscrc_cpass_run(zscrc_cpass *p, void *stream, zscrc_cpass_result 
         if (zs_launch_cpass_post(&a, zscrc_internal_gtab(), s))
             rc = ZSCRC_EHIP;
     }
-    /* the listed part of the verdict next to the counters, one copy back */
-    if (!rc && (hipMemcpyAsync(p->dblk + OFF_FLAGS, p->dflags_full, 4 * LIST_CAP, hipMemcpyDeviceToDevice, s) !=
-                    hipSuccess ||
-                hipMemcpyAsync(p->dblk + OFF_BAD, p->dbad_full, 8 * LIST_CAP, hipMemcpyDeviceToDevice, s) !=
-                    hipSuccess ||
-                hipMemcpyAsync(p->hblk, p->dblk, BLK, hipMemcpyDeviceToHost, s) != hipSuccess ||
+    /* the post kernel wrote the listed part of the verdict next to the
+     * counters: one copy back (two device-to-device copies of the lists
+     * before it cost a launch each) */
+    if (!rc && (hipMemcpyAsync(p->hblk, p->dblk, BLK, hipMemcpyDeviceToHost, s) != hipSuccess ||
                 hipStreamSynchronize(s) != hipSuccess))
         rc = ZSCRC_EHIP;
     if (rc)

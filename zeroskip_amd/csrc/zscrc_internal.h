@@ -153,6 +153,8 @@ struct CPassArgs {
     const uint64_t *bad;         /* the verdict's list (first `cap` of *nbad) */
     uint64_t cap;
     uint32_t *flags;             /* per listed entry: 0 bad, 1 stale, 2 undecided (host) */
+    uint64_t *bad_out;           /* the first `out_cap` entries of bad[], beside flags, for */
+    uint64_t out_cap;            /* the one copy back (flags holds out_cap entries)         */
     unsigned long long *nstale;
     uint32_t nspans;
     const uint32_t *span_raw;    /* raw registers from 0 */

@@ -2612,7 +2612,10 @@ __global__ __launch_bounds__(256) void cpass_post_kernel(CPassArgs a, const uint
                 flag = 2;
             }
         }
-        a.flags[k] = flag;
+        if (k < a.out_cap) { /* the listed part goes back to the host in one copy */
+            a.flags[k] = flag;
+            a.bad_out[k] = i;
+        }
         if (flag == 1)
             atomicAdd(a.nstale, 1ull);
     }
