@@ -50,7 +50,6 @@ struct zscrc_cpass {
     uint64_t cap = 0;
     int64_t *dspan_commit = nullptr;
     uint32_t *dspan_init = nullptr;
-    size_t head = 0;
     /* one stream: the raw spans on a second stream beside the verdict batch
      * measured slower (config 5: 1.659 vs 1.542 ms per pass,
      * profiles/r03/cpass_streams.jsonl) */
