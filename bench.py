@@ -535,6 +535,8 @@ def run_config4(args, world, rank, dev, stream):
         assert rep["commits"] == ncommit and rep["bad_commits"] == 0, rep
         e2e["verify_files_s"] = round(best, 4)
         e2e["verify_files_GBs"] = round(host.numel() / best / 1e9, 2)
+        e2e["verify_files_phases_s"] = {"copy": round(rep["copy_s"], 4), "verify_tail": round(rep["verify_tail_s"], 4),
+                                        "total_in_library": round(rep["total_s"], 4)}
         # write: host images -> H2D -> write_commits -> D2H of the images
         back = torch.empty(host.shape, dtype=torch.uint8, pin_memory=True)
         for kind, src, dst in (("pinned", pinned, back), ("pageable", host, torch.empty_like(host))):
