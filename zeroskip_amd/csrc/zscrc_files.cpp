@@ -149,8 +149,15 @@ struct Cache {
     uint32_t *h_st = nullptr;
     uint8_t *ddesc = nullptr;
     uint64_t ddesc_bytes = 0;
+    uint64_t *h_bad = nullptr; /* pinned: the verdict's count + listed indices */
+    uint8_t *dq = nullptr;     /* device: the stale-commit re-verification batch */
+    uint64_t dq_bytes = 0;
 };
 Cache g_cache[MAX_SLOTS];
+
+/* commits a group's verdict lists (more mismatches: the per-commit status
+ * arrays instead) */
+constexpr uint64_t VCAP = 65536;
 
 void cache_free(Cache &c)
 {
@@ -169,6 +176,10 @@ void cache_free(Cache &c)
         (void)hipFree(c.dimg);
     if (c.ddesc)
         (void)hipFree(c.ddesc);
+    if (c.h_bad)
+        (void)hipHostFree(c.h_bad);
+    if (c.dq)
+        (void)hipFree(c.dq);
     const int dev = c.dev;
     c.dev = dev; /* keep the binding; everything else reset */
     c.slot_bytes = 0;
@@ -181,6 +192,9 @@ void cache_free(Cache &c)
     c.h_st = nullptr;
     c.ddesc = nullptr;
     c.ddesc_bytes = 0;
+    c.h_bad = nullptr;
+    c.dq = nullptr;
+    c.dq_bytes = 0;
 }
 
 int grow_dev(uint8_t **p, uint64_t *have, uint64_t need)
@@ -235,6 +249,9 @@ int ensure_desc(Cache &c, uint64_t count)
         hipHostMalloc(reinterpret_cast<void **>(&c.h_st), 4 * count, hipHostMallocDefault) != hipSuccess)
         return ZSCRC_ENOMEM;
     c.dcap = count;
+    if (!c.h_bad &&
+        hipHostMalloc(reinterpret_cast<void **>(&c.h_bad), 8 * (VCAP + 1), hipHostMallocDefault) != hipSuccess)
+        return ZSCRC_ENOMEM;
     return ZSCRC_OK;
 }
 
@@ -529,7 +546,8 @@ int run_group(Call &C, Cache &cache, std::vector<Ext *> &G, int threads)
                 }
             }
         }
-        int r = grow_dev(&cache.ddesc, &cache.ddesc_bytes, 24 * ncommit + 4 * pieces.size() + 1024);
+        /* + the verdict (count + VCAP indices) after the raw registers */
+        int r = grow_dev(&cache.ddesc, &cache.ddesc_bytes, 24 * ncommit + 4 * pieces.size() + 8 * (VCAP + 2) + 1024);
         if (r)
             return r;
         doff = reinterpret_cast<uint64_t *>(cache.ddesc);
@@ -597,10 +615,17 @@ int run_group(Call &C, Cache &cache, std::vector<Ext *> &G, int threads)
      * the last byte is on the device */
     if (!rc && (hipEventRecord(done_ev, cs) != hipSuccess || hipStreamWaitEvent(ks, done_ev, 0) != hipSuccess))
         rc = ZSCRC_EHIP;
+    /* the verdict: a count and the indices of the commits that do not
+     * verify -- no per-commit output, no 4 B per commit back over PCIe and
+     * no host scan of them (the per-commit arrays only when more than VCAP
+     * commits fail) */
+    uint64_t *d_nbad = reinterpret_cast<uint64_t *>(
+        (reinterpret_cast<uintptr_t>(draw + pieces.size()) + 7) & ~uintptr_t(7));
+    const uint64_t vcap = std::min<uint64_t>(VCAP, ncommit);
     if (!rc && ncommit) {
-        rc = zscrc_device_verify_commits_bounded(cache.dimg, total, doff, dlen, nullptr, ncommit, max_len.load(),
-                                                 dcrc, dst, ks);
-        if (!rc && hipMemcpyAsync(cache.h_st, dst, 4 * ncommit, hipMemcpyDeviceToHost, ks) != hipSuccess)
+        rc = zscrc_device_verify_commits_verdict(cache.dimg, total, doff, dlen, nullptr, ncommit, max_len.load(),
+                                                 d_nbad, d_nbad + 1, vcap, ks);
+        if (!rc && hipMemcpyAsync(cache.h_bad, d_nbad, 8 * (vcap + 1), hipMemcpyDeviceToHost, ks) != hipSuccess)
             rc = ZSCRC_EHIP;
     }
     std::vector<uint32_t> raw(pieces.size());
@@ -639,11 +664,23 @@ int run_group(Call &C, Cache &cache, std::vector<Ext *> &G, int threads)
 
     /* mismatches (status != 1), by descriptor position -> extent */
     std::vector<uint64_t> badpos;
-    if (!rc) {
-        const uint32_t *st = cache.h_st;
-        for (uint64_t i = 0; i < ncommit; ++i)
-            if (st[i] != 1)
-                badpos.push_back(i);
+    if (!rc && ncommit) {
+        const uint64_t nbad = cache.h_bad[0];
+        if (nbad <= vcap) {
+            badpos.assign(cache.h_bad + 1, cache.h_bad + 1 + nbad);
+            std::sort(badpos.begin(), badpos.end());
+        } else {
+            /* more than the list holds: every commit's status */
+            rc = zscrc_device_verify_commits_bounded(cache.dimg, total, doff, dlen, nullptr, ncommit, max_len.load(),
+                                                     dcrc, dst, ks);
+            if (!rc && (hipMemcpyAsync(cache.h_st, dst, 4 * ncommit, hipMemcpyDeviceToHost, ks) != hipSuccess ||
+                        hipStreamSynchronize(ks) != hipSuccess))
+                rc = ZSCRC_EHIP;
+            const uint32_t *st = cache.h_st;
+            for (uint64_t i = 0; !rc && i < ncommit; ++i)
+                if (st[i] != 1)
+                    badpos.push_back(i);
+        }
     }
     std::vector<std::pair<uint64_t, size_t>> by_pos; /* (pos, extent) of extents with commits */
     if (!badpos.empty()) {
@@ -675,12 +712,13 @@ int run_group(Call &C, Cache &cache, std::vector<Ext *> &G, int threads)
             q[2 * m + c] = cache.h_off[i];
             q[3 * m + c] = cache.h_len[i];
         }
-        uint64_t *dq = nullptr;
-        e = hipMalloc(&dq, 4 * m * 8 + 3 * m * 4);
-        uint32_t *dprev = e == hipSuccess ? reinterpret_cast<uint32_t *>(dq + 4 * m) : nullptr;
-        if (e == hipSuccess)
-            e = hipMemcpy(dq, q.data(), 4 * m * 8, hipMemcpyHostToDevice);
-        rc = e == hipSuccess ? ZSCRC_OK : ZSCRC_EHIP;
+        /* a cached device buffer: a hipMalloc / hipFree per call cost a
+         * device-wide synchronisation each */
+        rc = grow_dev(&cache.dq, &cache.dq_bytes, 4 * m * 8 + 3 * m * 4);
+        uint64_t *dq = rc ? nullptr : reinterpret_cast<uint64_t *>(cache.dq);
+        uint32_t *dprev = dq ? reinterpret_cast<uint32_t *>(dq + 4 * m) : nullptr;
+        if (!rc && hipMemcpyAsync(dq, q.data(), 4 * m * 8, hipMemcpyHostToDevice, ks) != hipSuccess)
+            rc = ZSCRC_EHIP;
         if (!rc)
             rc = zscrc_device_batch_bounded(cache.dimg, dq, dq + m, nullptr, dprev, m, 0, prev_max, ks);
         if (!rc)
@@ -689,8 +727,6 @@ int run_group(Call &C, Cache &cache, std::vector<Ext *> &G, int threads)
         if (!rc && (hipMemcpyAsync(st2.data(), dprev + 2 * m, m * 4, hipMemcpyDeviceToHost, ks) != hipSuccess ||
                     hipStreamSynchronize(ks) != hipSuccess))
             rc = ZSCRC_EHIP;
-        if (dq)
-            (void)hipFree(dq);
     }
     if (!rc) {
         std::lock_guard<std::mutex> lk(C.acc.mu);
