@@ -143,6 +143,76 @@ def spot_check(host_out: np.ndarray, data: torch.Tensor, idx: np.ndarray, stride
     return bad
 
 
+def oracle_check_logs(host: np.ndarray, offs: np.ndarray, lens: np.ndarray, gpu_crc: np.ndarray,
+                      stale_per_file: int) -> dict:
+    """Outside the timed region, the CPU oracle (the checker,
+    oracle/zs_bulk_oracle.c) over a full-size image of [nfiles, size] log
+    files: (i) its own record walk of every file (zeroskip-record.c:283-331)
+    re-checking every stored commit CRC with the writer's semantics
+    (zeroskip-file.c:253-350); (ii) every live commit's CRC recomputed and
+    compared with the GPU's per-commit crc array of the same image."""
+    from oracle import oracle
+    cores = host_cores()
+    t0 = time.perf_counter()
+    w = oracle.walk_images(list(host), threads=cores)
+    commits, ok = int(w[:, 0].sum()), int(w[:, 1].sum())
+    clean_walk = bool((w[:, 3] == 0).all() and (w[:, 2] == host.shape[1]).all())
+    # the only stored CRCs that do not verify from seed 0: each file's stale
+    # zero-length finalise commit, its last (src/mfile.c:534-546)
+    stale_last = bool(((w[:, 0] - w[:, 1]) == stale_per_file).all() and
+                      (stale_per_file == 0 or (w[:, 5] == w[:, 0] - 1).all()))
+    live = lens > 0
+    want = oracle.commit_crcs(host.reshape(-1), offs[live], lens[live], threads=cores)
+    gpu_bad = int((gpu_crc[live] != want).sum())
+    return {"files_walked": int(host.shape[0]), "commits_walked": commits, "commits_verified_ok": ok,
+            "stale_finalise": commits - ok, "walk_clean": clean_walk and stale_last,
+            "gpu_crcs_compared": int(live.sum()), "mismatches": gpu_bad + (0 if clean_walk and stale_last else 1),
+            "checker": "oracle (oracle/zs_bulk_oracle.c): record walk of every file + every live commit's CRC "
+                       "recomputed, compared with the GPU's per-commit crc array",
+            "check_s": round(time.perf_counter() - t0, 2), "threads": cores}
+
+
+def oracle_check_db(db, finalised: int) -> dict:
+    """Outside the timed region, the CPU oracle over every byte of the
+    config-5 DB: each header CRC (zeroskip-header.c:105-170), the .zsdb CRC
+    (zeroskip-dotzsdb.c:160-235), its own walk of every active / finalised
+    file with every commit re-checked, and each packed file's records region
+    (hashed whole on host threads, the pieces joined by the zero shift) and
+    pointer section (zeroskip-packed.c:70-131, :278-339, :442)."""
+    import struct
+    from oracle import oracle
+    cores = host_cores()
+    t0 = time.perf_counter()
+    sig = 0x5A45524F534B4950
+    bad_headers = 0
+    logs, packed = [], []
+    for f in db.files:
+        im = f.image
+        ver, = struct.unpack(">I", im[8:12].tobytes())
+        sidx, eidx, stored = struct.unpack(">III", im[28:40].tobytes())
+        bad_headers += int(oracle.header_crc(sig, ver, im[12:28].tobytes(), sidx, eidx) != stored)
+        (packed if f.kind == zsfile.PACKED else logs).append(im)
+    w = oracle.walk_images(logs, threads=cores)
+    regions = [oracle.packed_image(im, threads=cores) for im in packed]
+    dz = db.dotzsdb
+    off, = struct.unpack(">Q", dz[8:16])
+    cur, dstored = struct.unpack(">II", dz[53:61])
+    dz_ok = oracle.dotzsdb_crc(sig, off, dz[16:53], cur) == dstored
+    commits, ok = int(w[:, 0].sum()), int(w[:, 1].sum())
+    region_ok = sum(int(r["records"]["status"] == 1) + int(r["pointers"]["status"] == 1) for r in regions)
+    walks_clean = bool((w[:, 3] == 0).all())
+    mism = bad_headers + (commits - ok - finalised) + (2 * len(regions) - region_ok) + int(not dz_ok) + \
+        int(not walks_clean)
+    return {"files": len(db.files), "headers_checked": len(db.files), "commits_walked": commits,
+            "commits_verified_ok": ok, "stale_finalise": commits - ok,
+            "regions_checked": len(regions), "region_bytes": int(sum(r["records"]["span_len"] for r in regions)),
+            "pointer_sections_checked": len(regions), "dotzsdb_ok": bool(dz_ok), "mismatches": int(mism),
+            "checker": "oracle (oracle/zs_bulk_oracle.c + zs_format_oracle.c): headers, .zsdb, a record walk of "
+                       "every log file with every commit re-checked, every packed records region and pointer "
+                       "section hashed whole on host threads",
+            "check_s": round(time.perf_counter() - t0, 2), "threads": cores}
+
+
 def traffic_for(key: str):
     tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
@@ -490,6 +560,11 @@ def run_config4(args, world, rank, dev, stream):
     offs_w, lens_w = offs[lens > 0].contiguous(), lens[lens > 0].contiguous()
     write_ms = _timed(lambda: zsfile.write_commits(flat, offs_w, lens_w, max_len=max_span, crc=False), 6, stream)
     write_crc_ms = _timed(lambda: zsfile.write_commits(flat, offs_w, lens_w, max_len=max_span), 6, stream)
+    # the writer's CRCs out of place (commit mode 3): the kernel of the
+    # host-image writer below -- 4 coalesced bytes per commit, no in-place store
+    crcs_ms = _timed(lambda: zsfile.commit_crcs(flat, offs_w, lens_w, max_len=max_span), 10, stream)
+    want_w = res["crc"][lens > 0]
+    assert torch.equal(zsfile.commit_crcs(flat, offs_w, lens_w, max_len=max_span), want_w)
 
     # NOTBATCHED (zsbench writeseq): one commit per ~2 MiB file, unbounded
     # (device length classes; the spans go to xteam_kernel's parts mode)
@@ -503,16 +578,28 @@ def run_config4(args, world, rank, dev, stream):
     nb_arr = {}
 
     def nb_arrays():
-        nb_arr["st"] = zsfile.verify_commits(img_nb.view(-1), o_nb, l_nb)[1]
+        nb_arr["crc"], nb_arr["st"] = zsfile.verify_commits(img_nb.view(-1), o_nb, l_nb)
     nb_arrays_ms = _timed(nb_arrays, 6, stream)
     assert bool((nb_arr["st"] == 1).all())
     nb_bytes = int(l_nb.sum().item()) + 24 * nf_nb
+    # the checker on the NOTBATCHED image: every ~2 MiB commit against the oracle
+    nb_parity = oracle_check_logs(img_nb.cpu().numpy(), o_nb.cpu().numpy(), l_nb.cpu().numpy(),
+                                  nb_arr["crc"].cpu().numpy().view(np.uint32), 0)
+    assert nb_parity["mismatches"] == 0, nb_parity
     del img_nb
+
+    # the checker at full size: every file walked and every commit CRC
+    # recomputed by the CPU oracle, the GPU's crc array compared
+    host = img.cpu()
+    parity = oracle_check_logs(host.numpy(), offs.cpu().numpy(), lens.cpu().numpy(),
+                               res["crc"].cpu().numpy().view(np.uint32), 1)
+    parity["notbatched"] = nb_parity
+    if parity["mismatches"] or parity["commits_walked"] != ncommit:
+        raise SystemExit(f"config4: the oracle disagrees with the GPU: {parity}")
 
     # end to end from host memory, both directions
     e2e = {}
     if rank == 0 and not args.no_e2e:
-        host = img.cpu()
         pinned = torch.empty(host.shape, dtype=torch.uint8, pin_memory=True)
         pinned.copy_(host)
         for kind, src in (("pageable", host), ("pinned", pinned)):
@@ -592,10 +679,36 @@ def run_config4(args, world, rank, dev, stream):
         assert torch.equal(back, pinned)
         e2e["write_pipelined_s"] = round(min(ts), 4)
         e2e["write_pipelined_GBs"] = round(host.numel() / min(ts) / 1e9, 2)
+        # the writer for a host image, CRCs back (zscrc_zs_fill_commits):
+        # image H2D in chunks, commit mode 3, 4 B per commit D2H, host threads
+        # patch the CRC fields -- the reference writer builds its commit
+        # records on the host (src/zeroskip-file.c:315-331).  The fields are
+        # zeroed first, so the first call is checked byte for byte.
+        ow_np = offs_w.cpu().numpy().astype(np.uint64)
+        lw_np = lens_w.cpu().numpy().astype(np.uint64)
+        fields = (ow_np + lw_np + 4)[:, None] + np.arange(4)
+        for kind, buf in (("pinned", pinned.view(-1)), ("pageable", host.view(-1).clone())):
+            arr = buf.numpy()
+            arr[fields] = 0
+            zsfile.fill_commits(buf, ow_np, lw_np, max_len=max_span)
+            assert torch.equal(buf, host.view(-1)), f"fill_commits ({kind}) differs from the GPU-written image"
+            ts, rep_f = [], None
+            for _ in range(3):
+                t0 = time.perf_counter()
+                rep_f = zsfile.fill_commits(buf, ow_np, lw_np, max_len=max_span)
+                ts.append(time.perf_counter() - t0)
+            e2e[f"write_crcs_{kind}_s"] = round(min(ts), 4)
+            e2e[f"write_crcs_{kind}_GBs"] = round(host.numel() / min(ts) / 1e9, 2)
+            e2e[f"write_crcs_{kind}_phases_s"] = {"h2d": round(rep_f["h2d_s"], 4), "total": round(rep_f["total_s"], 4),
+                                                  "chunks": rep_f["chunks"], "threads": rep_f["threads"]}
+            del buf, arr
+        e2e["write_crcs_pipelined_GBs"] = e2e["write_crcs_pinned_GBs"]
         e2e["note"] = ("verify: host file images -> verdicts, walks included (zscrc_zs_verify_files, "
                        f"{rep['threads']} host threads); write: host images -> H2D -> GPU commit writer -> "
                        "D2H of the images (image bytes / wall time), whole image at once or pipelined in "
-                       f"{len(chunks)} file-aligned chunks on three streams; PCIe-bound, never the line's value")
+                       f"{len(chunks)} file-aligned chunks on three streams; write_crcs: host image -> H2D chunks "
+                       "-> commit CRCs out of place -> 4 B per commit D2H -> host threads patch the image "
+                       "(zscrc_zs_fill_commits); PCIe-bound, never the line's value")
         del images, pinned, back
 
     nbytes = span_bytes + 8 * ncommit + 16 * ncommit   # spans + commit trailers + descriptors
@@ -609,14 +722,19 @@ def run_config4(args, world, rank, dev, stream):
                      "files": nfiles, "commits": ncommit, "parallelism": f"replica{world}"},
                     r, data="synthetic zsbench records (key %016d, 255 charset chars + NUL, fixed seed), "
                             "byte-exact zeroskip log images in HBM",
-                    verdict={"bad_commits": nbad, "stale_finalise_commits": nfiles},
+                    verdict={"bad_commits": nbad, "stale_finalise_commits": nfiles}, parity=parity,
                     per_commit_arrays={"ms": round(arrays_ms, 4),
                                        "GBs": round((nbytes + 8 * ncommit) / (arrays_ms * 1e-3) / 1e9, 1),
                                        "note": "zscrc_device_verify_commits_bounded: crc + status per commit "
                                                "(8 B of HBM writes per commit)"},
                     write={"ms": round(write_ms, 4), "GBs": round((span_bytes + 8 * ncommit) / (write_ms * 1e-3) / 1e9, 1),
                            "ms_with_crc_array": round(write_crc_ms, 4),
-                           "note": "zscrc_device_write_commits_bounded, CRCs into the image (d_crc NULL)"},
+                           "crc_array_ms": round(crcs_ms, 4),
+                           "crc_array_GBs": round((span_bytes + 8 * ncommit + 16 * ncommit + 4 * ncommit) /
+                                                  (crcs_ms * 1e-3) / 1e9, 1),
+                           "note": "ms: zscrc_device_write_commits_bounded, CRCs into the image (d_crc NULL); "
+                                   "crc_array_ms: zscrc_device_commit_crcs_bounded, the writer's CRCs to a "
+                                   "coalesced 4 B array, image untouched (the kernel of write_crcs in e2e)"},
                     notbatched={"files": nf_nb, "commits": nf_nb, "verify_ms": round(nb_ms, 4),
                                 "GBs": round(nb_bytes / (nb_ms * 1e-3) / 1e9, 1),
                                 "frac": round(nb_bytes / (nb_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -655,6 +773,10 @@ def run_config5(args, world, rank, dev, stream):
     elapsed = tm.run(step, args.steps, args.warmup)
     rep = step.rep
     assert rep.ok and rep.n_stale == args.finalised, (rep.ok, rep.n_bad, rep.n_stale, rep.walk_errors[:5])
+    # the checker over the whole DB (rank 0; every rank holds the same images)
+    parity = oracle_check_db(job.db, args.finalised) if rank == 0 else None
+    if parity and parity["mismatches"]:
+        raise SystemExit(f"config5: the oracle disagrees: {parity}")
     kern_ms = float(np.mean(tm.kern_ms))
     ncommit = len(job.c_off)
     local_bytes = job.local.bytes_checked
@@ -669,7 +791,7 @@ def run_config5(args, world, rank, dev, stream):
                                  f".zsdb), {rep.commits} commits", "db_bytes": job.plan.weight,
                      "files": rep.files, "commits": rep.commits,
                      "parallelism": f"split{world}" + ("+allgather_digests" if world > 1 else "")},
-                    r, scaling="strong",
+                    r, scaling="strong", parity=parity,
                     data="synthetic zeroskip DB generated on the GPU (tools/zsdb_gen.py), device-resident",
                     prepare={k: round(v, 4) if isinstance(v, float) else v for k, v in job.prepare_times.items()},
                     device_pass={"verified_spans": len(job.c_off), "longest_verified_span": job.c_max,

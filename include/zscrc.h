@@ -75,6 +75,7 @@ enum zscrc_status {
     ZSCRC_ENODEV = -2,   /* no usable gfx950 device          */
     ZSCRC_EHIP = -3,     /* HIP runtime error (see zscrc_last_error) */
     ZSCRC_ENOMEM = -4,   /* device or pinned allocation failed */
+    ZSCRC_EBUSY = -5,    /* a lock is held by someone else (zscrc_zs_repack: .zsdb.lock) */
 };
 
 /* flags */
@@ -306,6 +307,47 @@ int zscrc_device_write_commits_bounded(void *d_image, uint64_t image_size, const
                                        const uint64_t *d_span_len, size_t n, uint64_t max_len, uint32_t *d_crc,
                                        uint32_t *d_status, void *stream);
 
+/* Device: the writer's commit CRCs out of place -- d_crc[i] = the CRC
+ * zscrc_device_write_commits would store for span i (type read from its
+ * commit record), one coalesced 4-byte result per commit; the image is only
+ * read (nothing is stored into it).  d_status (may be NULL): 1 a commit
+ * record is there, 2 none (or not inside the image).  For images that live
+ * in host memory (zscrc_zs_fill_commits): only the CRCs come back over PCIe,
+ * the host patches its own image, as the reference writer builds the commit
+ * record on the host (src/zeroskip-file.c:315-331). */
+int zscrc_device_commit_crcs_bounded(const void *d_image, uint64_t image_size, const uint64_t *d_span_off,
+                                     const uint64_t *d_span_len, size_t n, uint64_t max_len, uint32_t *d_crc,
+                                     uint32_t *d_status, void *stream);
+
+/* The commit writer for an image in HOST memory (a log file being written,
+ * or a whole mmap'd log): every commit CRC computed on the current GPU and
+ * stored big-endian into the caller's image (BE32 at +4 of a short commit
+ * record, +20 of a long one) -- only the CRCs cross PCIe back, the image is
+ * copied to the device once, pipelined in chunks (ZSCRC_FILL_CHUNK, default
+ * 64 MiB) with host threads patching earlier chunks.  Span i is
+ * [span_off[i], +span_len[i]) of the image; spans sorted and disjoint
+ * (ZSCRC_EINVAL otherwise); the commit record's header words must already be
+ * in the image (zscrc_device_write_commits' contract), a span without one is
+ * counted in no_record and left alone.  max_len: a bound on the span lengths
+ * or ZSCRC_LEN_UNBOUNDED; spans longer than a chunk are streamed through the
+ * GPU (zscrc_stream_*).  A pinned image (hipHostMalloc / hipHostRegister) is
+ * copied straight from the caller's memory, a pageable one through pinned
+ * staging filled by `threads` host threads (0 = up to 16).  Synchronous. */
+typedef struct zscrc_fill_report {
+    uint64_t commits;          /* CRCs written into the image                */
+    uint64_t no_record;        /* spans with no commit record after them      */
+    uint64_t long_commits;     /* spans streamed on their own                 */
+    uint64_t bytes;            /* image bytes sent to the GPU                 */
+    uint64_t desc_bytes;       /* descriptor bytes sent (8 per commit)        */
+    uint64_t chunks;
+    int32_t staged;            /* 1 pageable image via pinned staging, 0 direct */
+    int32_t threads;
+    double h2d_s;              /* until the last chunk was on the GPU         */
+    double total_s;
+} zscrc_fill_report;
+int zscrc_zs_fill_commits(void *image, uint64_t size, const uint64_t *span_off, const uint64_t *span_len,
+                          size_t n, uint64_t max_len, int threads, zscrc_fill_report *rep);
+
 typedef struct zscrc_zs_report {
     int header_rc;            /* zscrc_zs_header_crc result */
     uint32_t header_stored, header_computed;
@@ -380,9 +422,16 @@ typedef struct zscrc_cpass_result {
     int32_t span_status[ZSCRC_CPASS_SPANS]; /* 1 ok, 0 mismatch, 2 no commit record,
                                              * -1 not checked (span_commit -1)            */
 } zscrc_cpass_result;
+/* The pass is bound to the device current at create (its buffers live
+ * there); run and destroy switch to it and restore the caller's device. */
 int zscrc_cpass_create(zscrc_cpass **p, const zscrc_cpass_spec *spec);
 /* Synchronous on `stream` (NULL = default). */
 int zscrc_cpass_run(zscrc_cpass *p, void *stream, zscrc_cpass_result *res);
+/* As zscrc_cpass_run; start_event / end_event (hipEvent_t, may be NULL) are
+ * recorded on `stream` before the first launch and right after the copy back
+ * is enqueued -- the device's part of the pass, without the host's wait. */
+int zscrc_cpass_run_timed(zscrc_cpass *p, void *stream, void *start_event, void *end_event,
+                          zscrc_cpass_result *res);
 void zscrc_cpass_destroy(zscrc_cpass *p);
 
 /* End to end from host memory: every CRC of n zeroskip file images (mmap'd
@@ -492,7 +541,13 @@ int zscrc_zs_dotzsdb_build(uint64_t offset, const char *uuidstr, uint32_t curidx
  * wins, deletes kept) into one packed file; else two or more packed files
  * -> the first two of the reference's pflist (the two newest; the older of
  * the two wins a key present in both, a winning delete drops the key); the
- * merged sources unlinked; .zsdb rewritten with its CRC.  Keys sorted on
+ * merged sources unlinked; .zsdb rewritten with its CRC.  The DB's update
+ * lock, .zsdb.lock, is created with O_EXCL before anything is read and held
+ * until the new .zsdb is renamed from it (zs_dotzsdb_update_begin / _end):
+ * ZSCRC_EBUSY if it is already held.  The packed file is written as
+ * "<path>.tmp" and renamed into place before any source is unlinked (a
+ * source of the same name -- one finalised file -- is replaced, never
+ * unlinked).  Keys sorted on
  * `threads` host threads (0 = up to 16); the packed file's records-region
  * and pointer CRCs computed on the GPU (zscrc_pack_*).  flags:
  * ZSCRC_PACK_FSYNC. */

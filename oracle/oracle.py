@@ -52,6 +52,17 @@ def lib() -> ctypes.CDLL:
         L.oracle_dotzsdb_crc.argtypes = [u64, u64, ctypes.c_char_p, u32]
         L.oracle_dotzsdb_crc.restype = u32
         L.oracle_get_sb4.argtypes = [vp]
+        # zs_bulk_oracle.c
+        L.oracle_walk_images.argtypes = [vp, vp, u64, vp, ctypes.c_int]
+        L.oracle_walk_images.restype = ctypes.c_int
+        L.oracle_span_crc.argtypes = [vp, u64, ctypes.c_int]
+        L.oracle_span_crc.restype = u32
+        L.oracle_packed_image.argtypes = [vp, u64, ctypes.c_int, vp]
+        L.oracle_packed_image.restype = None
+        L.oracle_write_commits.argtypes = [vp, vp, vp, u64, ctypes.c_int]
+        L.oracle_write_commits.restype = ctypes.c_int
+        L.oracle_commit_crcs.argtypes = [vp, vp, vp, u64, vp, ctypes.c_int]
+        L.oracle_commit_crcs.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -139,3 +150,58 @@ def crc32c_py(crc: int, data: bytes) -> int:
         for _ in range(8):
             r = (r >> 1) ^ (0x82F63B78 if r & 1 else 0)
     return r ^ 0xFFFFFFFF
+
+
+# ------------------------------------------------------------------ bulk (zs_bulk_oracle.c)
+WALK_FIELDS = ("commits", "ok", "end", "stop", "first_bad_off", "first_bad_idx")
+
+
+def walk_images(images, threads: int = 1) -> np.ndarray:
+    """[n, 6] uint64: the record walk of every active / finalised image
+    (zeroskip-record.c:283-331), each commit re-checked from seed 0 with the
+    writer's trailer semantics; columns as WALK_FIELDS (stop: 0 end of image,
+    1 truncated, 2 a type the walk does not advance over, 3 a commit record
+    that does not fit).  images: uint8 numpy arrays."""
+    arrs = [np.ascontiguousarray(a).view(np.uint8).reshape(-1) for a in images]
+    addr = np.array([a.ctypes.data for a in arrs], dtype=np.uint64)
+    size = np.array([a.nbytes for a in arrs], dtype=np.uint64)
+    out = np.zeros((len(arrs), 6), dtype=np.uint64)
+    assert lib().oracle_walk_images(addr.ctypes.data, size.ctypes.data, len(arrs), out.ctypes.data, threads) == 0
+    return out
+
+
+def span_crc(data: np.ndarray, threads: int = 1) -> int:
+    """crc32c(0, data) on `threads` threads (pieces joined by the zero shift)."""
+    a = np.ascontiguousarray(data).view(np.uint8).reshape(-1)
+    return lib().oracle_span_crc(a.ctypes.data, a.nbytes, threads)
+
+
+def packed_image(img: np.ndarray, threads: int = 1) -> dict:
+    """A packed file's two commits (zeroskip-packed.c:70-131, :278-339, :442):
+    status 1 ok / 0 bad / 2 layout, span offset and length of each."""
+    a = np.ascontiguousarray(img).view(np.uint8).reshape(-1)
+    out = np.zeros(6, dtype=np.uint64)
+    lib().oracle_packed_image(a.ctypes.data, a.nbytes, threads, out.ctypes.data)
+    o = [int(x) for x in out]
+    return {"pointers": {"status": o[0], "span_off": o[1], "span_len": o[2]},
+            "records": {"status": o[3], "span_off": o[4], "span_len": o[5]}}
+
+
+def write_commits(base: np.ndarray, offs, lens, threads: int = 1) -> None:
+    """The commit writer (zeroskip-file.c:253-350) in place: the record after
+    each span, whose type byte is already there, is written whole."""
+    assert base.flags.c_contiguous and base.dtype == np.uint8
+    o = np.ascontiguousarray(offs, dtype=np.uint64)
+    ln = np.ascontiguousarray(lens, dtype=np.uint64)
+    assert lib().oracle_write_commits(base.ctypes.data, o.ctypes.data, ln.ctypes.data, len(o), threads) == 0
+
+
+def commit_crcs(base: np.ndarray, offs, lens, threads: int = 1) -> np.ndarray:
+    """The CRC the writer stores for each span (nothing written)."""
+    b = np.ascontiguousarray(base).view(np.uint8).reshape(-1)
+    o = np.ascontiguousarray(offs, dtype=np.uint64)
+    ln = np.ascontiguousarray(lens, dtype=np.uint64)
+    out = np.zeros(len(o), dtype=np.uint32)
+    assert lib().oracle_commit_crcs(b.ctypes.data, o.ctypes.data, ln.ctypes.data, len(o), out.ctypes.data,
+                                    threads) == 0
+    return out

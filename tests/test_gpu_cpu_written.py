@@ -1,0 +1,118 @@
+"""GPU verification of images whose commit CRCs the CPU oracle wrote
+(tools/zsdb_gen.py writer="cpu": oracle/zs_bulk_oracle.c oracle_write_commits,
+the writer of src/zeroskip-file.c:253-350), so the GPU writer and the GPU
+verifier are never each other's only witness:
+
+* >= 1 M zsbench BATCHED commits (config 4's layout, 153 log files of 2 MiB)
+  verified by commit_kernel<false> -- verdict and per-commit arrays -- against
+  the oracle's stored CRCs, and the GPU writer reproducing the CPU-written
+  image byte for byte;
+* NOTBATCHED ~2 MiB spans (the parts mode) from the CPU writer;
+* a config-5-shaped DB (packed files with long commits, finalised files,
+  active file) written by the CPU, checked by `consistent` on the GPU.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle
+from tools import zsdb_gen as zg
+from zeroskip_amd import consistent as cs
+from zeroskip_amd import zsfile
+
+pytestmark = pytest.mark.gpu
+
+UUID = bytes(range(16))
+
+
+@pytest.fixture(scope="module")
+def batched(gpu):
+    ppf = zg.pairs_per_file(True)
+    nfiles = -(-1_000_000 // ppf)
+    g = torch.Generator(device=gpu)
+    g.manual_seed(0xC0DE)
+    img = zg.log_files(UUID, 0, nfiles, ppf, 0, True, g, gpu, writer="cpu")
+    offs, lens = zg.log_spans(nfiles, ppf, True, True, gpu)
+    torch.cuda.synchronize()
+    return img, offs, lens, nfiles
+
+
+def test_cpu_written_million_commits_verdict(batched):
+    img, offs, lens, nfiles = batched
+    assert offs.numel() >= 1_000_000 + nfiles
+    nbad, bad = zsfile.verify_commits_verdict(img.view(-1), offs, lens, max_len=312)
+    nbad = int(nbad.item())
+    stale = torch.nonzero(lens == 0).flatten()
+    assert nbad == nfiles
+    assert torch.equal(torch.sort(bad[:nbad]).values, stale)
+
+
+def test_cpu_written_million_commits_arrays(batched):
+    img, offs, lens, nfiles = batched
+    crc, st = zsfile.verify_commits(img.view(-1), offs, lens, max_len=312)
+    host = img.view(-1).cpu().numpy()
+    o, ln = offs.cpu().numpy(), lens.cpu().numpy()
+    st = st.cpu().numpy()
+    live = ln > 0
+    assert (st[live] == 1).all() and (st[~live] == 0).all()
+    # every computed CRC equals the oracle's (the stored field the CPU wrote)
+    want = oracle.commit_crcs(host, o[live], ln[live], threads=8)
+    got = crc.cpu().numpy().view(np.uint32)[live]
+    assert np.array_equal(got, want)
+    stored = host[(o[live] + ln[live] + 4)[:, None] + np.arange(4)].view(">u4").reshape(-1)
+    assert np.array_equal(stored, want)
+
+
+def test_gpu_writer_reproduces_cpu_image(batched):
+    img, offs, lens, nfiles = batched
+    live = lens > 0
+    o, ln = offs[live].contiguous(), lens[live].contiguous()
+    blank = img.clone().view(-1)
+    at = (o + ln + 4)[:, None] + torch.arange(4, device=o.device)
+    blank[at.reshape(-1)] = 0
+    assert not torch.equal(blank, img.view(-1))
+    zsfile.write_commits(blank, o, ln, max_len=312)
+    torch.cuda.synchronize()
+    assert torch.equal(blank, img.view(-1))
+
+
+def test_cpu_written_notbatched(gpu):
+    ppf = zg.pairs_per_file(False)
+    g = torch.Generator(device=gpu)
+    g.manual_seed(7)
+    nf = 24
+    img = zg.log_files(UUID, 0, nf, ppf, 0, False, g, gpu, batched=False, writer="cpu")
+    o, ln = zg.log_spans(nf, ppf, False, False, gpu)
+    nbad, _ = zsfile.verify_commits_verdict(img.view(-1), o, ln)
+    assert int(nbad.item()) == 0
+    crc, st = zsfile.verify_commits(img.view(-1), o, ln)
+    assert bool((st == 1).all())
+    want = oracle.commit_crcs(img.view(-1).cpu().numpy(), o.cpu().numpy(), ln.cpu().numpy(), threads=8)
+    assert np.array_equal(crc.cpu().numpy().view(np.uint32), want)
+
+
+def test_cpu_written_db_consistent(gpu):
+    db = zg.make_db(device=gpu, packed=2, packed_region_bytes=20 << 20, finalised=12, active_pairs=300,
+                    writer="cpu")
+    rep = cs.consistent(db)
+    assert rep.ok and rep.n_bad == 0 and rep.n_stale == 12
+    # the long records commits (> 16 MiB regions) came from the CPU writer
+    for name, v in db.items():
+        if name.endswith("-0-7") or name.endswith("-8-15"):
+            p = oracle.packed_image(v.cpu().numpy(), threads=4)
+            assert p["records"]["status"] == 1 and p["records"]["span_len"] > zg.MAX_SHORT
+            assert p["pointers"]["status"] == 1
+
+
+def test_fill_commits_host_million(batched):
+    """zscrc_zs_fill_commits on the >= 1 M-commit host image with its CRC
+    fields zeroed reproduces the CPU-written image byte for byte."""
+    img, offs, lens, nfiles = batched
+    host = img.view(-1).cpu().numpy()
+    live = (lens > 0).cpu().numpy()
+    o, ln = offs.cpu().numpy()[live], lens.cpu().numpy()[live]
+    blank = host.copy()
+    blank[(o + ln + 4)[:, None] + np.arange(4)] = 0
+    rep = zsfile.fill_commits(blank, o, ln, max_len=312)
+    assert rep["commits"] == len(o) and rep["no_record"] == 0 and rep["chunks"] > 1
+    assert np.array_equal(blank, host)

@@ -9,7 +9,7 @@ import pytest
 from oracle import oracle
 from oracle import zs_format as zf
 from zeroskip_amd import repack, zsfile
-from zeroskip_amd._lib import stats
+from zeroskip_amd._lib import ZscrcError, stats
 
 pytestmark = pytest.mark.gpu
 
@@ -188,3 +188,52 @@ def test_packer_abort_removes_file(gpu, tmp_path):
             p.add(b"a" * 16, b"x" * 100)
             raise RuntimeError("interrupted")
     assert not path.exists()
+
+
+def test_repack_dir_single_finalised_file(gpu, tmp_path):
+    """One finalise followed by a repack: the output name
+    zeroskip-<uuid>-<i>-<i> is the source's own.  The packed file replaces the
+    finalised file (written under a temporary name, renamed after the source
+    is unmapped); nothing is lost, the output is not unlinked."""
+    rng = np.random.default_rng(12)
+    w = zf.FileWriter(UUID, idx=4)
+    for t in range(300):
+        w.add(b"%016d" % int(rng.integers(0, 200)), rng.integers(0, 256, 100, dtype=np.uint8).tobytes())
+        w.commit()
+    img = w.image()
+    name = f"zeroskip-{UUIDSTR}-4-4"
+    (tmp_path / name).write_bytes(img)
+    (tmp_path / f"zeroskip-{UUIDSTR}-5").write_bytes(zf.FileWriter(UUID, idx=5).image())
+    _dotzsdb(tmp_path, 5)
+    rep = repack.repack_dir(str(tmp_path))
+    assert rep["branch"] == 1 and rep["path"] == str(tmp_path / name) and (rep["startidx"], rep["endidx"]) == (4, 4)
+    want = zf.packed_file(zf.repack_finalised([img]), UUID, 4, 4)
+    assert open(tmp_path / name, "rb").read() == want
+    assert sorted(os.listdir(tmp_path)) == sorted([".zsdb", name, f"zeroskip-{UUIDSTR}-5"])
+    r = zsfile.verify_image(want, zsfile.PACKED)
+    assert r["n_bad"] == 0 and r["n_commits"] == 2
+
+
+def test_repack_dir_lock_held(gpu, tmp_path):
+    """A held .zsdb.lock (another writer inside zs_dotzsdb_update_begin /
+    _end) makes repack refuse with ZSCRC_EBUSY and touch nothing; the lock
+    is released (removed) by a repack that ran."""
+    w = zf.FileWriter(UUID, idx=1)
+    w.add(b"k" * 16, b"v" * 40)
+    w.commit()
+    (tmp_path / f"zeroskip-{UUIDSTR}-1-1").write_bytes(w.image())
+    _dotzsdb(tmp_path, 2)
+    (tmp_path / ".zsdb.lock").write_bytes(b"held")
+    before = sorted(os.listdir(tmp_path))
+    with pytest.raises(ZscrcError, match="status -5"):
+        repack.repack_dir(str(tmp_path))
+    assert sorted(os.listdir(tmp_path)) == before
+    assert (tmp_path / ".zsdb.lock").read_bytes() == b"held"
+    os.unlink(tmp_path / ".zsdb.lock")
+    rep = repack.repack_dir(str(tmp_path))
+    assert rep["branch"] == 1 and not (tmp_path / ".zsdb.lock").exists()
+    # a repack that fails after taking the lock (bad .zsdb) releases it
+    (tmp_path / ".zsdb").write_bytes(b"\0" * 61)
+    with pytest.raises(ZscrcError):
+        repack.repack_dir(str(tmp_path))
+    assert not (tmp_path / ".zsdb.lock").exists()

@@ -13,11 +13,17 @@ Layout, oldest first (file names as zeroskip-filename.c:18-67 makes them):
   active     zeroskip-<uuid>-<n>       the same pairs, no finalise
   .zsdb      offset = active size, curidx = n (zeroskip-dotzsdb.c)
 
-Every CRC is written by the engine itself -- the commit CRCs by the GPU
-writer (zscrc_device_write_commits), header / .zsdb / stale-commit words by
-libzscrc's host functions -- so this is the engine acting as zeroskip's
-writer.  tests/test_gpu_consistent.py re-checks generated DBs with the
-independent oracle walker (oracle/zs_format.py).
+By default every CRC is written by the engine itself -- the commit CRCs by
+the GPU writer (zscrc_device_write_commits), header / .zsdb / stale-commit
+words by libzscrc's host functions -- so this is the engine acting as
+zeroskip's writer.  tests/test_gpu_consistent.py re-checks generated DBs with
+the independent oracle walker (oracle/zs_format.py).
+
+writer="cpu" (CLI --cpu-writer; test infrastructure) writes every commit CRC
+with the CPU oracle instead (oracle/zs_bulk_oracle.c oracle_write_commits,
+the writer of src/zeroskip-file.c:253-350, on host threads): images the GPU
+verifier then checks without the GPU writer ever having touched them, so
+writer and verifier are never each other's only witness.
 """
 from __future__ import annotations
 
@@ -76,13 +82,46 @@ def _charset_values(n: int, vlen: int, gen: torch.Generator, device) -> torch.Te
     return v
 
 
+def _cpu_threads() -> int:
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return max(1, min(n, int(omp)) if omp.isdigit() and int(omp) > 0 else n)
+
+
+def write_commits(flat: torch.Tensor, offs: torch.Tensor, lens: torch.Tensor, writer: str = "gpu") -> None:
+    """Commit CRCs of the spans [offs, +lens) of `flat` into their records:
+    the GPU writer, or (writer="cpu") the CPU oracle's writer on host threads
+    (the image goes to the host and back)."""
+    if writer == "gpu":
+        zsfile.write_commits(flat, offs, lens)
+        return
+    assert writer == "cpu", writer
+    from oracle import oracle     # test infrastructure: the checker acting as the writer
+    host = flat.cpu().numpy()
+    oracle.write_commits(host, offs.cpu().numpy(), lens.cpu().numpy(), threads=_cpu_threads())
+    flat.copy_(torch.from_numpy(host))
+
+
+def _span_crcs(flat: torch.Tensor, offs: torch.Tensor, lens: torch.Tensor, writer: str) -> list:
+    if writer == "gpu":
+        from zeroskip_amd.device import crc_batch
+        return [c & 0xFFFFFFFF for c in crc_batch(flat, offs, lens).cpu().tolist()]
+    from oracle import oracle
+    host = flat.cpu().numpy()
+    return [int(c) for c in oracle.batch(host, offs.cpu().numpy(), lens.cpu().numpy(), threads=_cpu_threads())]
+
+
 def log_files(uuid: bytes, first_idx: int, nfiles: int, pairs: int, first_pair: int,
-              finalise: bool, gen, device, batched: bool = True) -> torch.Tensor:
+              finalise: bool, gen, device, batched: bool = True, writer: str = "gpu") -> torch.Tensor:
     """[nfiles, size] uint8 zsbench log files (zsbench.c:159-217), commit
-    CRCs written by the GPU.  batched: one commit per pair (writeseqtxn);
-    else one commit closing each file (writeseq: the finalise at 2 MiB
-    commits the open transaction).  `finalise` (batched only) appends the
-    stale zero-length commit of zs_active_file_finalise."""
+    CRCs written by the GPU (writer="cpu": by the CPU oracle).  batched: one
+    commit per pair (writeseqtxn); else one commit closing each file
+    (writeseq: the finalise at 2 MiB commits the open transaction).
+    `finalise` (batched only) appends the stale zero-length commit of
+    zs_active_file_finalise."""
     pair = PAIR if batched else KEYREC + VALREC
     tail = 8 if (finalise or not batched) else 0
     size = HDR + pairs * pair + tail
@@ -101,18 +140,21 @@ def log_files(uuid: bytes, first_idx: int, nfiles: int, pairs: int, first_pair: 
         n = pairs * pair
         img[:, size - 8:] = _be64((T_COMMIT << 56) | (n << 32)).to(device)
         offs = (base[:, 0] + HDR).contiguous()
-        zsfile.write_commits(flat, offs, torch.full_like(offs, n))
+        write_commits(flat, offs, torch.full_like(offs, n), writer)
         return img
     body[:, :, 312:320] = _be64((T_COMMIT << 56) | (312 << 32)).to(device)
     offs = (base + HDR + torch.arange(pairs, dtype=torch.int64, device=device)[None, :] * PAIR).reshape(-1)
-    zsfile.write_commits(flat, offs, torch.full_like(offs, 312))
+    write_commits(flat, offs, torch.full_like(offs, 312), writer)
     if finalise:
         # mf->crc32 still holds crc32c(0, last span): the finalise commit hashes it
-        from zeroskip_amd.device import crc_batch
         last = (base[:, 0] + HDR + (pairs - 1) * PAIR).contiguous()
-        span_crc = crc_batch(flat, last, torch.full_like(last, 312)).cpu().tolist()
+        span_crc = _span_crcs(flat, last, torch.full_like(last, 312), writer)
         w = T_COMMIT << 56
-        tail = [w | crc32c_hw(c & 0xFFFFFFFF, struct.pack("<Q", w)) for c in span_crc]
+        if writer == "gpu":
+            tail = [w | crc32c_hw(c, struct.pack("<Q", w)) for c in span_crc]
+        else:
+            from oracle import oracle
+            tail = [w | oracle.commit_crc(c, 0) for c in span_crc]
         img[:, size - 8:] = torch.tensor([list(t.to_bytes(8, "big")) for t in tail],
                                          dtype=torch.uint8, device=device)
     return img
@@ -142,7 +184,7 @@ def pairs_per_file(batched: bool = True) -> int:
 
 
 def packed_file(uuid: bytes, s: int, e: int, region_bytes: int, vlen: int, first_key: int,
-                gen, device) -> tuple[torch.Tensor, int]:
+                gen, device, writer: str = "gpu") -> tuple[torch.Tensor, int]:
     """One packed file with ~region_bytes of key/value records in key order
     (and its record count)."""
     vrec = 16 + ((vlen + 7) & ~7)
@@ -182,15 +224,16 @@ def packed_file(uuid: bytes, s: int, e: int, region_bytes: int, vlen: int, first
         img[fo + 16:fo + 24] = _be64(T_2ND << 56).to(device)
     else:
         img[fo:fo + 8] = _be64((T_FINAL << 56) | (plen << 32)).to(device)
-    zsfile.write_commits(img, torch.tensor([HDR, p], dtype=torch.int64, device=device),
-                         torch.tensor([rlen, plen], dtype=torch.int64, device=device))
+    write_commits(img, torch.tensor([HDR, p], dtype=torch.int64, device=device),
+                  torch.tensor([rlen, plen], dtype=torch.int64, device=device), writer)
     return img, n
 
 
 def make_db(device="cuda", packed: int = 2, packed_region_bytes: int = 3 << 30, packed_vlen: int = 4064,
             finalised: int = 1024, active_pairs: int = 1000, seed: int = 0x5EED,
-            uuid: bytes = bytes(range(16))) -> dict:
-    """{file name: device uint8 tensor} + {".zsdb": bytes}; all on `device`."""
+            uuid: bytes = bytes(range(16)), writer: str = "gpu") -> dict:
+    """{file name: device uint8 tensor} + {".zsdb": bytes}; all on `device`.
+    writer: "gpu" (the engine) or "cpu" (the CPU oracle) writes the commit CRCs."""
     device = torch.device(device)
     gen = torch.Generator(device=device)
     gen.manual_seed(seed)
@@ -200,18 +243,19 @@ def make_db(device="cuda", packed: int = 2, packed_region_bytes: int = 3 << 30, 
     db, idx, key = {}, 0, 0
     span = 8
     for k in range(packed):
-        img, n = packed_file(uuid, idx, idx + span - 1, packed_region_bytes, packed_vlen, key, gen, device)
+        img, n = packed_file(uuid, idx, idx + span - 1, packed_region_bytes, packed_vlen, key, gen, device,
+                             writer)
         db[name(idx, idx + span - 1)] = img
         key += n
         idx += span
     pairs = pairs_per_file()
     if finalised:
-        logs = log_files(uuid, idx, finalised, pairs, key, True, gen, device)
+        logs = log_files(uuid, idx, finalised, pairs, key, True, gen, device, writer=writer)
         for f in range(finalised):
             db[name(idx + f, idx + f)] = logs[f]
         idx += finalised
         key += finalised * pairs
-    act = log_files(uuid, idx, 1, active_pairs, key, False, gen, device)[0]
+    act = log_files(uuid, idx, 1, active_pairs, key, False, gen, device, writer=writer)[0]
     db[name(idx)] = act
     db[".zsdb"] = dotzsdb(act.numel(), uuidstr.encode() + b"\0", idx)
     return db
@@ -235,6 +279,9 @@ if __name__ == "__main__":
     ap.add_argument("--packed", type=int, default=2)
     ap.add_argument("--packed-mib", type=int, default=3072)
     ap.add_argument("--finalised", type=int, default=1024)
+    ap.add_argument("--cpu-writer", action="store_true",
+                    help="commit CRCs written by the CPU oracle instead of the GPU writer (test infrastructure)")
     a = ap.parse_args()
-    d = make_db(packed=a.packed, packed_region_bytes=a.packed_mib << 20, finalised=a.finalised)
+    d = make_db(packed=a.packed, packed_region_bytes=a.packed_mib << 20, finalised=a.finalised,
+                writer="cpu" if a.cpu_writer else "gpu")
     print(write_dir(d, a.out), "bytes written to", a.out)

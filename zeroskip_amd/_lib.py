@@ -74,6 +74,7 @@ SIGNATURES = {
     "zscrc_abi_version": (_int, []),
     "zscrc_cpass_create": (_int, [_vp, _vp]),
     "zscrc_cpass_run": (_int, [_vp, _vp, _vp]),
+    "zscrc_cpass_run_timed": (_int, [_vp, _vp, _vp, _vp, _vp]),
     "zscrc_cpass_destroy": (None, [_vp]),
     "zscrc_device_verify_commits_verdict": (_int, [_vp, _u64, _vp, _vp, _vp, _sz, _u64, _vp, _vp, _sz, _vp]),
     "zscrc_pack_abort": (_int, [_vp]),
@@ -83,6 +84,8 @@ SIGNATURES = {
     "zscrc_set_devices": (_int, [_vp, _int]),
     "zscrc_files_devices": (_int, [_vp, _int]),
     "zscrc_release_cache": (None, []),
+    "zscrc_device_commit_crcs_bounded": (_int, [_vp, _u64, _vp, _vp, _sz, _u64, _vp, _vp, _vp]),
+    "zscrc_zs_fill_commits": (_int, [_vp, _u64, _vp, _vp, _sz, _u64, _int, _vp]),
 }
 ABI_VERSION = 3  # include/zscrc.h ZSCRC_ABI_VERSION
 

@@ -589,12 +589,17 @@ class Consistent:
         res = self._cres
         dev = self.buf.device
         stream = torch.cuda.current_stream(dev)
-        if events:
-            events[0].record(stream)
-        check(lib().zscrc_cpass_run(self._cpass, ctypes.c_void_p(stream.cuda_stream), ctypes.byref(res)),
-              "zscrc_cpass_run")
-        if events:
-            events[1].record(stream)
+        # the C pass switches to the device it was created on; the stream and
+        # the events are that device's (zscrc_cpass_run_timed records the end
+        # event before its host-side wait)
+        with torch.cuda.device(dev):
+            ev = (None, None)
+            if events:
+                for e in events:          # torch creates its events lazily, on the first record
+                    e.record(stream)
+                ev = (ctypes.c_void_p(events[0].cuda_event), ctypes.c_void_p(events[1].cuda_event))
+            check(lib().zscrc_cpass_run_timed(self._cpass, ctypes.c_void_p(stream.cuda_stream), ev[0], ev[1],
+                                              ctypes.byref(res)), "zscrc_cpass_run_timed")
         if res.n_undecided or not res.complete:
             return None
         t_dev = time.perf_counter()

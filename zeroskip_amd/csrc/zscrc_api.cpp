@@ -1113,7 +1113,8 @@ int zscrc_internal_verify_commits(const void *d_image, uint64_t image_size, cons
 {
     if (n == 0)
         return ZSCRC_OK;
-    if (!d_image || !d_off || !d_len || (!write && !d_crc) || (!write && !d_status))
+    /* write: 0 verify, 1 write in place, 2 the writer's CRCs into d_crc only */
+    if (!d_image || !d_off || !d_len || (write != 1 && !d_crc) || (!write && !d_status))
         return ZSCRC_EINVAL;
     DevCtx *c;
     int rc = get_ctx(&c);
@@ -1126,7 +1127,7 @@ int zscrc_internal_verify_commits(const void *d_image, uint64_t image_size, cons
     d.seed = d_seed;
     d.out = d_crc;
     d.status = d_status;
-    d.commit = write ? 2u : 1u;
+    d.commit = write == 2 ? 3u : write ? 2u : 1u;
     d.img_size = image_size;
     d.n = n;
     d.xor_io = 0xffffffffu;

@@ -38,6 +38,7 @@ constexpr uint64_t LIST_CAP = 4096; /* bad-list entries copied back per pass */
 
 struct zscrc_cpass {
     zscrc_cpass_spec spec;
+    int dev = 0; /* the device current at create: every buffer lives there */
     std::vector<uint64_t> span_off, span_len;
     std::vector<int64_t> span_commit;
     /* device block: [0] nbad, [1] nstale, then span_raw[64] (u32),
@@ -85,6 +86,10 @@ extern "C" int zscrc_cpass_create(zscrc_cpass **out, const zscrc_cpass_spec *spe
         return ZSCRC_ENODEV;
     zscrc_cpass *p = new zscrc_cpass;
     p->spec = *spec;
+    if (hipGetDevice(&p->dev) != hipSuccess) {
+        delete p;
+        return ZSCRC_ENODEV;
+    }
     p->span_off.assign(spec->span_off, spec->span_off + spec->nspans);
     p->span_len.assign(spec->span_len, spec->span_len + spec->nspans);
     p->span_commit.assign(spec->span_commit, spec->span_commit + spec->nspans);
@@ -123,11 +128,41 @@ extern "C" int zscrc_cpass_create(zscrc_cpass **out, const zscrc_cpass_spec *spe
     return ZSCRC_OK;
 }
 
+namespace {
+
+int cpass_run(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1, zscrc_cpass_result *res);
+
+} /* namespace */
+
 extern "C" int zscrc_cpass_run(zscrc_cpass *p, void *stream, zscrc_cpass_result *res)
+{
+    return zscrc_cpass_run_timed(p, stream, nullptr, nullptr, res);
+}
+
+extern "C" int zscrc_cpass_run_timed(zscrc_cpass *p, void *stream, void *start_event, void *end_event,
+                                     zscrc_cpass_result *res)
 {
     if (!p || !res)
         return ZSCRC_EINVAL;
-    hipStream_t s = static_cast<hipStream_t>(stream);
+    /* the pass runs on the device it was created on (its buffers and the
+     * operator table the kernels read are that device's), whatever device
+     * the caller has current; the caller's device is restored */
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess || (cur != p->dev && hipSetDevice(p->dev) != hipSuccess))
+        return ZSCRC_EHIP;
+    const int rc = cpass_run(p, static_cast<hipStream_t>(stream), static_cast<hipEvent_t>(start_event),
+                             static_cast<hipEvent_t>(end_event), res);
+    if (cur != p->dev)
+        (void)hipSetDevice(cur);
+    return rc;
+}
+
+namespace {
+
+int cpass_run(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1, zscrc_cpass_result *res)
+{
+    if (ev0 && hipEventRecord(ev0, s) != hipSuccess)
+        return ZSCRC_EHIP;
     const zscrc_cpass_spec &sp = p->spec;
     uint64_t *d_nbad = reinterpret_cast<uint64_t *>(p->dblk);
     uint32_t *d_raw = reinterpret_cast<uint32_t *>(p->dblk + OFF_RAW);
@@ -180,8 +215,13 @@ extern "C" int zscrc_cpass_run(zscrc_cpass *p, void *stream, zscrc_cpass_result 
     /* the post kernel wrote the listed part of the verdict next to the
      * counters: one copy back (two device-to-device copies of the lists
      * before it cost a launch each) */
-    if (!rc && (hipMemcpyAsync(p->hblk, p->dblk, BLK, hipMemcpyDeviceToHost, s) != hipSuccess ||
-                hipStreamSynchronize(s) != hipSuccess))
+    if (!rc && hipMemcpyAsync(p->hblk, p->dblk, BLK, hipMemcpyDeviceToHost, s) != hipSuccess)
+        rc = ZSCRC_EHIP;
+    /* the end event right behind the copy back: the device's part of the
+     * pass, without the host's wait and the list sorting below */
+    if (!rc && ev1 && hipEventRecord(ev1, s) != hipSuccess)
+        rc = ZSCRC_EHIP;
+    if (!rc && hipStreamSynchronize(s) != hipSuccess)
         rc = ZSCRC_EHIP;
     if (rc)
         return rc;
@@ -212,8 +252,15 @@ extern "C" int zscrc_cpass_run(zscrc_cpass *p, void *stream, zscrc_cpass_result 
     return ZSCRC_OK;
 }
 
+} /* namespace */
+
 extern "C" void zscrc_cpass_destroy(zscrc_cpass *p)
 {
-    if (p)
-        cpass_free(p);
+    if (!p)
+        return;
+    int cur = -1;
+    const bool sw = hipGetDevice(&cur) == hipSuccess && cur != p->dev && hipSetDevice(p->dev) == hipSuccess;
+    cpass_free(p);
+    if (sw)
+        (void)hipSetDevice(cur);
 }

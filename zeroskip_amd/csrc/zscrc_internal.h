@@ -34,11 +34,13 @@ struct BatchDesc {
     uint64_t len_hi;
     uint32_t fixed_seed;
     uint32_t xor_io;      /* 0xFFFFFFFF standard CRC, 0 raw registers */
-    /* zeroskip commits: commit = 1 (verify) / 2 (write): record i is the span
-     * of a commit record that starts right after it; out[i] receives the
-     * commit CRC (span + host-order trailer words); verify: status[i] 1 =
-     * matches the stored CRC, 0 = mismatch, 2 = no commit record there;
-     * write: the CRC is stored big-endian into the commit record. */
+    /* zeroskip commits: commit = 1 (verify) / 2 (write) / 3 (the writer's
+     * CRCs, out of place): record i is the span of a commit record that
+     * starts right after it; out[i] receives the commit CRC (span +
+     * host-order trailer words); verify: status[i] 1 = matches the stored
+     * CRC, 0 = mismatch, 2 = no commit record there; write: the CRC is stored
+     * big-endian into the commit record; 3: out[] only (status 1 / 2 as the
+     * writer's), nothing stored into the image. */
     uint32_t commit;
     uint32_t *status;     /* may be NULL */
     /* commit mode: bytes of the image at base.  A span whose commit word

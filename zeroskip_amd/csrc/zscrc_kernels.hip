@@ -437,7 +437,8 @@ __device__ __forceinline__ void emit(const BatchDesc &d, const Item &it, uint32_
     const uint32_t crc = r ^ 0xffffffffu;
     if (d.commit == 2 && st == 0)
         gstore32(reinterpret_cast<const void *>(crc_at), __builtin_bswap32(crc));
-    const uint32_t status = st == 2 ? 2u : (d.commit == 2 || crc == stored ? 1u : 0u);
+    /* commit 3 (the writer's CRCs out of place): out[] only, image untouched */
+    const uint32_t status = st == 2 ? 2u : (d.commit >= 2 || crc == stored ? 1u : 0u);
     if (d.bad_count) {
         /* verdict mode: a clean commit writes nothing */
         if (status != 1) {
@@ -3251,7 +3252,7 @@ __global__ __launch_bounds__(256) void part_fold_kernel(FoldPair fp, const uint3
         const uint32_t crc = reg ^ 0xffffffffu;
         if (d.commit == 2 && nt)
             gstore32(reinterpret_cast<const void *>(crc_at), __builtin_bswap32(crc));
-        const uint32_t status = nt == 0 ? 2u : (d.commit == 2 || crc == stored ? 1u : 0u);
+        const uint32_t status = nt == 0 ? 2u : (d.commit >= 2 || crc == stored ? 1u : 0u);
         if (d.bad_count) {
             if (status != 1) {
                 const unsigned long long k = atomicAdd(d.bad_count, 1ull);
@@ -3574,5 +3575,33 @@ extern "C" int zs_launch_span_fold(const zs::SpanFold *f, const uint32_t *gtab, 
     uint32_t blocks = (f->w + zs::FWG - 1) / zs::FWG;
     blocks = blocks < 1 ? 1 : blocks > 256 ? 256 : blocks;
     hipLaunchKernelGGL(zs::span_fold_kernel, dim3(blocks), dim3(zs::FWG), 0, stream, *f, gtab);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+/* ------------------------------------------------ fill-commits descriptors */
+namespace zs {
+/* zscrc_zs_fill_commits sends each chunk's span descriptors as 32-bit
+ * (offset within the chunk, length) pairs -- 8 B per commit over PCIe
+ * instead of 16 -- and widens them here for the commit kernels. */
+__global__ __launch_bounds__(256) void widen_desc_kernel(const uint32_t *__restrict__ pairs, uint64_t *__restrict__ off,
+                                                         uint64_t *__restrict__ len, uint64_t n)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint2 p = reinterpret_cast<const uint2 *>(pairs)[i];
+        off[i] = p.x;
+        len[i] = p.y;
+    }
+}
+} /* namespace zs */
+
+extern "C" int zs_launch_widen_desc(const uint32_t *pairs, uint64_t *off, uint64_t *len, uint64_t n,
+                                    hipStream_t stream)
+{
+    if (n == 0)
+        return 0;
+    uint64_t blocks = (n + 255) / 256;
+    blocks = blocks > 2048 ? 2048 : blocks;
+    hipLaunchKernelGGL(zs::widen_desc_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, pairs, off, len, n);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }

@@ -23,7 +23,22 @@
  *     files are unlinked (:1555-1562);
  *   always: .zsdb rewritten with its CRC recomputed (zs_dotzsdb_update_end,
  *     src/zeroskip-dotzsdb.c:477-555: host-order fields hashed, :514-529),
- *     through a temporary file renamed over it.
+ *     through .zsdb.lock renamed over it.
+ *
+ * Locking: as zs_dotzsdb_update_begin (src/zeroskip-dotzsdb.c:376-471,
+ * file_lock_acquire, src/file-lock.c:128-131), .zsdb.lock is created with
+ * O_CREAT | O_EXCL before .zsdb is read or the directory listed, and held
+ * until the new .zsdb is renamed from it; a lock already held makes the call
+ * return ZSCRC_EBUSY at once (the reference retries with back-off).
+ *
+ * The packed file is written under a temporary name (".tmp" suffix: not a
+ * zeroskip file name) and renamed into place after the sources are unmapped,
+ * then the sources are unlinked -- except one whose name the output took.
+ * With a single finalised file zeroskip-<uuid>-<i>-<i> the output's name is
+ * the source's: the reference then truncates the source it is reading and
+ * unlinks the file it just wrote (src/zeroskip.c:1470-1497, survivable there
+ * only because the records were copied into its memtree first); here the
+ * rename replaces the source and nothing is lost.
  *
  * Records are listed by zscrc_zs_records (C: the record walk of
  * src/zeroskip-record.c:283-331 for active / finalised files, the pointer
@@ -33,6 +48,7 @@
  * no per-record language crossing on the repack path.
  */
 #include <dirent.h>
+#include <errno.h>
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -352,24 +368,37 @@ extern "C" int zscrc_zs_repack(const char *dbdir, unsigned flags, int threads, z
                 threads = std::min(threads, atoi(e));
     }
     const std::string dir(dbdir);
+    const std::string lock_path = dir + "/.zsdb.lock", dot_path = dir + "/.zsdb";
+    /* the update lock first (zs_dotzsdb_update_begin), held to the end */
+    int lockfd = open(lock_path.c_str(), O_WRONLY | O_CREAT | O_EXCL, 0644);
+    if (lockfd < 0)
+        return errno == EEXIST ? ZSCRC_EBUSY : ZSCRC_EINVAL;
+    auto unlock = [&](int code) {
+        if (lockfd >= 0) {
+            close(lockfd);
+            unlink(lock_path.c_str());
+            lockfd = -1;
+        }
+        return code;
+    };
     /* .zsdb: zs_dotzsdb_update_begin reads and checks it (:400-446) */
     uint8_t dot[DOTZSDB_SIZE];
     {
-        FILE *fp = fopen((dir + "/.zsdb").c_str(), "rb");
+        FILE *fp = fopen(dot_path.c_str(), "rb");
         if (!fp)
-            return ZSCRC_EINVAL;
+            return unlock(ZSCRC_EINVAL);
         const size_t got = fread(dot, 1, sizeof dot, fp);
         fclose(fp);
         uint32_t st = 0, cp = 0;
         if (got != sizeof dot || zscrc_zs_dotzsdb_crc(dot, sizeof dot, &st, &cp) != ZSCRC_OK || st != cp)
-            return ZSCRC_EINVAL;
+            return unlock(ZSCRC_EINVAL);
     }
     char uuidstr[37];
     memcpy(uuidstr, dot + 16, 36);
     uuidstr[36] = 0;
     uint8_t uuid[16];
     if (!parse_uuid(uuidstr, uuid))
-        return ZSCRC_EINVAL;
+        return unlock(ZSCRC_EINVAL);
     const uint64_t dot_off = be64(dot + 8);
     uint32_t curidx;
     memcpy(&curidx, dot + 53, 4);
@@ -378,7 +407,7 @@ extern "C" int zscrc_zs_repack(const char *dbdir, unsigned flags, int threads, z
     std::vector<DbFile> fin, pk;
     DIR *d = opendir(dbdir);
     if (!d)
-        return ZSCRC_EINVAL;
+        return unlock(ZSCRC_EINVAL);
     for (struct dirent *de; (de = readdir(d)) != nullptr;) {
         DbFile f;
         if (!parse_name(de->d_name, f) || strncmp(de->d_name + 9, uuidstr, UUID_CHARS) != 0)
@@ -490,6 +519,7 @@ extern "C" int zscrc_zs_repack(const char *dbdir, unsigned flags, int threads, z
     }
     const double t_merge = now_s();
 
+    std::string tmp_out;
     if (!rc && rep->branch) {
         uint32_t s = (uint32_t)src[0].s, e = (uint32_t)src[0].e;
         for (const auto &f : src) {
@@ -500,8 +530,9 @@ extern "C" int zscrc_zs_repack(const char *dbdir, unsigned flags, int threads, z
         rep->endidx = e;
         rep->files_merged = src.size();
         snprintf(rep->path, sizeof rep->path, "%s/zeroskip-%s-%u-%u", dbdir, uuidstr, s, e);
+        tmp_out = std::string(rep->path) + ".tmp";
         zscrc_packer *w = nullptr;
-        rc = zscrc_pack_open(&w, rep->path, uuid, s, e, 0, flags);
+        rc = zscrc_pack_open(&w, tmp_out.c_str(), uuid, s, e, 0, flags);
         for (size_t i = 0; !rc && i < all.size(); ++i)
             rc = zscrc_pack_add(w, all[i].k, all[i].kl, all[i].v, all[i].vl);
         if (w) {
@@ -516,27 +547,35 @@ extern "C" int zscrc_zs_repack(const char *dbdir, unsigned flags, int threads, z
     for (auto &f : src)
         if (f.img)
             munmap(const_cast<uint8_t *>(f.img), f.size);
-    /* the merged sources go (src/zeroskip.c:1489-1497, :1555-1562) */
+    /* the output into place (replacing a source of the same name), then
+     * the merged sources go (src/zeroskip.c:1489-1497, :1555-1562) -- never
+     * the output itself */
+    if (!rc && rep->branch && rename(tmp_out.c_str(), rep->path) != 0)
+        rc = ZSCRC_EINVAL;
+    if (rc && !tmp_out.empty())
+        unlink(tmp_out.c_str());
     if (!rc)
-        for (auto &f : src)
-            unlink((dir + "/" + f.name).c_str());
-    /* zs_dotzsdb_update_end: .zsdb rewritten, CRC recomputed, via rename */
+        for (auto &f : src) {
+            const std::string path = dir + "/" + f.name;
+            if (path != rep->path)
+                unlink(path.c_str());
+        }
+    /* zs_dotzsdb_update_end: .zsdb rewritten into the held lock file, CRC
+     * recomputed, renamed over .zsdb (file_lock_rename) */
     if (!rc) {
         uint8_t out[DOTZSDB_SIZE];
         zscrc_zs_dotzsdb_build(dot_off, uuidstr, curidx, out);
-        const std::string tmp = dir + "/.zsdb.lock", fin_path = dir + "/.zsdb";
-        const int fd = open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
-        bool ok = fd >= 0 && write(fd, out, sizeof out) == (ssize_t)sizeof out;
-        if (fd >= 0) {
-            if (flags & ZSCRC_PACK_FSYNC)
-                ok = ok && fsync(fd) == 0;
-            close(fd);
-        }
-        ok = ok && rename(tmp.c_str(), fin_path.c_str()) == 0;
+        bool ok = write(lockfd, out, sizeof out) == (ssize_t)sizeof out;
+        if (flags & ZSCRC_PACK_FSYNC)
+            ok = ok && fsync(lockfd) == 0;
+        ok = ok && rename(lock_path.c_str(), dot_path.c_str()) == 0;
+        close(lockfd);
+        lockfd = -1;
         if (!ok)
             rc = ZSCRC_EINVAL;
         rep->dotzsdb_crc = be64(out + 53) & 0xFFFFFFFFull;
     }
+    unlock(rc);
     rep->list_s = t_list - t_open;
     rep->merge_s = t_merge - t_list;
     rep->write_s = t_write - t_merge;

@@ -268,6 +268,14 @@ int zscrc_device_write_commits_bounded(void *d_image, uint64_t image_size, const
                                          stream, 1, max_len);
 }
 
+int zscrc_device_commit_crcs_bounded(const void *d_image, uint64_t image_size, const uint64_t *d_span_off,
+                                     const uint64_t *d_span_len, size_t n, uint64_t max_len, uint32_t *d_crc,
+                                     uint32_t *d_status, void *stream)
+{
+    return zscrc_internal_verify_commits(d_image, image_size, d_span_off, d_span_len, nullptr, d_crc, d_status, n,
+                                         stream, 2, max_len);
+}
+
 int zscrc_device_write_commits(void *d_image, uint64_t image_size, const uint64_t *d_span_off,
                                const uint64_t *d_span_len, size_t n, uint32_t *d_crc, uint32_t *d_status,
                                void *stream)

@@ -157,6 +157,57 @@ def write_commits(d_image: torch.Tensor, span_off: torch.Tensor, span_len: torch
     return (crc, st) if status else crc
 
 
+def commit_crcs(d_image: torch.Tensor, span_off: torch.Tensor, span_len: torch.Tensor,
+                max_len: int | None = None, status: bool = False):
+    """The writer's commit CRCs out of place (zscrc_device_commit_crcs_bounded):
+    an int32 tensor, crc[i] = what zscrc_device_write_commits would store for
+    span i; the image is only read.  status=True: (crc, status), 1 a commit
+    record is there, 2 none."""
+    n = span_off.numel()
+    size = d_image.numel() * d_image.element_size()
+    crc = torch.empty(n, dtype=torch.int32, device=d_image.device)
+    st = torch.empty(n, dtype=torch.int32, device=d_image.device) if status else None
+    with torch.cuda.device(d_image.device):
+        check(lib().zscrc_device_commit_crcs_bounded(
+            d_image.data_ptr(), size, span_off.data_ptr(), span_len.data_ptr(), n,
+            LEN_UNBOUNDED if max_len is None else max_len, crc.data_ptr(), None if st is None else st.data_ptr(),
+            torch.cuda.current_stream(d_image.device).cuda_stream), "zscrc_device_commit_crcs_bounded")
+    return (crc, st) if status else crc
+
+
+class FillReport(ctypes.Structure):
+    """zscrc_fill_report (include/zscrc.h)."""
+    _fields_ = [("commits", ctypes.c_uint64), ("no_record", ctypes.c_uint64), ("long_commits", ctypes.c_uint64),
+                ("bytes", ctypes.c_uint64), ("desc_bytes", ctypes.c_uint64), ("chunks", ctypes.c_uint64),
+                ("staged", ctypes.c_int32), ("threads", ctypes.c_int32), ("h2d_s", ctypes.c_double),
+                ("total_s", ctypes.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+def fill_commits(image, span_off, span_len, max_len: int | None = None, threads: int = 0) -> dict:
+    """The commit writer for a HOST image (zscrc_zs_fill_commits): every
+    commit CRC computed on the current GPU and stored into `image` in place
+    (a writable uint8 numpy array or CPU tensor; pinned memory is copied
+    directly, pageable memory through pinned staging).  span_off / span_len:
+    sorted, disjoint spans (uint64 numpy arrays or CPU tensors)."""
+    if isinstance(image, torch.Tensor):
+        assert not image.is_cuda and image.is_contiguous()
+        ptr, size = image.data_ptr(), image.numel() * image.element_size()
+    else:
+        assert image.flags.c_contiguous and image.flags.writeable
+        ptr, size = image.ctypes.data, image.nbytes
+    o = np.ascontiguousarray(span_off.numpy() if isinstance(span_off, torch.Tensor) else span_off, dtype=np.uint64)
+    ln = np.ascontiguousarray(span_len.numpy() if isinstance(span_len, torch.Tensor) else span_len, dtype=np.uint64)
+    assert o.shape == ln.shape
+    rep = FillReport()
+    check(lib().zscrc_zs_fill_commits(ptr, size, o.ctypes.data, ln.ctypes.data, len(o),
+                                      LEN_UNBOUNDED if max_len is None else max_len, threads, ctypes.byref(rep)),
+          "zscrc_zs_fill_commits")
+    return rep.as_dict()
+
+
 class FilesReport(ctypes.Structure):
     """zscrc_files_report (include/zscrc.h)."""
     _fields_ = [("files", ctypes.c_uint64), ("commits", ctypes.c_uint64), ("bytes", ctypes.c_uint64),
