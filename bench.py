@@ -502,6 +502,26 @@ def _timed(fn, reps: int, stream) -> float:
     return float(np.median(ts))
 
 
+def _timed_ab(fns, reps: int, stream, rounds: int = 3) -> list:
+    """ms per call of each fn, measured as _timed does but interleaved: each
+    round times every fn once (reps calls back to back between two events);
+    the median over rounds."""
+    for fn in fns:
+        fn()
+    torch.cuda.synchronize()
+    ts = [[] for _ in fns]
+    for _ in range(rounds):
+        for k, fn in enumerate(fns):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            for _ in range(reps):
+                fn()
+            b.record(stream)
+            torch.cuda.synchronize()
+            ts[k].append(a.elapsed_time(b) / reps)
+    return [float(np.median(t)) for t in ts]
+
+
 def run_config4(args, world, rank, dev, stream):
     """zsbench writeseqtxn replay (10 M pairs as byte-exact log files).  One
     step = the verdict of every commit on the GPU
@@ -573,13 +593,23 @@ def run_config4(args, world, rank, dev, stream):
     img_nb = zg.log_files(uuid, 0, nf_nb, ppf_nb, 0, False, gen, dev, batched=False)
     o_nb, l_nb = zg.log_spans(nf_nb, ppf_nb, False, False, dev)
     nbo = (torch.empty(1, dtype=torch.int64, device=dev), torch.empty(64, dtype=torch.int64, device=dev))
-    nb_ms = _timed(lambda: zsfile.verify_commits_verdict(img_nb.view(-1), o_nb, l_nb, out=nbo), 6, stream)
-    assert int(nbo[0].item()) == 0
+    # the walk knows the commits' length range: classes outside it get no
+    # launch (zscrc_device_verify_commits_verdict_range)
+    nb_lo, nb_hi = int(l_nb.min().item()), int(l_nb.max().item())
     nb_arr = {}
+
+    def nb_verdict():
+        zsfile.verify_commits_verdict(img_nb.view(-1), o_nb, l_nb, out=nbo, min_len=nb_lo, max_len=nb_hi)
+
+    def nb_verdict_unranged():
+        zsfile.verify_commits_verdict(img_nb.view(-1), o_nb, l_nb, out=nbo)
 
     def nb_arrays():
         nb_arr["crc"], nb_arr["st"] = zsfile.verify_commits(img_nb.view(-1), o_nb, l_nb)
-    nb_arrays_ms = _timed(nb_arrays, 6, stream)
+    # interleaved, so no form sees a different power / clock state
+    nb_ms, nb_unranged_ms, nb_arrays_ms = _timed_ab([nb_verdict, nb_verdict_unranged, nb_arrays], 6, stream)
+    nb_verdict()
+    assert int(nbo[0].item()) == 0
     assert bool((nb_arr["st"] == 1).all())
     nb_bytes = int(l_nb.sum().item()) + 24 * nf_nb
     # the checker on the NOTBATCHED image: every ~2 MiB commit against the oracle
@@ -738,7 +768,11 @@ def run_config4(args, world, rank, dev, stream):
                     notbatched={"files": nf_nb, "commits": nf_nb, "verify_ms": round(nb_ms, 4),
                                 "GBs": round(nb_bytes / (nb_ms * 1e-3) / 1e9, 1),
                                 "frac": round(nb_bytes / (nb_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                                "arrays_ms": round(nb_arrays_ms, 4)},
+                                "verify_unranged_ms": round(nb_unranged_ms, 4),
+                                "arrays_ms": round(nb_arrays_ms, 4),
+                                "note": "verify_ms: the verdict with the walk's length range (min/max span), "
+                                        "unranged: without it, arrays: per-commit crc + status; the three "
+                                        "timed interleaved"},
                     e2e=e2e, gen_s=round(t_gen, 2))
     if rank == 0 and world == 1 and not args.no_cpu:
         k = 200_000

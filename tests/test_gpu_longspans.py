@@ -187,3 +187,27 @@ def test_segment_plans(gpu, db, nseg, monkeypatch):
     d = torch.from_numpy(h).cuda()
     nbad, bad = _with_opt(0, lambda: zsfile.verify_commits_verdict(d, o, ln))
     assert int(nbad.item()) == len(hit) and set(bad[:len(hit)].cpu().tolist()) == hit
+
+
+@pytest.mark.parametrize("opt", [0, MULTI_CLASSIFY], ids=["single-classify", "multi-classify"])
+def test_verdict_range_long_only(gpu, db, opt):
+    """zscrc_device_verify_commits_verdict_range with the walk's range: only
+    the class-3 commits (every length > g16_max), so classes 0-2 get no
+    launch and the classify counts commits outside the image itself -- the
+    verdict equals the unranged one, corruptions and an out-of-image commit
+    included."""
+    host, offs, lens, commits = db
+    long_i = [i for i in range(len(commits)) if lens[i] > (1 << 20)]
+    h = host.copy()
+    a, b = long_i[0], long_i[-1]
+    h[offs[a] + 7] ^= 0x20
+    h[commits[b]["commit_off"] + (20 if lens[b] > (1 << 24) else 4)] ^= 0x01
+    o_np = np.concatenate([offs[long_i], [len(h) - (2 << 20)]])     # this one's record is past the end
+    l_np = np.concatenate([lens[long_i], [(2 << 20) + 16]])
+    d = torch.from_numpy(h).cuda()
+    o, ln = torch.from_numpy(o_np).cuda(), torch.from_numpy(l_np).cuda()
+    want = {long_i.index(a), long_i.index(b), len(long_i)}
+    for lo in (0, int(l_np.min())):
+        nbad, bad = _with_opt(opt, lambda: zsfile.verify_commits_verdict(d, o, ln, max_len=int(l_np.max()),
+                                                                         min_len=lo))
+        assert int(nbad.item()) == len(want) and set(bad[:len(want)].cpu().tolist()) == want, lo

@@ -532,7 +532,8 @@ def test_fixed_multi(gpu, stride, length, n, k):
         assert np.array_equal(u32(raws[b]), ref)
 
 
-@pytest.mark.parametrize("shift,n", [(0, 4099), (16, 1000), (48, 128), (3, 777), (0, 1)])
+@pytest.mark.parametrize("shift,n", [(0, 4099), (16, 1000), (48, 128), (3, 777), (0, 1), (0, 1 << 20),
+                                     (0, 128 * 4 * 37 + 129)])
 def test_fixed_multi_64_offsets(gpu, shift, n):
     """64-byte record batches at base offsets: 16-byte aligned bases take the
     coalesced chunk kernel (multi64_kernel; ragged last chunks), others the
@@ -541,7 +542,7 @@ def test_fixed_multi_64_offsets(gpu, shift, n):
     big = to_dev(rand_bytes(k * (64 * n + 64) + 64, n + shift), gpu)
     bufs = [big[shift + b * (64 * n + 64):] for b in range(k)]
     hosts = [b.cpu().numpy() for b in bufs]
-    for opt in (0, 2):
+    for opt in (0, 2, 1 << 21):     # multi64_kernel, the piece walk, multi64d_kernel (staged results)
         lib().zscrc_set_opt(opt)
         try:
             outs = zd.crc_fixed_multi(bufs, 64, 64, n, seed=0xC0C0)

@@ -86,6 +86,8 @@ SIGNATURES = {
     "zscrc_release_cache": (None, []),
     "zscrc_device_commit_crcs_bounded": (_int, [_vp, _u64, _vp, _vp, _sz, _u64, _vp, _vp, _vp]),
     "zscrc_zs_fill_commits": (_int, [_vp, _u64, _vp, _vp, _sz, _u64, _int, _vp]),
+    "zscrc_device_verify_commits_verdict_range": (_int, [_vp, _u64, _vp, _vp, _vp, _sz, _u64, _u64, _vp, _vp, _sz,
+                                                         _vp]),
 }
 ABI_VERSION = 3  # include/zscrc.h ZSCRC_ABI_VERSION
 

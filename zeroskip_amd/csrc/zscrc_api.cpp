@@ -396,9 +396,17 @@ int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s, int depth_hi
  * Classes 2-3 with fewer records than two per team are cut into equal parts
  * (unit ~ class bytes / items wanted, plan_kernel) and a fold kernel combines
  * each record's part registers. */
-int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1, uint64_t g16);
+int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1, uint64_t g16, uint64_t min_len,
+                          uint64_t max_len);
 
-int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t max_len = ZSCRC_LEN_UNBOUNDED)
+/* [min_len, max_len]: a range the caller knows every length lies in (the
+ * host walk that found the spans does); classes outside it get no launch.
+ * Results never depend on the range: a record outside it is still
+ * classified and handled by its class's kernel, only the launches the
+ * range rules out are skipped -- so a wrong range may leave such records
+ * unprocessed, which is why the range must hold. */
+int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t max_len = ZSCRC_LEN_UNBOUNDED,
+                   uint64_t min_len = 0)
 {
     const uint64_t g1 = g_g1_max, g16 = g_g16_max;
     {
@@ -431,7 +439,7 @@ int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t max_len =
     std::lock_guard<std::recursive_mutex> lk(c->mu);
     int rc = scratch_acquire(c, s);
     if (!rc)
-        rc = launch_classes_locked(c, d, s, g1, g16);
+        rc = launch_classes_locked(c, d, s, g1, g16, min_len, max_len);
     const int rc2 = scratch_release(c, s);
     return rc ? rc : rc2;
 }
@@ -439,7 +447,8 @@ int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t max_len =
 /* batches up to this many records classify in one single-block launch */
 constexpr uint64_t SMALL_CLASSIFY = 16384;
 
-int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1, uint64_t g16)
+int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1, uint64_t g16, uint64_t min_len,
+                          uint64_t max_len)
 {
     const uint64_t n = d.n;
     uint64_t b1 = g16 < 8191 ? g16 : 8191;
@@ -529,6 +538,13 @@ int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1
     cl.commit = d.commit != 0;
     cl.img_size = d.img_size;
     cl.zero_count = d.bad_count;
+    /* a verdict batch whose range starts above class 0: no class-0 launch,
+     * the scatter counts out-of-image commits into the verdict */
+    if (d.commit && d.bad_count && min_len > g1) {
+        cl.verdict_nocommit = 1;
+        cl.bad_idx = d.bad_idx;
+        cl.bad_cap = d.bad_cap;
+    }
     {
         /* class 0 goes to burst_kernel (walk 9, the default), which walks
          * the caller's arrays and skips longer records: no class-0 list */
@@ -565,7 +581,14 @@ int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1
      * buffers are per class); the folds last */
     zs::BatchDesc fold[2];
     int nfold = 0;
+    /* class k holds lengths in (lower[k], upper[k]]; out-of-image commits
+     * are class 0 (length 0) */
+    const uint64_t lower[4] = {0, g1, b1, b2}, upper[4] = {g1, b1, b2, ~0ull};
     for (const int k : {3, 0, 1, 2}) {
+        const bool empty = (k > 0 && upper[k] < min_len) || (k == 0 && min_len > g1 && (!d.commit || cl.verdict_nocommit)) ||
+                           (k > 0 && lower[k] >= max_len);
+        if (empty)
+            continue; /* the caller's range rules this class out: no launch */
         zs::BatchDesc dk = d;
         dk.klass = (uint32_t)k;
         if (k == 0 && cl.direct_ok)
@@ -1139,6 +1162,17 @@ int zscrc_device_verify_commits_verdict(const void *d_image, uint64_t image_size
                                         uint64_t max_len, uint64_t *d_nbad, uint64_t *d_bad, size_t cap,
                                         void *stream)
 {
+    return zscrc_device_verify_commits_verdict_range(d_image, image_size, d_span_off, d_span_len, d_seed, n, 0,
+                                                     max_len, d_nbad, d_bad, cap, stream);
+}
+
+int zscrc_device_verify_commits_verdict_range(const void *d_image, uint64_t image_size, const uint64_t *d_span_off,
+                                              const uint64_t *d_span_len, const uint32_t *d_seed, size_t n,
+                                              uint64_t min_len, uint64_t max_len, uint64_t *d_nbad, uint64_t *d_bad,
+                                              size_t cap, void *stream)
+{
+    if (min_len > max_len)
+        return ZSCRC_EINVAL;
     if (!d_nbad || (cap && !d_bad) || (n && (!d_image || !d_span_off || !d_span_len)))
         return ZSCRC_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1168,7 +1202,7 @@ int zscrc_device_verify_commits_verdict(const void *d_image, uint64_t image_size
     d.bad_count = reinterpret_cast<unsigned long long *>(d_nbad);
     d.bad_idx = d_bad;
     d.bad_cap = cap;
-    return launch_classes(c, d, s, max_len);
+    return launch_classes(c, d, s, max_len, min_len);
 }
 
 const char *zscrc_last_error(void) { return t_err; }

@@ -271,7 +271,7 @@ struct Ext {
     uint64_t ncommit = 0;
     uint64_t pos = 0;               /* its commits: [pos, pos + ncommit) of the descriptor arrays */
     bool placed = false;            /* written to the pinned arrays by its walker */
-    uint64_t max_len = 0;
+    uint64_t max_len = 0, min_len = ~0ull;
     uint32_t raw = 0;               /* EXT_PIECE: raw register of its bytes */
 };
 
@@ -338,8 +338,10 @@ void walk_ext(const uint8_t *img, uint64_t size, int kind, FileInfo &fi, Ext &x)
     x.off.resize(n);
     x.len.resize(n);
     x.ncommit = n;
-    for (size_t i = 0; i < n; ++i)
+    for (size_t i = 0; i < n; ++i) {
         x.max_len = std::max(x.max_len, x.len[i]);
+        x.min_len = std::min(x.min_len, x.len[i]);
+    }
 }
 
 /* The walker's spans -> descriptor arrays at pos (device offsets). */
@@ -455,7 +457,7 @@ int run_group(Call &C, Cache &cache, std::vector<Ext *> &G, int threads)
     std::atomic<int64_t> free_upto{NSLOT};
     std::atomic<size_t> walks_left{ng};
     std::atomic<uint64_t> dpos{0};          /* descriptor bump index */
-    std::atomic<uint64_t> max_len{0};
+    std::atomic<uint64_t> max_len{0}, min_len{~0ull};
     const uint64_t dcap = cache.dcap;
 
     auto worker = [&]() {
@@ -470,6 +472,9 @@ int run_group(Call &C, Cache &cache, std::vector<Ext *> &G, int threads)
                          C.fi[x.file], x);
                 uint64_t m = max_len.load(std::memory_order_relaxed);
                 while (x.max_len > m && !max_len.compare_exchange_weak(m, x.max_len))
+                    ;
+                m = min_len.load(std::memory_order_relaxed);
+                while (x.min_len < m && !min_len.compare_exchange_weak(m, x.min_len))
                     ;
                 /* descriptors straight into the pinned arrays (any order:
                  * results go back by position) */
@@ -623,8 +628,10 @@ int run_group(Call &C, Cache &cache, std::vector<Ext *> &G, int threads)
         (reinterpret_cast<uintptr_t>(draw + pieces.size()) + 7) & ~uintptr_t(7));
     const uint64_t vcap = std::min<uint64_t>(VCAP, ncommit);
     if (!rc && ncommit) {
-        rc = zscrc_device_verify_commits_verdict(cache.dimg, total, doff, dlen, nullptr, ncommit, max_len.load(),
-                                                 d_nbad, d_nbad + 1, vcap, ks);
+        /* the walks' length range: classes outside it get no launch */
+        rc = zscrc_device_verify_commits_verdict_range(cache.dimg, total, doff, dlen, nullptr, ncommit,
+                                                       std::min(min_len.load(), max_len.load()), max_len.load(),
+                                                       d_nbad, d_nbad + 1, vcap, ks);
         if (!rc && hipMemcpyAsync(cache.h_bad, d_nbad, 8 * (vcap + 1), hipMemcpyDeviceToHost, ks) != hipSuccess)
             rc = ZSCRC_EHIP;
     }

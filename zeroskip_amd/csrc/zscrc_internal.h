@@ -78,7 +78,10 @@ struct BatchDesc {
                              (SplitPlan::seg), 262144 = diagnostic: multi64_kernel
                              stores its results into one L2-resident window (wrong results),
                              524288 = small variable batches classify in two multi-block
-                             passes and plan launches instead of one single-block launch */
+                             passes and plan launches instead of one single-block launch,
+                             1 << 20 = diagnostic: multi64 without hashing (the load + store
+                             shape alone, wrong results), 1 << 21 = multi64d_kernel (results
+                             staged in LDS per group of chunks, one contiguous write) */
     uint32_t *part_out;
     /* commit verdict mode (bad_count != NULL): no per-record out / status;
      * every commit whose status is not 1 is counted in *bad_count and its
@@ -240,6 +243,12 @@ struct Classify {
     /* commit verdict batches: the bad-commit counter, zeroed by the first
      * classify launch (the class kernels run after it on the stream) */
     unsigned long long *zero_count;
+    /* verdict batches whose class 0 gets no launch (the caller's length
+     * range starts above it): the scatter counts every commit outside the
+     * image into zero_count / bad_idx itself */
+    int verdict_nocommit;
+    uint64_t *bad_idx;
+    uint64_t bad_cap;
 };
 
 /* K fixed-stride batches of one launch (zscrc_device_fixed_multi): batch b

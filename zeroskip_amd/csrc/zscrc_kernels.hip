@@ -1796,14 +1796,22 @@ __global__ __launch_bounds__(WG) void multi64_kernel(BatchDesc d, MultiBatch m, 
             xpose16(reinterpret_cast<uint32_t (&)[16]>(w[16 * q]));
             r[q] = w[16 * q] ^ R0; /* register before word k, XOR word k */
         }
+        if (d.opt & (1u << 20)) { /* diagnostic: the load + store shape alone (wrong results) */
 #pragma unroll
-        for (int k = 1; k < 16; ++k)
+            for (int k = 1; k < 16; ++k)
+#pragma unroll
+                for (int q = 0; q < K; ++q)
+                    r[q] ^= w[16 * q + k];
+        } else {
+#pragma unroll
+            for (int k = 1; k < 16; ++k)
+#pragma unroll
+                for (int q = 0; q < K; ++q)
+                    r[q] = m4x<ZS_MULTI_B3>(L, r[q], w[16 * q + k], c_lo, c_hi);
 #pragma unroll
             for (int q = 0; q < K; ++q)
-                r[q] = m4x<ZS_MULTI_B3>(L, r[q], w[16 * q + k], c_lo, c_hi);
-#pragma unroll
-        for (int q = 0; q < K; ++q)
-            r[q] = m4(L, r[q], c_lo, c_hi);
+                r[q] = m4(L, r[q], c_lo, c_hi);
+        }
         uint32_t *out = m.out[p.b];
         uint64_t r0 = p.k * RPC + (uint64_t)lane;
         if (d.opt & 262144) /* diagnostic: results into one L2-resident 64 KiB window (wrong results) */
@@ -1823,6 +1831,148 @@ __global__ __launch_bounds__(WG) void multi64_kernel(BatchDesc d, MultiBatch m, 
         advance(pl);
         m64_issue<K>(m, n, pl, voff, dummy, b0);
         hash(b1, ph);
+        advance(ph);
+    }
+}
+
+/*
+ * multi64d_kernel (tuning bit 1 << 21, an A/B form of multi64_kernel<2>):
+ * the results written in bigger, later bursts.  A wave takes GROUP adjacent
+ * chunks at a time (GROUP x 128 records), keeps their results in its 2 KiB of
+ * LDS (the 32 KiB left beside the 128 KiB of slice tables) and writes them as
+ * one contiguous 2 KiB block after the group's reads -- eight coalesced
+ * 256-byte stores back to back instead of two after every chunk.  Config 2's
+ * counters put its stall on load latency under the mix of reads and result
+ * writes; this tests whether fewer, larger write bursts shorten
+ * it.  Tuning bit 1 << 20 (both forms, diagnostic): no hashing -- each result
+ * is the XOR of its record's words (wrong results), the load + store shape
+ * alone.
+ */
+constexpr int M64_GROUP = 4;
+
+template <int K>
+__device__ __forceinline__ void m64d_issue(const MultiBatch &m, uint64_t n, uint64_t b, uint64_t k, bool ok,
+                                           uint32_t voff, uintptr_t dummy, uint32_t (&w)[16 * K])
+{
+    constexpr uint64_t CHUNK = 4096ull * K;
+    const uintptr_t base = ok ? reinterpret_cast<uintptr_t>(m.base[b]) : dummy;
+    const uintptr_t sb = uni64(base + (ok ? k * CHUNK : 0));
+    const uint64_t room = ok ? base + n * 64 - 16 - sb : 0;
+    const uint32_t lim = __builtin_amdgcn_readfirstlane((uint32_t)(room < 0xffffffffull ? room : 0xffffffffull));
+#pragma unroll
+    for (int i = 0; i < 4 * K; ++i) {
+        const uint32_t o = voff + 1024u * (uint32_t)i;
+        const u32x4 v = __builtin_nontemporal_load((g4p)(sb + (o < lim ? o : lim)));
+        w[4 * i + 0] = v.x;
+        w[4 * i + 1] = v.y;
+        w[4 * i + 2] = v.z;
+        w[4 * i + 3] = v.w;
+    }
+}
+
+__global__ __launch_bounds__(WG) void multi64d_kernel(BatchDesc d, MultiBatch m, const uint32_t *__restrict__ gtab)
+{
+    constexpr int K = 2;
+    constexpr uint64_t RPC = 64ull * K;                    /* records per chunk */
+    constexpr uint32_t SW = (uint32_t)(M64_GROUP * RPC);   /* staged results per wave */
+    __shared__ __attribute__((aligned(16))) char L[OFF_U + 4 * SW * WAVES];
+    const uint64_t n = d.n;
+    const uint64_t cpb = (n + RPC - 1) / RPC;              /* chunks per batch */
+    const uint64_t gpb = (cpb + M64_GROUP - 1) / M64_GROUP; /* groups per batch */
+    const uint64_t items = gpb * m.nb;
+    const uint64_t wave = uni64((uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6));
+    const uint64_t nw = (uint64_t)gridDim.x * WAVES;
+    if ((uint64_t)blockIdx.x * WAVES >= items)
+        return;
+    fill_lds<1>(L, gtab);
+    __syncthreads();
+    const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+    const uint32_t c_lo = (uint32_t)(lane & 31) << 2;
+    const uint32_t c_hi = c_lo | 0x10000u;
+    const uint32_t voff = 64u * (uint32_t)c + 16u * (uint32_t)g;
+    const uintptr_t dummy = reinterpret_cast<uintptr_t>(gtab);
+    const uint32_t R0 = d.fixed_seed ^ d.xor_io;
+    const bool nohash = (d.opt & (1u << 20)) != 0;
+    uint32_t *S = reinterpret_cast<uint32_t *>(L + OFF_U) + SW * (threadIdx.x >> 6);
+    const uint64_t step_b = nw / gpb, step_g = nw - step_b * gpb;
+    /* position: batch b, group q, chunk j of the group */
+    struct Pos {
+        uint64_t b, q;
+        int j;
+    };
+    auto advance = [&](Pos &p) {
+        if (++p.j < M64_GROUP)
+            return;
+        p.j = 0;
+        p.q += step_g;
+        p.b += step_b;
+        if (p.q >= gpb) {
+            p.q -= gpb;
+            ++p.b;
+        }
+    };
+    auto chunk_ok = [&](const Pos &p) { return p.b < m.nb && p.q * M64_GROUP + p.j < cpb; };
+    uint32_t b0[16 * K], b1[16 * K];
+    Pos ph, pl;
+    ph.b = wave / gpb;
+    ph.q = wave - ph.b * gpb;
+    ph.j = 0;
+    pl = ph;
+    m64d_issue<K>(m, n, pl.b, pl.q * M64_GROUP + pl.j, chunk_ok(pl), voff, dummy, b0);
+    auto hash = [&](uint32_t (&w)[16 * K], const Pos &p) {
+        uint32_t r[K];
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            xpose16(reinterpret_cast<uint32_t (&)[16]>(w[16 * q]));
+            r[q] = w[16 * q] ^ R0;
+        }
+        if (nohash) {
+#pragma unroll
+            for (int k = 1; k < 16; ++k)
+#pragma unroll
+                for (int q = 0; q < K; ++q)
+                    r[q] ^= w[16 * q + k];
+        } else {
+#pragma unroll
+            for (int k = 1; k < 16; ++k)
+#pragma unroll
+                for (int q = 0; q < K; ++q)
+                    r[q] = m4x<ZS_MULTI_B3>(L, r[q], w[16 * q + k], c_lo, c_hi);
+#pragma unroll
+            for (int q = 0; q < K; ++q)
+                r[q] = m4(L, r[q], c_lo, c_hi);
+        }
+#pragma unroll
+        for (int q = 0; q < K; ++q)
+            S[RPC * p.j + 64 * q + lane] = r[q] ^ d.xor_io;
+        if (p.j == M64_GROUP - 1 || p.q * M64_GROUP + p.j + 1 >= cpb) {
+            /* the group's results: one contiguous block, written after its reads */
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            uint32_t *out = m.out[p.b];
+            const uint64_t r0 = p.q * M64_GROUP * RPC;
+#pragma unroll
+            for (uint32_t i = 0; i < SW / 64; ++i) {
+                const uint64_t at = r0 + 64 * i + (uint64_t)lane;
+                if (at < n)
+                    out[at] = S[64 * i + lane];
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    };
+    while (ph.b < m.nb) {
+        advance(pl);
+        m64d_issue<K>(m, n, pl.b, pl.q * M64_GROUP + pl.j, chunk_ok(pl), voff, dummy, b1);
+        if (chunk_ok(ph))
+            hash(b0, ph);
+        advance(ph);
+        if (ph.b >= m.nb)
+            break;
+        advance(pl);
+        m64d_issue<K>(m, n, pl.b, pl.q * M64_GROUP + pl.j, chunk_ok(pl), voff, dummy, b0);
+        if (chunk_ok(ph))
+            hash(b1, ph);
         advance(ph);
     }
 }
@@ -2782,10 +2932,15 @@ __device__ __forceinline__ void classify_scatter(const Classify &c, const uint32
             if (c.commit && !commit_fits(c.img_size, off, len)) {
                 off = NO_COMMIT_OFF;
                 len = 0;
+                if (c.verdict_nocommit) { /* no class-0 launch: the verdict here */
+                    const unsigned long long k = atomicAdd(c.zero_count, 1ull);
+                    if (k < c.bad_cap)
+                        c.bad_idx[k] = rec;
+                }
             }
             cls = class_of(c, len);
-            if (cls == 0 && c.direct_ok)
-                cls = -1; /* the class-0 kernel reads the caller's arrays */
+            if (cls == 0 && (c.direct_ok || c.verdict_nocommit))
+                cls = -1; /* the class-0 kernel reads the caller's arrays / has no launch */
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -2834,7 +2989,7 @@ __device__ void classify_single(const Classify &c, uint32_t *cnt, const unsigned
         c.bytes[threadIdx.x] = bsum[threadIdx.x];
     }
     __syncthreads();
-    if (!(c.direct_ok && cnt[0] == c.n))
+    if (!(c.direct_ok && cnt[0] == c.n) || c.verdict_nocommit)
         classify_scatter(c, slot, pos, r0, r1);
     __threadfence();
     __syncthreads();
@@ -2846,9 +3001,11 @@ __device__ void classify_single(const Classify &c, uint32_t *cnt, const unsigned
 __global__ __launch_bounds__(CWG) void classify_kernel(Classify c)
 {
     __shared__ uint32_t cnt[4], slot[4], pos[4];
-    if (c.zero_count && c.pass == 0 && blockIdx.x == 0 && threadIdx.x == 0)
+    if (c.zero_count && c.pass == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
         *c.zero_count = 0ull;
-    if (c.pass == 1 && c.direct_ok && ((const volatile uint32_t *)c.count)[0] == c.n)
+        __threadfence(); /* before the scatter's verdict atomics (single-block classify) */
+    }
+    if (c.pass == 1 && c.direct_ok && !c.verdict_nocommit && ((const volatile uint32_t *)c.count)[0] == c.n)
         return; /* one class: its kernel reads the caller's arrays directly */
     const uint64_t per = (c.n + gridDim.x - 1) / gridDim.x;
     const uint64_t r0 = (uint64_t)blockIdx.x * per;
@@ -3544,7 +3701,9 @@ extern "C" int zs_launch_multi(const zs::BatchDesc *d, const zs::MultiBatch *m, 
     bool packed64 = d->fixed_len == 64 && d->stride == 64 && !(d->opt & 2);
     for (uint32_t b = 0; b < m->nb && packed64; ++b)
         packed64 = (reinterpret_cast<uintptr_t>(m->base[b]) & 15) == 0;
-    if (packed64) /* two chains per lane (three measured slower: VGPR spills) */
+    if (packed64 && (d->opt & (1u << 21))) /* A/B: results staged per group of chunks */
+        hipLaunchKernelGGL(zs::multi64d_kernel, dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
+    else if (packed64) /* two chains per lane (three measured slower: VGPR spills) */
         hipLaunchKernelGGL(zs::multi64_kernel<2>, dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
     else
         hipLaunchKernelGGL(zs::multi_kernel, dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);

@@ -114,11 +114,13 @@ def verify_commits(d_image: torch.Tensor, span_off: torch.Tensor, span_len: torc
 
 def verify_commits_verdict(d_image: torch.Tensor, span_off: torch.Tensor, span_len: torch.Tensor,
                            seed: torch.Tensor | None = None, max_len: int | None = None, cap: int = 4096,
-                           out: tuple | None = None):
+                           out: tuple | None = None, min_len: int = 0):
     """Device verdict (zscrc_device_verify_commits_verdict): (nbad, bad)
     int64 device tensors -- nbad[0] = commits that do not verify, bad[:min(
     nbad, cap)] their indices in no particular order.  No per-commit output.
-    `out`: preallocated (nbad, bad) tensors to reuse."""
+    `out`: preallocated (nbad, bad) tensors to reuse.  min_len / max_len: a
+    range every span length lies in (zscrc_device_verify_commits_verdict_range:
+    classes outside it get no launch)."""
     n = span_off.numel()
     size = d_image.numel() * d_image.element_size()
     dev = d_image.device
@@ -127,11 +129,11 @@ def verify_commits_verdict(d_image: torch.Tensor, span_off: torch.Tensor, span_l
     nbad, bad = out
     assert seed is None or (seed.numel() == n and seed.dtype == torch.int32)
     with torch.cuda.device(dev):
-        check(lib().zscrc_device_verify_commits_verdict(
+        check(lib().zscrc_device_verify_commits_verdict_range(
             d_image.data_ptr(), size, span_off.data_ptr(), span_len.data_ptr(),
-            None if seed is None else seed.data_ptr(), n, LEN_UNBOUNDED if max_len is None else max_len,
+            None if seed is None else seed.data_ptr(), n, min_len, LEN_UNBOUNDED if max_len is None else max_len,
             nbad.data_ptr(), bad.data_ptr(), min(cap, bad.numel()),
-            torch.cuda.current_stream(dev).cuda_stream), "zscrc_device_verify_commits_verdict")
+            torch.cuda.current_stream(dev).cuda_stream), "zscrc_device_verify_commits_verdict_range")
     return nbad, bad
 
 
