@@ -206,3 +206,58 @@ def test_native_entry_point(gpu, tmp_path):
     assert nat["first_bad"].startswith(f"{f}:{c['commit_off']}:")
     (tmp_path / ".zsdb").write_bytes(b"short")
     assert cs.consistent_native(str(tmp_path))["dotzsdb"] == 0
+
+
+def test_eight_slots_config5_shape(gpu, tmp_path):
+    """Multi-GPU readiness on one GPU: zscrc_zs_consistent with eight device
+    slots (ZSCRC_DEVICES=0,...,0 -- what an 8-GPU node gives it) on a
+    config-5-shaped DB whose commit CRCs the CPU oracle wrote (two packed
+    files with > 16 MiB records regions, finalised files with stale finalise
+    commits, an active file): the records regions are cut at the slot bounds
+    and folded on the host.  Clean, then one flipped byte on each side of
+    every slot bound that falls inside a region -- each found as the one bad
+    commit of that file."""
+    from tools import zsdb_gen as zg
+    db = zg.make_db(device="cpu", packed=2, packed_region_bytes=24 << 20, finalised=20, active_pairs=500,
+                    writer="cpu")
+    files = {n: (v.numpy() if hasattr(v, "numpy") else np.frombuffer(v, np.uint8)) for n, v in db.items()}
+    for n, v in files.items():
+        (tmp_path / n).write_bytes(v.tobytes())
+    slots = 8
+    os.environ["ZSCRC_DEVICES"] = ",".join(["0"] * slots)
+    try:
+        rep = cs.consistent_native(str(tmp_path))
+        assert rep["consistent"] == 1 and rep["stale_empty_commits"] == 20 and rep["bad_commits"] == 0
+        # the slot bounds (zscrc_files.cpp: W = packed files from their
+        # records region on, others whole; cuts 4 KiB-aligned in a region)
+        order = sorted((n for n in files if n != ".zsdb"), key=lambda n: cs.parse_name(n)[2:])
+        W = sum(files[n].nbytes - (40 if cs.parse_name(n)[0] == 2 else 0) for n in order)
+        at, cuts = 0, []
+        for n in order:
+            if cs.parse_name(n)[0] == 2:
+                rlen = oracle_region_len(files[n])
+                for s in range(1, slots):
+                    b = W * s // slots
+                    if at < b < at + rlen:
+                        cuts.append((n, 40 + (b - at) // 4096 * 4096))
+                at += files[n].nbytes - 40
+            else:
+                at += files[n].nbytes
+        assert len(cuts) >= 4, cuts
+        for n, cut in cuts:
+            for p in (cut - 1, cut):
+                img = files[n].copy()
+                img[p] ^= 0x08
+                (tmp_path / n).write_bytes(img.tobytes())
+                r = cs.consistent_native(str(tmp_path))
+                assert r["consistent"] == 0 and r["bad_commits"] == 1, (n, p, r)
+                assert r["first_bad"].startswith(n + ":"), r["first_bad"]
+            (tmp_path / n).write_bytes(files[n].tobytes())
+        assert cs.consistent_native(str(tmp_path))["consistent"] == 1
+    finally:
+        del os.environ["ZSCRC_DEVICES"]
+
+
+def oracle_region_len(img) -> int:
+    from oracle import oracle
+    return oracle.packed_image(img)["records"]["span_len"]

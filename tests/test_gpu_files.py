@@ -154,3 +154,37 @@ def test_device_slots_split_region(gpu, devs, group):
     assert rep["bad_commits"] == 2 and rep["first_bad_file"] == 7 and rep["first_bad_what"] == 3
     assert rep["header_errors"] == rep["walk_errors"] == 0
     assert rep_ok7["bad_commits"] == 1 and rep_ok7["first_bad_file"] == 20
+
+
+def test_three_slots_region_spans_every_bound(gpu):
+    """zscrc_set_devices([0, 0, 0]): a packed file whose records region holds
+    both slot bounds (it is most of the DB's bytes), so all three slots hash
+    a piece of it and the host folds three raw registers; one flipped byte on
+    each side of each cut is found, and the clean DB verifies."""
+    rng = np.random.default_rng(21)
+    recs = sorted((b"%016d" % i, bytes(rng.integers(0, 256, int(rng.integers(4000, 8000)), dtype=np.uint8)))
+                  for i in range(5000))
+    packed = np.frombuffer(zf.packed_file(recs, UUID, 0, 3), np.uint8).copy()
+    small = [np.frombuffer(build_active(20, seed=s), np.uint8).copy() for s in (1, 2)]
+    imgs = [small[0], packed, small[1]]
+    kinds = [zsfile.FINALISED, zsfile.PACKED, zsfile.FINALISED]
+    roff = 40
+    rlen = zf.packed_check(packed.tobytes())[1]["span_len"]
+    W = small[0].nbytes + (packed.nbytes - roff) + small[1].nbytes
+    cuts = []
+    for s in (1, 2):
+        b = W * s // 3 - small[0].nbytes
+        assert 0 < b < rlen
+        cuts.append(roff + b // 4096 * 4096)
+    zsfile.set_devices([0, 0, 0])
+    try:
+        rep = zsfile.verify_files(imgs, kinds, threads=6)
+        assert rep["devices"] == 3 and rep["bad_commits"] == 0 and rep["commits"] == _expected(imgs, kinds)[0]
+        for cut in cuts:
+            for p in (cut - 1, cut):
+                packed[p] ^= 0x40
+                r = zsfile.verify_files(imgs, kinds, threads=6)
+                packed[p] ^= 0x40
+                assert r["bad_commits"] == 1 and r["first_bad_file"] == 1 and r["first_bad_what"] == 3, (p, r)
+    finally:
+        zsfile.set_devices(None)

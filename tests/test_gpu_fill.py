@@ -94,7 +94,7 @@ def _log_images(seed, long_value=False):
     return np.frombuffer(b"".join(parts), np.uint8).copy(), commits
 
 
-@pytest.mark.parametrize("chunk", [None, 1 << 20], ids=["default", "1MiB-chunks"])
+@pytest.mark.parametrize("chunk", [None, 128 << 10], ids=["default", "128KiB-chunks"])
 @pytest.mark.parametrize("pinned", [False, True], ids=["pageable", "pinned"])
 def test_fill_commits_byte_exact(gpu, chunk, pinned, monkeypatch):
     img, commits = _log_images(3)

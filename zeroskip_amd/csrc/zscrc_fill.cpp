@@ -213,7 +213,7 @@ extern "C" int zscrc_zs_fill_commits(void *image, uint64_t size, const uint64_t 
     }
     uint64_t chunk = CHUNK_DEFAULT;
     if (const char *e = getenv("ZSCRC_FILL_CHUNK"))
-        chunk = std::max<uint64_t>(1u << 20, strtoull(e, nullptr, 0));
+        chunk = std::max<uint64_t>(64u << 10, strtoull(e, nullptr, 0));
     chunk = std::min<uint64_t>((chunk + 4095) & ~4095ull, 1ull << 31); /* 32-bit offsets within a chunk */
 
     /* the plan: chunks by binary search over the span ends (sorted and

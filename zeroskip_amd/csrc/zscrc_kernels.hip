@@ -2626,6 +2626,7 @@ __global__ __launch_bounds__(BWG) void commit_kernel(BatchDesc d, const uint32_t
     const uint64_t count = d.n;
     if ((uint64_t)blockIdx.x * BWG >= count)
         return;
+    const uint64_t t_entry = __builtin_amdgcn_s_memrealtime();
     {
         uint4 *L4 = reinterpret_cast<uint4 *>(L);
         for (int i = threadIdx.x; i < 8192; i += BWG) {
@@ -2655,6 +2656,8 @@ __global__ __launch_bounds__(BWG) void commit_kernel(BatchDesc d, const uint32_t
     BDesc q;
     bdesc_load(d, i, count, q);
     uint32_t w[5][16];
+    const uint64_t t_fill = __builtin_amdgcn_s_memrealtime();
+    uint32_t rounds = 0, runs = 0;
     for (;;) {
         BRec b;
         burst_meta<false, true>(d, nullptr, true, count, i, lo, b, q, true);
@@ -2664,6 +2667,8 @@ __global__ __launch_bounds__(BWG) void commit_kernel(BatchDesc d, const uint32_t
         b.run = false;
         run_check(d, b, lane);
         const bool run = __builtin_amdgcn_readfirstlane((uint32_t)b.run) != 0;
+        ++rounds;
+        runs += run ? 1u : 0u;
         if (run)
             run_issue<5, !WR>(b, w, lane);
         else
@@ -2679,6 +2684,16 @@ __global__ __launch_bounds__(BWG) void commit_kernel(BatchDesc d, const uint32_t
                 burst_hash<5, false>(d, b, w, L, lo, c_lo, c_hi);
         }
         i += nthr;
+    }
+    /* diagnostic (zscrc_diag_wave_times): entry, after the table fill, end,
+     * rounds | run rounds << 32, per wave */
+    uint64_t *wt = zs_wave_times;
+    if (wt && lane == 0) {
+        const uint64_t wave = (uint64_t)blockIdx.x * (BWG / 64) + (threadIdx.x >> 6);
+        wt[4 * wave + 0] = t_entry;
+        wt[4 * wave + 1] = t_fill;
+        wt[4 * wave + 2] = __builtin_amdgcn_s_memrealtime();
+        wt[4 * wave + 3] = (uint64_t)rounds | ((uint64_t)runs << 32);
     }
 }
 
