@@ -716,7 +716,7 @@ def run_config4(args, world, rank, dev, stream):
         # zeroed first, so the first call is checked byte for byte.
         ow_np = offs_w.cpu().numpy().astype(np.uint64)
         lw_np = lens_w.cpu().numpy().astype(np.uint64)
-        fields = (ow_np + lw_np + 4)[:, None] + np.arange(4)
+        fields = (ow_np + lw_np + 4).astype(np.int64)[:, None] + np.arange(4, dtype=np.int64)
         for kind, buf in (("pinned", pinned.view(-1)), ("pageable", host.view(-1).clone())):
             arr = buf.numpy()
             arr[fields] = 0

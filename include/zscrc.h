@@ -154,9 +154,23 @@ const char *zscrc_last_error(void);
 /* counters: [0] scalar calls on CPU, [1] scalar calls offloaded,
  * [2] kernel launches, [3] bytes checksummed on the GPU */
 void zscrc_stats(uint64_t out[4]);
-/* scalar calls of at least `min_bytes` go to the GPU (0 = never; default from
- * env ZSCRC_GPU_MIN, else never). */
+/* Scalar offload of the drop-in symbols (crc32c_hw, crc32c, map / buf /
+ * cstring / iovec): a call of at least the threshold runs on the GPU
+ * (falling back to the CPU silently if that fails, unless ZSCRC_STRICT=1).
+ * Two thresholds: the warm one once this process has a device context, the
+ * cold one before (the first GPU call pays HIP init).  Defaults: the
+ * crossovers against one CPU core measured on MI355X (DESIGN.md §5,
+ * profiles/r04/crossover.jsonl); env ZSCRC_GPU_MIN sets both, 0 = never;
+ * ZSCRC_GPU_MIN_COLD the cold one alone.  zscrc_set_gpu_min sets both. */
 void zscrc_set_gpu_min(uint64_t min_bytes);
+/* warm / cold thresholds apart (warm 0 = never offload) */
+void zscrc_set_gpu_min_pair(uint64_t warm, uint64_t cold);
+/* the threshold in force: cold != 0 -> before any device context exists */
+uint64_t zscrc_gpu_min(int cold);
+/* Create the current device's context and the scalar-offload buffers now
+ * (a zeroskip process that wants large crc32_end calls offloaded from the
+ * first one: call it at open).  0 or a negative status. */
+int zscrc_warmup(void);
 /* team size tuning: records <= g1_max bytes (default 640) use one lane each,
  * <= g16_max (default 1 MiB) a 16-lane team, larger a 64-lane (whole
  * wavefront) team. */

@@ -11,7 +11,9 @@
  * prints one JSON line: the span CRC, the span length, and libzscrc's counters
  * (scalar calls on the CPU / offloaded to the GPU).
  *
- * usage: mfile_demo FILE PIECE_BYTES PIECES
+ * usage: mfile_demo FILE PIECE_BYTES PIECES [warm]
+ *   warm: call zscrc_warmup() first (what a GPU-enabled zeroskip process does
+ *   at open), so the offload threshold in force is the warm one.
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -37,9 +39,13 @@ static void fill(unsigned char *p, uint64_t n)
 
 int main(int argc, char **argv)
 {
-    if (argc != 4) {
-        fprintf(stderr, "usage: %s FILE PIECE_BYTES PIECES\n", argv[0]);
+    if (argc != 4 && !(argc == 5 && strcmp(argv[4], "warm") == 0)) {
+        fprintf(stderr, "usage: %s FILE PIECE_BYTES PIECES [warm]\n", argv[0]);
         return 2;
+    }
+    if (argc == 5 && zscrc_warmup() != ZSCRC_OK) {
+        fprintf(stderr, "zscrc_warmup: %s\n", zscrc_last_error());
+        return 1;
     }
     const uint64_t piece = strtoull(argv[2], NULL, 0), pieces = strtoull(argv[3], NULL, 0);
     struct mfile *mf = NULL;

@@ -259,6 +259,7 @@ def test_host_batch(gpu):
 
 
 def test_scalar_offload(gpu):
+    saved = (lib().zscrc_gpu_min(0), lib().zscrc_gpu_min(1))
     before = stats()
     lib().zscrc_set_gpu_min(1 << 20)
     try:
@@ -268,10 +269,26 @@ def test_scalar_offload(gpu):
         small = d[:37]
         assert zc.crc32c_hw(0, small) == oracle.crc32c_hw(0, small)
     finally:
-        lib().zscrc_set_gpu_min(0)
+        lib().zscrc_set_gpu_min_pair(*saved)
     after = stats()
     assert after[1] - before[1] == 2   # both large calls ran on the GPU
     assert after[0] - before[0] == 1   # the 37-byte call stayed on the CPU
+
+
+def test_scalar_offload_cached_and_pieces(gpu):
+    """The cached per-device offload stream (no allocation per call) over
+    sizes that take one piece, several pieces and a ragged last piece, with
+    seeds; each call on the GPU and equal to the oracle."""
+    saved = (lib().zscrc_gpu_min(0), lib().zscrc_gpu_min(1))
+    lib().zscrc_set_gpu_min(1)
+    try:
+        for n in (1, 4095, (4 << 20) + 17, (33 << 20) + 5, (97 << 20) + 1):
+            d = rand_bytes(n, n)
+            before = stats()
+            assert zc.crc32c_hw(0xA5A5A5A5, d) == oracle.crc32c_hw(0xA5A5A5A5, d), n
+            assert stats()[1] - before[1] == 1, n
+    finally:
+        lib().zscrc_set_gpu_min_pair(*saved)
 
 
 @pytest.mark.parametrize("mode", ["team16", "xteam", "qteam"])

@@ -8,7 +8,8 @@ T="python -u -m pytest --maxfail=10 -q --timeout 300 --timeout-method thread"
 for step in "$@"; do
   case "$step" in
     newtests) timeout -k 10 600 $T tests/test_gpu_fill.py tests/test_gpu_cpu_written.py tests/test_gpu_repack.py tests/test_gpu_longspans.py \
-                tests/test_gpu_consistent.py > gpurun_out/newtests.log 2>&1 ;;
+                tests/test_gpu_consistent.py tests/test_gpu_append.py tests/test_gpu_files.py \
+                tests/test_gpu_parity.py > gpurun_out/newtests.log 2>&1 ;;
     gputests) timeout -k 10 900 $T -m gpu tests > gpurun_out/gputests.log 2>&1 ;;
     smoke)    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
     bench2|bench3|bench4|bench5)
@@ -22,6 +23,8 @@ for step in "$@"; do
                 --no-cpu --packed-mib 1024 --finalised 256 > gpurun_out/rehearse5_n8.json \
                 2> gpurun_out/rehearse5_n8.err ;;
     cwaves)   timeout -k 10 600 python tools/commit_waves.py > gpurun_out/commit_waves.jsonl 2> gpurun_out/commit_waves.err ;;
+    ab4)      AB_CASES=config4_verdict timeout -k 10 600 python tools/opt_ab.py 0 2048 \
+                > gpurun_out/ab4.jsonl 2> gpurun_out/ab4.err ;;
     ab2)      AB_CASES=config2_multi32 timeout -k 10 600 python tools/opt_ab.py 0 2097152 1048576 3145728 262144 \
                 > gpurun_out/ab2.jsonl 2> gpurun_out/ab2.err ;;
     crossover) timeout -k 10 600 python tools/crossover.py > gpurun_out/crossover.jsonl 2> gpurun_out/crossover.err ;;

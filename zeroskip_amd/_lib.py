@@ -39,6 +39,9 @@ SIGNATURES = {
     "zscrc_last_error": (ctypes.c_char_p, []),
     "zscrc_stats": (None, [_vp]),
     "zscrc_set_gpu_min": (None, [_u64]),
+    "zscrc_gpu_min": (_u64, [_int]),
+    "zscrc_set_gpu_min_pair": (None, [_u64, _u64]),
+    "zscrc_warmup": (_int, []),
     "zscrc_set_teams": (None, [_u64, _u64]),
     "zscrc_set_small_team": (None, [_int]),
     "zscrc_team_for": (_int, [_u64, _u64]),

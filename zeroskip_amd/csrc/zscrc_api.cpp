@@ -61,7 +61,18 @@ constexpr uint64_t SEG_MIN = 1u << 10;
 
 thread_local char t_err[256];
 std::atomic<uint64_t> g_stat[4];
-std::atomic<uint64_t> g_gpu_min{0};
+/* Scalar offload thresholds of the drop-in symbols (crc32c_hw & co.): a call
+ * of at least g_gpu_min bytes goes to the GPU once this process has a device
+ * context (warm), at least g_gpu_min_cold before (the first offloaded call
+ * pays HIP init, ~0.1-0.2 s).  Defaults are the crossovers measured against
+ * one CPU core on a pageable buffer (tools/crossover.py,
+ * profiles/r04/crossover.jsonl); env ZSCRC_GPU_MIN sets both (0 = never),
+ * ZSCRC_GPU_MIN_COLD the cold one alone. */
+constexpr uint64_t GPU_MIN_WARM_DEFAULT = 64ull << 20;
+constexpr uint64_t GPU_MIN_COLD_DEFAULT = 8ull << 30;
+std::atomic<uint64_t> g_gpu_min{GPU_MIN_WARM_DEFAULT};
+std::atomic<uint64_t> g_gpu_min_cold{GPU_MIN_COLD_DEFAULT};
+std::atomic<bool> g_warm{false}; /* a device context exists in this process */
 std::atomic<uint64_t> g_g1_max{640};
 std::atomic<uint64_t> g_g16_max{1u << 20};
 std::atomic<int> g_split_team{64}; /* team size on split long records */
@@ -124,7 +135,10 @@ void env_init()
 {
     const char *s = getenv("ZSCRC_GPU_MIN");
     if (s)
-        g_gpu_min = strtoull(s, nullptr, 0);
+        g_gpu_min = g_gpu_min_cold = strtoull(s, nullptr, 0);
+    s = getenv("ZSCRC_GPU_MIN_COLD");
+    if (s && g_gpu_min)
+        g_gpu_min_cold = strtoull(s, nullptr, 0);
     s = getenv("ZSCRC_STRICT");
     g_strict = s && *s && *s != '0';
     s = getenv("ZSCRC_G1_MAX");
@@ -221,6 +235,7 @@ int get_ctx(DevCtx **out)
     }
     c.ncu = ncu;
     c.ready = true;
+    g_warm = true;
     *out = &c;
     return ZSCRC_OK;
 }
@@ -711,18 +726,49 @@ int span_impl(DevCtx *c, const void *d_buf, uint64_t len, uint32_t seed, uint32_
     return ZSCRC_OK;
 }
 
-/* Scalar call offloaded to the GPU (chunked copy/CRC pipeline of Part 4,
- * straight from the caller's memory); returns false to fall back to the CPU. */
+/* Scalar call offloaded to the GPU: the chunked copy/CRC pipeline of Part 4
+ * straight from the caller's memory, on a stream object cached per device
+ * (buffers, streams and events opened once; per call only the copies, the
+ * launches and one synchronisation).  Pieces of len / 8 (4-64 MiB) keep the
+ * H2D copy of piece k+1 beside the CRC of piece k for mid-size calls.
+ * Returns false to fall back to the CPU (no device, an error, or another
+ * thread using this device's offload right now). */
+struct ScalarOffload {
+    std::mutex mu;
+    zscrc_stream *s = nullptr;
+};
+ScalarOffload g_scalar[MAX_DEV];
+int stream_submit(zscrc_stream *s, const void *src, uint64_t n);
+int stream_collect(zscrc_stream *s, uint32_t *crc);
+void stream_reset(zscrc_stream *s, uint32_t seed);
+void stream_set_piece(zscrc_stream *s, uint64_t piece);
+void stream_free(zscrc_stream *s);
+
 bool gpu_scalar(uint32_t crc, const void *buf, size_t len, uint32_t *res)
 {
-    zscrc_stream *st = nullptr;
-    if (zscrc_stream_open(&st, crc, 0, ZSCRC_STREAM_NOCOPY))
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEV)
         return false;
-    const int rc = zscrc_stream_update(st, buf, len);
+    ScalarOffload &so = g_scalar[dev];
+    std::unique_lock<std::mutex> lk(so.mu, std::try_to_lock);
+    if (!lk.owns_lock())
+        return false;
+    if (!so.s && zscrc_stream_open(&so.s, crc, 64ull << 20, ZSCRC_STREAM_NOCOPY)) {
+        so.s = nullptr;
+        return false;
+    }
+    zscrc_stream *s = so.s;
+    stream_reset(s, crc);
+    stream_set_piece(s, (len / 8 + 4095) & ~4095ull);
+    const int rc = zscrc_stream_update(s, buf, len);
     uint32_t r = 0;
-    const int rc2 = zscrc_stream_final(st, &r);
-    if (rc || rc2)
+    const int rc2 = stream_collect(s, &r);
+    if (rc || rc2) {
+        /* a failed pass: drop the cached stream (the next call reopens) */
+        stream_free(s);
+        so.s = nullptr;
         return false;
+    }
     *res = r;
     return true;
 }
@@ -747,8 +793,8 @@ uint32_t crc32c_sw(uint32_t crc, const void *buf, size_t len)
 uint32_t crc32c_hw(uint32_t crc, const void *buf, size_t len)
 {
     std::call_once(g_env_once, env_init);
-    const uint64_t gmin = g_gpu_min;
-    if (gmin && len >= gmin && buf) {
+    const uint64_t gmin = g_warm ? g_gpu_min.load() : g_gpu_min_cold.load();
+    if (gmin && g_gpu_min && len >= gmin && buf) {
         uint32_t r;
         if (gpu_scalar(crc, buf, len, &r)) {
             g_stat[1]++;
@@ -1217,6 +1263,36 @@ void zscrc_set_gpu_min(uint64_t min_bytes)
 {
     std::call_once(g_env_once, env_init);
     g_gpu_min = min_bytes;
+    g_gpu_min_cold = min_bytes;
+}
+
+void zscrc_set_gpu_min_pair(uint64_t warm, uint64_t cold)
+{
+    std::call_once(g_env_once, env_init);
+    g_gpu_min = warm;
+    g_gpu_min_cold = cold;
+}
+
+uint64_t zscrc_gpu_min(int cold)
+{
+    std::call_once(g_env_once, env_init);
+    return cold ? g_gpu_min_cold.load() : g_gpu_min.load();
+}
+
+int zscrc_warmup(void)
+{
+    DevCtx *c;
+    int rc = get_ctx(&c);
+    if (rc)
+        return rc;
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEV)
+        return ZSCRC_ENODEV;
+    ScalarOffload &so = g_scalar[dev];
+    std::lock_guard<std::mutex> lk(so.mu);
+    if (!so.s && (rc = zscrc_stream_open(&so.s, 0, 64ull << 20, ZSCRC_STREAM_NOCOPY)) != ZSCRC_OK)
+        so.s = nullptr;
+    return rc;
 }
 
 void zscrc_set_prefetch(int g, int depth)
@@ -1359,6 +1435,7 @@ struct zscrc_stream {
     int slot = 0;
     uint64_t fill = 0;   /* copy mode: bytes staged in hpin[slot] */
     uint64_t total = 0;
+    uint64_t piece = 0;  /* NOCOPY: bytes per submitted piece (<= chunk; 0 = chunk) */
     int err = 0;
 };
 
@@ -1497,8 +1574,9 @@ int zscrc_stream_update(zscrc_stream *s, const void *buf, size_t len)
     const uint8_t *p = static_cast<const uint8_t *>(buf);
     if (s->flags & ZSCRC_STREAM_NOCOPY) {
         /* straight from the caller's (unchanging) memory, chunk by chunk */
+        const uint64_t pc = s->piece && s->piece < s->chunk ? s->piece : s->chunk;
         while (len) {
-            const uint64_t n = len < s->chunk ? len : s->chunk;
+            const uint64_t n = len < pc ? len : pc;
             int rc = stream_submit(s, p, n);
             if (rc)
                 return rc;
@@ -1575,10 +1653,14 @@ int zscrc_internal_stream_advance(zscrc_stream *s, uint64_t n, int flush, const 
     return ZSCRC_OK;
 }
 
-int zscrc_stream_final(zscrc_stream *s, uint32_t *crc)
+} /* extern "C" */
+
+namespace {
+
+/* The CRC of everything submitted (final() without the free): the chunk
+ * registers folded on the host, reg = shift(reg, len_k) ^ raw_k. */
+int stream_collect(zscrc_stream *s, uint32_t *crc)
 {
-    if (!s)
-        return ZSCRC_EINVAL;
     int rc = s->err;
     if (!rc && s->fill) {
         const uint64_t n = s->fill;
@@ -1594,13 +1676,46 @@ int zscrc_stream_final(zscrc_stream *s, uint32_t *crc)
             rc = stream_fail(s, "stream final", e);
     }
     if (!rc && crc) {
-        const uint32_t kx = zs_gf2_xpow8n(s->chunk);
+        const uint64_t l0 = s->lens.empty() ? s->chunk : s->lens[0];
+        const uint32_t kx = zs_gf2_xpow8n(l0);
         uint32_t reg = 0;
         for (size_t i = 0; i < raw.size(); ++i)
-            reg = (s->lens[i] == s->chunk ? zs_gf2_mul(reg, kx) : zs_gf2_shift(reg, s->lens[i])) ^ raw[i];
+            reg = (s->lens[i] == l0 ? zs_gf2_mul(reg, kx) : zs_gf2_shift(reg, s->lens[i])) ^ raw[i];
         reg ^= zs_gf2_shift(s->seed ^ 0xffffffffu, s->total);
         *crc = reg ^ 0xffffffffu;
     }
+    return rc;
+}
+
+/* A finished stream ready for the next span from `seed`: its buffers,
+ * streams and events are kept (the scalar offload reuses one per device --
+ * opening a stream allocates and freeing it synchronises the device, ~7 ms
+ * per call, profiles/r04/crossover_before.jsonl). */
+void stream_reset(zscrc_stream *s, uint32_t seed)
+{
+    s->seed = seed;
+    s->lens.clear();
+    s->slot = 0;
+    s->fill = 0;
+    s->total = 0;
+    s->err = 0;
+}
+
+/* NOCOPY pieces of `piece` bytes, within [4 MiB, chunk] */
+void stream_set_piece(zscrc_stream *s, uint64_t piece)
+{
+    s->piece = piece < (4ull << 20) ? (4ull << 20) : piece > s->chunk ? s->chunk : piece;
+}
+
+} /* namespace */
+
+extern "C" {
+
+int zscrc_stream_final(zscrc_stream *s, uint32_t *crc)
+{
+    if (!s)
+        return ZSCRC_EINVAL;
+    const int rc = stream_collect(s, crc);
     stream_free(s);
     return rc;
 }
