@@ -3,7 +3,7 @@
 the writer of src/zeroskip-file.c:253-350), so the GPU writer and the GPU
 verifier are never each other's only witness:
 
-* >= 1 M zsbench BATCHED commits (config 4's layout, 153 log files of 2 MiB)
+* >= 1.1 M zsbench BATCHED commits (config 4's layout, 168 log files of 2 MiB)
   verified by commit_kernel<false> -- verdict and per-commit arrays -- against
   the oracle's stored CRCs, and the GPU writer reproducing the CPU-written
   image byte for byte;
@@ -28,7 +28,7 @@ UUID = bytes(range(16))
 @pytest.fixture(scope="module")
 def batched(gpu):
     ppf = zg.pairs_per_file(True)
-    nfiles = -(-1_000_000 // ppf)
+    nfiles = -(-1_100_000 // ppf)   # > 2^20 commits: commit_kernel's dynamic tail is on
     g = torch.Generator(device=gpu)
     g.manual_seed(0xC0DE)
     img = zg.log_files(UUID, 0, nfiles, ppf, 0, True, g, gpu, writer="cpu")
@@ -39,7 +39,7 @@ def batched(gpu):
 
 def test_cpu_written_million_commits_verdict(batched):
     img, offs, lens, nfiles = batched
-    assert offs.numel() >= 1_000_000 + nfiles
+    assert offs.numel() >= 1_100_000 + nfiles
     nbad, bad = zsfile.verify_commits_verdict(img.view(-1), offs, lens, max_len=312)
     nbad = int(nbad.item())
     stale = torch.nonzero(lens == 0).flatten()
@@ -116,3 +116,40 @@ def test_fill_commits_host_million(batched):
     rep = zsfile.fill_commits(blank, o, ln, max_len=312)
     assert rep["commits"] == len(o) and rep["no_record"] == 0 and rep["chunks"] > 1
     assert np.array_equal(blank, host)
+
+
+DYN_OFF = 1 << 22   # zs::BatchDesc::opt: commit_kernel with static rounds only
+
+
+def test_dynamic_tail_verdicts(batched):
+    """commit_kernel's dynamic tail (pooled rounds handed out by per-XCD
+    atomics, counters zeroed by each launch's last wave): corruptions spread
+    over the image -- in static rounds and in pooled ones near the end -- are
+    all found, launch after launch, and every per-commit CRC and status
+    equals the static schedule's."""
+    from zeroskip_amd._lib import lib
+    img, offs, lens, nfiles = batched
+    flat = img.view(-1).clone()
+    n = offs.numel()
+    rng = np.random.default_rng(9)
+    live = torch.nonzero(lens > 0).flatten().cpu().numpy()
+    hit = np.unique(np.concatenate([rng.choice(live, 40, replace=False), live[-64:][::7], live[:3]]))
+    at = (offs.cpu().numpy()[hit] + 100).astype(np.int64)
+    flat[torch.from_numpy(at).to(flat.device)] ^= 0x11
+    stale = set(torch.nonzero(lens == 0).flatten().cpu().tolist())
+    want = set(hit.tolist()) | stale
+    for _ in range(3):
+        nbad, bad = zsfile.verify_commits_verdict(flat, offs, lens, max_len=312, cap=8192)
+        k = int(nbad.item())
+        assert k == len(want) and set(bad[:k].cpu().tolist()) == want
+    crc_d, st_d = zsfile.verify_commits(flat, offs, lens, max_len=312)
+    lib().zscrc_set_opt(DYN_OFF)
+    try:
+        crc_s, st_s = zsfile.verify_commits(flat, offs, lens, max_len=312)
+        nbad_s, _ = zsfile.verify_commits_verdict(flat, offs, lens, max_len=312)
+        torch.cuda.synchronize()
+    finally:
+        lib().zscrc_set_opt(0)
+    assert torch.equal(crc_d, crc_s) and torch.equal(st_d, st_s) and int(nbad_s.item()) == len(want)
+    assert set(torch.nonzero(st_d != 1).flatten().cpu().tolist()) == want
+    assert n > 1 << 20

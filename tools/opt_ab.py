@@ -45,6 +45,7 @@ def main():
              "config4_verify": lambda: zsfile.verify_commits(img, offs, lens, max_len=mx),
              "config4_write": lambda: zsfile.write_commits(img, ow, lw, max_len=mx),
              "config4_write_nocrc": lambda: zsfile.write_commits(img, ow, lw, max_len=mx, crc=False),
+             "config4_crcs": lambda: zsfile.commit_crcs(img, ow, lw, max_len=mx),
              "config4_verdict": lambda: zsfile.verify_commits_verdict(img, offs, lens, max_len=mx, out=vout),
              "config4_nb": lambda: zsfile.verify_commits(img_nb, o_nb, l_nb)[1],
              "fixed_320x312": lambda: zd.crc_fixed(fx, 320, 312, 10_000_000),

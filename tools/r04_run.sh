@@ -23,7 +23,7 @@ for step in "$@"; do
                 --no-cpu --packed-mib 1024 --finalised 256 > gpurun_out/rehearse5_n8.json \
                 2> gpurun_out/rehearse5_n8.err ;;
     cwaves)   timeout -k 10 600 python tools/commit_waves.py > gpurun_out/commit_waves.jsonl 2> gpurun_out/commit_waves.err ;;
-    ab4)      AB_CASES=config4_verdict timeout -k 10 600 python tools/opt_ab.py 0 2048 \
+    ab4)      AB_CASES=config4_verdict,config4_write,config4_crcs timeout -k 10 600 python tools/opt_ab.py 0 4194304 \
                 > gpurun_out/ab4.jsonl 2> gpurun_out/ab4.err ;;
     ab2)      AB_CASES=config2_multi32 timeout -k 10 600 python tools/opt_ab.py 0 2097152 1048576 3145728 262144 \
                 > gpurun_out/ab2.jsonl 2> gpurun_out/ab2.err ;;

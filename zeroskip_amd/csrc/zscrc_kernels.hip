@@ -2619,6 +2619,59 @@ __global__ __launch_bounds__(NB == 1 ? 1024 : BWG) void burst_kernel(BatchDesc d
  * verifier only needs the verdict (src/zeroskip-record.c:188-273 reports a
  * mismatch).
  */
+/*
+ * commit_kernel's rounds (64 consecutive commits per wave and round).  Every
+ * wave of a launch does the same number of rounds, yet per-wave rates differ
+ * by ~10 %: config 4's verdict has waves ending between 544 us (p10) and
+ * 644 us (max) with 76-77 rounds each (profiles/r04/commit_waves.jsonl) --
+ * the last ~10 % of the launch is the slowest waves finishing alone.  So
+ * the rounds are split: a static phase (wave w takes rounds w + t nw for
+ * t < ks, ks ~ 85 % of its share: no atomics) and a dynamic tail -- the rest
+ * cut into eight pools, one per XCD (workgroups go to XCDs round-robin, so
+ * blockIdx.x % 8), each handed out a round per atomic from its own counter
+ * (eight addresses: no single serialising counter); a wave whose pool is
+ * empty draws from the next ones.  A round's index is fetched two rounds
+ * ahead, so the atomic's latency hides behind a round of loads.  The last
+ * wave to finish zeroes the counters for the next launch on the stream.
+ */
+struct RoundSched {
+    uint64_t w, nw, nr;   /* this wave, waves, rounds */
+    uint64_t ks, base;    /* static rounds per wave; the first pooled round (ks nw) */
+    uint32_t x, tried;    /* this wave's pool; pools found empty so far */
+    bool dyn;
+};
+
+__device__ __forceinline__ uint64_t pool_lo(const RoundSched &s, uint32_t p)
+{
+    return s.base + (s.nr - s.base) * p / 8;
+}
+
+/* Wait for / check the round a fetch returned; on an empty pool, draw
+ * (synchronously: only at the very end) from the next pools.  Wave-uniform. */
+__device__ __forceinline__ uint64_t pool_take(const BatchDesc &d, RoundSched &s, uint64_t got, int lane)
+{
+    for (;;) {
+        const uint32_t p = (s.x + s.tried) & 7u;
+        const uint64_t j = __builtin_amdgcn_readfirstlane((uint32_t)__shfl(got, 0)) |
+                           ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(__shfl(got, 0) >> 32)) << 32);
+        if (pool_lo(s, p) + j < pool_lo(s, p + 1))
+            return pool_lo(s, p) + j;
+        if (++s.tried >= 8)
+            return s.nr; /* every pool empty: no more rounds */
+        const uint32_t q = (s.x + s.tried) & 7u;
+        got = lane == 0 ? atomicAdd(&d.dyn[DYN_STRIDE * q], 1ull) : 0ull;
+    }
+}
+
+/* Issue the fetch of a pooled round (its value is taken two rounds later). */
+__device__ __forceinline__ uint64_t pool_issue(const BatchDesc &d, const RoundSched &s, int lane)
+{
+    if (s.tried >= 8)
+        return ~0ull >> 1; /* past every pool: pool_take returns nr */
+    const uint32_t p = (s.x + s.tried) & 7u;
+    return lane == 0 ? atomicAdd(&d.dyn[DYN_STRIDE * p], 1ull) : 0ull;
+}
+
 template <bool WR>
 __global__ __launch_bounds__(BWG) void commit_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
 {
@@ -2650,19 +2703,43 @@ __global__ __launch_bounds__(BWG) void commit_kernel(BatchDesc d, const uint32_t
     const uint32_t c_hi = c_lo | 0x10000u;
     const uintptr_t lo = reinterpret_cast<uintptr_t>(d.base) & ~uintptr_t(3);
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(gtab);
-    const uint64_t nthr = (uint64_t)gridDim.x * BWG;
     uint32_t *S = reinterpret_cast<uint32_t *>(L + OFF_RUN) + RUN_WORDS * (threadIdx.x >> 6);
-    uint64_t i = (uint64_t)blockIdx.x * BWG + threadIdx.x;
+    /* the rounds: static, then the pooled tail (RoundSched) */
+    RoundSched rs;
+    rs.w = uni64((uint64_t)blockIdx.x * (BWG / 64) + (threadIdx.x >> 6));
+    rs.nw = (uint64_t)gridDim.x * (BWG / 64);
+    rs.nr = (count + 63) / 64;
+    rs.x = blockIdx.x & 7u;
+    rs.tried = 0;
+    /* the tail needs every workgroup in the launch (the last-wave reset) and
+     * enough rounds per wave to be worth a pool */
+    rs.dyn = d.dyn && count >= (uint64_t)gridDim.x * BWG * 8;
+    rs.ks = rs.dyn ? (rs.nr / rs.nw) * 85 / 100 : ~0ull >> 1;
+    rs.base = rs.dyn ? rs.ks * rs.nw : rs.nr;
+    auto round_of = [&](uint64_t t, uint64_t fetched) -> uint64_t {
+        if (t < rs.ks) {
+            const uint64_t r = rs.w + t * rs.nw;
+            return r < rs.nr ? r : rs.nr;
+        }
+        return pool_take(d, rs, fetched, lane);
+    };
+    uint64_t f0 = rs.ks == 0 ? pool_issue(d, rs, lane) : 0ull;
+    uint64_t r_cur = round_of(0, f0);
+    uint64_t f1 = rs.ks <= 1 ? pool_issue(d, rs, lane) : 0ull;
+    uint64_t r_nxt = round_of(1, f1);
+    uint64_t i = 64 * r_cur + (uint64_t)lane;
     BDesc q;
     bdesc_load(d, i, count, q);
     uint32_t w[5][16];
     const uint64_t t_fill = __builtin_amdgcn_s_memrealtime();
     uint32_t rounds = 0, runs = 0;
-    for (;;) {
+    for (uint64_t t = 0;; ++t) {
         BRec b;
         burst_meta<false, true>(d, nullptr, true, count, i, lo, b, q, true);
         if (!__any(b.ok))
             break;
+        /* round t + 2's index, fetched now when it is pooled */
+        const uint64_t f2 = t + 2 >= rs.ks ? pool_issue(d, rs, lane) : 0ull;
         commit_next(b, lane);
         b.run = false;
         run_check(d, b, lane);
@@ -2673,7 +2750,8 @@ __global__ __launch_bounds__(BWG) void commit_kernel(BatchDesc d, const uint32_t
             run_issue<5, !WR>(b, w, lane);
         else
             burst_issue_x(b, dummy, w, lane);
-        bdesc_load(d, i + nthr, count, q);
+        const uint64_t i_nxt = 64 * r_nxt + (uint64_t)lane;
+        bdesc_load(d, i_nxt, count, q);
         commit_load(b);
         xpose_burst(w);
         if (run) {
@@ -2683,7 +2761,19 @@ __global__ __launch_bounds__(BWG) void commit_kernel(BatchDesc d, const uint32_t
             if (b.ok)
                 burst_hash<5, false>(d, b, w, L, lo, c_lo, c_hi);
         }
-        i += nthr;
+        i = i_nxt;
+        r_cur = r_nxt;
+        r_nxt = round_of(t + 2, f2);
+    }
+    if (rs.dyn && lane == 0) {
+        /* the last wave out zeroes the pools for the next launch */
+        __threadfence();
+        const unsigned long long done = atomicAdd(&d.dyn[DYN_STRIDE * 8], 1ull);
+        if (done == rs.nw - 1) {
+            for (uint32_t p = 0; p < 8; ++p)
+                atomicExch(&d.dyn[DYN_STRIDE * p], 0ull);
+            atomicExch(&d.dyn[DYN_STRIDE * 8], 0ull);
+        }
     }
     /* diagnostic (zscrc_diag_wave_times): entry, after the table fill, end,
      * rounds | run rounds << 32, per wave */
