@@ -118,15 +118,14 @@ def test_fill_commits_host_million(batched):
     assert np.array_equal(blank, host)
 
 
-DYN_OFF = 1 << 22   # zs::BatchDesc::opt: commit_kernel with static rounds only
+STATIC_ROUNDS = 1 << 22   # zs::BatchDesc::opt: commit_kernel's static schedule (rounds not dealt)
 
 
-def test_dynamic_tail_verdicts(batched):
-    """commit_kernel's dynamic tail (pooled rounds handed out by per-XCD
-    atomics, counters zeroed by each launch's last wave): corruptions spread
-    over the image -- in static rounds and in pooled ones near the end -- are
-    all found, launch after launch, and every per-commit CRC and status
-    equals the static schedule's."""
+def test_dealt_rounds_verdicts(batched):
+    """commit_kernel's rounds dealt to a workgroup's waves by an LDS counter:
+    corruptions spread over the image -- the first rounds, random ones and
+    the last ones -- are all found, launch after launch, and every per-commit
+    CRC and status equals the static schedule's."""
     from zeroskip_amd._lib import lib
     img, offs, lens, nfiles = batched
     flat = img.view(-1).clone()
@@ -143,13 +142,14 @@ def test_dynamic_tail_verdicts(batched):
         k = int(nbad.item())
         assert k == len(want) and set(bad[:k].cpu().tolist()) == want
     crc_d, st_d = zsfile.verify_commits(flat, offs, lens, max_len=312)
-    lib().zscrc_set_opt(DYN_OFF)
-    try:
-        crc_s, st_s = zsfile.verify_commits(flat, offs, lens, max_len=312)
-        nbad_s, _ = zsfile.verify_commits_verdict(flat, offs, lens, max_len=312)
-        torch.cuda.synchronize()
-    finally:
-        lib().zscrc_set_opt(0)
-    assert torch.equal(crc_d, crc_s) and torch.equal(st_d, st_s) and int(nbad_s.item()) == len(want)
+    for opt in (STATIC_ROUNDS,):
+        lib().zscrc_set_opt(opt)
+        try:
+            crc_s, st_s = zsfile.verify_commits(flat, offs, lens, max_len=312)
+            nbad_s, _ = zsfile.verify_commits_verdict(flat, offs, lens, max_len=312)
+            torch.cuda.synchronize()
+        finally:
+            lib().zscrc_set_opt(0)
+        assert torch.equal(crc_d, crc_s) and torch.equal(st_d, st_s) and int(nbad_s.item()) == len(want), opt
     assert set(torch.nonzero(st_d != 1).flatten().cpu().tolist()) == want
     assert n > 1 << 20

@@ -52,7 +52,18 @@ def waves(name, fn, nwaves, opt=0):
     # per-wave least squares: work_us ~ x * run rounds + y * quad rounds
     A = np.stack([runs, quads], 1).astype(np.float64)
     coef, *_ = np.linalg.lstsq(A, work, rcond=None)
-    row = {"case": name, "opt": opt, "ms_per_call_back_to_back": round(ms, 4), "waves": int(live.sum()),
+    # where the spread lives: inside a workgroup (its 8 waves) or between
+    # workgroups (CUs), and between XCDs (blockIdx.x % 8)
+    wid = np.nonzero(live)[0]
+    blk = wid // BWG_WAVES
+    ub = np.unique(blk)
+    bmax = np.array([end[blk == b].max() for b in ub])
+    bmin = np.array([end[blk == b].min() for b in ub])
+    xcd = ub % 8
+    spread = {"within_block_range_us_p50": round(float(np.median(bmax - bmin)), 1),
+              "block_end_us_p10_p50_max": [round(float(np.percentile(bmax, q)), 1) for q in (10, 50, 100)],
+              "xcd_block_end_us_median": [round(float(np.median(bmax[xcd == x])), 1) for x in range(8)]}
+    row = {"case": name, "opt": opt, "spread": spread, "ms_per_call_back_to_back": round(ms, 4), "waves": int(live.sum()),
            "kernel_us": round(float(end.max()), 1), "entry_us_max": round(float(ent.max()), 1),
            "fill_us_p50_max": [round(float(np.median(fill - ent)), 2), round(float((fill - ent).max()), 2)],
            "end_us_p10_p50_p90_max": [round(float(np.percentile(end, q)), 1) for q in (10, 50, 90, 100)],
@@ -77,7 +88,8 @@ def main():
     mx = int(lens.max().item())
     vout = (torch.empty(1, dtype=torch.int64, device=dev), torch.empty(4096, dtype=torch.int64, device=dev))
     fn = lambda: zsfile.verify_commits_verdict(img, offs, lens, max_len=mx, out=vout)  # noqa: E731
-    waves("config4 verdict", fn, nw)
+    waves("config4 verdict, static rounds (1 << 22)", fn, nw, 1 << 22)
+    waves("config4 verdict (rounds dealt per workgroup)", fn, nw)
     waves("config4 verdict, no trailer / stores (diag 8192)", fn, nw, 8192)
     waves("config4 verdict, no chains (diag 4096)", fn, nw, 4096)
     waves("config4 verdict, no run rounds (2048)", fn, nw, 2048)

@@ -61,7 +61,14 @@ def main():
         offs, lens = zg.log_spans(nfiles, ppf, True, True, dev)
         live = lens > 0
         ow, lw = offs[live].contiguous(), lens[live].contiguous()
-        run = lambda k: zsfile.write_commits(img.view(-1), ow, lw, max_len=312, crc=False)  # noqa: E731
+        if os.environ.get("C4_CRCS"):       # the writer's CRCs out of place (commit mode 3)
+            crc = torch.empty(ow.numel(), dtype=torch.int32, device=dev)
+            from zeroskip_amd._lib import check as _ck, lib as _lb
+            run = lambda k: _ck(_lb().zscrc_device_commit_crcs_bounded(  # noqa: E731
+                img.data_ptr(), img.numel(), ow.data_ptr(), lw.data_ptr(), ow.numel(), 312, crc.data_ptr(), None,
+                torch.cuda.current_stream().cuda_stream), "crcs")
+        else:
+            run = lambda k: zsfile.write_commits(img.view(-1), ow, lw, max_len=312, crc=False)  # noqa: E731
     elif cfg == "config5":
         from tools import zsdb_gen as zg
         from zeroskip_amd import consistent as cs

@@ -27,6 +27,7 @@ for step in "$@"; do
                 > gpurun_out/ab4.jsonl 2> gpurun_out/ab4.err ;;
     ab2)      AB_CASES=config2_multi32 timeout -k 10 600 python tools/opt_ab.py 0 2097152 1048576 3145728 262144 \
                 > gpurun_out/ab2.jsonl 2> gpurun_out/ab2.err ;;
+    pmc4crcs) C4_CRCS=1 bash tools/pmc_traffic.sh config4w 5 ;;
     crossover) timeout -k 10 600 python tools/crossover.py > gpurun_out/crossover.jsonl 2> gpurun_out/crossover.err ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

@@ -123,12 +123,6 @@ struct DevCtx {
     size_t classes_bytes = 0;
     void *parts = nullptr;     /* part registers of split long records */
     size_t parts_bytes = 0;
-    /* commit_kernel's dynamic-tail counters: a ring of DYN_SLOTS blocks of
-     * zs::DYN_WORDS, zeroed once; each launch takes the next block (its last
-     * wave zeroes it again), so launches in flight on other streams do not
-     * share counters */
-    unsigned long long *dyn = nullptr;
-    std::atomic<uint32_t> dyn_next{0};
     hipEvent_t last = nullptr; /* end of the last scratch user's work ... */
     hipStream_t last_stream = nullptr; /* ... enqueued on this stream */
     bool last_valid = false;
@@ -411,28 +405,6 @@ int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s, int depth_hi
     return ZSCRC_OK;
 }
 
-constexpr uint32_t DYN_SLOTS = 256;
-
-/* The next block of commit_kernel's dynamic-tail counters (NULL: none, the
- * kernel then runs static rounds only). */
-unsigned long long *dyn_block(DevCtx *c)
-{
-    {
-        std::lock_guard<std::recursive_mutex> lk(c->mu);
-        if (!c->dyn) {
-            void *p = nullptr;
-            const size_t bytes = (size_t)DYN_SLOTS * zs::DYN_WORDS * 8;
-            if (hipMalloc(&p, bytes) != hipSuccess || hipMemset(p, 0, bytes) != hipSuccess) {
-                if (p)
-                    (void)hipFree(p);
-                return nullptr;
-            }
-            c->dyn = static_cast<unsigned long long *>(p);
-        }
-    }
-    return c->dyn + (size_t)(c->dyn_next.fetch_add(1) % DYN_SLOTS) * zs::DYN_WORDS;
-}
-
 /* A variable-length batch: a device-side classify kernel sorts the records
  * into four length classes (lists + counts stay on the device: no host
  * round trip), then one persistent launch per class walks its list:
@@ -472,10 +444,8 @@ int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t max_len =
             }
         }
         if (max_len <= g1 && d.commit && !d.desc && !(d.opt & 32768) && w0 < 0) {
-            /* bounded commit batch: commit_kernel (run rounds, verdicts, the
-             * dynamic tail unless tuning bit 1 << 22) */
-            if (!(d.opt & (1u << 22)))
-                d.dyn = dyn_block(c);
+            /* bounded commit batch: commit_kernel (run rounds, verdicts,
+             * rounds dealt per workgroup) */
             if (zs_launch_commit(&d, c->gtab, c->ncu, s)) {
                 set_err("commit kernel launch", hipGetLastError());
                 return ZSCRC_EHIP;

@@ -82,7 +82,8 @@ struct BatchDesc {
                              1 << 20 = diagnostic: multi64 without hashing (the load + store
                              shape alone, wrong results), 1 << 21 = multi64d_kernel (results
                              staged in LDS per group of chunks, one contiguous write),
-                             1 << 22 = commit_kernel with static rounds only (no dynamic tail) */
+                             1 << 22 = commit_kernel with static rounds (not dealt per
+                             workgroup) */
     uint32_t *part_out;
     /* commit verdict mode (bad_count != NULL): no per-record out / status;
      * every commit whose status is not 1 is counted in *bad_count and its
@@ -97,14 +98,7 @@ struct BatchDesc {
      * class's bytes laid end to end (part_fold_kernel's last-part shift) */
     const uint64_t *rec_start;
     const uint32_t *seg_first; /* segment plans: first part of segment w */
-    /* commit_kernel's dynamic tail (DYN_WORDS counters, zero at launch; the
-     * launch's last wave zeroes them again): NULL = static rounds only */
-    unsigned long long *dyn;
 };
-
-/* commit_kernel's dynamic tail: pool p's counter at dyn[DYN_STRIDE * p]
- * (p = 0..7, one per XCD), the finished-wave counter at dyn[DYN_STRIDE * 8] */
-constexpr uint32_t DYN_STRIDE = 32, DYN_WORDS = DYN_STRIDE * 9;
 
 /* A fixed-stride batch for xteam_kernel (what it reads of a BatchDesc: few
  * kernel arguments, few SGPRs).  last_len = fixed_len when there is none. */

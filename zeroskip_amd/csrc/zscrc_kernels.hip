@@ -2621,65 +2621,62 @@ __global__ __launch_bounds__(NB == 1 ? 1024 : BWG) void burst_kernel(BatchDesc d
  */
 /*
  * commit_kernel's rounds (64 consecutive commits per wave and round).  Every
- * wave of a launch does the same number of rounds, yet per-wave rates differ
- * by ~10 %: config 4's verdict has waves ending between 544 us (p10) and
- * 644 us (max) with 76-77 rounds each (profiles/r04/commit_waves.jsonl) --
- * the last ~10 % of the launch is the slowest waves finishing alone.  So
- * the rounds are split: a static phase (wave w takes rounds w + t nw for
- * t < ks, ks ~ 85 % of its share: no atomics) and a dynamic tail -- the rest
- * cut into eight pools, one per XCD (workgroups go to XCDs round-robin, so
- * blockIdx.x % 8), each handed out a round per atomic from its own counter
- * (eight addresses: no single serialising counter); a wave whose pool is
- * empty draws from the next ones.  A round's index is fetched two rounds
- * ahead, so the atomic's latency hides behind a round of loads.  The last
- * wave to finish zeroes the counters for the next launch on the stream.
+ * wave does the same number of rounds, yet per-wave rates differ: config 4's
+ * verdict with one static share per wave has waves ending between 616 us
+ * (p10) and 694 us (max), and the spread lives inside the workgroups -- the
+ * median workgroup's 8 waves end 61 us apart while the workgroups' last
+ * waves end within 26 us of each other (profiles/r04/commit_waves_dealing.jsonl).
+ * So each workgroup deals its own rounds to its waves: slot k of workgroup b
+ * is round 8 b + k % 8 + (k / 8) nw -- the static schedule's rounds of that
+ * workgroup, in the same order -- handed out by an LDS counter, one round
+ * per atomic.  A wave fetches the index of the round after next during the
+ * round before it needs its descriptors (issued after that round's loads and
+ * taken after its hash), so the counter's latency stays hidden.  Measured
+ * interleaved (profiles/r04/ab_config4_dealing.jsonl): verdict 0.666 ->
+ * 0.647 ms, writer 1.010 -> 0.979, CRC array 0.740 -> 0.722; the same
+ * rounds dealt from eight device-wide per-XCD pools instead measured 0.705
+ * (memory-side atomics at 2,048 waves: their queue was slower than a round).
+ * Tuning bit 1 << 22: the static schedule (wave w, rounds w + t nw).
  */
 struct RoundSched {
-    uint64_t w, nw, nr;   /* this wave, waves, rounds */
-    uint64_t ks, base;    /* static rounds per wave; the first pooled round (ks nw) */
-    uint32_t x, tried;    /* this wave's pool; pools found empty so far */
-    bool dyn;
+    uint64_t w, nw, nr; /* this wave, waves, rounds */
+    bool deal;          /* rounds dealt by the workgroup's LDS counter */
+    uint32_t *lctr;
 };
 
-__device__ __forceinline__ uint64_t pool_lo(const RoundSched &s, uint32_t p)
+/* slot k of this workgroup: round 8 b + k % 8 + (k / 8) nw */
+__device__ __forceinline__ uint64_t deal_round(const RoundSched &s, uint64_t k)
 {
-    return s.base + (s.nr - s.base) * p / 8;
+    const uint64_t r = (uint64_t)blockIdx.x * (BWG / 64) + (k % (BWG / 64)) + (k / (BWG / 64)) * s.nw;
+    return r < s.nr ? r : s.nr;
 }
 
-/* Wait for / check the round a fetch returned; on an empty pool, draw
- * (synchronously: only at the very end) from the next pools.  Wave-uniform. */
-__device__ __forceinline__ uint64_t pool_take(const BatchDesc &d, RoundSched &s, uint64_t got, int lane)
+/* Round t's index: dealt (from the slot fetched by deal_issue) or static.
+ * Wave-uniform. */
+__device__ __forceinline__ uint64_t round_at(const RoundSched &s, uint64_t t, uint32_t fetched)
 {
-    for (;;) {
-        const uint32_t p = (s.x + s.tried) & 7u;
-        const uint64_t j = __builtin_amdgcn_readfirstlane((uint32_t)__shfl(got, 0)) |
-                           ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(__shfl(got, 0) >> 32)) << 32);
-        if (pool_lo(s, p) + j < pool_lo(s, p + 1))
-            return pool_lo(s, p) + j;
-        if (++s.tried >= 8)
-            return s.nr; /* every pool empty: no more rounds */
-        const uint32_t q = (s.x + s.tried) & 7u;
-        got = lane == 0 ? atomicAdd(&d.dyn[DYN_STRIDE * q], 1ull) : 0ull;
-    }
+    if (s.deal)
+        return deal_round(s, __builtin_amdgcn_readfirstlane(__shfl(fetched, 0)));
+    const uint64_t r = s.w + t * s.nw;
+    return r < s.nr ? r : s.nr;
 }
 
-/* Issue the fetch of a pooled round (its value is taken two rounds later). */
-__device__ __forceinline__ uint64_t pool_issue(const BatchDesc &d, const RoundSched &s, int lane)
+__device__ __forceinline__ uint32_t deal_issue(const RoundSched &s, int lane)
 {
-    if (s.tried >= 8)
-        return ~0ull >> 1; /* past every pool: pool_take returns nr */
-    const uint32_t p = (s.x + s.tried) & 7u;
-    return lane == 0 ? atomicAdd(&d.dyn[DYN_STRIDE * p], 1ull) : 0ull;
+    return s.deal && lane == 0 ? atomicAdd(s.lctr, 1u) : 0u;
 }
 
 template <bool WR>
 __global__ __launch_bounds__(BWG) void commit_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
 {
     __shared__ __attribute__((aligned(16))) char L[OFF_RUN + 4 * RUN_WORDS * (BWG / 64)];
+    __shared__ uint32_t lctr;
     const uint64_t count = d.n;
     if ((uint64_t)blockIdx.x * BWG >= count)
         return;
     const uint64_t t_entry = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0)
+        lctr = 0;
     {
         uint4 *L4 = reinterpret_cast<uint4 *>(L);
         for (int i = threadIdx.x; i < 8192; i += BWG) {
@@ -2704,29 +2701,15 @@ __global__ __launch_bounds__(BWG) void commit_kernel(BatchDesc d, const uint32_t
     const uintptr_t lo = reinterpret_cast<uintptr_t>(d.base) & ~uintptr_t(3);
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(gtab);
     uint32_t *S = reinterpret_cast<uint32_t *>(L + OFF_RUN) + RUN_WORDS * (threadIdx.x >> 6);
-    /* the rounds: static, then the pooled tail (RoundSched) */
+    /* the rounds: dealt per workgroup (RoundSched) */
     RoundSched rs;
     rs.w = uni64((uint64_t)blockIdx.x * (BWG / 64) + (threadIdx.x >> 6));
     rs.nw = (uint64_t)gridDim.x * (BWG / 64);
     rs.nr = (count + 63) / 64;
-    rs.x = blockIdx.x & 7u;
-    rs.tried = 0;
-    /* the tail needs every workgroup in the launch (the last-wave reset) and
-     * enough rounds per wave to be worth a pool */
-    rs.dyn = d.dyn && count >= (uint64_t)gridDim.x * BWG * 8;
-    rs.ks = rs.dyn ? (rs.nr / rs.nw) * 85 / 100 : ~0ull >> 1;
-    rs.base = rs.dyn ? rs.ks * rs.nw : rs.nr;
-    auto round_of = [&](uint64_t t, uint64_t fetched) -> uint64_t {
-        if (t < rs.ks) {
-            const uint64_t r = rs.w + t * rs.nw;
-            return r < rs.nr ? r : rs.nr;
-        }
-        return pool_take(d, rs, fetched, lane);
-    };
-    uint64_t f0 = rs.ks == 0 ? pool_issue(d, rs, lane) : 0ull;
-    uint64_t r_cur = round_of(0, f0);
-    uint64_t f1 = rs.ks <= 1 ? pool_issue(d, rs, lane) : 0ull;
-    uint64_t r_nxt = round_of(1, f1);
+    rs.deal = !(d.opt & (1u << 22));
+    rs.lctr = &lctr;
+    uint64_t r_cur = round_at(rs, 0, deal_issue(rs, lane));
+    uint64_t r_nxt = round_at(rs, 1, deal_issue(rs, lane));
     uint64_t i = 64 * r_cur + (uint64_t)lane;
     BDesc q;
     bdesc_load(d, i, count, q);
@@ -2738,8 +2721,7 @@ __global__ __launch_bounds__(BWG) void commit_kernel(BatchDesc d, const uint32_t
         burst_meta<false, true>(d, nullptr, true, count, i, lo, b, q, true);
         if (!__any(b.ok))
             break;
-        /* round t + 2's index, fetched now when it is pooled */
-        const uint64_t f2 = t + 2 >= rs.ks ? pool_issue(d, rs, lane) : 0ull;
+
         commit_next(b, lane);
         b.run = false;
         run_check(d, b, lane);
@@ -2753,6 +2735,10 @@ __global__ __launch_bounds__(BWG) void commit_kernel(BatchDesc d, const uint32_t
         const uint64_t i_nxt = 64 * r_nxt + (uint64_t)lane;
         bdesc_load(d, i_nxt, count, q);
         commit_load(b);
+        /* round t + 2's index, fetched now when it is pooled: issued after the
+         * round's loads, so waiting for them does not wait for the atomic
+         * (vmcnt counts in issue order); taken after the hash */
+        const uint32_t f2 = deal_issue(rs, lane);
         xpose_burst(w);
         if (run) {
             run_hash(d, b, w, L, S, lane, c_lo, c_hi);
@@ -2763,17 +2749,7 @@ __global__ __launch_bounds__(BWG) void commit_kernel(BatchDesc d, const uint32_t
         }
         i = i_nxt;
         r_cur = r_nxt;
-        r_nxt = round_of(t + 2, f2);
-    }
-    if (rs.dyn && lane == 0) {
-        /* the last wave out zeroes the pools for the next launch */
-        __threadfence();
-        const unsigned long long done = atomicAdd(&d.dyn[DYN_STRIDE * 8], 1ull);
-        if (done == rs.nw - 1) {
-            for (uint32_t p = 0; p < 8; ++p)
-                atomicExch(&d.dyn[DYN_STRIDE * p], 0ull);
-            atomicExch(&d.dyn[DYN_STRIDE * 8], 0ull);
-        }
+        r_nxt = round_at(rs, t + 2, f2);
     }
     /* diagnostic (zscrc_diag_wave_times): entry, after the table fill, end,
      * rounds | run rounds << 32, per wave */
