@@ -559,7 +559,7 @@ def test_fixed_multi_64_offsets(gpu, shift, n):
     big = to_dev(rand_bytes(k * (64 * n + 64) + 64, n + shift), gpu)
     bufs = [big[shift + b * (64 * n + 64):] for b in range(k)]
     hosts = [b.cpu().numpy() for b in bufs]
-    for opt in (0, 2, 1 << 21):     # multi64_kernel, the piece walk, multi64d_kernel (staged results)
+    for opt in (0, 2, 1 << 21, 1 << 23):   # multi64 (chunks dealt), the piece walk, multi64d, multi64's static walk
         lib().zscrc_set_opt(opt)
         try:
             outs = zd.crc_fixed_multi(bufs, 64, 64, n, seed=0xC0C0)

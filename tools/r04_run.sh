@@ -7,6 +7,8 @@ mkdir -p gpurun_out
 T="python -u -m pytest --maxfail=10 -q --timeout 300 --timeout-method thread"
 for step in "$@"; do
   case "$step" in
+    parity)   timeout -k 10 600 $T tests/test_gpu_parity.py tests/test_gpu_cpu_written.py tests/test_gpu_runs.py \
+                > gpurun_out/parity.log 2>&1 ;;
     newtests) timeout -k 10 600 $T tests/test_gpu_fill.py tests/test_gpu_cpu_written.py tests/test_gpu_repack.py tests/test_gpu_longspans.py \
                 tests/test_gpu_consistent.py tests/test_gpu_append.py tests/test_gpu_files.py \
                 tests/test_gpu_parity.py > gpurun_out/newtests.log 2>&1 ;;
@@ -25,7 +27,7 @@ for step in "$@"; do
     cwaves)   timeout -k 10 600 python tools/commit_waves.py > gpurun_out/commit_waves.jsonl 2> gpurun_out/commit_waves.err ;;
     ab4)      AB_CASES=config4_verdict,config4_write,config4_crcs timeout -k 10 600 python tools/opt_ab.py 0 4194304 \
                 > gpurun_out/ab4.jsonl 2> gpurun_out/ab4.err ;;
-    ab2)      AB_CASES=config2_multi32 timeout -k 10 600 python tools/opt_ab.py 0 2097152 1048576 3145728 262144 \
+    ab2)      AB_CASES=config2_multi32 timeout -k 10 600 python tools/opt_ab.py 0 8388608 2097152 \
                 > gpurun_out/ab2.jsonl 2> gpurun_out/ab2.err ;;
     pmc4crcs) C4_CRCS=1 bash tools/pmc_traffic.sh config4w 5 ;;
     crossover) timeout -k 10 600 python tools/crossover.py > gpurun_out/crossover.jsonl 2> gpurun_out/crossover.err ;;

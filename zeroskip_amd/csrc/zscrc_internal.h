@@ -83,7 +83,8 @@ struct BatchDesc {
                              shape alone, wrong results), 1 << 21 = multi64d_kernel (results
                              staged in LDS per group of chunks, one contiguous write),
                              1 << 22 = commit_kernel with static rounds (not dealt per
-                             workgroup) */
+                             workgroup), 1 << 23 = multi64_kernel's static walk (chunks not
+                             dealt per workgroup) */
     uint32_t *part_out;
     /* commit verdict mode (bad_count != NULL): no per-record out / status;
      * every commit whose status is not 1 is counted in *bad_count and its

@@ -1787,6 +1787,36 @@ __global__ __launch_bounds__(WG) void multi64_kernel(BatchDesc d, MultiBatch m, 
     M64Pos ph, pl; /* hashing / loading position, the load one chunk ahead */
     ph.b = wave / cpb;
     ph.k = wave - ph.b * cpb;
+    /* the workgroup's chunks dealt to its waves by an LDS counter (slot s:
+     * item 16 B + s % 16 + (s / 16) nw, the static order), as commit_kernel
+     * deals its rounds: per-wave rates differ inside a workgroup, and the
+     * static shares left its fast waves idle at the end (interleaved A/B,
+     * profiles/r04/ab_config2_dealing.jsonl: 0.497 -> 0.475 ms per 32
+     * batches).  Tuning bit 1 << 23: the static walk. */
+    const bool deal = !(d.opt & (1u << 23));
+    auto item_pos = [&](uint32_t slot, M64Pos &p) {
+        const uint64_t it = (uint64_t)blockIdx.x * WAVES + slot % WAVES + (uint64_t)(slot / WAVES) * nw;
+        if (it >= items) {
+            p.b = m.nb;
+            p.k = 0;
+            return;
+        }
+        p.b = it / cpb;
+        p.k = it - p.b * cpb;
+    };
+    __shared__ uint32_t lslot;
+    if (deal) {
+        if (threadIdx.x == 0)
+            lslot = 0;
+        __syncthreads();
+        uint32_t s0 = lane == 0 ? atomicAdd(&lslot, 1u) : 0u;
+        item_pos(__builtin_amdgcn_readfirstlane(__shfl(s0, 0)), ph);
+    }
+    uint32_t snext = deal && lane == 0 ? atomicAdd(&lslot, 1u) : 0u; /* the item after the next */
+    auto deal_advance = [&](M64Pos &p) {
+        item_pos(__builtin_amdgcn_readfirstlane(__shfl(snext, 0)), p);
+        snext = lane == 0 ? atomicAdd(&lslot, 1u) : 0u;
+    };
     pl = ph;
     m64_issue<K>(m, n, pl, voff, dummy, b0);
     auto hash = [&](uint32_t (&w)[16 * K], const M64Pos &p) {
@@ -1821,6 +1851,22 @@ __global__ __launch_bounds__(WG) void multi64_kernel(BatchDesc d, MultiBatch m, 
             if (r0 + 64 * q < n)
                 out[r0 + 64 * q] = r[q] ^ d.xor_io;
     };
+    if (deal) {
+        M64Pos pn;
+        while (ph.b < m.nb) {
+            deal_advance(pn);
+            m64_issue<K>(m, n, pn, voff, dummy, b1);
+            hash(b0, ph);
+            ph = pn;
+            if (ph.b >= m.nb)
+                break;
+            deal_advance(pn);
+            m64_issue<K>(m, n, pn, voff, dummy, b0);
+            hash(b1, ph);
+            ph = pn;
+        }
+        return;
+    }
     while (ph.b < m.nb) {
         advance(pl);
         m64_issue<K>(m, n, pl, voff, dummy, b1);
