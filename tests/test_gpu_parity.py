@@ -291,7 +291,7 @@ def test_scalar_offload_cached_and_pieces(gpu):
         lib().zscrc_set_gpu_min_pair(*saved)
 
 
-@pytest.mark.parametrize("mode", ["team16", "xteam", "qteam"])
+@pytest.mark.parametrize("mode", ["team16", "xteam", "qteam-static", "qteam"])
 def test_config3_headline_dispatch(gpu, mode):
     """BASELINE config 3 at full size through the exact call bench.py times:
     zscrc_device_fixed on 65,536 x 64 KiB chunks (4 GiB), seed 0, flags 0 --
@@ -303,10 +303,12 @@ def test_config3_headline_dispatch(gpu, mode):
     g.manual_seed(0x9E3779B9)
     d = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=gpu, generator=g)
     lib().zscrc_set_xteam(1, 32768 if mode == "xteam" else 256 << 10)
-    lib().zscrc_set_qteam(1 if mode == "qteam" else 0)
+    lib().zscrc_set_qteam(1 if mode.startswith("qteam") else 0)
+    lib().zscrc_set_opt(QSTATIC if mode == "qteam-static" else 0)
     try:
         name = lib().zscrc_fixed_kernel(d.data_ptr(), L, L, n).decode()
-        assert name == {"team16": "team_kernel<16>", "xteam": "xteam_kernel", "qteam": "qteam_kernel"}[mode]
+        assert name == {"team16": "team_kernel<16>", "xteam": "xteam_kernel",
+                        "qteam": "qteam_dyn_kernel+qfold_kernel", "qteam-static": "qteam_kernel"}[mode]
         out = torch.empty(n, dtype=torch.int32, device=gpu)
         from zeroskip_amd._lib import check
         check(lib().zscrc_device_fixed(d.data_ptr(), L, L, 0, out.data_ptr(), n, 0,
@@ -317,6 +319,7 @@ def test_config3_headline_dispatch(gpu, mode):
     finally:
         lib().zscrc_set_xteam(1, 256 << 10)
         lib().zscrc_set_qteam(QTEAM_DEFAULT)
+        lib().zscrc_set_opt(0)
     ref = oracle.batch(host, n=n, stride=L, fixed_len=L, impl="hw", threads=min(16, os.cpu_count() or 1))
     bad = np.nonzero(got != ref)[0]
     assert bad.size == 0, bad[:10]
@@ -348,7 +351,12 @@ def test_xteam_shapes(gpu):
         lib().zscrc_set_teams(*DEFAULT_TEAMS)
 
 
-def test_qteam_shapes(gpu):
+QDEAL = 1 << 25    # zs::BatchDesc::opt: qteam records cut into parts dealt per workgroup, at any size
+QSTATIC = 1 << 24  # qteam's static walk at any size
+
+
+@pytest.mark.parametrize("opt", [0, QDEAL], ids=["static", "dealt-parts"])
+def test_qteam_shapes(gpu, opt, monkeypatch):
     """qteam_kernel (coalesced 16-lane column-quad teams) on ragged shapes of
     equal-length records: a partial last group of four, unaligned bases (the
     first record's front-padded step clamped at the buffer start), ragged
@@ -356,6 +364,9 @@ def test_qteam_shapes(gpu):
     the oracle; shapes it must not take (a different last length, stride
     not a multiple of 4) go to team_kernel<16>."""
     lib().zscrc_set_qteam(1)
+    lib().zscrc_set_opt(opt)
+    if opt:
+        monkeypatch.setenv("ZSCRC_QDYN_P", "3")     # parts of 3 KiB: ragged first parts, many per record
     try:
         for stride, length, n, off in [(8192, 8192, 16385, 0), (8200, 8195, 16390, 1), (16384, 12000, 16387, 3),
                                        (65540, 65537, 16385, 2), (12288, 9000, 16400, 0), (2048, 2048, 16387, 0),
@@ -363,7 +374,8 @@ def test_qteam_shapes(gpu):
                                        (4096, 8192, 16384, 0), (0, 9000, 16386, 1)]:   # overlapping, stride 0
             data = rand_bytes(stride * (n - 1) + length + off, stride + length + n)
             dd = to_dev(data[off:], gpu)
-            assert lib().zscrc_fixed_kernel(dd.data_ptr(), stride, length, n).decode() == "qteam_kernel"
+            assert lib().zscrc_fixed_kernel(dd.data_ptr(), stride, length, n).decode() == \
+                ("qteam_dyn_kernel+qfold_kernel" if opt else "qteam_kernel")
             out = u32(zd.crc_fixed(dd, stride, length, n, seed=0xA5A5))
             ref = _oracle_seeded(data[off:], stride, length, n, 0xA5A5)
             bad = np.nonzero(out != ref)[0]
@@ -376,6 +388,7 @@ def test_qteam_shapes(gpu):
         assert lib().zscrc_fixed_kernel(d.data_ptr(), 8194, 8192, 16384).decode() == "team_kernel<16>"
     finally:
         lib().zscrc_set_qteam(QTEAM_DEFAULT)
+        lib().zscrc_set_opt(0)
 
 
 @pytest.mark.parametrize("qteam,opt", [(1, 4), (1, 8), (0, 16)], ids=["qteam-xor3-1", "qteam-xor3-2", "team16-xor3"])

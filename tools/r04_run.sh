@@ -27,9 +27,16 @@ for step in "$@"; do
     cwaves)   timeout -k 10 600 python tools/commit_waves.py > gpurun_out/commit_waves.jsonl 2> gpurun_out/commit_waves.err ;;
     ab4)      AB_CASES=config4_verdict,config4_write,config4_crcs timeout -k 10 600 python tools/opt_ab.py 0 4194304 \
                 > gpurun_out/ab4.jsonl 2> gpurun_out/ab4.err ;;
+    ab3)      AB_CASES=config3,fixed_16KiB,fixed_4KiB timeout -k 10 600 python tools/opt_ab.py 0 16777216 \
+                > gpurun_out/ab3.jsonl 2> gpurun_out/ab3.err ;;
+    ab3p)     for P in 8 32; do ZSCRC_QDYN_P=$P AB_CASES=config3 timeout -k 10 300 python tools/opt_ab.py 0 16777216 \
+                || exit $?; done > gpurun_out/ab3p.jsonl 2> gpurun_out/ab3p.err ;;
+    spreadq)  WS_OPT=16777216 timeout -k 10 600 python tools/wave_spread.py > gpurun_out/wave_spread_q.jsonl \
+                2> gpurun_out/wave_spread_q.err ;;
     ab2)      AB_CASES=config2_multi32 timeout -k 10 600 python tools/opt_ab.py 0 8388608 2097152 \
                 > gpurun_out/ab2.jsonl 2> gpurun_out/ab2.err ;;
     pmc4crcs) C4_CRCS=1 bash tools/pmc_traffic.sh config4w 5 ;;
+    spread)   timeout -k 10 600 python tools/wave_spread.py > gpurun_out/wave_spread.jsonl 2> gpurun_out/wave_spread.err ;;
     crossover) timeout -k 10 600 python tools/crossover.py > gpurun_out/crossover.jsonl 2> gpurun_out/crossover.err ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

@@ -42,6 +42,8 @@ int zs_launch_multi(const zs::BatchDesc *d, const zs::MultiBatch *m, const uint3
                     hipStream_t stream);
 int zs_launch_xteam(int depth, const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
 int zs_launch_commit(const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
+int zs_launch_qdyn(const zs::BatchDesc *bd, const zs::QDyn *q, uint32_t K, uint32_t K_last, const uint32_t *gtab,
+                   int grid, hipStream_t stream);
 int zs_launch_xparts(const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
 int zs_launch_spans(const zs::XDesc *x, const zs::XMulti *m, const zs::SpanFolds *fs, const uint32_t *gtab,
                     int grid, hipStream_t stream);
@@ -122,6 +124,8 @@ struct DevCtx {
     void *classes = nullptr;   /* class lists + counters of variable batches */
     size_t classes_bytes = 0;
     void *parts = nullptr;     /* part registers of split long records */
+    void *qparts = nullptr;    /* qteam_dyn_kernel: part registers */
+    size_t qparts_bytes = 0;
     size_t parts_bytes = 0;
     hipEvent_t last = nullptr; /* end of the last scratch user's work ... */
     hipStream_t last_stream = nullptr; /* ... enqueued on this stream */
@@ -373,6 +377,61 @@ bool qteam_fits(const zs::BatchDesc &d)
            d.stride <= (1ull << 30);
 }
 
+/* Big qteam batches: records cut into parts dealt per workgroup (config 3
+ * 0.640 -> 0.633 ms, 16 KiB records -2.9 %, 4 KiB -2.3 %, interleaved,
+ * profiles/r04/ab_config3_qdeal.jsonl); small ones keep the static walk (the
+ * fold launch is ~1 % of a 4 GiB pass).  Tuning bit 1 << 24: never, 1 << 25:
+ * always. */
+bool qdeal_for(const DevCtx *c, const zs::BatchDesc &d)
+{
+    if (d.opt & (1u << 24))
+        return false;
+    const uint64_t ngroups = (d.n + 3) / 4;
+    return (d.opt & (1u << 25)) || (d.n * d.fixed_len >= (1ull << 30) && ngroups >= 2ull * c->ncu * 16);
+}
+
+/* qteam with each workgroup's units dealt to its waves:
+ * every record cut into parts of P 1 KiB steps (env ZSCRC_QDYN_P, default
+ * 16), parts folded per record by a second launch. */
+int launch_qdyn(DevCtx *c, const zs::BatchDesc &d, hipStream_t s)
+{
+    uint32_t P = 16;
+    if (const char *e = getenv("ZSCRC_QDYN_P")) {
+        const unsigned long v = strtoul(e, nullptr, 0);
+        if (v >= 1 && v <= 4096)
+            P = (uint32_t)v;
+    }
+    const uint64_t ph = reinterpret_cast<uintptr_t>(d.base) & 3;
+    const uint64_t span = ((ph + d.fixed_len) & ~uint64_t(3)) - ph;
+    const uint64_t S = (span + 1023) / 1024;
+    const uint64_t tail = d.fixed_len - span;
+    const uint32_t np = (uint32_t)((S + P - 1) / P);
+    const uint64_t ngroups = (d.n + 3) / 4;
+    /* a workgroup's slots: its groups x np (32-bit) */
+    if (ngroups / ((uint64_t)c->ncu * 16) * np >= (1ull << 31))
+        return ZSCRC_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    int rc = scratch_acquire(c, s);
+    if (rc)
+        return rc;
+    rc = grow(&c->qparts, &c->qparts_bytes, (size_t)d.n * np * sizeof(uint32_t));
+    if (!rc) {
+        zs::QDyn q;
+        q.part_out = static_cast<uint32_t *>(c->qparts);
+        q.P = P;
+        q.np = np;
+        const uint32_t K = zs_gf2_xpow8n(1024ull * P), K_last = zs_gf2_xpow8n(1024ull * P + tail);
+        if (zs_launch_qdyn(&d, &q, K, K_last, c->gtab, c->ncu, s)) {
+            set_err("qteam dyn launch", hipGetLastError());
+            rc = ZSCRC_EHIP;
+        } else {
+            g_stat[2]++;
+        }
+    }
+    const int rc2 = scratch_release(c, s);
+    return rc ? rc : rc2;
+}
+
 int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s, int depth_hint = -1)
 {
     /* fixed-stride form when no per-record arrays are involved */
@@ -392,6 +451,8 @@ int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s, int depth_hi
     const int xt = g_xteam;
     const bool xteam = g == 64 && fixed && xt && g_depth[2] < 0 && depth_hint < 0 && d.fixed_len >= g_xteam_min;
     const bool qteam = g == 16 && fixed && g_qteam && g_depth[1] < 0 && depth_hint < 0 && qteam_fits(d);
+    if (qteam && qdeal_for(c, d))
+        return launch_qdyn(c, d, s);
     int rc = qteam       ? zs_launch_xteam(16, &d, c->gtab, c->ncu, s)
              : xteam     ? zs_launch_xteam(xt, &d, c->gtab, c->ncu, s)
              : depth >= 9 ? zs_launch_burst(fixed, depth == 10, nb, &dx, c->gtab, c->ncu, s)
@@ -1349,7 +1410,7 @@ const char *zscrc_fixed_kernel(const void *d_base, uint64_t stride, uint64_t len
     if (g == 64 && g_xteam && g_depth[2] < 0 && len >= g_xteam_min)
         return "xteam_kernel";
     if (g == 16 && g_qteam && g_depth[1] < 0 && qteam_fits(d))
-        return "qteam_kernel";
+        return qdeal_for(c, d) ? "qteam_dyn_kernel+qfold_kernel" : "qteam_kernel";
     static const char *names[] = {"team_kernel<1>/short_kernel/burst_kernel", "team_kernel<2>",
                                   "team_kernel<16>", "team_kernel<64>"};
     return names[g == 1 ? 0 : g == 2 ? 1 : g == 16 ? 2 : 3];

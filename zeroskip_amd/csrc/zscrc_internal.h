@@ -84,7 +84,9 @@ struct BatchDesc {
                              staged in LDS per group of chunks, one contiguous write),
                              1 << 22 = commit_kernel with static rounds (not dealt per
                              workgroup), 1 << 23 = multi64_kernel's static walk (chunks not
-                             dealt per workgroup) */
+                             dealt per workgroup), 1 << 24 = qteam_kernel's static walk on big
+                             batches too (not parts dealt per workgroup: qteam_dyn_kernel +
+                             qfold_kernel), 1 << 25 = parts dealt on small batches too */
     uint32_t *part_out;
     /* commit verdict mode (bad_count != NULL): no per-record out / status;
      * every commit whose status is not 1 is counted in *bad_count and its
@@ -112,6 +114,14 @@ struct XDesc {
     uint64_t last_len;
     uint32_t seed;
     uint32_t xor_io;
+};
+
+/* qteam_dyn_kernel (tuning bit 1 << 24): records cut into np parts of P
+ * 1 KiB steps, each workgroup's units dealt by an LDS counter */
+struct QDyn {
+    uint32_t *part_out; /* raw register of part p of record r at r * np + p */
+    uint32_t P;         /* 1 KiB steps per part (part 0: the rest)          */
+    uint32_t np;        /* parts per record                                */
 };
 
 /* Up to SPANS_MAX spans in one xteam_kernel launch (zscrc_device_spans):

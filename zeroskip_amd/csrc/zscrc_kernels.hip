@@ -1306,6 +1306,211 @@ __global__ __launch_bounds__(WG) void qteam_kernel(XDesc d, const uint32_t *__re
     }
 }
 
+/*
+ * qteam_dyn_kernel: qteam_kernel's hashing with each workgroup's work dealt
+ * to its waves.  Per-wave timestamps put config 3's static walk's waves'
+ * ends between 535 us (p10) and 634 us (max), and the spread lives inside
+ * the workgroups: the median workgroup's 16 waves end 85 us apart, the
+ * workgroups' last waves within 20 us of each other
+ * (profiles/r04/wave_spread.jsonl) -- yet a static share is four groups of
+ * four 64 KiB records per wave, too coarse to rebalance.  So every record is
+ * cut into np parts of P 1 KiB steps (part 0 the rest, 1..P steps, so the
+ * parts end on the record's step grid), a *unit* is one part of a group of
+ * four records, and a workgroup deals its own groups' units (its static
+ * groups 16 b + i % 16 + (i / 16) nw, in that order) to its waves from an LDS
+ * counter: the next unit's index fetched a unit ahead, the load cursor one
+ * step ahead across unit boundaries, each buffer tagged with its unit and
+ * step.  A unit ends like a record: team fold, raw register of the part to
+ * part_out[rec * np + part]; qfold_kernel then runs the Horner pass per
+ * record (x^(8 * 1024 P) between parts, x^(8 (1024 P + tail)) before the
+ * last).  (Round 3 dealt the units from one device-wide counter: 1.02 ms
+ * against 0.645 -- the counter serialised.)
+ */
+template <int B3>
+__global__ __launch_bounds__(WG) void qteam_dyn_kernel(XDesc d, QDyn q, const uint32_t *__restrict__ gtab)
+{
+    __shared__ __attribute__((aligned(16))) char L[LDS_BYTES];
+    /* the LDS counter in the bytes fill_lds<16> leaves free (its Z tables
+     * end after four) */
+    uint32_t &lctr = *reinterpret_cast<uint32_t *>(L + OFF_Z + 4 * 4096);
+    const uint64_t t_entry = __builtin_amdgcn_s_memrealtime();
+    const uint64_t ngroups = (d.n + 3) / 4;
+    const uint32_t np = q.np, P = q.P;
+    if ((uint64_t)blockIdx.x * WAVES >= ngroups)
+        return;
+    if (threadIdx.x == 0)
+        lctr = 0;
+    fill_lds<16>(L, gtab);
+    __syncthreads();
+    const uint64_t t_fill = __builtin_amdgcn_s_memrealtime();
+    const int lane = threadIdx.x & 63, g = lane >> 4, t = (lane >> 2) & 3, h = lane & 3;
+    const int j = 4 * g + h; /* piece of the team's step */
+    const uint32_t c_lo = (uint32_t)(lane & 31) << 2;
+    const uint32_t c_hi = c_lo | 0x10000u;
+    const uint64_t wave = uni64((uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6));
+    const uint64_t nwaves = (uint64_t)gridDim.x * WAVES;
+    const uintptr_t base = reinterpret_cast<uintptr_t>(d.base);
+    const uint64_t len = d.fixed_len;
+    const uint64_t ph = base & 3;
+    const uint64_t span = ((ph + len) & ~uint64_t(3)) - ph;
+    const uint32_t S = (uint32_t)((span + 1023) / 1024);
+    const uint64_t pad = (uint64_t)S * 1024 - span;
+    const uint32_t tail = (uint32_t)(len - span);
+    const uint32_t R0 = d.seed ^ d.xor_io;
+    const uintptr_t dummy = reinterpret_cast<uintptr_t>(gtab);
+    const uintptr_t lo = base & ~uintptr_t(3);
+    const uint64_t gstride = 4 * d.stride;
+    const uint32_t voff = (uint32_t)((uint64_t)t * d.stride) + 64u * (uint32_t)h + 16u * (uint32_t)g;
+    /* part p = steps [part_lo(p), part_hi(p)) */
+    auto part_hi = [&](uint32_t p) { return S - (np - 1 - p) * P; };
+    auto part_lo = [&](uint32_t p) { return p ? S - (np - p) * P : 0u; };
+    /* the workgroup's LDS counter; its answer stays in lane 0's register
+     * until the unit is started */
+    auto fetch = [&]() -> uint32_t {
+        uint32_t u = 0;
+        if (lane == 0)
+            u = atomicAdd(&lctr, 1u);
+        return u;
+    };
+
+    /* a unit as (group k, part p); k = ngroups: none left */
+    auto issue = [&](uint64_t k, uint32_t s, uint32_t (&w)[16]) {
+        const bool any = k < ngroups;
+        const uintptr_t sb = uni64(any ? base + k * gstride + (uint64_t)s * 1024 - pad : dummy);
+        if (any && (sb < lo || 4 * k + 4 > d.n)) {
+            const bool live = 4 * k + (uint64_t)t < d.n;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                uintptr_t a = sb + voff + 256u * (uint32_t)i;
+                a = !live ? dummy : a < lo ? lo : a;
+                const u32x4 v = __builtin_nontemporal_load((g4p)a);
+                w[4 * i + 0] = v.x;
+                w[4 * i + 1] = v.y;
+                w[4 * i + 2] = v.z;
+                w[4 * i + 3] = v.w;
+            }
+            return;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const u32x4 v = __builtin_nontemporal_load((g4p)(sb + (any ? voff + 256u * (uint32_t)i : 0u)));
+            w[4 * i + 0] = v.x;
+            w[4 * i + 1] = v.y;
+            w[4 * i + 2] = v.z;
+            w[4 * i + 3] = v.w;
+        }
+    };
+
+    uint32_t acc = 0;
+    auto hash = [&](uint32_t (&w)[16], uint64_t k, uint32_t p, uint32_t s) {
+        xpose16(w);
+        const uint64_t rec = 4 * k + (uint64_t)t;
+        const uintptr_t A = base + rec * d.stride;
+        if (s == 0 || (s == 1 && pad > 1020)) {
+            XItem it;
+            it.A = A;
+            it.R0 = R0;
+            fix_piece(it, A - pad + (uint64_t)s * 1024 + 64 * (uintptr_t)j, lo, w);
+        }
+        if (s + 1 < part_hi(p)) {
+            acc = piece<true, B3>(L, acc, w, c_lo, c_hi);
+            return false;
+        }
+        acc = piece<false, B3>(L, acc, w, c_lo, c_hi);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const uint32_t sh = op4(L, OFF_Z + 4096u * kk, acc);
+            const uint32_t other = __shfl(sh, lane - (kk < 2 ? (1 << kk) : (16 << (kk - 2))));
+            acc ^= (j & (1 << kk)) ? other : 0u;
+        }
+        if (j == 15 && rec < d.n) {
+            if (p + 1 == np) {
+                const g8p e = (g8p)(A + span);
+                for (uint32_t i = 0; i < tail; ++i)
+                    acc = byte_step(L, acc, e[i], c_hi);
+            }
+            q.part_out[rec * np + p] = acc;
+        }
+        acc = 0;
+        return true;
+    };
+
+    /* load cursor (lk, lp, ls) one step ahead of the hashing; the unit after
+     * it (nk, np_) taken when it was */
+    uint64_t lk;
+    uint32_t lp;
+    /* slot u of this workgroup: part u % np of its (u / np)-th group */
+    auto decode = [&](uint32_t raw, uint64_t &k, uint32_t &p) {
+        const uint32_t u = __builtin_amdgcn_readlane(raw, 0);
+        const uint32_t gi = u / np;
+        const uint64_t grp = (uint64_t)blockIdx.x * WAVES + gi % WAVES + (uint64_t)(gi / WAVES) * nwaves;
+        k = grp < ngroups ? grp : ngroups;
+        p = grp < ngroups ? u - gi * np : 0u;
+    };
+    decode(fetch(), lk, lp);
+    uint32_t pend = lk < ngroups ? fetch() : 0xffffffffu; /* the next unit, read when lk ends */
+    uint32_t ls = lk < ngroups ? part_lo(lp) : 0u;
+    auto advance_load = [&]() {
+        if (lk >= ngroups)
+            return;
+        if (++ls == part_hi(lp)) {
+            decode(pend, lk, lp);
+            if (lk < ngroups) {
+                ls = part_lo(lp);
+                pend = fetch();
+            }
+        }
+    };
+    uint32_t b0[16], b1[16];
+    uint64_t k0 = lk, k1;
+    uint32_t p0 = lp, p1, s0 = ls, s1;
+    uint32_t units = 0;
+    issue(lk, ls, b0);
+    while (k0 < ngroups) {
+        advance_load();
+        k1 = lk;
+        p1 = lp;
+        s1 = ls;
+        issue(k1, s1, b1);
+        units += hash(b0, k0, p0, s0) ? 1u : 0u;
+        if (k1 >= ngroups)
+            break;
+        advance_load();
+        k0 = lk;
+        p0 = lp;
+        s0 = ls;
+        issue(k0, s0, b0);
+        units += hash(b1, k1, p1, s1) ? 1u : 0u;
+    }
+    uint64_t *wt = zs_wave_times; /* diagnostic (zscrc_diag_wave_times) */
+    if (wt && lane == 0) {
+        wt[4 * wave + 0] = t_entry;
+        wt[4 * wave + 1] = t_fill;
+        wt[4 * wave + 2] = __builtin_amdgcn_s_memrealtime();
+        wt[4 * wave + 3] = units;
+    }
+}
+
+/* Per record of a qteam_dyn_kernel batch: Horner over its np part
+ * registers, the output CRC. */
+__global__ __launch_bounds__(256) void qfold_kernel(XDesc d, QDyn q, uint32_t K, uint32_t K_last,
+                                                    const uint32_t *__restrict__ gtab)
+{
+    __shared__ __attribute__((aligned(16))) char T[4096];
+    load_gmul_table(T, gtab);
+    __syncthreads();
+    const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t rec = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; rec < d.n; rec += nthr) {
+        const uint32_t *pr = q.part_out + rec * q.np;
+        uint32_t reg = pr[0];
+        for (uint32_t p = 1; p + 1 < q.np; ++p)
+            reg = gmul_t(T, reg, K) ^ pr[p];
+        if (q.np > 1)
+            reg = gmul_t(T, reg, K_last) ^ pr[q.np - 1];
+        d.out[rec] = reg ^ d.xor_io;
+    }
+}
+
 /* ------------------------------------------------------ short records */
 /*
  * One lane per record, records <= g1_max bytes (zsbench's 312-byte commit
@@ -3802,6 +4007,29 @@ extern "C" int zs_launch_burst(int fixed, int xp, int nb, const zs::BatchDesc *d
     else
         ZS_BURST(false, false, 5);
 #undef ZS_BURST
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+/* qteam with units dealt per workgroup + the per-record part fold (tuning bit 1 << 24) */
+extern "C" int zs_launch_qdyn(const zs::BatchDesc *bd, const zs::QDyn *q, uint32_t K, uint32_t K_last,
+                              const uint32_t *gtab, int grid, hipStream_t stream)
+{
+    zs::XDesc x;
+    memset(&x, 0, sizeof x);
+    x.base = bd->base;
+    x.out = bd->out;
+    x.n = bd->n;
+    x.stride = bd->stride;
+    x.fixed_len = bd->fixed_len;
+    x.last_len = bd->fixed_len;
+    x.seed = bd->fixed_seed;
+    x.xor_io = bd->xor_io;
+    hipLaunchKernelGGL(zs::qteam_dyn_kernel<ZS_QTEAM_B3>, dim3(grid), dim3(zs::WG), 0, stream, x, *q, gtab);
+    if (hipGetLastError() != hipSuccess)
+        return -3;
+    const uint64_t fb = (bd->n + 255) / 256;
+    hipLaunchKernelGGL(zs::qfold_kernel, dim3(fb < 1024 ? (unsigned)fb : 1024u), dim3(256), 0, stream, x, *q, K,
+                       K_last, gtab);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
