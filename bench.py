@@ -63,6 +63,49 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
+def box_info(index: int | None = None) -> dict:
+    """What tells one GPU box from another (read-only sysfs of the device
+    this rank runs on, taken after the timed region): clock levels, power
+    cap, firmware, the card's id.  Config 2 and 4's rates move 10-15 % from
+    box to box while the streaming read and config 3 stay level (DESIGN.md
+    1.8), so every line records the box it was measured on."""
+    info = {}
+    try:
+        p = torch.cuda.get_device_properties(torch.cuda.current_device() if index is None else index)
+        bdf = "%04x:%02x:%02x.0" % (p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
+        info["pci"] = bdf
+        base = f"/sys/bus/pci/devices/{bdf}"
+
+        def rd(name):
+            try:
+                with open(os.path.join(base, name)) as f:
+                    return f.read().strip()
+            except OSError:
+                return None
+        for key in ("pp_dpm_sclk", "pp_dpm_mclk", "pp_dpm_fclk"):
+            v = rd(key)
+            if v:
+                levels = [ln.split(":", 1)[1].strip().rstrip("*").strip() for ln in v.splitlines() if ":" in ln]
+                info[key + "_levels"] = levels
+        for key in ("power_dpm_force_performance_level", "vbios_version", "unique_id", "current_link_speed",
+                    "current_link_width"):
+            v = rd(key)
+            if v:
+                info[key] = v
+        hw = os.path.join(base, "hwmon")
+        if os.path.isdir(hw):
+            for h in sorted(os.listdir(hw)):
+                for key in ("power1_cap", "power1_cap_max"):
+                    try:
+                        with open(os.path.join(hw, h, key)) as f:
+                            info[key + "_W"] = round(int(f.read().strip()) / 1e6, 1)
+                    except (OSError, ValueError):
+                        pass
+    except Exception as e:  # a fingerprint never fails a bench line
+        info["error"] = repr(e)[:120]
+    return info
+
+
 def _repeat(fn, budget: float) -> tuple[int, float]:
     from oracle import oracle
     done, t0 = 0, oracle.now()
@@ -291,6 +334,7 @@ def line(args, world, elapsed, total_bytes, config, roofline, scaling="weak", da
         "roofline": roofline,
     }
     d.update(extra)
+    d["box"] = box_info()
     return d
 
 
@@ -729,7 +773,8 @@ def run_config4(args, world, rank, dev, stream):
                 ts.append(time.perf_counter() - t0)
             e2e[f"write_crcs_{kind}_s"] = round(min(ts), 4)
             e2e[f"write_crcs_{kind}_GBs"] = round(host.numel() / min(ts) / 1e9, 2)
-            e2e[f"write_crcs_{kind}_phases_s"] = {"h2d": round(rep_f["h2d_s"], 4), "total": round(rep_f["total_s"], 4),
+            e2e[f"write_crcs_{kind}_phases_s"] = {"setup": round(rep_f["setup_s"], 5), "h2d": round(rep_f["h2d_s"], 4),
+                                                  "total": round(rep_f["total_s"], 4),
                                                   "chunks": rep_f["chunks"], "threads": rep_f["threads"]}
             del buf, arr
         e2e["write_crcs_pipelined_GBs"] = e2e["write_crcs_pinned_GBs"]

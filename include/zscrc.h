@@ -196,6 +196,11 @@ void zscrc_set_xteam(int mode, uint64_t min_len);
  * team_kernel<16> on equal-length fixed-stride records of >= 2 KiB (stride a
  * multiple of 4): mode 0 = off, 1 = on (env ZSCRC_QTEAM) */
 void zscrc_set_qteam(int mode);
+/* tuning: spans on xteam_kernel cut into per_wave segments per wave, dealt to
+ * each workgroup's waves by an LDS counter (default 16, the most; env
+ * ZSCRC_XDEAL); 0 = the static walk, two contiguous segments per wave.
+ * Returns the previous setting. */
+unsigned zscrc_set_xdeal(unsigned per_wave);
 /* tuning bits (env ZSCRC_OPT), for A/B runs: 1 = hash five-piece record
  * bursts as one chain instead of three; 2 = 64-byte record batches of
  * zscrc_device_fixed_multi by the per-lane piece walk instead of coalesced
@@ -369,6 +374,7 @@ typedef struct zscrc_fill_report {
     int32_t threads;
     double h2d_s;              /* until the last chunk was on the GPU         */
     double total_s;
+    double setup_s;            /* until the first chunk's copy was queued     */
 } zscrc_fill_report;
 int zscrc_zs_fill_commits(void *image, uint64_t size, const uint64_t *span_off, const uint64_t *span_len,
                           size_t n, uint64_t max_len, int threads, zscrc_fill_report *rep);

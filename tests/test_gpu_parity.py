@@ -226,6 +226,47 @@ def test_span(gpu, length, offset):
     assert out[0] == oracle.crc32c_hw(0xC0FFEE, data[offset:offset + length])
 
 
+@pytest.mark.parametrize("per_wave", [16, 4, 0], ids=["dealt16", "dealt4", "static"])
+def test_span_xteam_dealt(gpu, per_wave):
+    """Spans on xteam_kernel (forced down to 16 KiB spans with a 4 KiB
+    threshold): per_wave segments per wave dealt per workgroup by the LDS
+    counter, or the static walk's two -- unaligned offsets, ragged last
+    segments, seeds, and SEG_MIN-sized segments (more segments than the
+    grid's waves x per_wave would give)."""
+    old = lib().zscrc_set_xdeal(per_wave)
+    lib().zscrc_set_xteam(1, 4096)
+    try:
+        for length, offset in [(16 << 10, 0), ((16 << 10) + 3, 1), ((1 << 20) - 1, 2), ((64 << 20) + 13, 2),
+                               ((300 << 20) + 5, 1), (513 << 20, 0)]:
+            data = rand_bytes(length + offset + 16, length + per_wave)
+            out = u32(zd.crc_span(to_dev(data, gpu), seed=0xC0FFEE, length=length, offset=offset))
+            assert out[0] == oracle.crc32c_hw(0xC0FFEE, data[offset:offset + length]), (length, offset)
+    finally:
+        lib().zscrc_set_xteam(1, 256 << 10)
+        lib().zscrc_set_xdeal(old)
+
+
+def test_span_3gib_dealt_vs_static(gpu):
+    """A 3 GiB span at an odd offset (xteam_kernel by default: 64 Ki segments
+    dealt per workgroup) against the threaded oracle (seed 0) and, seeded,
+    against the static walk."""
+    n = (3 << 30) + 12345
+    g = torch.Generator(device=gpu)
+    g.manual_seed(31)
+    d = torch.randint(0, 256, (n + 3,), dtype=torch.uint8, device=gpu, generator=g)
+    dealt0 = u32(zd.crc_span(d, length=n, offset=3))[0]
+    dealt7 = u32(zd.crc_span(d, seed=7, length=n, offset=3))[0]
+    old = lib().zscrc_set_xdeal(0)
+    try:
+        static7 = u32(zd.crc_span(d, seed=7, length=n, offset=3))[0]
+    finally:
+        lib().zscrc_set_xdeal(old)
+    host = d[3:].cpu().numpy()
+    del d
+    assert dealt7 == static7
+    assert dealt0 == oracle.span_crc(host, threads=min(16, os.cpu_count() or 1))
+
+
 def test_span_equals_fold_of_records(gpu):
     # size-independent property at BASELINE config-3 record size: one span CRC
     # over N chunks == combine-chain of the N per-chunk CRCs

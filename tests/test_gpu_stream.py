@@ -48,15 +48,26 @@ def test_default_chunk_large(gpu):
     assert s.crc == oracle.crc32c_hw(0, data)
 
 
+@pytest.mark.parametrize("per_wave", [16, 0], ids=["dealt", "static"])
 @pytest.mark.parametrize("shape", ["mixed", "equal", "fallback_short", "fallback_many"])
-def test_device_spans(gpu, shape):
+def test_device_spans(gpu, shape, per_wave):
     """zscrc_device_spans (one segment launch + one fold launch for up to 8
     spans) against the oracle: spans of very different lengths, unaligned
     offsets, seeds, standard and raw registers; short or many spans take
-    the per-span path."""
+    the per-span path.  The segments dealt per workgroup (16 per wave) or
+    on the static walk (two per wave)."""
     import torch
     from oracle import oracle
     from zeroskip_amd import device as zd
+    from zeroskip_amd._lib import lib
+    old = lib().zscrc_set_xdeal(per_wave)
+    try:
+        _device_spans(gpu, shape, torch, oracle, zd)
+    finally:
+        lib().zscrc_set_xdeal(old)
+
+
+def _device_spans(gpu, shape, torch, oracle, zd):
     rng = np.random.default_rng(11)
     host = rng.integers(0, 256, (300 << 20) + 4096, dtype=np.uint8)
     d = torch.from_numpy(host).to(gpu)

@@ -42,6 +42,10 @@ def main():
              "fixed_4KiB": lambda: zd.crc_fixed(c3, 4096, 4096, 1 << 20),
              "fixed_1MiB": lambda: zd.crc_fixed(c3, 1 << 20, 1 << 20, 4096),
              "span_3GiB": lambda: zd.crc_span(c3[:3 << 30]),
+             # config 5's multi-span launch shape: two ~3 GiB records regions
+             # and their pointer sections in one xteam launch + one fold
+             "spans_config5": lambda: zd.crc_spans(c3, [0, 1 << 30, 3 << 30, (3 << 30) + (200 << 20)],
+                                                   [3 << 30, 3 << 30, 200 << 20, 180 << 20]),
              "config4_verify": lambda: zsfile.verify_commits(img, offs, lens, max_len=mx),
              "config4_write": lambda: zsfile.write_commits(img, ow, lw, max_len=mx),
              "config4_write_nocrc": lambda: zsfile.write_commits(img, ow, lw, max_len=mx, crc=False),

@@ -51,7 +51,15 @@ def main():
         img = zg.log_files(bytes(range(16)), 0, nfiles, ppf, 0, False, g, dev, batched=False)
         offs, lens = zg.log_spans(nfiles, ppf, False, False, dev)
         vout = (torch.empty(1, dtype=torch.int64, device=dev), torch.empty(64, dtype=torch.int64, device=dev))
-        run = lambda k: zsfile.verify_commits_verdict(img.view(-1), offs, lens, out=vout)  # noqa: E731
+        lo, hi = int(lens.min().item()), int(lens.max().item())
+        mode = os.environ.get("C4NB_MODE", "range")
+        if mode == "arrays":                # per-commit crc + status arrays
+            run = lambda k: zsfile.verify_commits(img.view(-1), offs, lens)  # noqa: E731
+        elif mode == "unranged":
+            run = lambda k: zsfile.verify_commits_verdict(img.view(-1), offs, lens, out=vout)  # noqa: E731
+        else:                               # the bench line's verdict: the walk's length range
+            run = lambda k: zsfile.verify_commits_verdict(img.view(-1), offs, lens, out=vout,  # noqa: E731
+                                                          min_len=lo, max_len=hi)
     elif cfg == "config4w":
         # the writer side of config 4: every live commit's CRC recomputed and stored
         from tools import zsdb_gen as zg

@@ -17,6 +17,17 @@ for step in "$@"; do
     bench2|bench3|bench4|bench5)
               timeout -k 10 600 python bench.py --workload config${step#bench} > gpurun_out/$step.json \
                 2> gpurun_out/$step.err ;;
+    bench4s)  ZSCRC_OPT=4194304 timeout -k 10 600 python bench.py --workload config4 --no-e2e --no-cpu \
+                >> gpurun_out/bench4s.jsonl 2>> gpurun_out/bench4s.err ;;
+    bench4q)  timeout -k 10 600 python bench.py --workload config4 --no-e2e --no-cpu \
+                >> gpurun_out/bench4q.jsonl 2>> gpurun_out/bench4q.err ;;
+    abspan)   AB_CASES=span_3GiB,spans_config5 timeout -k 10 600 python tools/opt_ab.py 0 67108864 \
+                > gpurun_out/abspan.jsonl 2> gpurun_out/abspan.err ;;
+    nbseq)    bash tools/nb_seq.sh ;;
+    tracebench) bash tools/trace_bench.sh config3 config4 config2 config5 ;;
+    spantests) timeout -k 10 600 $T tests/test_gpu_stream.py tests/test_gpu_parity.py -k "span" \
+                > gpurun_out/spantests.log 2>&1 ;;
+    fillsweep) timeout -k 10 600 python tools/fill_sweep.py > gpurun_out/fill_sweep.jsonl 2> gpurun_out/fill_sweep.err ;;
     rehearse5)
               BENCH_SHARE_GPU=1 BENCH_DIST=gloo timeout -k 10 900 python bench.py --gpus 2 --workload config5 \
                 --no-cpu > gpurun_out/rehearse5_n2.json 2> gpurun_out/rehearse5_n2.err ;;

@@ -55,7 +55,11 @@ def main():
     out = torch.empty(65536, dtype=torch.int32, device=dev)
     waves("config 3: 65,536 x 64 KiB (qteam_kernel)", lambda: zd.crc_fixed(c4, 65536, 65536, 65536, out=out),
           ncu * 16, 16)
-    waves("3 GiB span (xteam segments)", lambda: zd.crc_span(c4[:3 << 30]), ncu * 16, 16)
+    old = lib().zscrc_set_xdeal(0)
+    waves("3 GiB span (xteam segments, static: two per wave)", lambda: zd.crc_span(c4[:3 << 30]), ncu * 16, 16)
+    lib().zscrc_set_xdeal(old)
+    waves("3 GiB span (xteam segments, 16 per wave dealt per workgroup)", lambda: zd.crc_span(c4[:3 << 30]),
+          ncu * 16, 16)
     waves("4,096 x 1 MiB records (xteam_kernel)", lambda: zd.crc_fixed(c4, 1 << 20, 1 << 20, 4096), ncu * 16, 16)
 
 

@@ -49,6 +49,7 @@ SIGNATURES = {
     "zscrc_xteam_for": (_int, [_u64, _u64]),
     "zscrc_set_opt": (None, [ctypes.c_uint]),
     "zscrc_set_qteam": (None, [_int]),
+    "zscrc_set_xdeal": (ctypes.c_uint, [ctypes.c_uint]),
     "zscrc_fixed_kernel": (ctypes.c_char_p, [_vp, _u64, _u64, _sz]),
     "zscrc_set_prefetch": (None, [_int, _int]),
     "zscrc_diag_stream_read": (_int, [_vp, _u64, _vp, _int, _vp]),

@@ -44,9 +44,9 @@ int zs_launch_xteam(int depth, const zs::BatchDesc *d, const uint32_t *gtab, int
 int zs_launch_commit(const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
 int zs_launch_qdyn(const zs::BatchDesc *bd, const zs::QDyn *q, uint32_t K, uint32_t K_last, const uint32_t *gtab,
                    int grid, hipStream_t stream);
-int zs_launch_xparts(const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
+int zs_launch_xparts(const zs::BatchDesc *d, const uint32_t *gtab, int grid, int deal, hipStream_t stream);
 int zs_launch_spans(const zs::XDesc *x, const zs::XMulti *m, const zs::SpanFolds *fs, const uint32_t *gtab,
-                    int grid, hipStream_t stream);
+                    int grid, int deal, hipStream_t stream);
 int zs_launch_mismatch_rows(const uint32_t *st, const uint32_t *crc, const int64_t *end, const uint8_t *img,
                             uint64_t img_size, uint64_t n, int64_t *hdr, int64_t *rows, uint32_t cap,
                             hipStream_t stream);
@@ -94,6 +94,15 @@ std::atomic<int> g_xteam{1};
 /* tuning bits copied into every BatchDesc (zs::BatchDesc::opt; env ZSCRC_OPT) */
 std::atomic<uint32_t> g_opt{0};
 std::atomic<uint64_t> g_xteam_min{256u << 10};
+/* spans on xteam_kernel: segments per wave, dealt per workgroup by an LDS
+ * counter (env ZSCRC_XDEAL, at most 16, which zscrc_span_scratch_bytes
+ * covers; 0 or tuning bit 1 << 26: the static walk's two per wave) */
+constexpr uint32_t XDEAL_MAX = 16;
+std::atomic<uint32_t> g_xdeal{XDEAL_MAX};
+uint32_t xdeal_for(uint32_t opt)
+{
+    return (opt & zs::OPT_XSTATIC) ? 0u : g_xdeal.load();
+}
 /* coalesced non-temporal 16-lane teams (qteam_kernel) in place of
  * team_kernel<16>'s two-level walk on equal-length fixed-stride records of
  * >= g_qteam_min bytes: 0 = off, 1 = on */
@@ -179,6 +188,8 @@ void env_init()
     s = getenv("ZSCRC_XTEAM_MIN");
     if (s)
         g_xteam_min = strtoull(s, nullptr, 0);
+    if ((s = getenv("ZSCRC_XDEAL")))
+        g_xdeal = (uint32_t)std::min<unsigned long>(strtoul(s, nullptr, 0), XDEAL_MAX);
 }
 
 bool is_gfx950(int dev)
@@ -544,11 +555,18 @@ int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1
     /* split target per class: two items per team of the launch */
     auto split_items = [&](int g) { return 2u * (uint32_t)c->ncu * 16u * (uint32_t)(64 / g); };
     const size_t T = split_items(16) > split_items(gs) ? split_items(16) : split_items(gs);
-    /* parts buffer, one half per split class (2, 3): part registers (< 2T),
-     * part_rec (< 2T), part_base (< T) */
-    /* + class 3's segment plan: rec_start (< T records, 64-bit) and
-     * seg_first (one per wave + 1) */
-    const size_t part_bytes = (2 * 5 * T + 2 * T + T + 64) * sizeof(uint32_t);
+    /* class 3 on xteam_kernel's parts mode: a segment plan of one segment per
+     * wave, or xdeal per wave dealt per workgroup */
+    const bool xparts = g_xteam && !(d.opt & 65536);
+    const bool xseg = xparts && !(d.opt & (256 | 131072));
+    const uint32_t xdeal = xseg ? xdeal_for(d.opt) : 0u;
+    const size_t nseg3 = (size_t)c->ncu * 16u * (xdeal ? xdeal : 1u);
+    const size_t P3 = 2 * T > T + nseg3 ? 2 * T : T + nseg3;
+    /* parts buffer: class 2 part registers (< 2T), part_rec (< 2T),
+     * part_base (< T); class 3 part registers and part_rec (< P3 each: at
+     * most T records + one part per segment), part_base (< T); class 3's
+     * segment plan: rec_start (< T records, 64-bit) and seg_first (nseg3 + 1) */
+    const size_t part_bytes = (5 * T + 2 * P3 + T + 2 * T + nseg3 + 64) * sizeof(uint32_t);
     {
         int rc = grow(&c->classes, &c->classes_bytes, list_bytes);
         if (!rc)
@@ -568,7 +586,6 @@ int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1
      * folded per record afterwards.  Class 3 (> g16_max): parts on
      * xteam_kernel's coalesced whole-wave teams, every record through the
      * part fold. */
-    const bool xparts = g_xteam && !(d.opt & 65536);
     zs::PlanArgs pa[2];
     uint32_t *part_out[2];
     for (int k = 2; k < 4; ++k) {
@@ -585,13 +602,15 @@ int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1
         p.always_split = k == 3 && xparts ? 1u : 0u;
         p.gtab = c->gtab;
         p.plan = plans;
+        const size_t cap = k == 3 ? P3 : 2 * T;
         part_out[k - 2] = static_cast<uint32_t *>(c->parts) + (k == 3 ? 5 * T : 0);
-        p.part_rec = part_out[k - 2] + 2 * T;
-        p.part_base = p.part_rec + 2 * T;
-        if (k == 3 && xparts && !(d.opt & (256 | 131072))) {
-            /* class 3 on xteam_kernel: one segment per wave of its grid */
-            uint32_t *ext = static_cast<uint32_t *>(c->parts) + 10 * T;
-            p.nseg = (uint32_t)c->ncu * 16u;
+        p.part_rec = part_out[k - 2] + cap;
+        p.part_base = p.part_rec + cap;
+        if (k == 3 && xseg) {
+            /* class 3 on xteam_kernel: a segment per wave of its grid, or
+             * xdeal per wave dealt per workgroup */
+            uint32_t *ext = p.part_base + T;
+            p.nseg = (uint32_t)nseg3;
             /* test hook: fewer segments than waves (several records per
              * segment at small sizes) */
             if (const char *e = getenv("ZSCRC_XSEGS")) {
@@ -599,7 +618,9 @@ int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1
                 if (v >= 1 && v < p.nseg)
                     p.nseg = (uint32_t)v;
             }
-            p.max_parts = (uint32_t)T; /* part_base / rec_start hold T records */
+            /* part_base / rec_start hold T records: count <= T, and the parts
+             * (<= count + nseg <= T + nseg3) fit P3 */
+            p.max_parts = (uint32_t)(T + p.nseg);
             p.rec_start = reinterpret_cast<uint64_t *>(ext);
             p.seg_first = ext + 2 * T;
         }
@@ -692,7 +713,7 @@ int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1
         }
         int rc;
         if (k == 3 && xparts) {
-            rc = zs_launch_xparts(&dk, c->gtab, c->ncu, s) ? ZSCRC_EHIP : ZSCRC_OK;
+            rc = zs_launch_xparts(&dk, c->gtab, c->ncu, xdeal != 0, s) ? ZSCRC_EHIP : ZSCRC_OK;
             if (rc)
                 set_err("xparts launch", hipGetLastError());
             else
@@ -740,7 +761,10 @@ int span_impl(DevCtx *c, const void *d_buf, uint64_t len, uint32_t seed, uint32_
         g = 64;
         nteams = (uint64_t)c->ncu * 16;
     }
-    uint64_t seg = (len + 2 * nteams - 1) / (2 * nteams);
+    /* xteam: g_xdeal segments per wave dealt per workgroup (else two) */
+    const uint32_t deal = g == 64 ? xdeal_for(d.opt) : 0u;
+    const uint64_t per_wave = deal > 2 ? deal : 2;
+    uint64_t seg = (len + per_wave * nteams - 1) / (per_wave * nteams);
     seg = (seg + 1023) & ~1023ull;
     if (seg < SEG_MIN)
         seg = SEG_MIN;
@@ -760,7 +784,17 @@ int span_impl(DevCtx *c, const void *d_buf, uint64_t len, uint32_t seed, uint32_
     d.fixed_seed = 0;
     d.xor_io = 0;
     d.out = part;
-    int rc = launch(c, g, d, s);
+    int rc;
+    if (deal) { /* the segments are shorter than launch()'s xteam bound */
+        d.opt |= zs::OPT_XDEAL;
+        rc = zs_launch_xteam(g_xteam, &d, c->gtab, c->ncu, s) ? ZSCRC_EHIP : ZSCRC_OK;
+        if (rc)
+            set_err("span launch", hipGetLastError());
+        else
+            g_stat[2]++;
+    } else {
+        rc = launch(c, g, d, s);
+    }
     if (rc)
         return rc;
     zs::SpanFold f;
@@ -1000,7 +1034,8 @@ int zscrc_device_fixed_multi(const void *const *d_bases, uint32_t *const *d_outs
 size_t zscrc_span_scratch_bytes(uint64_t len)
 {
     (void)len;
-    return 4u * (2u * 256u * 64u + 16u); /* <= 2 segments per 16-lane team on 256 CUs */
+    /* <= 2 segments per 16-lane team, or XDEAL_MAX per whole-wave team, on 256 CUs */
+    return 4u * (XDEAL_MAX * 256u * 16u + 16u);
 }
 
 int zscrc_device_span(const void *d_buf, uint64_t len, uint32_t seed, uint32_t *d_out,
@@ -1055,9 +1090,11 @@ int zscrc_device_spans(const void *const *d_bufs, const uint64_t *lens, const ui
     std::lock_guard<std::recursive_mutex> lk(c->mu);
     hipStream_t s = static_cast<hipStream_t>(stream);
     const uint32_t xio = (flags & ZSCRC_RAW) ? 0u : 0xffffffffu;
-    /* one segment size for every span (two segments per wave in all), so a
-     * short span is as many segments as its length needs, not one wave's walk */
-    const uint64_t target = 2ull * (uint64_t)c->ncu * 16;
+    /* one segment size for every span (g_xdeal segments per wave in all,
+     * dealt per workgroup; or two, static), so a short span is as many
+     * segments as its length needs, not one wave's walk */
+    const uint32_t deal = xdeal_for(g_opt);
+    const uint64_t target = (uint64_t)(deal > 2 ? deal : 2) * (uint64_t)c->ncu * 16;
     uint64_t seg = ((total + target - 1) / target + 1023) & ~1023ull;
     if (seg < SEG_MIN)
         seg = SEG_MIN;
@@ -1106,7 +1143,7 @@ int zscrc_device_spans(const void *const *d_bufs, const uint64_t *lens, const ui
         x.stride = seg;
         x.fixed_len = seg;
         x.last_len = seg;
-        if (zs_launch_spans(&x, &m, &fs, c->gtab, c->ncu, s)) {
+        if (zs_launch_spans(&x, &m, &fs, c->gtab, c->ncu, deal != 0, s)) {
             set_err("multi-span launch", hipGetLastError());
             rc = ZSCRC_EHIP;
         } else {
@@ -1423,6 +1460,12 @@ int zscrc_xteam_for(uint64_t len, uint64_t n)
         return 0;
     return team_for(len, n, c->ncu, len, 0) == 64 && g_xteam && g_depth[2] < 0 && len >= g_xteam_min ? g_xteam.load()
                                                                                                         : 0;
+}
+
+unsigned zscrc_set_xdeal(unsigned per_wave)
+{
+    std::call_once(g_env_once, env_init);
+    return g_xdeal.exchange(std::min<unsigned>(per_wave, XDEAL_MAX));
 }
 
 void zscrc_set_qteam(int mode)

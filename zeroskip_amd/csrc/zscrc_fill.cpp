@@ -103,7 +103,40 @@ struct Cache {
     uint64_t host_commits = 0;
     uint32_t *hpairs = nullptr; /* 2 x n */
     uint32_t *hcrc = nullptr;   /* n */
+    /* copy / kernel / copy-back streams and per-chunk events, kept across
+     * calls: creating and destroying them per call cost milliseconds */
+    hipStream_t cs = nullptr, ks = nullptr, os = nullptr;
+    std::vector<hipEvent_t> h2d, kern, d2h;
 };
+
+int ensure_sync(Cache &c, size_t nk)
+{
+    if (!c.cs && (hipStreamCreateWithFlags(&c.cs, hipStreamNonBlocking) != hipSuccess ||
+                  hipStreamCreateWithFlags(&c.ks, hipStreamNonBlocking) != hipSuccess ||
+                  hipStreamCreateWithFlags(&c.os, hipStreamNonBlocking) != hipSuccess)) {
+        for (hipStream_t *s : {&c.cs, &c.ks, &c.os}) {
+            if (*s)
+                (void)hipStreamDestroy(*s);
+            *s = nullptr;
+        }
+        return ZSCRC_EHIP;
+    }
+    while (c.h2d.size() < nk) {
+        hipEvent_t a = nullptr, b = nullptr, d = nullptr;
+        if (hipEventCreateWithFlags(&a, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&b, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&d, hipEventDisableTiming) != hipSuccess) {
+            for (hipEvent_t x : {a, b, d})
+                if (x)
+                    (void)hipEventDestroy(x);
+            return ZSCRC_EHIP;
+        }
+        c.h2d.push_back(a);
+        c.kern.push_back(b);
+        c.d2h.push_back(d);
+    }
+    return ZSCRC_OK;
+}
 constexpr int MAX_DEV = 64;
 Cache g_cache[MAX_DEV];
 
@@ -259,22 +292,10 @@ extern "C" int zscrc_zs_fill_commits(void *image, uint64_t size, const uint64_t 
     max_len = std::min<uint64_t>(max_len, MAX_SHORT);
 
     const size_t nk = chunks.size();
-    hipStream_t cs = nullptr, ks = nullptr, os = nullptr;
-    std::vector<hipEvent_t> h2d(nk, nullptr), kern(nk, nullptr), d2h(nk, nullptr);
-    hipError_t e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking);
-    if (e == hipSuccess)
-        e = hipStreamCreateWithFlags(&ks, hipStreamNonBlocking);
-    if (e == hipSuccess)
-        e = hipStreamCreateWithFlags(&os, hipStreamNonBlocking);
-    for (size_t k = 0; e == hipSuccess && k < nk; ++k) {
-        e = hipEventCreateWithFlags(&h2d[k], hipEventDisableTiming);
-        if (e == hipSuccess)
-            e = hipEventCreateWithFlags(&kern[k], hipEventDisableTiming);
-        if (e == hipSuccess)
-            e = hipEventCreateWithFlags(&d2h[k], hipEventDisableTiming);
-    }
-    if (e != hipSuccess)
-        rc = ZSCRC_EHIP;
+    if (!rc && nk)
+        rc = ensure_sync(c, nk);
+    hipStream_t cs = c.cs, ks = c.ks, os = c.os;
+    const std::vector<hipEvent_t> &h2d = c.h2d, &kern = c.kern, &d2h = c.d2h;
 
     /* tasks, in order: chunk k's descriptors and staging copies; chunk k's
      * patches after chunk k + LAG's copies (its D2H is queued by then) */
@@ -379,10 +400,12 @@ extern "C" int zscrc_zs_fill_commits(void *image, uint64_t size, const uint64_t 
             pool.emplace_back(worker);
 
     double t_h2d = t0;
-    for (size_t k = 0; !rc && k < nk; ++k) {
-        const Chunk &ch = chunks[k];
+    auto wait_ready = [&](size_t k) {
         while (ready[k].load(std::memory_order_acquire) > 0)
             std::this_thread::yield();
+    };
+    for (size_t k = 0; !rc && k < nk; ++k) {
+        const Chunk &ch = chunks[k];
         const int r = (int)(k % RING);
         const uint64_t m = ch.i1 - ch.i0;
         const uint64_t shift = ch.lo & 255; /* the image's alignment within 256 B, kept on the device */
@@ -391,9 +414,18 @@ extern "C" int zscrc_zs_fill_commits(void *image, uint64_t size, const uint64_t 
         if (k >= (size_t)RING && (hipStreamWaitEvent(cs, kern[k - RING], 0) != hipSuccess ||
                                   hipStreamWaitEvent(cs, d2h[k - RING], 0) != hipSuccess))
             rc = ZSCRC_EHIP;
+        /* a pinned image goes on the wire before its descriptors are built;
+         * a staged one once its slot is filled (the slot copies are in ready) */
+        if (staged)
+            wait_ready(k);
         const void *src = staged ? static_cast<const void *>(c.slot[k % NSLOT]) : img + ch.lo;
-        if (!rc && (hipMemcpyAsync(dimg, src, ch.hi - ch.lo, hipMemcpyHostToDevice, cs) != hipSuccess ||
-                    hipMemcpyAsync(c.dpairs[r], c.hpairs + 2 * ch.i0, 8 * m, hipMemcpyHostToDevice, cs) !=
+        if (!rc && hipMemcpyAsync(dimg, src, ch.hi - ch.lo, hipMemcpyHostToDevice, cs) != hipSuccess)
+            rc = ZSCRC_EHIP;
+        if (k == 0)
+            rep->setup_s = now_s() - t0;
+        if (!staged)
+            wait_ready(k);
+        if (!rc && (hipMemcpyAsync(c.dpairs[r], c.hpairs + 2 * ch.i0, 8 * m, hipMemcpyHostToDevice, cs) !=
                         hipSuccess ||
                     hipEventRecord(h2d[k], cs) != hipSuccess))
             rc = ZSCRC_EHIP;
@@ -420,22 +452,12 @@ extern "C" int zscrc_zs_fill_commits(void *image, uint64_t size, const uint64_t 
         stop = 1;
     for (auto &t : pool)
         t.join();
-    if (!rc && (hipStreamSynchronize(ks) != hipSuccess || hipStreamSynchronize(os) != hipSuccess))
+    /* every queued copy and kernel drained before the call returns (an error
+     * part-way leaves work queued on the cached streams otherwise) */
+    if (cs && ks && os &&
+        (hipStreamSynchronize(cs) != hipSuccess || hipStreamSynchronize(ks) != hipSuccess ||
+         hipStreamSynchronize(os) != hipSuccess) && !rc)
         rc = ZSCRC_EHIP;
-    for (size_t k = 0; k < nk; ++k) {
-        if (h2d[k])
-            (void)hipEventDestroy(h2d[k]);
-        if (kern[k])
-            (void)hipEventDestroy(kern[k]);
-        if (d2h[k])
-            (void)hipEventDestroy(d2h[k]);
-    }
-    if (cs)
-        (void)hipStreamDestroy(cs);
-    if (ks)
-        (void)hipStreamDestroy(ks);
-    if (os)
-        (void)hipStreamDestroy(os);
     if (!rc && bad_order)
         rc = ZSCRC_EINVAL; /* unsorted or overlapping spans: what was patched may be wrong */
 

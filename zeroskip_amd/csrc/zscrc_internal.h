@@ -86,7 +86,10 @@ struct BatchDesc {
                              workgroup), 1 << 23 = multi64_kernel's static walk (chunks not
                              dealt per workgroup), 1 << 24 = qteam_kernel's static walk on big
                              batches too (not parts dealt per workgroup: qteam_dyn_kernel +
-                             qfold_kernel), 1 << 25 = parts dealt on small batches too */
+                             qfold_kernel), 1 << 25 = parts dealt on small batches too,
+                             1 << 26 = spans on xteam_kernel's static walk (two segments per
+                             wave, not 16 dealt per workgroup); OPT_XDEAL (1 << 30) is set
+                             by the span launches themselves, not a tuning bit */
     uint32_t *part_out;
     /* commit verdict mode (bad_count != NULL): no per-record out / status;
      * every commit whose status is not 1 is counted in *bad_count and its
@@ -129,6 +132,8 @@ struct QDyn {
  * from base[s], the last one last[s]; block 0 presets *out[s] = preset[s]
  * (the constant terms the fold XORs into). */
 constexpr int SPANS_MAX = 8;
+constexpr uint32_t OPT_XSTATIC = 1u << 26; /* tuning: spans on the static walk           */
+constexpr uint32_t OPT_XDEAL = 1u << 30;   /* internal: this batch is a span's dealt segments */
 struct XMulti {
     uint32_t k;
     uint32_t preset[SPANS_MAX];

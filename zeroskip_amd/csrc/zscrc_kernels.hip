@@ -1023,12 +1023,27 @@ __device__ __forceinline__ void xnext(const XDesc &d, const XMulti &m, const XPa
  * one scalar load per wave. */
 __device__ uint64_t *zs_wave_times = nullptr;
 
-template <int MODE>
+/* DEAL: the launch holds many more items than waves -- a span's segments
+ * (modes 0 and 1; zscrc_api.cpp span_impl / zscrc_device_spans: 16 per
+ * wave), a segment plan's segments (mode 2, plan_segments with 16 per wave;
+ * an item is the segment's part range [seg_first[j], seg_first[j + 1])), or
+ * a per-record plan's parts -- and a workgroup deals its own (its static
+ * items 16 b + i % 16 + (i / 16) nw, in that order) to its waves from an LDS
+ * counter: the next item fetched an item ahead, the load walk one step ahead
+ * across items, the hashing walk taking the record / part the load walk
+ * moved to; each result stored on its own.  Per-wave timestamps put the
+ * static walk's waves' ends on a 3 GiB span between 424 us (p10) and 503 us,
+ * the median workgroup's 16 waves 57 us apart
+ * (profiles/r04/wave_spread.jsonl), as with qteam. */
+template <int MODE, bool DEAL = false>
 __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp, const uint32_t *__restrict__ gtab)
 {
     const uint64_t t_entry = __builtin_amdgcn_s_memrealtime();
     constexpr bool MULTI = MODE == 1;
     __shared__ __attribute__((aligned(16))) char L[LDS_BYTES];
+    /* DEAL: the workgroup's counter in the bytes after fill_lds<64>'s six Z tables */
+    static_assert(OFF_Z + 6 * 4096 + 4 <= LDS_BYTES, "no room for the LDS counter");
+    uint32_t &lctr = *reinterpret_cast<uint32_t *>(L + OFF_Z + 6 * 4096);
     if (MODE == 2) { /* parts of a split class: their count is on the device */
         d.n = __builtin_amdgcn_readfirstlane(((const volatile uint32_t *)&xp.plan[xp.klass].parts)[0]);
         xp.seg = __builtin_amdgcn_readfirstlane(((const volatile uint32_t *)&xp.plan[xp.klass].seg)[0]);
@@ -1040,6 +1055,8 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp,
         return;
     if (MULTI && blockIdx.x == 0 && threadIdx.x < m.k)
         m.out[threadIdx.x][0] = m.preset[threadIdx.x]; /* the fold kernel (next on the stream) XORs into it */
+    if (DEAL && threadIdx.x == 0)
+        lctr = 0;
     fill_lds<64>(L, gtab);
     __syncthreads();
     const uint64_t t_fill = __builtin_amdgcn_s_memrealtime();
@@ -1060,11 +1077,71 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp,
         }
     }
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(gtab);
-
+    /* DEAL: the workgroup's counter (lane 0 asks; the answer stays in its
+     * register until the item is started) */
+    auto fetch = [&]() -> uint32_t {
+        uint32_t u = 0;
+        if (lane == 0)
+            u = atomicAdd(&lctr, 1u);
+        return u;
+    };
+    const uint64_t nitems = (MODE == 2 && xp.seg) ? xp.seg : d.n;
+    auto deal_item = [&](uint32_t raw) -> uint64_t {
+        const uint32_t u = __builtin_amdgcn_readlane(raw, 0);
+        const uint64_t w = (uint64_t)blockIdx.x * WAVES + u % WAVES + (uint64_t)(u / WAVES) * nteams;
+        return w < nitems ? w : nitems;
+    };
     XLoad ld;
-    ld.w = wbeg;
-    ld.wend = wend;
+    /* the dealt item j as the load walk's range [ld.w, ld.wend) of records /
+     * parts; none left (or an empty segment: the later ones are empty too):
+     * ld.w = ld.wend = d.n */
+    auto begin_item = [&](uint64_t j) -> bool {
+        ld.w = ld.wend = d.n;
+        if (j >= nitems)
+            return false;
+        if (MODE == 2 && xp.seg) {
+            const uint64_t a = __builtin_amdgcn_readfirstlane(((g32p)xp.seg_first)[j]);
+            const uint64_t b = __builtin_amdgcn_readfirstlane(((g32p)xp.seg_first)[j + 1]);
+            if (a >= b)
+                return false;
+            ld.w = a;
+            ld.wend = b;
+            return true;
+        }
+        ld.w = j;
+        ld.wend = j + 1;
+        return true;
+    };
+    uint32_t pend = 0, items = 0;
+    if (DEAL) {
+        if (begin_item(deal_item(fetch())))
+            pend = fetch();
+        wbeg = ld.w;
+        wend = d.n; /* the hashing walk's bound: it follows the load walk */
+    } else {
+        ld.w = wbeg;
+        ld.wend = wend;
+    }
     xrec<MODE>(d, m, xp, ld);
+    /* the load walk's next step: a dealt item after the current one */
+    auto advance = [&]() {
+        if (!DEAL) {
+            xnext<MODE>(d, m, xp, ld);
+            return;
+        }
+        if (ld.ok && ld.left) {
+            --ld.left;
+            ld.V += XSTEP;
+            return;
+        }
+        if (ld.w >= ld.wend)
+            return;
+        if (ld.w + 1 < ld.wend)
+            ++ld.w; /* the item's next record / part */
+        else if (begin_item(deal_item(pend)))
+            pend = fetch();
+        xrec<MODE>(d, m, xp, ld);
+    };
     uint32_t b0[16], b1[16];
     const uint32_t voff = 64u * (uint32_t)c + 16u * (uint32_t)g;
     xissue(ld.V, ld.ok, voff, dummy, ld.lo, b0);
@@ -1085,13 +1162,21 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp,
         }
     };
     /* hash the step in w (the hashing walk's position it / s) */
+    /* the hashing walk's next item: the one the load walk (a step ahead) is on */
+    auto next_item = [&]() { return DEAL ? ld.w : it.w + 1; };
     auto hash = [&](uint32_t (&w)[16]) {
         if (it.S == 0) { /* < 8 bytes: byte-serial (every lane, same result) */
             uint32_t r = it.R0;
             for (uint64_t i = 0; i < it.len; ++i)
                 r = byte_step(L, r, ((g8p)it.A)[i], c_hi);
-            stash_put(r ^ d.xor_io);
-            ok = xitem<MODE>(d, m, xp, it.w + 1, wend, it);
+            if (DEAL) {
+                if (lane == 0)
+                    d.out[it.w] = r ^ d.xor_io;
+                ++items;
+            } else {
+                stash_put(r ^ d.xor_io);
+            }
+            ok = xitem<MODE>(d, m, xp, next_item(), wend, it);
             return;
         }
         xpose16(w);
@@ -1115,18 +1200,24 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp,
         if (tail && lane == 63)
             for (uint32_t i = 0; i < tail; ++i)
                 acc = byte_step(L, acc, ((g8p)it.E)[i], c_hi);
-        stash_put(__shfl(acc, 63) ^ d.xor_io);
+        if (DEAL) {
+            if (lane == 63)
+                d.out[it.w] = acc ^ d.xor_io;
+            ++items;
+        } else {
+            stash_put(__shfl(acc, 63) ^ d.xor_io);
+        }
         acc = 0;
         s = 0;
-        ok = xitem<MODE>(d, m, xp, it.w + 1, wend, it);
+        ok = xitem<MODE>(d, m, xp, next_item(), wend, it);
     };
     while (ok) {
-        xnext<MODE>(d, m, xp, ld);
+        advance();
         xissue(ld.V, ld.ok, voff, dummy, ld.lo, b1);
         hash(b0);
         if (!ok)
             break;
-        xnext<MODE>(d, m, xp, ld);
+        advance();
         xissue(ld.V, ld.ok, voff, dummy, ld.lo, b0);
         hash(b1);
     }
@@ -1138,7 +1229,7 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp,
         wt[4 * team + 0] = t_entry;
         wt[4 * team + 1] = t_fill;
         wt[4 * team + 2] = t_end;
-        wt[4 * team + 3] = wend - wbeg;
+        wt[4 * team + 3] = DEAL ? items : wend - wbeg;
     }
 }
 
@@ -3934,13 +4025,17 @@ extern "C" int zs_launch_xteam(int depth, const zs::BatchDesc *bd, const uint32_
         none.k = 0;
         zs::XParts np;
         memset(&np, 0, sizeof np);
-        hipLaunchKernelGGL(zs::xteam_kernel<0>, dim3(grid), dim3(zs::WG), 0, stream, *d, none, np, gtab);
+        if (bd->opt & zs::OPT_XDEAL) /* a span's segments, dealt per workgroup */
+            hipLaunchKernelGGL((zs::xteam_kernel<0, true>), dim3(grid), dim3(zs::WG), 0, stream, *d, none, np, gtab);
+        else
+            hipLaunchKernelGGL(zs::xteam_kernel<0>, dim3(grid), dim3(zs::WG), 0, stream, *d, none, np, gtab);
     }
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
 /* the parts of a split length class on the coalesced whole-wave teams */
-extern "C" int zs_launch_xparts(const zs::BatchDesc *bd, const uint32_t *gtab, int grid, hipStream_t stream)
+extern "C" int zs_launch_xparts(const zs::BatchDesc *bd, const uint32_t *gtab, int grid, int deal,
+                                hipStream_t stream)
 {
     zs::XDesc x;
     memset(&x, 0, sizeof x);
@@ -3960,7 +4055,10 @@ extern "C" int zs_launch_xparts(const zs::BatchDesc *bd, const uint32_t *gtab, i
     p.rec_start = bd->rec_start;
     p.seg_first = bd->seg_first;
     p.seg = 0; /* read from the plan on the device */
-    hipLaunchKernelGGL(zs::xteam_kernel<2>, dim3(grid), dim3(zs::WG), 0, stream, x, none, p, gtab);
+    if (deal) /* segments (or parts) dealt per workgroup */
+        hipLaunchKernelGGL((zs::xteam_kernel<2, true>), dim3(grid), dim3(zs::WG), 0, stream, x, none, p, gtab);
+    else
+        hipLaunchKernelGGL(zs::xteam_kernel<2>, dim3(grid), dim3(zs::WG), 0, stream, x, none, p, gtab);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -4066,11 +4164,14 @@ extern "C" int zs_launch_multi(const zs::BatchDesc *d, const zs::MultiBatch *m, 
 }
 
 extern "C" int zs_launch_spans(const zs::XDesc *x, const zs::XMulti *m, const zs::SpanFolds *fs,
-                               const uint32_t *gtab, int grid, hipStream_t stream)
+                               const uint32_t *gtab, int grid, int deal, hipStream_t stream)
 {
     zs::XParts np;
     memset(&np, 0, sizeof np);
-    hipLaunchKernelGGL(zs::xteam_kernel<1>, dim3(grid), dim3(zs::WG), 0, stream, *x, *m, np, gtab);
+    if (deal)
+        hipLaunchKernelGGL((zs::xteam_kernel<1, true>), dim3(grid), dim3(zs::WG), 0, stream, *x, *m, np, gtab);
+    else
+        hipLaunchKernelGGL(zs::xteam_kernel<1>, dim3(grid), dim3(zs::WG), 0, stream, *x, *m, np, gtab);
     if (hipGetLastError() != hipSuccess)
         return -3;
     uint32_t bx = 1;

@@ -182,7 +182,7 @@ class FillReport(ctypes.Structure):
     _fields_ = [("commits", ctypes.c_uint64), ("no_record", ctypes.c_uint64), ("long_commits", ctypes.c_uint64),
                 ("bytes", ctypes.c_uint64), ("desc_bytes", ctypes.c_uint64), ("chunks", ctypes.c_uint64),
                 ("staged", ctypes.c_int32), ("threads", ctypes.c_int32), ("h2d_s", ctypes.c_double),
-                ("total_s", ctypes.c_double)]
+                ("total_s", ctypes.c_double), ("setup_s", ctypes.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
