@@ -292,9 +292,11 @@ class Timer:
     def __init__(self, world: int, dev):
         self.world, self.dev = world, dev
 
-    def run(self, step, steps: int, warmup: int) -> float:
+    def run(self, step, steps: int, warmup: int, drain=None) -> float:
         for _ in range(warmup):
             step(None)
+        if drain:
+            drain()
         torch.cuda.synchronize()
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(steps)]
@@ -304,6 +306,8 @@ class Timer:
         t0 = time.perf_counter()
         for i in range(steps):
             step(ev[i])
+        if drain:       # outstanding asynchronous work of the steps, inside the timed region
+            drain()
         torch.cuda.synchronize()
         if self.world > 1:
             dist.barrier()
@@ -354,18 +358,34 @@ def run_config3(args, world, rank, dev, stream):
     g = torch.Generator(device=dev)
     g.manual_seed(0x9E3779B9 + rank)
     data = torch.randint(0, 256, (NCHUNK * CHUNK,), dtype=torch.uint8, device=dev, generator=g)
-    out = torch.empty(NCHUNK, dtype=torch.int32, device=dev)
-    gathered = torch.empty(NCHUNK * world, dtype=torch.int32, device=dev) if world > 1 else None
+    # two digest buffers: step k's all-gather (async, on the collective's own
+    # stream) runs beside step k+1's kernel; a buffer is reused only after
+    # the gather that read it is done, and every gather completes inside the
+    # timed region (drain)
+    outs = [torch.empty(NCHUNK, dtype=torch.int32, device=dev) for _ in range(2)]
+    gathered = [torch.empty(NCHUNK * world, dtype=torch.int32, device=dev) for _ in range(2)] if world > 1 else None
+    pend, nstep = [None, None], [0]
 
     def step(ev):
+        i = nstep[0] % 2
+        nstep[0] += 1
+        if pend[i] is not None:
+            pend[i].wait()
+            pend[i] = None
         if ev:
             ev[0].record(stream)
-        check(lib().zscrc_device_fixed(data.data_ptr(), CHUNK, CHUNK, 0, out.data_ptr(), NCHUNK,
+        check(lib().zscrc_device_fixed(data.data_ptr(), CHUNK, CHUNK, 0, outs[i].data_ptr(), NCHUNK,
                                        0, stream.cuda_stream), "zscrc_device_fixed")
         if ev:
             ev[1].record(stream)
         if world > 1:
-            dist.all_gather_into_tensor(gathered, out)
+            pend[i] = dist.all_gather_into_tensor(gathered[i], outs[i], async_op=True)
+
+    def drain():
+        for i in range(2):
+            if pend[i] is not None:
+                pend[i].wait()
+                pend[i] = None
 
     # The same-GPU read ceiling is measured first, right before the warmup:
     # config 3 runs at the package's 1400 W cap, and the power controller's
@@ -375,8 +395,12 @@ def run_config3(args, world, rank, dev, stream):
     # its loaded operating point as a sustained checksum job finds it.
     read_peak = read_ceiling(data, NCHUNK * CHUNK, stream)
     tm = Timer(world, dev)
-    elapsed = tm.run(step, args.steps, args.warmup)
+    elapsed = tm.run(step, args.steps, args.warmup, drain=drain)
     kern_ms = float(np.mean(tm.kern_ms))
+    out = outs[(nstep[0] - 1) % 2]   # the last timed step's digests
+    if world > 1:
+        # every rank's digests of the last step, as gathered
+        assert torch.equal(gathered[(nstep[0] - 1) % 2][rank * NCHUNK:(rank + 1) * NCHUNK], out)
     # after the timed region, reported beside it (never the value): the
     # kernel over 200 back-to-back calls, the sustained power-capped rate
     sus = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(200)]

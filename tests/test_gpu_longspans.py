@@ -7,8 +7,8 @@ classify -> plan -> parts (xteam_kernel's parts mode for class 3, team<16>
 parts for class 2) -> part fold; every CRC, status, verdict and written CRC
 against the format oracle, on both class-3 routes (xteam parts and team<64>
 parts, tuning bit 65536; the segment plan -- the class's bytes end to end
-cut into 16 equal segments per wave dealt per workgroup, or one per wave on the static walk, bit
-1 << 26 -- and per-record parts, bit 256) and both classify forms (one single-block launch
+cut into one equal segment per wave, or 16 per wave dealt per workgroup, bit 1 << 27 -- and
+per-record parts, bit 256) and both classify forms (one single-block launch
 with the plans, or two passes and plan launches: bit 524288), with corruptions at a record's first byte, its
 last span byte, its stored CRC and bytes either side of a part boundary."""
 import numpy as np
@@ -25,9 +25,9 @@ pytestmark = pytest.mark.gpu
 TEAM64_PARTS = 65536  # zs::BatchDesc::opt: class 3 on team<64> parts instead of xteam parts
 MULTI_CLASSIFY = 524288  # opt: two multi-block classify passes + plan launches (not the single-block one)
 RECORD_PARTS = 256  # opt: class 3 parts cut per record instead of the segment plan
-XSTATIC = 1 << 26  # opt: one segment per wave on xteam's static walk (not 16 per wave dealt per workgroup)
-OPTS = [0, TEAM64_PARTS, MULTI_CLASSIFY, RECORD_PARTS, XSTATIC]
-IDS = ["xteam-segments-dealt", "team64-parts", "multi-classify", "xteam-record-parts", "xteam-segments-static"]
+XDEAL_PARTS = 1 << 27  # opt: segment plans of 16 segments per wave dealt per workgroup (default: one per wave)
+OPTS = [0, TEAM64_PARTS, MULTI_CLASSIFY, RECORD_PARTS, XDEAL_PARTS]
+IDS = ["xteam-segments", "team64-parts", "multi-classify", "xteam-record-parts", "xteam-segments-dealt"]
 
 # transaction sizes in bytes of value payload: class 3 (> g16_max) records
 # of 0.3-3 MiB, one past 16 MiB (long commit), class 2 and short ones beside

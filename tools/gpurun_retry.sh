@@ -4,7 +4,7 @@
 # off).  A call that ran (any exit status of the command) is never repeated.
 # usage: tools/gpurun_retry.sh TIMEOUT 'command'
 t=$1; shift
-for attempt in 1 2 3 4 5 6 7 8; do
+for attempt in $(seq 1 40); do
     rm -f gpurun_out/.last_call.json
     /usr/local/graft/bin/gpurun --timeout "$t" -- "$@" > /tmp/gpurun_attempt.log 2>&1
     rc=$?

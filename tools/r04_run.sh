@@ -23,11 +23,20 @@ for step in "$@"; do
                 >> gpurun_out/bench4q.jsonl 2>> gpurun_out/bench4q.err ;;
     abspan)   AB_CASES=span_3GiB,spans_config5 timeout -k 10 600 python tools/opt_ab.py 0 67108864 \
                 > gpurun_out/abspan.jsonl 2> gpurun_out/abspan.err ;;
+    pmc2box)  timeout -k 10 180 python -c "import json, bench; print(json.dumps(bench.box_info(0)))" > gpurun_out/box.json \
+                2> gpurun_out/box.err && bash tools/pmc_case.sh config2 && bash tools/pmc_case.sh config3 ;;
     nbseq)    bash tools/nb_seq.sh ;;
+    xdeal)    timeout -k 10 600 python tools/xdeal_ab.py > gpurun_out/xdeal_ab.jsonl 2> gpurun_out/xdeal_ab.err ;;
+    abnb)     AB_CASES=config4_nb timeout -k 10 600 python tools/opt_ab.py 0 67108864 \
+                > gpurun_out/abnb.jsonl 2> gpurun_out/abnb.err ;;
+    longtests) timeout -k 10 600 $T tests/test_gpu_longspans.py > gpurun_out/longtests.log 2>&1 ;;
     tracebench) bash tools/trace_bench.sh config3 config4 config2 config5 ;;
     spantests) timeout -k 10 600 $T tests/test_gpu_stream.py tests/test_gpu_parity.py -k "span" \
                 > gpurun_out/spantests.log 2>&1 ;;
     fillsweep) timeout -k 10 600 python tools/fill_sweep.py > gpurun_out/fill_sweep.jsonl 2> gpurun_out/fill_sweep.err ;;
+    rehearse3)
+              BENCH_SHARE_GPU=1 BENCH_DIST=gloo timeout -k 10 600 python bench.py --gpus 2 --workload config3 \
+                --no-cpu > gpurun_out/rehearse3_n2.json 2> gpurun_out/rehearse3_n2.err ;;
     rehearse5)
               BENCH_SHARE_GPU=1 BENCH_DIST=gloo timeout -k 10 900 python bench.py --gpus 2 --workload config5 \
                 --no-cpu > gpurun_out/rehearse5_n2.json 2> gpurun_out/rehearse5_n2.err ;;

@@ -559,7 +559,11 @@ int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1
      * wave, or xdeal per wave dealt per workgroup */
     const bool xparts = g_xteam && !(d.opt & 65536);
     const bool xseg = xparts && !(d.opt & (256 | 131072));
-    const uint32_t xdeal = xseg ? xdeal_for(d.opt) : 0u;
+    /* dealt segment plans (16 per wave) measured slower on NOTBATCHED: the
+     * single-block plan of ~67 k parts 27 -> 85 us, the parts' geometry loads
+     * and the fold outweigh the balance (0.559 -> 0.603 ms interleaved,
+     * profiles/r04/ab_notbatched_xdeal.jsonl); tuning bit 1 << 27 for A/B */
+    const uint32_t xdeal = xseg && (d.opt & zs::OPT_XDEAL_PARTS) ? xdeal_for(d.opt) : 0u;
     const size_t nseg3 = (size_t)c->ncu * 16u * (xdeal ? xdeal : 1u);
     const size_t P3 = 2 * T > T + nseg3 ? 2 * T : T + nseg3;
     /* parts buffer: class 2 part registers (< 2T), part_rec (< 2T),

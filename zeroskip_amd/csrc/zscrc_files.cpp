@@ -152,8 +152,50 @@ struct Cache {
     uint64_t *h_bad = nullptr; /* pinned: the verdict's count + listed indices */
     uint8_t *dq = nullptr;     /* device: the stale-commit re-verification batch */
     uint64_t dq_bytes = 0;
+    /* copy and compute streams and their events, kept across calls (creating
+     * and destroying them per group cost milliseconds per call) */
+    hipStream_t cs = nullptr, ks = nullptr;
+    hipEvent_t slot_ev[NSLOT] = {};
+    hipEvent_t done_ev = nullptr;
 };
 Cache g_cache[MAX_SLOTS];
+
+void sync_free(Cache &c)
+{
+    for (hipStream_t s : {c.cs, c.ks})
+        if (s) {
+            (void)hipStreamSynchronize(s);
+            (void)hipStreamDestroy(s);
+        }
+    for (auto &e : c.slot_ev)
+        if (e)
+            (void)hipEventDestroy(e);
+    if (c.done_ev)
+        (void)hipEventDestroy(c.done_ev);
+    c.cs = c.ks = nullptr;
+    for (auto &e : c.slot_ev)
+        e = nullptr;
+    c.done_ev = nullptr;
+}
+
+int ensure_sync(Cache &c)
+{
+    if (c.cs && c.ks && c.done_ev)
+        return ZSCRC_OK;
+    sync_free(c);
+    hipError_t e = hipStreamCreateWithFlags(&c.cs, hipStreamNonBlocking);
+    if (e == hipSuccess)
+        e = hipStreamCreateWithFlags(&c.ks, hipStreamNonBlocking);
+    for (int k = 0; e == hipSuccess && k < NSLOT; ++k)
+        e = hipEventCreateWithFlags(&c.slot_ev[k], hipEventDisableTiming);
+    if (e == hipSuccess)
+        e = hipEventCreateWithFlags(&c.done_ev, hipEventDisableTiming);
+    if (e != hipSuccess) {
+        sync_free(c);
+        return ZSCRC_EHIP;
+    }
+    return ZSCRC_OK;
+}
 
 /* commits a group's verdict lists (more mismatches: the per-commit status
  * arrays instead) */
@@ -180,6 +222,7 @@ void cache_free(Cache &c)
         (void)hipHostFree(c.h_bad);
     if (c.dq)
         (void)hipFree(c.dq);
+    sync_free(c);
     const int dev = c.dev;
     c.dev = dev; /* keep the binding; everything else reset */
     c.slot_bytes = 0;
@@ -438,17 +481,10 @@ int run_group(Call &C, Cache &cache, std::vector<Ext *> &G, int threads)
     for (; qf < ng; ++qf)
         tasks.push_back({1, qf, 0});
 
-    hipStream_t cs = nullptr, ks = nullptr;
-    hipEvent_t slot_ev[NSLOT] = {}, done_ev = nullptr;
-    hipError_t e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking);
-    if (e == hipSuccess)
-        e = hipStreamCreateWithFlags(&ks, hipStreamNonBlocking);
-    for (int k = 0; e == hipSuccess && k < NSLOT; ++k)
-        e = hipEventCreateWithFlags(&slot_ev[k], hipEventDisableTiming);
-    if (e == hipSuccess)
-        e = hipEventCreateWithFlags(&done_ev, hipEventDisableTiming);
-    if (e != hipSuccess)
-        rc = ZSCRC_EHIP;
+    if (!rc)
+        rc = ensure_sync(cache);
+    hipStream_t cs = cache.cs, ks = cache.ks;
+    hipEvent_t *slot_ev = cache.slot_ev, done_ev = cache.done_ev;
 
     std::atomic<uint64_t> next{0};
     std::atomic<int> stop{0};
@@ -751,15 +787,11 @@ int run_group(Call &C, Cache &cache, std::vector<Ext *> &G, int threads)
             C.acc.first(x.file, cache.h_off[i] - x.dev_off + x.lo + cache.h_len[i], ZSCRC_FILES_BAD_COMMIT);
         }
     }
-    for (int k = 0; k < NSLOT; ++k)
-        if (slot_ev[k])
-            (void)hipEventDestroy(slot_ev[k]);
-    if (done_ev)
-        (void)hipEventDestroy(done_ev);
-    if (cs)
-        (void)hipStreamDestroy(cs);
-    if (ks)
-        (void)hipStreamDestroy(ks);
+    /* nothing of this group left queued on the cached streams (error paths
+     * included) before the buffers serve another group */
+    for (hipStream_t q : {cs, ks})
+        if (q && hipStreamSynchronize(q) != hipSuccess && !rc)
+            rc = ZSCRC_EHIP;
     {
         std::lock_guard<std::mutex> lk(C.tmu);
         C.copy_s = std::max(C.copy_s, t_copied - t_start);

@@ -88,7 +88,9 @@ struct BatchDesc {
                              batches too (not parts dealt per workgroup: qteam_dyn_kernel +
                              qfold_kernel), 1 << 25 = parts dealt on small batches too,
                              1 << 26 = spans on xteam_kernel's static walk (two segments per
-                             wave, not 16 dealt per workgroup); OPT_XDEAL (1 << 30) is set
+                             wave, not 16 dealt per workgroup), 1 << 27 = class-3 segment
+                             plans dealt per workgroup too (g_xdeal segments per wave; default
+                             one per wave, static); OPT_XDEAL (1 << 30) is set
                              by the span launches themselves, not a tuning bit */
     uint32_t *part_out;
     /* commit verdict mode (bad_count != NULL): no per-record out / status;
@@ -133,6 +135,7 @@ struct QDyn {
  * (the constant terms the fold XORs into). */
 constexpr int SPANS_MAX = 8;
 constexpr uint32_t OPT_XSTATIC = 1u << 26; /* tuning: spans on the static walk           */
+constexpr uint32_t OPT_XDEAL_PARTS = 1u << 27; /* tuning: class-3 segment plans dealt too */
 constexpr uint32_t OPT_XDEAL = 1u << 30;   /* internal: this batch is a span's dealt segments */
 struct XMulti {
     uint32_t k;
@@ -161,6 +164,8 @@ struct XParts {
     const uint64_t *rec_start; /* segment plans: see SplitPlan::seg */
     const uint32_t *seg_first; /* segment plans: first part of segment w */
     uint32_t seg;              /* the plan's seg (read on the device)     */
+    uint32_t first_rec;        /* the class's first record in desc (device) */
+    uint64_t U;                /* the plan's unit / segment bytes (device)  */
 };
 
 /* consistent's device post pass (zscrc_cpass, cpass_post_kernel): the

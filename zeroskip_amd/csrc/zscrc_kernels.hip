@@ -827,16 +827,13 @@ __device__ __forceinline__ void xgeom(const XDesc &d, const XMulti &m, const XPa
         R0 = d.seed ^ d.xor_io;
         return;
     }
-    if (MODE == 2) {
-        uint32_t first = 0;
-        for (uint32_t k = 0; k < xp.klass; ++k)
-            first += __builtin_amdgcn_readfirstlane(((g32p)xp.class_count)[k]);
+    if (MODE == 2) { /* xp.first_rec / xp.U: read once per wave at kernel start */
         const uint32_t idx = __builtin_amdgcn_readfirstlane(((g32p)xp.part_rec)[w]);
-        const RecDesc *r = xp.desc + first + idx;
+        const RecDesc *r = xp.desc + xp.first_rec + idx;
         typedef const __attribute__((address_space(1))) uint64_t *g64p;
         const uint64_t off = uni64(((g64p)r)[0]), rlen = uni64(((g64p)r)[1]);
         const uint32_t seed = __builtin_amdgcn_readfirstlane(((g32p)r)[4]);
-        const uint64_t U = uni64(((g64p)(xp.plan + xp.klass))[0]);
+        const uint64_t U = xp.U;
         const uint64_t part = w - __builtin_amdgcn_readfirstlane(((g32p)xp.part_base)[idx]);
         uint64_t a;
         if (xp.seg) { /* the part is segment j0 + part's piece of the record */
@@ -861,29 +858,6 @@ __device__ __forceinline__ void xgeom(const XDesc &d, const XMulti &m, const XPa
     len = w + 1 == m.first[k + 1] ? m.last[k] : m.seg[k];
     A = reinterpret_cast<uintptr_t>(m.base[k]) + j * m.seg[k];
     lo = reinterpret_cast<uintptr_t>(m.base[k]) & ~uintptr_t(3);
-}
-
-template <int MODE>
-__device__ __forceinline__ bool xitem(const XDesc &d, const XMulti &m, const XParts &xp, uint64_t w, uint64_t wend,
-                                      XItem &it)
-{
-    if (w >= wend)
-        return false;
-    uintptr_t A, lo;
-    uint64_t len;
-    uint32_t R0;
-    xgeom<MODE>(d, m, xp, w, A, len, lo, R0);
-    const uintptr_t E = len < 8 ? A : ((A + len) & ~uintptr_t(3));
-    const uint32_t S = len < 8 ? 0u : (uint32_t)((E - A + XSTEP - 1) / XSTEP);
-    it.A = A;
-    it.E = E;
-    it.V0 = E - (uint64_t)S * XSTEP;
-    it.S = S;
-    it.len = len;
-    it.w = w;
-    it.R0 = R0;
-    it.lo = lo;
-    return true;
 }
 
 /* Issue the four coalesced nt loads of the step at `step` (wave-uniform):
@@ -987,6 +961,9 @@ struct XLoad {
     uint32_t left; /* steps of the record after this one */
     bool ok;       /* a record with >= 8 bytes: loads */
     uintptr_t lo;  /* the record's buffer clamp bound */
+    XItem cur;     /* the record's whole geometry: the hashing walk, one step
+                      behind, takes it when it reaches the record (one
+                      geometry per record, not one per walk) */
 };
 
 template <int MODE>
@@ -1001,6 +978,14 @@ __device__ __forceinline__ void xrec(const XDesc &d, const XMulti &m, const XPar
     l.V = E - S * XSTEP;
     l.left = S ? (uint32_t)(S - 1) : 0u;
     l.ok = l.w < l.wend && S; /* a record without loads: its one position reads the dummy */
+    l.cur.A = A;
+    l.cur.E = E;
+    l.cur.V0 = l.V;
+    l.cur.S = (uint32_t)S;
+    l.cur.len = len;
+    l.cur.w = l.w;
+    l.cur.R0 = R0;
+    l.cur.lo = l.lo;
 }
 
 template <int MODE>
@@ -1049,6 +1034,11 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp,
         xp.seg = __builtin_amdgcn_readfirstlane(((const volatile uint32_t *)&xp.plan[xp.klass].seg)[0]);
         d.out = xp.part_out;
         d.xor_io = 0; /* raw part registers */
+        uint32_t first = 0;
+        for (uint32_t k = 0; k < xp.klass; ++k)
+            first += __builtin_amdgcn_readfirstlane(((g32p)xp.class_count)[k]);
+        xp.first_rec = first;
+        xp.U = uni64(((const __attribute__((address_space(1))) uint64_t *)(xp.plan + xp.klass))[0]);
     }
     /* segment plans: wave w takes segment w's parts (every block works) */
     if ((MODE != 2 || !xp.seg) && (uint64_t)blockIdx.x * WAVES >= d.n)
@@ -1146,7 +1136,15 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp,
     const uint32_t voff = 64u * (uint32_t)c + 16u * (uint32_t)g;
     xissue(ld.V, ld.ok, voff, dummy, ld.lo, b0);
     XItem it;
-    bool ok = xitem<MODE>(d, m, xp, wbeg, wend, it);
+    /* the hashing walk's next record / part: the one the load walk (a step
+     * ahead; at the start, level) is on, with the geometry it computed */
+    auto take = [&]() -> bool {
+        if (ld.w >= wend)
+            return false;
+        it = ld.cur;
+        return true;
+    };
+    bool ok = take();
     uint32_t s = 0;
     uint32_t acc = 0;
     /* Results wait in a register (lane k: the k-th record of the current
@@ -1162,8 +1160,6 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp,
         }
     };
     /* hash the step in w (the hashing walk's position it / s) */
-    /* the hashing walk's next item: the one the load walk (a step ahead) is on */
-    auto next_item = [&]() { return DEAL ? ld.w : it.w + 1; };
     auto hash = [&](uint32_t (&w)[16]) {
         if (it.S == 0) { /* < 8 bytes: byte-serial (every lane, same result) */
             uint32_t r = it.R0;
@@ -1176,7 +1172,7 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp,
             } else {
                 stash_put(r ^ d.xor_io);
             }
-            ok = xitem<MODE>(d, m, xp, next_item(), wend, it);
+            ok = take();
             return;
         }
         xpose16(w);
@@ -1209,7 +1205,7 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp,
         }
         acc = 0;
         s = 0;
-        ok = xitem<MODE>(d, m, xp, next_item(), wend, it);
+        ok = take();
     };
     while (ok) {
         advance();
@@ -3528,6 +3524,22 @@ __device__ __forceinline__ void plan_write(const PlanArgs &a, SplitPlan *pl, con
     }
 }
 
+/* part_rec for a chunk of 1024 records whose first parts are sbase[0..1024]
+ * (LDS; sbase[1024] = the chunk's end): wave wv writes the parts of its 64
+ * records one record after another, 64 parts per store instruction -- a few
+ * uniform iterations per record, where a binary search per part was a chain
+ * of ten dependent LDS reads for every one of ~67 k parts of a 16-per-wave
+ * segment plan. */
+__device__ __forceinline__ void fill_part_rec(uint32_t *part_rec, const uint32_t *sbase, uint32_t c0, int wv, int lane)
+{
+    for (int i = 0; i < 64; ++i) {
+        const int r = wv * 64 + i;
+        const uint32_t q0 = sbase[r], q1 = sbase[r + 1];
+        for (uint32_t q = q0 + (uint32_t)lane; q < q1; q += 64)
+            part_rec[q] = c0 + (uint32_t)r;
+    }
+}
+
 /* Segment plan (SplitPlan::seg): the class's bytes end to end cut into
  * nseg segments of G bytes (G >= bytes / nseg, a multiple of 64), segment
  * w for wave w of the xteam_kernel launch; record r (its first byte at S_r
@@ -3595,18 +3607,8 @@ __device__ void plan_segments(const PlanArgs &a, const RecDesc *list, SplitPlan 
                 a.seg_first[j] = pbase + (uint32_t)(j - j0);
         }
         __syncthreads();
-        const uint32_t lo = sbase[0], hi = sbase[1024];
-        for (uint32_t q = lo + t; q < hi; q += 1024) {
-            uint32_t a0 = 0, a1 = 1024;
-            while (a1 - a0 > 1) {
-                const uint32_t mid = (a0 + a1) >> 1;
-                if (sbase[mid] <= q)
-                    a0 = mid;
-                else
-                    a1 = mid;
-            }
-            a.part_rec[q] = c0 + a0;
-        }
+        const uint32_t hi = sbase[1024];
+        fill_part_rec(a.part_rec, sbase, c0, wv, lane);
         running = hi;
         run_bytes += ctot;
         __syncthreads();
@@ -3682,19 +3684,8 @@ __device__ void plan_block(const PlanArgs &a, uint32_t first, uint32_t count, ui
         if (r < count)
             a.part_base[r] = incl - np;
         __syncthreads();
-        const uint32_t lo = sbase[0], hi = sbase[1024];
-        for (uint32_t q = lo + t; q < hi; q += 1024) {
-            /* largest i with sbase[i] <= q: the record holding part q */
-            uint32_t a0 = 0, a1 = 1024;
-            while (a1 - a0 > 1) {
-                const uint32_t mid = (a0 + a1) >> 1;
-                if (sbase[mid] <= q)
-                    a0 = mid;
-                else
-                    a1 = mid;
-            }
-            a.part_rec[q] = c0 + a0;
-        }
+        const uint32_t hi = sbase[1024];
+        fill_part_rec(a.part_rec, sbase, c0, wv, lane);
         running = hi;
         __syncthreads();
     }
