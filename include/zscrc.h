@@ -197,9 +197,10 @@ void zscrc_set_xteam(int mode, uint64_t min_len);
  * multiple of 4): mode 0 = off, 1 = on (env ZSCRC_QTEAM) */
 void zscrc_set_qteam(int mode);
 /* tuning: spans on xteam_kernel cut into per_wave segments per wave, dealt to
- * each workgroup's waves by an LDS counter (default 16, the most; env
- * ZSCRC_XDEAL); 0 = the static walk, two contiguous segments per wave.
- * Returns the previous setting. */
+ * each workgroup's waves by an LDS counter (default 16, the most; a
+ * multi-span launch, zscrc_device_spans, takes at most 4; env ZSCRC_XDEAL);
+ * 0 = the static walk, two contiguous segments per wave.  Returns the
+ * previous setting. */
 unsigned zscrc_set_xdeal(unsigned per_wave);
 /* tuning bits (env ZSCRC_OPT), for A/B runs: 1 = hash five-piece record
  * bursts as one chain instead of three; 2 = 64-byte record batches of

@@ -1097,7 +1097,11 @@ int zscrc_device_spans(const void *const *d_bufs, const uint64_t *lens, const ui
     /* one segment size for every span (g_xdeal segments per wave in all,
      * dealt per workgroup; or two, static), so a short span is as many
      * segments as its length needs, not one wave's walk */
-    const uint32_t deal = xdeal_for(g_opt);
+    /* at most 4 segments per wave here: on config 5's shape (two 3 GiB
+     * regions + two pointer sections) 4 per wave 1.014 ms, static 1.021, 16
+     * per wave 1.028; a lone 3 GiB span wants 16 (0.502 against 0.523)
+     * (interleaved, profiles/r04/ab_spans_xdeal.jsonl) */
+    const uint32_t deal = std::min<uint32_t>(xdeal_for(g_opt), 4u);
     const uint64_t target = (uint64_t)(deal > 2 ? deal : 2) * (uint64_t)c->ncu * 16;
     uint64_t seg = ((total + target - 1) / target + 1023) & ~1023ull;
     if (seg < SEG_MIN)

@@ -3525,18 +3525,26 @@ __device__ __forceinline__ void plan_write(const PlanArgs &a, SplitPlan *pl, con
 }
 
 /* part_rec for a chunk of 1024 records whose first parts are sbase[0..1024]
- * (LDS; sbase[1024] = the chunk's end): wave wv writes the parts of its 64
- * records one record after another, 64 parts per store instruction -- a few
- * uniform iterations per record, where a binary search per part was a chain
- * of ten dependent LDS reads for every one of ~67 k parts of a 16-per-wave
- * segment plan. */
+ * (LDS; sbase[1024] = the chunk's end): a record of at most 8 parts is
+ * written by its own lane; a longer one by the whole wave, 64 parts per store
+ * instruction, the wave's long records found by a ballot -- no per-part
+ * search (a binary search per part was ten dependent LDS reads for each of
+ * the parts). */
 __device__ __forceinline__ void fill_part_rec(uint32_t *part_rec, const uint32_t *sbase, uint32_t c0, int wv, int lane)
 {
-    for (int i = 0; i < 64; ++i) {
-        const int r = wv * 64 + i;
-        const uint32_t q0 = sbase[r], q1 = sbase[r + 1];
-        for (uint32_t q = q0 + (uint32_t)lane; q < q1; q += 64)
+    const int r = wv * 64 + lane;
+    const uint32_t q0 = sbase[r], q1 = sbase[r + 1];
+    const bool small = q1 - q0 <= 8;
+    if (small)
+        for (uint32_t q = q0; q < q1; ++q)
             part_rec[q] = c0 + (uint32_t)r;
+    uint64_t big = __ballot(!small);
+    while (big) {
+        const int i = __ffsll((unsigned long long)big) - 1;
+        big &= big - 1;
+        const uint32_t a = __builtin_amdgcn_readlane(q0, i), b = __builtin_amdgcn_readlane(q1, i);
+        for (uint32_t q = a + (uint32_t)lane; q < b; q += 64)
+            part_rec[q] = c0 + (uint32_t)(wv * 64 + i);
     }
 }
 
