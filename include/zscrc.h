@@ -223,6 +223,11 @@ int zscrc_diag_stream_read(const void *d_buf, uint64_t len, void *d_scratch4, in
  * LDS table fill, end, in s_memrealtime ticks of 100 MHz, and the wave's
  * record / part count) or NULL to stop. */
 int zscrc_diag_wave_times(void *d_buf);
+/* Diagnostic: phase end times of the single-block classify + plan launch of
+ * variable commit batches (<= 16,384 records) -- d_buf (device, 8 x 8 bytes:
+ * entry, count pass, scatter, plan table, plan scan, plan tail, plan write,
+ * end; s_memrealtime ticks of 100 MHz) or NULL to stop. */
+int zscrc_diag_classify_times(void *d_buf);
 /* Number of gfx950 devices visible (0 if none / no HIP runtime). */
 int zscrc_device_count(void);
 

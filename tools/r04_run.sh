@@ -21,11 +21,17 @@ for step in "$@"; do
                 >> gpurun_out/bench4s.jsonl 2>> gpurun_out/bench4s.err ;;
     bench4q)  timeout -k 10 600 python bench.py --workload config4 --no-e2e --no-cpu \
                 >> gpurun_out/bench4q.jsonl 2>> gpurun_out/bench4q.err ;;
+    bench5q|bench5s|bench5x)   # config 5: default / static commit rounds (1 << 22) / static span segments (1 << 26)
+              case "$step" in bench5q) o=0 ;; bench5s) o=4194304 ;; bench5x) o=67108864 ;; esac
+              ZSCRC_OPT=$o timeout -k 10 600 python bench.py --workload config5 --no-cpu \
+                >> gpurun_out/$step.jsonl 2>> gpurun_out/$step.err ;;
     abspan)   AB_CASES=span_3GiB,spans_config5 timeout -k 10 600 python tools/opt_ab.py 0 67108864 \
                 > gpurun_out/abspan.jsonl 2> gpurun_out/abspan.err ;;
     pmc2box)  timeout -k 10 180 python -c "import json, bench; print(json.dumps(bench.box_info(0)))" > gpurun_out/box.json \
                 2> gpurun_out/box.err && bash tools/pmc_case.sh config2 && bash tools/pmc_case.sh config3 ;;
     nbseq)    bash tools/nb_seq.sh ;;
+    cphases)  timeout -k 10 300 python tools/classify_phases.py > gpurun_out/classify_phases.jsonl \
+                2> gpurun_out/classify_phases.err ;;
     xdeal)    timeout -k 10 600 python tools/xdeal_ab.py > gpurun_out/xdeal_ab.jsonl 2> gpurun_out/xdeal_ab.err ;;
     abnb)     AB_CASES=config4_nb timeout -k 10 600 python tools/opt_ab.py 0 67108864 \
                 > gpurun_out/abnb.jsonl 2> gpurun_out/abnb.err ;;

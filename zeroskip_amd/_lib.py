@@ -54,6 +54,7 @@ SIGNATURES = {
     "zscrc_set_prefetch": (None, [_int, _int]),
     "zscrc_diag_stream_read": (_int, [_vp, _u64, _vp, _int, _vp]),
     "zscrc_diag_wave_times": (_int, [_vp]),
+    "zscrc_diag_classify_times": (_int, [_vp]),
     "zscrc_device_count": (_int, []),
     "zscrc_zs_walk": (_int, [_vp, _u64, _vp, _vp, _sz, _vp, _vp]),
     "zscrc_zs_packed_spans": (_int, [_vp, _u64, _vp, _vp]),

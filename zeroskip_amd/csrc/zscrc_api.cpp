@@ -33,6 +33,7 @@ int zs_launch_span_fold(const zs::SpanFold *f, const uint32_t *gtab, hipStream_t
 int zs_launch_short(int fixed, int pf, const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
 int zs_launch_stream_read(const void *buf, uint64_t n, uint32_t *out, int grid, hipStream_t stream);
 int zs_set_wave_times(uint64_t *p);
+int zs_set_classify_times(uint64_t *p);
 int zs_launch_classify(const zs::Classify *c, hipStream_t stream);
 int zs_launch_part_fold(const zs::BatchDesc *d, int nd, const uint32_t *gtab, hipStream_t stream);
 int zs_launch_plan(const zs::PlanArgs *a, hipStream_t stream);
@@ -1266,6 +1267,19 @@ int zscrc_diag_wave_times(void *d_buf)
         return rc;
     if (zs_set_wave_times(static_cast<uint64_t *>(d_buf))) {
         set_err("hipMemcpyToSymbol(zs_wave_times)", hipGetLastError());
+        return ZSCRC_EHIP;
+    }
+    return ZSCRC_OK;
+}
+
+int zscrc_diag_classify_times(void *d_buf)
+{
+    DevCtx *c;
+    int rc = get_ctx(&c);
+    if (rc)
+        return rc;
+    if (zs_set_classify_times(static_cast<uint64_t *>(d_buf))) {
+        set_err("hipMemcpyToSymbol(zs_classify_times)", hipGetLastError());
         return ZSCRC_EHIP;
     }
     return ZSCRC_OK;

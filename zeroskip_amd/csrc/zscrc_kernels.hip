@@ -1007,6 +1007,15 @@ __device__ __forceinline__ void xnext(const XDesc &d, const XMulti &m, const XPa
  * its record / part count at zs_wave_times + 4 * wave.  Null in production:
  * one scalar load per wave. */
 __device__ uint64_t *zs_wave_times = nullptr;
+/* Diagnostic (zscrc_diag_classify_times): the single-block classify's phase
+ * ends (s_memrealtime) at zs_classify_times[0..7]; null in production. */
+__device__ uint64_t *zs_classify_times = nullptr;
+__device__ __forceinline__ void cstamp(int k)
+{
+    uint64_t *t = zs_classify_times;
+    if (t && threadIdx.x == 0)
+        t[k] = __builtin_amdgcn_s_memrealtime();
+}
 
 /* DEAL: the launch holds many more items than waves -- a span's segments
  * (modes 0 and 1; zscrc_api.cpp span_impl / zscrc_device_spans: 16 per
@@ -1232,6 +1241,11 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp,
 extern "C" int zs_set_wave_times(uint64_t *p)
 {
     return hipMemcpyToSymbol(HIP_SYMBOL(zs_wave_times), &p, sizeof p) == hipSuccess ? 0 : -3;
+}
+
+extern "C" int zs_set_classify_times(uint64_t *p)
+{
+    return hipMemcpyToSymbol(HIP_SYMBOL(zs_classify_times), &p, sizeof p) == hipSuccess ? 0 : -3;
 }
 
 /* ------------------------------------------- coalesced 16-lane teams */
@@ -3412,6 +3426,7 @@ __device__ void classify_single(const Classify &c, uint32_t *cnt, const unsigned
         classify_scatter(c, slot, pos, r0, r1);
     __threadfence();
     __syncthreads();
+    cstamp(2); /* scatter done */
     for (int k = 2; k < 4; ++k)
         if (c.plan[k - 2].target)
             plan_block(c.plan[k - 2], slot[k], cnt[k], bsum[k], sbase, wsum, T);
@@ -3420,6 +3435,8 @@ __device__ void classify_single(const Classify &c, uint32_t *cnt, const unsigned
 __global__ __launch_bounds__(CWG) void classify_kernel(Classify c)
 {
     __shared__ uint32_t cnt[4], slot[4], pos[4];
+    if (c.single)
+        cstamp(0);
     if (c.zero_count && c.pass == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
         *c.zero_count = 0ull;
         __threadfence(); /* before the scatter's verdict atomics (single-block classify) */
@@ -3482,7 +3499,9 @@ __global__ __launch_bounds__(CWG) void classify_kernel(Classify c)
     }
     __syncthreads();
     if (c.single) {
+        cstamp(1); /* count pass done */
         classify_single(c, cnt, bsum, r0, r1);
+        cstamp(7);
         return;
     }
     if (c.pass == 0) {
@@ -3567,6 +3586,7 @@ __device__ void plan_segments(const PlanArgs &a, const RecDesc *list, SplitPlan 
     const uint64_t used = (bytes + G - 1) / G;
     load_gmul_table(T, a.gtab);
     __syncthreads();
+    cstamp(3); /* plan: table loaded */
     uint32_t running = 0;
     uint64_t run_bytes = 0;
     for (uint32_t c0 = 0; c0 < count; c0 += 1024) {
@@ -3621,9 +3641,12 @@ __device__ void plan_segments(const PlanArgs &a, const RecDesc *list, SplitPlan 
         run_bytes += ctot;
         __syncthreads();
     }
+    cstamp(4); /* plan: records scanned, parts listed */
     for (uint64_t j = used + t; j <= a.nseg; j += 1024)
         a.seg_first[j] = running;
+    cstamp(5);
     plan_write(a, pl, T, G, running, a.nseg);
+    cstamp(6);
 }
 
 /* Split plan of one length class (one block; runs after the scatter): with
