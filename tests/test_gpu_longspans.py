@@ -191,7 +191,10 @@ def test_segment_plans(gpu, db, nseg, monkeypatch):
     assert int(nbad.item()) == len(hit) and set(bad[:len(hit)].cpu().tolist()) == hit
 
 
-@pytest.mark.parametrize("opt", [0, MULTI_CLASSIFY], ids=["single-classify", "multi-classify"])
+NO_ONLY3 = 1 << 28  # opt: the single-block classify's count + scatter passes instead of the fused class-3-only pass
+
+
+@pytest.mark.parametrize("opt", [0, MULTI_CLASSIFY, NO_ONLY3], ids=["single-classify", "multi-classify", "no-only3"])
 def test_verdict_range_long_only(gpu, db, opt):
     """zscrc_device_verify_commits_verdict_range with the walk's range: only
     the class-3 commits (every length > g16_max), so classes 0-2 get no
@@ -213,3 +216,39 @@ def test_verdict_range_long_only(gpu, db, opt):
         nbad, bad = _with_opt(opt, lambda: zsfile.verify_commits_verdict(d, o, ln, max_len=int(l_np.max()),
                                                                          min_len=lo))
         assert int(nbad.item()) == len(want) and set(bad[:len(want)].cpu().tolist()) == want, lo
+
+
+@pytest.mark.parametrize("opt", [0, NO_ONLY3], ids=["only3", "count-scatter"])
+def test_verdict_range_empty_entries(gpu, db, opt):
+    """The fused class-3-only classify (Classify::only3) lists a commit
+    outside the image as an empty entry with no parts: such entries first,
+    in the middle and last, between real long commits (one corrupt), give
+    the same verdict as the count + scatter passes and list every one."""
+    host, offs, lens, commits = db
+    long_i = [i for i in range(len(commits)) if lens[i] > (1 << 20)]
+    h = host.copy()
+    bad_rec = long_i[len(long_i) // 2]
+    h[offs[bad_rec] + lens[bad_rec] // 2] ^= 0x10
+    past = [len(h) - (1 << 20), len(h) - 5]                      # records past the image end
+    o_l, l_l, want = [past[0]], [(2 << 20)], {0}
+    for k, i in enumerate(long_i):
+        o_l.append(offs[i])
+        l_l.append(lens[i])
+        if i == bad_rec:
+            want.add(len(o_l) - 1)
+        if k == len(long_i) // 3:
+            o_l.append(past[1])
+            l_l.append((1 << 21) + 9)
+            want.add(len(o_l) - 1)
+    o_l.append(past[0] + 3)
+    l_l.append((3 << 20) + 1)
+    want.add(len(o_l) - 1)
+    d = torch.from_numpy(h).cuda()
+    o = torch.from_numpy(np.array(o_l, np.int64)).cuda()
+    ln = torch.from_numpy(np.array(l_l, np.int64)).cuda()
+    nbad, bad = _with_opt(opt, lambda: zsfile.verify_commits_verdict(d, o, ln, max_len=int(max(l_l)),
+                                                                     min_len=int(min(l_l))))
+    assert int(nbad.item()) == len(want) and set(bad[:len(want)].cpu().tolist()) == want
+    # and the per-commit arrays agree on which commits fail
+    _, st = _with_opt(opt, lambda: zsfile.verify_commits(d, o, ln))
+    assert set(np.nonzero(st.cpu().numpy() != 1)[0].tolist()) == want

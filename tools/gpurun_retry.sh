@@ -12,10 +12,12 @@ for attempt in $(seq 1 40); do
     if grep -q "backing off\|stopped responding while being prepared\|no box\|status=transient" /tmp/gpurun_attempt.log && [ "$status" != "ok" ]; then
         wait_s=$(grep -o "retry in [0-9]*s" /tmp/gpurun_attempt.log | grep -o "[0-9]*" | head -1)
         echo "attempt $attempt: transient, retrying in $(( ${wait_s:-60} + 15 ))s"
+        { cat /tmp/gpurun_attempt.log; cat gpurun_out/.last_call.json 2>/dev/null; } >> /tmp/gpurun_attempts_all.log
         sleep $(( ${wait_s:-60} + 15 ))
         continue
     fi
     tail -3 /tmp/gpurun_attempt.log
+    cat /tmp/gpurun_attempt.log >> /tmp/gpurun_attempts_all.log
     exit $rc
 done
 echo "gave up after transient failures"

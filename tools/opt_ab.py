@@ -32,6 +32,8 @@ def main():
     img_nb = zg.log_files(bytes(range(16)), 0, nb_files, zg.pairs_per_file(False), 0, False, g, dev,
                           batched=False).view(-1) if "config4_nb" in (os.environ.get("AB_CASES") or "") else None
     o_nb, l_nb = zg.log_spans(nb_files, zg.pairs_per_file(False), False, False, dev)
+    nb_lo, nb_hi = int(l_nb.min().item()), int(l_nb.max().item())
+    vout_nb = (torch.empty(1, dtype=torch.int64, device=dev), torch.empty(64, dtype=torch.int64, device=dev))
     fx = torch.randint(0, 256, (320 * 10_000_000,), dtype=torch.uint8, device=dev, generator=g)
     only = os.environ.get("AB_CASES")
     bufs = torch.randint(0, 256, (32, 64 << 20), dtype=torch.uint8, device=dev, generator=g)
@@ -52,6 +54,9 @@ def main():
              "config4_crcs": lambda: zsfile.commit_crcs(img, ow, lw, max_len=mx),
              "config4_verdict": lambda: zsfile.verify_commits_verdict(img, offs, lens, max_len=mx, out=vout),
              "config4_nb": lambda: zsfile.verify_commits(img_nb, o_nb, l_nb)[1],
+             # the bench's NOTBATCHED verdict: the walk's length range given
+             "config4_nb_verdict": lambda: zsfile.verify_commits_verdict(img_nb, o_nb, l_nb, out=vout_nb,
+                                                                         min_len=nb_lo, max_len=nb_hi)[0],
              "fixed_320x312": lambda: zd.crc_fixed(fx, 320, 312, 10_000_000),
              "config2_multi32": lambda: torch.stack(zd.crc_fixed_multi(blist, 64, 64, 1 << 20)),
              "config2_warm32": lambda: torch.stack(zd.crc_fixed_multi([blist[0]] * 32, 64, 64, 1 << 20))}

@@ -33,8 +33,12 @@ for step in "$@"; do
     cphases)  timeout -k 10 300 python tools/classify_phases.py > gpurun_out/classify_phases.jsonl \
                 2> gpurun_out/classify_phases.err ;;
     xdeal)    timeout -k 10 600 python tools/xdeal_ab.py > gpurun_out/xdeal_ab.jsonl 2> gpurun_out/xdeal_ab.err ;;
+    xdealnb)  XD_NB=1 timeout -k 10 600 python tools/xdeal_ab.py 0 2 4 8 16 > gpurun_out/xdeal_nb.jsonl \
+                2> gpurun_out/xdeal_nb.err ;;
     abnb)     AB_CASES=config4_nb timeout -k 10 600 python tools/opt_ab.py 0 67108864 \
                 > gpurun_out/abnb.jsonl 2> gpurun_out/abnb.err ;;
+    abonly3)  AB_CASES=config4_nb_verdict,config4_nb timeout -k 10 600 python tools/opt_ab.py 0 268435456 \
+                > gpurun_out/abonly3.jsonl 2> gpurun_out/abonly3.err ;;
     longtests) timeout -k 10 600 $T tests/test_gpu_longspans.py > gpurun_out/longtests.log 2>&1 ;;
     tracebench) bash tools/trace_bench.sh config3 config4 config2 config5 ;;
     spantests) timeout -k 10 600 $T tests/test_gpu_stream.py tests/test_gpu_parity.py -k "span" \

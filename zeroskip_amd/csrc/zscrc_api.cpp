@@ -661,6 +661,12 @@ int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1
     /* small batches: one single-block classify launch that also writes the
      * counters and both plans (no memset, no second pass, no plan launches) */
     cl.single = n <= SMALL_CLASSIFY && !(d.opt & 524288) ? 1 : 0;
+    /* a verdict batch whose range is all class 3, on a segment plan: the
+     * fused single pass (Classify::only3; tuning bit 1 << 28: off) */
+    cl.only3 = cl.single && cl.verdict_nocommit && min_len > b2 && xseg && pa[1].nseg &&
+                       !(d.opt & zs::OPT_NO_ONLY3)
+                   ? 1
+                   : 0;
     if (cl.single) {
         cl.plan[0] = pa[0];
         cl.plan[1] = pa[1];

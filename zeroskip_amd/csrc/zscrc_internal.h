@@ -90,7 +90,8 @@ struct BatchDesc {
                              1 << 26 = spans on xteam_kernel's static walk (two segments per
                              wave, not 16 dealt per workgroup), 1 << 27 = class-3 segment
                              plans dealt per workgroup too (g_xdeal segments per wave; default
-                             one per wave, static); OPT_XDEAL (1 << 30) is set
+                             one per wave, static), 1 << 28 = no fused class-3-only classify
+                             (Classify::only3); OPT_XDEAL (1 << 30) is set
                              by the span launches themselves, not a tuning bit */
     uint32_t *part_out;
     /* commit verdict mode (bad_count != NULL): no per-record out / status;
@@ -136,6 +137,7 @@ struct QDyn {
 constexpr int SPANS_MAX = 8;
 constexpr uint32_t OPT_XSTATIC = 1u << 26; /* tuning: spans on the static walk           */
 constexpr uint32_t OPT_XDEAL_PARTS = 1u << 27; /* tuning: class-3 segment plans dealt too */
+constexpr uint32_t OPT_NO_ONLY3 = 1u << 28;    /* tuning: no fused class-3-only classify */
 constexpr uint32_t OPT_XDEAL = 1u << 30;   /* internal: this batch is a span's dealt segments */
 struct XMulti {
     uint32_t k;
@@ -272,6 +274,12 @@ struct Classify {
     int verdict_nocommit;
     uint64_t *bad_idx;
     uint64_t bad_cap;
+    /* only3 = 1 (single, verdict_nocommit, a range above class 2 and a
+     * class-3 segment plan): no count or scatter pass -- one pass writes
+     * the class-3 list in record order (a commit outside the image: counted
+     * into the verdict, an empty NO_COMMIT_OFF entry with no parts) with
+     * each record's start, then the plan from the values in registers */
+    int only3;
 };
 
 /* K fixed-stride batches of one launch (zscrc_device_fixed_multi): batch b

@@ -3398,19 +3398,18 @@ __device__ __forceinline__ void classify_scatter(const Classify &c, const uint32
 }
 
 __device__ void plan_block(const PlanArgs &a, uint32_t first, uint32_t count, uint64_t bytes, uint32_t *sbase,
-                           uint32_t *wsum, char *T);
+                           uint32_t *wsum, char *T, bool t_ready);
 
 /* classify_kernel with one block (Classify::single): the counts are the
  * block's own, so the counters, byte totals and class offsets are written,
  * the scatter follows in the same launch, then the split plans of classes 2
  * and 3 from the same counts. */
 __device__ void classify_single(const Classify &c, uint32_t *cnt, const unsigned long long *bsum, uint64_t r0,
-                                uint64_t r1)
+                                uint64_t r1, char *T)
 {
     __shared__ uint32_t slot[4], pos[4];
     __shared__ uint32_t sbase[1025];
     __shared__ uint32_t wsum[16];
-    __shared__ __attribute__((aligned(16))) char T[4096];
     if (threadIdx.x < 4) {
         uint32_t base = 0;
         for (uint32_t k = 0; k < threadIdx.x; ++k)
@@ -3429,14 +3428,111 @@ __device__ void classify_single(const Classify &c, uint32_t *cnt, const unsigned
     cstamp(2); /* scatter done */
     for (int k = 2; k < 4; ++k)
         if (c.plan[k - 2].target)
-            plan_block(c.plan[k - 2], slot[k], cnt[k], bsum[k], sbase, wsum, T);
+            plan_block(c.plan[k - 2], slot[k], cnt[k], bsum[k], sbase, wsum, T, true);
+}
+
+/* classify_kernel with Classify::only3: every record is a class-3 record
+ * (the caller's length range starts above class 2) or a commit outside the
+ * image, so the list is the caller's records in order, class 3 alone: one
+ * pass loads each record once, counts an out-of-image commit into the
+ * verdict and lists it as an empty entry (no parts; part_fold_kernel skips
+ * it), writes the descriptor and sums the lengths, which stay in registers
+ * (<= 16 records per thread) for the plan -- the count pass, the scatter and
+ * the plan's reload of the list are gone
+ * (tools/classify_phases.py: 5.7 + 5.9 us of the 23 us launch). */
+constexpr uint32_t ONLY3_MAX = 16 * CWG;
+__device__ __forceinline__ uint64_t block_scan64(uint64_t v, unsigned long long *ws, uint64_t *tot);
+__device__ __forceinline__ uint64_t seg_unit(const PlanArgs &a, uint64_t bytes);
+__device__ __forceinline__ void seg_chunk(const PlanArgs &a, uint32_t count, uint32_t c0, uint64_t len, uint64_t S,
+                                          uint64_t G, uint32_t &running, uint32_t *sbase, uint32_t *wsum);
+__device__ __forceinline__ void plan_write(const PlanArgs &a, SplitPlan *pl, const char *T, uint64_t unit,
+                                           uint32_t parts, uint32_t seg);
+
+__device__ void classify_only3(const Classify &c, char *T)
+{
+    __shared__ unsigned long long ws[16];
+    __shared__ uint32_t sbase[1025];
+    __shared__ uint32_t wsum[16];
+    const int t = threadIdx.x;
+    const uint32_t n = (uint32_t)c.n;
+    const PlanArgs &a = c.plan[1];
+    const __attribute__((address_space(1))) uint64_t *lens = (const __attribute__((address_space(1))) uint64_t *)c.len;
+    const __attribute__((address_space(1))) uint64_t *offs = (const __attribute__((address_space(1))) uint64_t *)c.off;
+    uint64_t L[16];
+    uint64_t run_bytes = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        L[i] = 0;
+        if ((uint32_t)i * CWG >= n)
+            continue;
+        const uint32_t r = (uint32_t)i * CWG + t;
+        uint64_t len = 0, off = NO_COMMIT_OFF;
+        if (r < n) {
+            len = lens[r];
+            off = offs[r];
+            if (!commit_fits(c.img_size, off, len)) {
+                off = NO_COMMIT_OFF;
+                len = 0;
+                const unsigned long long k = atomicAdd(c.zero_count, 1ull);
+                if (k < c.bad_cap)
+                    c.bad_idx[k] = r;
+            }
+            RecDesc rd;
+            rd.off = off;
+            rd.len = len;
+            rd.seed = c.seed ? ((g32p)c.seed)[r] : 0u;
+            rd.rec = r;
+            c.desc[r] = rd;
+        }
+        uint64_t ctot;
+        (void)block_scan64(len, ws, &ctot);
+        L[i] = len;
+        run_bytes += ctot;
+    }
+    if (t < 4) { /* class 3 alone, listed from desc[0] */
+        c.count[t] = t == 3 ? n : 0u;
+        c.count[4 + t] = t == 3 ? n : 0u;
+        c.bytes[t] = t == 3 ? run_bytes : 0ull;
+    }
+    if (t == 0) { /* class 2: no records */
+        SplitPlan *p2 = c.plan[0].plan + 2;
+        p2->unit = 0;
+        p2->parts = 0;
+        p2->direct = 1;
+        p2->K = 0x80000000u;
+        p2->seg = 0;
+    }
+    cstamp(2);
+    /* the plan (plan_segments, lengths and starts from the registers) */
+    const uint64_t G = seg_unit(a, run_bytes);
+    const uint64_t used = (run_bytes + G - 1) / G;
+    uint32_t running = 0;
+    uint64_t start = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        if ((uint32_t)i * CWG < n) { /* the records' starts: a scan of the lengths in registers */
+            uint64_t ctot;
+            const uint64_t S = start + block_scan64(L[i], ws, &ctot);
+            seg_chunk(a, n, (uint32_t)i * CWG, L[i], S, G, running, sbase, wsum);
+            start += ctot;
+        }
+    cstamp(4);
+    for (uint64_t j = used + t; j <= a.nseg; j += CWG)
+        a.seg_first[j] = running;
+    plan_write(a, a.plan + 3, T, G, running, a.nseg);
+    cstamp(6);
 }
 
 __global__ __launch_bounds__(CWG) void classify_kernel(Classify c)
 {
     __shared__ uint32_t cnt[4], slot[4], pos[4];
-    if (c.single)
+    /* single-block form: the plans' gmul table loaded now, beside the count
+     * pass (the pass's barriers publish it) */
+    __shared__ __attribute__((aligned(16))) char T[4096];
+    if (c.single) {
         cstamp(0);
+        load_gmul_table(T, c.plan[1].gtab);
+    }
     if (c.zero_count && c.pass == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
         *c.zero_count = 0ull;
         __threadfence(); /* before the scatter's verdict atomics (single-block classify) */
@@ -3454,6 +3550,11 @@ __global__ __launch_bounds__(CWG) void classify_kernel(Classify c)
         pos[threadIdx.x] = 0;
     }
     __syncthreads();
+    if (c.single && c.only3 && c.n <= ONLY3_MAX) { /* the zeroed verdict counter and the table: published by the barrier */
+        classify_only3(c, T);
+        cstamp(7);
+        return;
+    }
     uint32_t local[4] = {0, 0, 0, 0};
     uint64_t lbytes[4] = {0, 0, 0, 0};
     constexpr int CL = 8; /* lengths in flight per thread */
@@ -3500,7 +3601,7 @@ __global__ __launch_bounds__(CWG) void classify_kernel(Classify c)
     __syncthreads();
     if (c.single) {
         cstamp(1); /* count pass done */
-        classify_single(c, cnt, bsum, r0, r1);
+        classify_single(c, cnt, bsum, r0, r1, T);
         cstamp(7);
         return;
     }
@@ -3543,6 +3644,19 @@ __device__ __forceinline__ void plan_write(const PlanArgs &a, SplitPlan *pl, con
     }
 }
 
+/* K = x^(8 unit) by the calling wave (a six-level product tree, every lane
+ * ends with it); T: the gmul table in LDS. */
+__device__ __forceinline__ uint32_t plan_k(const PlanArgs &a, const char *T, uint64_t unit)
+{
+    const int lane = threadIdx.x & 63;
+    const uint32_t *pow2 = a.gtab + GT_POW2;
+    uint32_t v = (lane < 56 && ((unit >> lane) & 1)) ? pow2[lane] : 0x80000000u;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1)
+        v = gmul_t(T, v, __shfl_xor(v, o));
+    return v;
+}
+
 /* part_rec for a chunk of 1024 records whose first parts are sbase[0..1024]
  * (LDS; sbase[1024] = the chunk's end): a record of at most 8 parts is
  * written by its own lane; a longer one by the whole wave, 64 parts per store
@@ -3567,6 +3681,73 @@ __device__ __forceinline__ void fill_part_rec(uint32_t *part_rec, const uint32_t
     }
 }
 
+/* One chunk of a segment plan: thread t holds record r = c0 + t of the
+ * class list (len; S = its first byte with the class's records laid end to
+ * end; len 0 past the count or for an empty entry).  Writes part_base,
+ * rec_start, the seg_first entries of the segments starting inside each
+ * record and part_rec; `running` is the parts before the chunk. */
+__device__ __forceinline__ void seg_chunk(const PlanArgs &a, uint32_t count, uint32_t c0, uint64_t len, uint64_t S,
+                                          uint64_t G, uint32_t &running, uint32_t *sbase, uint32_t *wsum)
+{
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const uint32_t r = c0 + t;
+    const uint64_t j0 = S / G;
+    const uint32_t np = len ? (uint32_t)((S + len - 1) / G - j0 + 1) : 0u;
+    /* exclusive scan of the part counts: part_base */
+    uint32_t x = np;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(x, o);
+        if (lane >= o)
+            x += u;
+    }
+    if (lane == 63)
+        wsum[wv] = x;
+    __syncthreads();
+    uint32_t poff = 0;
+    for (int i = 0; i < wv; ++i)
+        poff += wsum[i];
+    const uint32_t pbase = running + poff + x - np;
+    sbase[t] = pbase;
+    if (t == 1023)
+        sbase[1024] = pbase + np;
+    if (r < count) {
+        a.part_base[r] = pbase;
+        a.rec_start[r] = S;
+        /* the segments that start inside this record */
+        for (uint64_t j = (S + G - 1) / G; j * G < S + len; ++j)
+            a.seg_first[j] = pbase + (uint32_t)(j - j0);
+    }
+    __syncthreads();
+    const uint32_t hi = sbase[1024];
+    fill_part_rec(a.part_rec, sbase, c0, wv, lane);
+    running = hi;
+    __syncthreads();
+}
+
+/* Exclusive block-wide scan of one 64-bit value per thread (1024 threads):
+ * returns the sum before this thread, *tot the block's total. */
+__device__ __forceinline__ uint64_t block_scan64(uint64_t v, unsigned long long *ws, uint64_t *tot)
+{
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const uint64_t mine = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t u = __shfl_up(v, o);
+        if (lane >= o)
+            v += u;
+    }
+    if (lane == 63)
+        ws[wv] = v;
+    __syncthreads();
+    uint64_t woff = 0, ctot = 0;
+    for (int i = 0; i < 16; ++i) {
+        woff += i < wv ? ws[i] : 0ull;
+        ctot += ws[i];
+    }
+    __syncthreads(); /* ws reusable */
+    *tot = ctot;
+    return woff + v - mine;
+}
+
 /* Segment plan (SplitPlan::seg): the class's bytes end to end cut into
  * nseg segments of G bytes (G >= bytes / nseg, a multiple of 64), segment
  * w for wave w of the xteam_kernel launch; record r (its first byte at S_r
@@ -3574,72 +3755,34 @@ __device__ __forceinline__ void fill_part_rec(uint32_t *part_rec, const uint32_t
  * (S_r, a block-wide 64-bit scan), part_base (scan of the part counts),
  * part_rec, and seg_first[j] = the part holding byte j G (every segment
  * starts inside exactly one record), seg_first[j >= used] = all parts. */
-__device__ void plan_segments(const PlanArgs &a, const RecDesc *list, SplitPlan *pl, uint32_t count,
-                              uint64_t bytes, uint32_t *sbase, uint32_t *wsum, char *T)
+__device__ __forceinline__ uint64_t seg_unit(const PlanArgs &a, uint64_t bytes)
 {
-    __shared__ unsigned long long wsum64[16];
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     uint64_t G = (bytes + a.nseg - 1) / a.nseg;
     G = (G + 63) & ~63ull;
-    if (G < a.unit_min)
-        G = a.unit_min;
+    return G < a.unit_min ? a.unit_min : G;
+}
+
+__device__ void plan_segments(const PlanArgs &a, const RecDesc *list, SplitPlan *pl, uint32_t count,
+                              uint64_t bytes, uint32_t *sbase, uint32_t *wsum, char *T, bool t_ready)
+{
+    __shared__ unsigned long long wsum64[16];
+    const int t = threadIdx.x;
+    const uint64_t G = seg_unit(a, bytes);
     const uint64_t used = (bytes + G - 1) / G;
-    load_gmul_table(T, a.gtab);
-    __syncthreads();
+    if (!t_ready) {
+        load_gmul_table(T, a.gtab);
+        __syncthreads();
+    }
     cstamp(3); /* plan: table loaded */
     uint32_t running = 0;
     uint64_t run_bytes = 0;
     for (uint32_t c0 = 0; c0 < count; c0 += 1024) {
         const uint32_t r = c0 + t;
         const uint64_t len = r < count ? ((const volatile uint64_t *)&list[r].len)[0] : 0ull;
-        /* exclusive 64-bit scan of the lengths: S_r */
-        uint64_t v = len;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint64_t u = __shfl_up(v, o);
-            if (lane >= o)
-                v += u;
-        }
-        if (lane == 63)
-            wsum64[wv] = v;
-        __syncthreads();
-        uint64_t woff = 0, ctot = 0;
-        for (int i = 0; i < 16; ++i) {
-            woff += i < wv ? wsum64[i] : 0ull;
-            ctot += wsum64[i];
-        }
-        const uint64_t S = run_bytes + woff + v - len;
-        const uint64_t j0 = S / G;
-        const uint32_t np = len ? (uint32_t)((S + len - 1) / G - j0 + 1) : 0u;
-        /* exclusive scan of the part counts: part_base */
-        uint32_t x = np;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t u = __shfl_up(x, o);
-            if (lane >= o)
-                x += u;
-        }
-        if (lane == 63)
-            wsum[wv] = x;
-        __syncthreads();
-        uint32_t poff = 0;
-        for (int i = 0; i < wv; ++i)
-            poff += wsum[i];
-        const uint32_t pbase = running + poff + x - np;
-        sbase[t] = pbase;
-        if (t == 1023)
-            sbase[1024] = pbase + np;
-        if (r < count) {
-            a.part_base[r] = pbase;
-            a.rec_start[r] = S;
-            /* the segments that start inside this record */
-            for (uint64_t j = (S + G - 1) / G; j * G < S + len; ++j)
-                a.seg_first[j] = pbase + (uint32_t)(j - j0);
-        }
-        __syncthreads();
-        const uint32_t hi = sbase[1024];
-        fill_part_rec(a.part_rec, sbase, c0, wv, lane);
-        running = hi;
+        uint64_t ctot;
+        const uint64_t S = run_bytes + block_scan64(len, wsum64, &ctot);
+        seg_chunk(a, count, c0, len, S, G, running, sbase, wsum);
         run_bytes += ctot;
-        __syncthreads();
     }
     cstamp(4); /* plan: records scanned, parts listed */
     for (uint64_t j = used + t; j <= a.nseg; j += 1024)
@@ -3660,7 +3803,7 @@ __device__ void plan_segments(const PlanArgs &a, const RecDesc *list, SplitPlan 
  * a small batch right after its scatter (the list read with device-coherent
  * loads). */
 __device__ void plan_block(const PlanArgs &a, uint32_t first, uint32_t count, uint64_t bytes, uint32_t *sbase,
-                           uint32_t *wsum, char *T)
+                           uint32_t *wsum, char *T, bool t_ready)
 {
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const RecDesc *list = a.desc + first;
@@ -3676,7 +3819,7 @@ __device__ void plan_block(const PlanArgs &a, uint32_t first, uint32_t count, ui
         return;
     }
     if (a.nseg && (uint64_t)count + a.nseg <= a.max_parts) {
-        plan_segments(a, list, pl, count, bytes, sbase, wsum, T);
+        plan_segments(a, list, pl, count, bytes, sbase, wsum, T, t_ready);
         return;
     }
     /* each record adds at most one partial part: with unit >= bytes /
@@ -3690,8 +3833,10 @@ __device__ void plan_block(const PlanArgs &a, uint32_t first, uint32_t count, ui
         unit = a.unit_min;
     if (count >= a.target) /* always_split: one part per record */
         unit = ~0ull >> 8;
-    load_gmul_table(T, a.gtab);
-    __syncthreads();
+    if (!t_ready) {
+        load_gmul_table(T, a.gtab);
+        __syncthreads();
+    }
     uint32_t running = 0;
     for (uint32_t c0 = 0; c0 < count; c0 += 1024) {
         const uint32_t r = c0 + t;
@@ -3733,7 +3878,7 @@ __global__ __launch_bounds__(1024) void plan_kernel(PlanArgs a)
     uint32_t first = 0;
     for (uint32_t k = 0; k < a.klass; ++k)
         first += a.count[k];
-    plan_block(a, first, a.count[a.klass], a.bytes[a.klass], sbase, wsum, T);
+    plan_block(a, first, a.count[a.klass], a.bytes[a.klass], sbase, wsum, T, false);
 }
 
 
@@ -3809,6 +3954,8 @@ __global__ __launch_bounds__(256) void part_fold_kernel(FoldPair fp, const uint3
         if (!ok || sub)
             continue;
         const RecDesc r = list[idx];
+        if (r.off == NO_COMMIT_OFF)
+            continue; /* Classify::only3's empty entry: counted by the classify, no parts */
         const uint64_t len = r.len;
         const uint32_t pb = d.part_base[idx];
         const uint32_t m = (idx + 1 < count ? d.part_base[idx + 1] : nparts) - pb; /* 1.. parts */
