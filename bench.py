@@ -674,8 +674,11 @@ def run_config4(args, world, rank, dev, stream):
 
     def nb_arrays():
         nb_arr["crc"], nb_arr["st"] = zsfile.verify_commits(img_nb.view(-1), o_nb, l_nb)
-    # interleaved, so no form sees a different power / clock state
-    nb_ms, nb_unranged_ms, nb_arrays_ms = _timed_ab([nb_verdict, nb_verdict_unranged, nb_arrays], 6, stream)
+    # interleaved, so no form sees a different power / clock state; blocks of
+    # 20 calls (6 could not resolve the forms' ~13 us difference,
+    # tools/nb_forms.py)
+    nb_ms, nb_unranged_ms, nb_arrays_ms = _timed_ab([nb_verdict, nb_verdict_unranged, nb_arrays], 20, stream,
+                                                    rounds=5)
     nb_verdict()
     assert int(nbo[0].item()) == 0
     assert bool((nb_arr["st"] == 1).all())

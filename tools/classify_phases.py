@@ -45,15 +45,23 @@ def main():
                 fn()
                 torch.cuda.synchronize()
                 t = buf.cpu().numpy().astype(np.int64)
-                rows.append([(t[k + 1] - t[k]) / 100.0 if t[k + 1] and t[k] else None for k in range(7)])
+                # each phase from the last stamp before it (the fused class-3-only
+                # pass stamps 0, 2, 4, 6, 7 only)
+                row = []
+                for k in range(7):
+                    prev = max((j for j in range(k + 1) if t[j]), default=None)
+                    row.append((t[k + 1] - t[prev]) / 100.0 if t[k + 1] and prev is not None else None)
+                row.append((t[7] - t[0]) / 100.0 if t[7] and t[0] else None)
+                rows.append(row)
         finally:
             check(lib().zscrc_diag_classify_times(None), "classify times off")
         med = {}
         for k, n in enumerate(NAMES):
             v = [r[k] for r in rows if r[k] is not None]
             med[n] = round(float(np.median(v)), 2) if v else None
+        tot = [r[7] for r in rows if r[7] is not None]
         print(json.dumps({"form": name, "commits": int(offs.numel()), "phase_us_median": med,
-                          "total_us_median": round(float(np.median([sum(x for x in r if x) for r in rows])), 2)}),
+                          "entry_to_end_us_median": round(float(np.median(tot)), 2) if tot else None}),
               flush=True)
 
 

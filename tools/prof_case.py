@@ -53,7 +53,13 @@ def main():
         vout = (torch.empty(1, dtype=torch.int64, device=dev), torch.empty(64, dtype=torch.int64, device=dev))
         lo, hi = int(lens.min().item()), int(lens.max().item())
         mode = os.environ.get("C4NB_MODE", "range")
-        if mode == "arrays":                # per-commit crc + status arrays
+        forms = [lambda k: zsfile.verify_commits_verdict(img.view(-1), offs, lens, out=vout, min_len=lo,  # noqa: E731
+                                                         max_len=hi),
+                 lambda k: zsfile.verify_commits_verdict(img.view(-1), offs, lens, out=vout),  # noqa: E731
+                 lambda k: zsfile.verify_commits(img.view(-1), offs, lens)]  # noqa: E731
+        if mode == "mixed":                 # pass k: form k % 3 (ranged verdict, verdict, arrays), one process
+            run = lambda k: forms[k % 3](k)  # noqa: E731
+        elif mode == "arrays":              # per-commit crc + status arrays
             run = lambda k: zsfile.verify_commits(img.view(-1), offs, lens)  # noqa: E731
         elif mode == "unranged":
             run = lambda k: zsfile.verify_commits_verdict(img.view(-1), offs, lens, out=vout)  # noqa: E731

@@ -30,6 +30,11 @@ for step in "$@"; do
     pmc2box)  timeout -k 10 180 python -c "import json, bench; print(json.dumps(bench.box_info(0)))" > gpurun_out/box.json \
                 2> gpurun_out/box.err && bash tools/pmc_case.sh config2 && bash tools/pmc_case.sh config3 ;;
     nbseq)    bash tools/nb_seq.sh ;;
+    nbforms)  timeout -k 10 300 python tools/nb_forms.py > gpurun_out/nb_forms.json 2> gpurun_out/nb_forms.err ;;
+    nbmix)    ( cd /tmp && export TMPDIR=/tmp && C4NB_MODE=mixed timeout -k 10 300 rocprofv3 --kernel-trace --stats \
+                --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/nbmix -o run -- \
+                python3 $GRAFT_REPO_ROOT/tools/prof_case.py config4nb 90 > $GRAFT_REPO_ROOT/gpurun_out/nbmix.log 2>&1 ) && \
+              python tools/nb_mixed_summary.py gpurun_out/nbmix 15 > gpurun_out/nbmix.json ;;
     cphases)  timeout -k 10 300 python tools/classify_phases.py > gpurun_out/classify_phases.jsonl \
                 2> gpurun_out/classify_phases.err ;;
     xdeal)    timeout -k 10 600 python tools/xdeal_ab.py > gpurun_out/xdeal_ab.jsonl 2> gpurun_out/xdeal_ab.err ;;
