@@ -320,8 +320,10 @@ int zscrc_device_verify_commits_verdict(const void *d_image, uint64_t image_size
  * min_len <= every span length <= max_len (the walk that found the commits
  * knows both): the length classes the range rules out get no launch --
  * NOTBATCHED's ~2 MiB commits run the classify, the long-record parts and
- * their fold only.  Commits outside the image still count as bad.  The range
- * must hold (a span outside it may go unverified). */
+ * their fold only; a range above the 16-lane bound on a batch of at most
+ * 16,384 commits classifies in one fused pass (no count or scatter pass).
+ * Commits outside the image still count as bad.  The range must hold (a span
+ * outside it may go unverified). */
 int zscrc_device_verify_commits_verdict_range(const void *d_image, uint64_t image_size, const uint64_t *d_span_off,
                                               const uint64_t *d_span_len, const uint32_t *d_seed, size_t n,
                                               uint64_t min_len, uint64_t max_len, uint64_t *d_nbad, uint64_t *d_bad,
