@@ -27,6 +27,8 @@ for step in "$@"; do
                 >> gpurun_out/$step.jsonl 2>> gpurun_out/$step.err ;;
     abspan)   AB_CASES=span_3GiB,spans_config5 timeout -k 10 600 python tools/opt_ab.py 0 67108864 \
                 > gpurun_out/abspan.jsonl 2> gpurun_out/abspan.err ;;
+    pmc4box)  timeout -k 10 180 python -c "import json, bench; print(json.dumps(bench.box_info(0)))" > gpurun_out/box4.json \
+                2> gpurun_out/box4.err && bash tools/pmc_case.sh config4 ;;
     pmc2box)  timeout -k 10 180 python -c "import json, bench; print(json.dumps(bench.box_info(0)))" > gpurun_out/box.json \
                 2> gpurun_out/box.err && bash tools/pmc_case.sh config2 && bash tools/pmc_case.sh config3 ;;
     nbseq)    bash tools/nb_seq.sh ;;
