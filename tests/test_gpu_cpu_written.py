@@ -119,6 +119,7 @@ def test_fill_commits_host_million(batched):
 
 
 STATIC_ROUNDS = 1 << 22   # zs::BatchDesc::opt: commit_kernel's static schedule (rounds not dealt)
+NO_RUNSPLIT = 1 << 29     # opt: one commit_kernel (not the run-only kernel + the listed leftover rounds)
 
 
 def test_dealt_rounds_verdicts(batched):
@@ -142,7 +143,7 @@ def test_dealt_rounds_verdicts(batched):
         k = int(nbad.item())
         assert k == len(want) and set(bad[:k].cpu().tolist()) == want
     crc_d, st_d = zsfile.verify_commits(flat, offs, lens, max_len=312)
-    for opt in (STATIC_ROUNDS,):
+    for opt in (STATIC_ROUNDS, NO_RUNSPLIT, STATIC_ROUNDS | NO_RUNSPLIT):
         lib().zscrc_set_opt(opt)
         try:
             crc_s, st_s = zsfile.verify_commits(flat, offs, lens, max_len=312)
@@ -153,3 +154,34 @@ def test_dealt_rounds_verdicts(batched):
         assert torch.equal(crc_d, crc_s) and torch.equal(st_d, st_s) and int(nbad_s.item()) == len(want), opt
     assert set(torch.nonzero(st_d != 1).flatten().cpu().tolist()) == want
     assert n > 1 << 20
+
+
+def test_split_commit_batches_writer_and_crcs(batched):
+    """The split bounded commit batch (the run-only commit_kernel at 12 waves
+    per CU + commit_kernel on the listed leftover rounds: file boundaries,
+    stale finalise commits, the last partial round) against one
+    commit_kernel: the writer's CRCs into a zeroed copy of the image byte for
+    byte, the CRC array, and the per-commit arrays."""
+    from zeroskip_amd._lib import lib
+    img, offs, lens, nfiles = batched
+    flat = img.view(-1)
+    live = lens > 0
+    ow, lw = offs[live].contiguous(), lens[live].contiguous()
+    fields = (ow + lw + 4).view(-1, 1) + torch.arange(4, device=ow.device).view(1, -1)
+    out = {}
+    for opt in (0, NO_RUNSPLIT):
+        lib().zscrc_set_opt(opt)
+        try:
+            z = flat.clone()
+            z[fields.view(-1)] = 0
+            zsfile.write_commits(z, ow, lw, max_len=312, crc=False)
+            crcs = zsfile.commit_crcs(flat, ow, lw, max_len=312)
+            arr = zsfile.verify_commits(flat, offs, lens, max_len=312)
+            torch.cuda.synchronize()
+        finally:
+            lib().zscrc_set_opt(0)
+        out[opt] = (z, crcs, arr)
+    assert torch.equal(out[0][0], flat)                 # the split writer restores every CRC field
+    assert torch.equal(out[NO_RUNSPLIT][0], flat)
+    assert torch.equal(out[0][1], out[NO_RUNSPLIT][1])
+    assert torch.equal(out[0][2][0], out[NO_RUNSPLIT][2][0]) and torch.equal(out[0][2][1], out[NO_RUNSPLIT][2][1])

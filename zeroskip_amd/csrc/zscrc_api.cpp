@@ -136,6 +136,8 @@ struct DevCtx {
     void *parts = nullptr;     /* part registers of split long records */
     void *qparts = nullptr;    /* qteam_dyn_kernel: part registers */
     size_t qparts_bytes = 0;
+    void *rlist = nullptr;     /* split commit batches: leftover-round count + list */
+    size_t rlist_bytes = 0;
     size_t parts_bytes = 0;
     hipEvent_t last = nullptr; /* end of the last scratch user's work ... */
     hipStream_t last_stream = nullptr; /* ... enqueued on this stream */
@@ -491,6 +493,49 @@ int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s, int depth_hi
 int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1, uint64_t g16, uint64_t min_len,
                           uint64_t max_len);
 
+/* A bounded commit batch (every span within the one-lane bound): commit_kernel
+ * -- run rounds, verdicts, rounds dealt per workgroup.  Batches of at least
+ * 12 rounds per wave run split (zscrc_kernels.hip, commit_kernel RO): the
+ * run-only kernel at 12 waves per CU lists every other round, then
+ * commit_kernel takes those.  Tuning bit 1 << 29: one commit_kernel. */
+int launch_commit(DevCtx *c, zs::BatchDesc d, hipStream_t s)
+{
+    const uint64_t nr = (d.n + 63) / 64;
+    if ((d.opt & zs::OPT_NO_RUNSPLIT) || nr < (uint64_t)c->ncu * 12 || nr >= (1ull << 32)) {
+        if (zs_launch_commit(&d, c->gtab, c->ncu, s)) {
+            set_err("commit kernel launch", hipGetLastError());
+            return ZSCRC_EHIP;
+        }
+        g_stat[2]++;
+        return ZSCRC_OK;
+    }
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    int rc = scratch_acquire(c, s);
+    if (!rc)
+        rc = grow(&c->rlist, &c->rlist_bytes, 4 * (nr + 1));
+    if (!rc) {
+        uint32_t *cnt = static_cast<uint32_t *>(c->rlist);
+        hipError_t e = hipMemsetAsync(cnt, 0, sizeof(uint32_t), s);
+        if (e != hipSuccess) {
+            set_err("hipMemsetAsync(round count)", e);
+            rc = ZSCRC_EHIP;
+        }
+        d.round_count = cnt;
+        d.round_list = cnt + 1;
+        for (int mode = 1; !rc && mode <= 2; ++mode) {
+            d.round_mode = mode;
+            if (zs_launch_commit(&d, c->gtab, c->ncu, s)) {
+                set_err("commit kernel launch", hipGetLastError());
+                rc = ZSCRC_EHIP;
+            } else {
+                g_stat[2]++;
+            }
+        }
+    }
+    const int rc2 = scratch_release(c, s);
+    return rc ? rc : rc2;
+}
+
 /* [min_len, max_len]: a range the caller knows every length lies in (the
  * host walk that found the spans does); classes outside it get no launch.
  * Results never depend on the range: a record outside it is still
@@ -516,16 +561,8 @@ int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t max_len =
                 return ZSCRC_EHIP;
             }
         }
-        if (max_len <= g1 && d.commit && !d.desc && !(d.opt & 32768) && w0 < 0) {
-            /* bounded commit batch: commit_kernel (run rounds, verdicts,
-             * rounds dealt per workgroup) */
-            if (zs_launch_commit(&d, c->gtab, c->ncu, s)) {
-                set_err("commit kernel launch", hipGetLastError());
-                return ZSCRC_EHIP;
-            }
-            g_stat[2]++;
-            return ZSCRC_OK;
-        }
+        if (max_len <= g1 && d.commit && !d.desc && !(d.opt & 32768) && w0 < 0)
+            return launch_commit(c, d, s); /* bounded commit batch */
         if (max_len <= g1 && (w0 < 0 || w0 >= 9))
             return launch(c, 1, d, s, walk_for(1, 0, 1));
     }

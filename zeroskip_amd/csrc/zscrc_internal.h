@@ -91,7 +91,9 @@ struct BatchDesc {
                              wave, not 16 dealt per workgroup), 1 << 27 = class-3 segment
                              plans dealt per workgroup too (g_xdeal segments per wave; default
                              one per wave, static), 1 << 28 = no fused class-3-only classify
-                             (Classify::only3); OPT_XDEAL (1 << 30) is set
+                             (Classify::only3), 1 << 29 = bounded commit batches on one
+                             commit_kernel (not the run-only kernel + leftover rounds);
+                             OPT_XDEAL (1 << 30) is set
                              by the span launches themselves, not a tuning bit */
     uint32_t *part_out;
     /* commit verdict mode (bad_count != NULL): no per-record out / status;
@@ -107,6 +109,13 @@ struct BatchDesc {
      * class's bytes laid end to end (part_fold_kernel's last-part shift) */
     const uint64_t *rec_start;
     const uint32_t *seg_first; /* segment plans: first part of segment w */
+    /* commit_kernel's split form: round_mode 1 = the run-only kernel (12
+     * waves per CU) appends every round that is not a run round to
+     * round_list (*round_count, zeroed before); 2 = commit_kernel takes its
+     * rounds from that list */
+    int round_mode;
+    uint32_t *round_list;
+    uint32_t *round_count;
 };
 
 /* A fixed-stride batch for xteam_kernel (what it reads of a BatchDesc: few
@@ -138,6 +147,7 @@ constexpr int SPANS_MAX = 8;
 constexpr uint32_t OPT_XSTATIC = 1u << 26; /* tuning: spans on the static walk           */
 constexpr uint32_t OPT_XDEAL_PARTS = 1u << 27; /* tuning: class-3 segment plans dealt too */
 constexpr uint32_t OPT_NO_ONLY3 = 1u << 28;    /* tuning: no fused class-3-only classify */
+constexpr uint32_t OPT_NO_RUNSPLIT = 1u << 29; /* tuning: bounded commit batches in one commit_kernel */
 constexpr uint32_t OPT_XDEAL = 1u << 30;   /* internal: this batch is a span's dealt segments */
 struct XMulti {
     uint32_t k;

@@ -2695,6 +2695,86 @@ __device__ __forceinline__ void run_hash(const BatchDesc &d, BRec &b, uint32_t (
     emit(d, b.it, reg, L, c_lo, c_hi);
 }
 
+/* The run-only commit_kernel's scratch (12 waves per CU leave no room for
+ * run_hash's 448 words per wave beside the tables): 64 record accumulators
+ * the pieces' shifted registers are XOR-ed into (LDS atomics: CRC
+ * linearity), then 128 words of commit words. */
+constexpr uint32_t RUN_WORDS_RO = 64 + 128;
+
+template <int P0, int NP, int NB>
+__device__ __forceinline__ void run_chains_ro(const BRec &b, uint32_t (&w)[NB][16], const char *L, uint32_t *S,
+                                              int lane, uint32_t c_lo, uint32_t c_hi, uint32_t opt)
+{
+    uint32_t y[NP];
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+        const int p = P0 + q;
+        const uint32_t P = 64u * p + (uint32_t)lane;
+        const uint32_t r = (P * 205u) >> 10; /* P / 5 for P < 1024 */
+        const uint32_t r0 = __shfl(b.it.R0, (int)r);
+        if (P == 5u * r) { /* piece 0 of record r */
+            if (r) {       /* the previous record's commit word */
+                S[64 + 2 * (r - 1)] = w[p][0];
+                S[65 + 2 * (r - 1)] = w[p][1];
+            }
+            w[p][0] = 0;
+            w[p][1] = 0;
+            w[p][2] ^= r0;
+        }
+        y[q] = w[p][0];
+    }
+    if (!(opt & 4096)) {
+#pragma unroll
+        for (int k = 1; k < 16; ++k)
+#pragma unroll
+            for (int q = 0; q < NP; ++q)
+                y[q] = m4x<ZS_COMMIT_B3>(L, y[q], w[P0 + q][k], c_lo, c_hi);
+    } else {
+#pragma unroll
+        for (int k = 1; k < 16; ++k)
+#pragma unroll
+            for (int q = 0; q < NP; ++q)
+                y[q] ^= w[P0 + q][k];
+    }
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+        const uint32_t P = 64u * (P0 + q) + (uint32_t)lane;
+        const uint32_t r = (P * 205u) >> 10;
+        const uint32_t m = P - 5u * r;
+        const uint32_t raw = m4(L, y[q], c_lo, c_hi);
+        const uint32_t tb = OFF_U + (m == 3 ? 0u : m == 2 ? 4096u : m == 1 ? OFF_Z192 : OFF_Z2);
+        const uint32_t sh = op4(L, tb, raw);
+        atomicXor(&S[r], m == 4 ? raw : sh);
+    }
+}
+
+/* run_hash for the run-only commit_kernel (RUN_WORDS_RO scratch). */
+__device__ __forceinline__ void run_hash_ro(const BatchDesc &d, BRec &b, uint32_t (&w)[5][16], const char *L,
+                                            uint32_t *S, int lane, uint32_t c_lo, uint32_t c_hi)
+{
+    asm volatile("" : "+v"(lane));
+    S[lane] = 0; /* the wave's record accumulators (its LDS ops stay in order) */
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    run_chains_ro<0, 3>(b, w, L, S, lane, c_lo, c_hi, d.opt);
+    run_chains_ro<3, 2>(b, w, L, S, lane, c_lo, c_hi, d.opt);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t reg = S[lane];
+    if (b.cnext) {
+        b.it.c0 = S[64 + 2 * lane];
+        b.it.c1 = S[65 + 2 * lane];
+    }
+    if (d.opt & 8192) { /* diagnostic: no per-record trailer / stores */
+        if (reg == 0x9E3779B9u)
+            gstore32(d.out, reg);
+        return;
+    }
+    emit(d, b.it, reg, L, c_lo, c_hi);
+}
+
 /* FX: fixed-stride batch (the bitop3-folded chain measured faster there) */
 template <int NB, bool FX>
 __device__ __forceinline__ void burst_hash(const BatchDesc &d, BRec &b, uint32_t (&w)[NB][16], const char *L,
@@ -2991,16 +3071,26 @@ __global__ __launch_bounds__(NB == 1 ? 1024 : BWG) void burst_kernel(BatchDesc d
  * Tuning bit 1 << 22: the static schedule (wave w, rounds w + t nw).
  */
 struct RoundSched {
-    uint64_t w, nw, nr; /* this wave, waves, rounds */
+    uint64_t w, nw, nr; /* this wave, waves, rounds of the batch */
+    uint64_t ns;        /* slots: rounds, or the round list's length */
+    const uint32_t *list; /* round_mode 2: slot -> round */
+    uint32_t wpb;       /* waves per workgroup */
     bool deal;          /* rounds dealt by the workgroup's LDS counter */
     uint32_t *lctr;
 };
 
-/* slot k of this workgroup: round 8 b + k % 8 + (k / 8) nw */
+/* slot k's round (nr: none left) */
+__device__ __forceinline__ uint64_t slot_round(const RoundSched &s, uint64_t k)
+{
+    if (k >= s.ns)
+        return s.nr;
+    return s.list ? (uint64_t)__builtin_amdgcn_readfirstlane(((g32p)s.list)[k]) : k;
+}
+
+/* dealt slot k of this workgroup: slot wpb b + k % wpb + (k / wpb) nw */
 __device__ __forceinline__ uint64_t deal_round(const RoundSched &s, uint64_t k)
 {
-    const uint64_t r = (uint64_t)blockIdx.x * (BWG / 64) + (k % (BWG / 64)) + (k / (BWG / 64)) * s.nw;
-    return r < s.nr ? r : s.nr;
+    return slot_round(s, (uint64_t)blockIdx.x * s.wpb + (k % s.wpb) + (k / s.wpb) * s.nw);
 }
 
 /* Round t's index: dealt (from the slot fetched by deal_issue) or static.
@@ -3009,8 +3099,7 @@ __device__ __forceinline__ uint64_t round_at(const RoundSched &s, uint64_t t, ui
 {
     if (s.deal)
         return deal_round(s, __builtin_amdgcn_readfirstlane(__shfl(fetched, 0)));
-    const uint64_t r = s.w + t * s.nw;
-    return r < s.nr ? r : s.nr;
+    return slot_round(s, s.w + t * s.nw);
 }
 
 __device__ __forceinline__ uint32_t deal_issue(const RoundSched &s, int lane)
@@ -3018,20 +3107,40 @@ __device__ __forceinline__ uint32_t deal_issue(const RoundSched &s, int lane)
     return s.deal && lane == 0 ? atomicAdd(s.lctr, 1u) : 0u;
 }
 
-template <bool WR>
-__global__ __launch_bounds__(BWG) void commit_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
+/*
+ * RO (BatchDesc::round_mode 1): the run rounds only, at 12 waves per CU.
+ * commit_kernel holds 232 VGPRs, so 8 waves per CU; its counters against
+ * qteam_kernel's (profiles/r04/pmc_config4_box.json) put config 4's time
+ * per byte at wave-cycles / resident waves -- occupancy.  Without the quad
+ * bursts the kernel fits 168 VGPRs (three waves per SIMD); the run rounds'
+ * scratch shrinks to 192 words per wave (run_hash_ro) so twelve fit beside
+ * the tables.  Every round that is not a run round (file boundaries, odd
+ * spans: ~1 % of config 4's) is listed for a second launch of commit_kernel
+ * in round_mode 2, which takes its rounds from the list.
+ */
+template <bool WR, bool RO = false>
+__global__ __launch_bounds__(RO ? 768 : BWG) void commit_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
 {
-    __shared__ __attribute__((aligned(16))) char L[OFF_RUN + 4 * RUN_WORDS * (BWG / 64)];
-    __shared__ uint32_t lctr;
+    constexpr int TPB = RO ? 768 : BWG;
+    constexpr uint32_t NWV = TPB / 64;
+    constexpr uint32_t SW = RO ? RUN_WORDS_RO : RUN_WORDS;
+    /* RO: the workgroup's leftover rounds gathered here and listed with one
+     * global atomic at the end (an atomic per round on one address would
+     * serialise a batch with few run rounds); past LB, one atomic each */
+    constexpr uint32_t LB = RO ? 1536 : 0;
+    __shared__ __attribute__((aligned(16))) char L[OFF_RUN + 4 * SW * NWV + 4 * LB];
+    __shared__ uint32_t lctr, lcnt;
     const uint64_t count = d.n;
-    if ((uint64_t)blockIdx.x * BWG >= count)
+    if ((uint64_t)blockIdx.x * TPB >= count)
         return;
     const uint64_t t_entry = __builtin_amdgcn_s_memrealtime();
-    if (threadIdx.x == 0)
+    if (threadIdx.x == 0) {
         lctr = 0;
+        lcnt = 0;
+    }
     {
         uint4 *L4 = reinterpret_cast<uint4 *>(L);
-        for (int i = threadIdx.x; i < 8192; i += BWG) {
+        for (int i = threadIdx.x; i < 8192; i += TPB) {
             const int dw = i * 4;
             const int e = (dw >> 6) & 255;
             const int tj = (dw >> 14) * 2 + ((dw >> 5) & 1);
@@ -3039,7 +3148,7 @@ __global__ __launch_bounds__(BWG) void commit_kernel(BatchDesc d, const uint32_t
             L4[i] = make_uint4(v, v, v, v);
         }
         uint32_t *Z = reinterpret_cast<uint32_t *>(L + OFF_U);
-        for (int i = threadIdx.x; i < 1024; i += BWG) {
+        for (int i = threadIdx.x; i < 1024; i += TPB) {
             Z[i] = gtab[GT_Z + i];               /* shift 64  */
             Z[1024 + i] = gtab[GT_Z + 1024 + i]; /* shift 128 */
             Z[2048 + i] = gtab[GT_Z + 2048 + i]; /* shift 256 */
@@ -3052,12 +3161,16 @@ __global__ __launch_bounds__(BWG) void commit_kernel(BatchDesc d, const uint32_t
     const uint32_t c_hi = c_lo | 0x10000u;
     const uintptr_t lo = reinterpret_cast<uintptr_t>(d.base) & ~uintptr_t(3);
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(gtab);
-    uint32_t *S = reinterpret_cast<uint32_t *>(L + OFF_RUN) + RUN_WORDS * (threadIdx.x >> 6);
-    /* the rounds: dealt per workgroup (RoundSched) */
+    uint32_t *S = reinterpret_cast<uint32_t *>(L + OFF_RUN) + SW * (threadIdx.x >> 6);
+    /* the rounds: dealt per workgroup (RoundSched); round_mode 2: the
+     * leftover rounds the run-only launch listed */
     RoundSched rs;
-    rs.w = uni64((uint64_t)blockIdx.x * (BWG / 64) + (threadIdx.x >> 6));
-    rs.nw = (uint64_t)gridDim.x * (BWG / 64);
+    rs.w = uni64((uint64_t)blockIdx.x * NWV + (threadIdx.x >> 6));
+    rs.nw = (uint64_t)gridDim.x * NWV;
     rs.nr = (count + 63) / 64;
+    rs.wpb = NWV;
+    rs.list = !RO && d.round_mode == 2 ? d.round_list : nullptr;
+    rs.ns = rs.list ? __builtin_amdgcn_readfirstlane(((const volatile uint32_t *)d.round_count)[0]) : rs.nr;
     rs.deal = !(d.opt & (1u << 22));
     rs.lctr = &lctr;
     uint64_t r_cur = round_at(rs, 0, deal_issue(rs, lane));
@@ -3078,6 +3191,23 @@ __global__ __launch_bounds__(BWG) void commit_kernel(BatchDesc d, const uint32_t
         b.run = false;
         run_check(d, b, lane);
         const bool run = __builtin_amdgcn_readfirstlane((uint32_t)b.run) != 0;
+        if (RO && !run) { /* not a run round: listed for the second launch */
+            if (lane == 0) {
+                uint32_t *lbuf = reinterpret_cast<uint32_t *>(L + OFF_RUN + 4 * SW * NWV);
+                const uint32_t k = atomicAdd(&lcnt, 1u);
+                if (k < LB)
+                    lbuf[k] = (uint32_t)r_cur;
+                else
+                    d.round_list[atomicAdd(d.round_count, 1u)] = (uint32_t)r_cur;
+            }
+            const uint64_t i_nxt = 64 * r_nxt + (uint64_t)lane;
+            bdesc_load(d, i_nxt, count, q);
+            const uint32_t f2 = deal_issue(rs, lane);
+            i = i_nxt;
+            r_cur = r_nxt;
+            r_nxt = round_at(rs, t + 2, f2);
+            continue;
+        }
         ++rounds;
         runs += run ? 1u : 0u;
         if (run)
@@ -3092,7 +3222,9 @@ __global__ __launch_bounds__(BWG) void commit_kernel(BatchDesc d, const uint32_t
          * (vmcnt counts in issue order); taken after the hash */
         const uint32_t f2 = deal_issue(rs, lane);
         xpose_burst(w);
-        if (run) {
+        if (RO) {
+            run_hash_ro(d, b, w, L, S, lane, c_lo, c_hi);
+        } else if (run) {
             run_hash(d, b, w, L, S, lane, c_lo, c_hi);
         } else {
             commit_take(b, w);
@@ -3103,10 +3235,21 @@ __global__ __launch_bounds__(BWG) void commit_kernel(BatchDesc d, const uint32_t
         r_cur = r_nxt;
         r_nxt = round_at(rs, t + 2, f2);
     }
+    if (RO) { /* the workgroup's gathered leftover rounds to the list */
+        __syncthreads();
+        __shared__ uint32_t lbase;
+        const uint32_t nl = lcnt < LB ? lcnt : LB;
+        if (threadIdx.x == 0)
+            lbase = nl ? atomicAdd(d.round_count, nl) : 0u;
+        __syncthreads();
+        const uint32_t *lbuf = reinterpret_cast<const uint32_t *>(L + OFF_RUN + 4 * SW * NWV);
+        for (uint32_t j = threadIdx.x; j < nl; j += TPB)
+            d.round_list[lbase + j] = lbuf[j];
+    }
     /* diagnostic (zscrc_diag_wave_times): entry, after the table fill, end,
      * rounds | run rounds << 32, per wave */
     uint64_t *wt = zs_wave_times;
-    if (wt && lane == 0) {
+    if (!RO && wt && lane == 0) { /* (the tools size the buffer for 8 waves per CU) */
         const uint64_t wave = (uint64_t)blockIdx.x * (BWG / 64) + (threadIdx.x >> 6);
         wt[4 * wave + 0] = t_entry;
         wt[4 * wave + 1] = t_fill;
@@ -4308,7 +4451,11 @@ extern "C" int zs_launch_cpass_post(const zs::CPassArgs *a, const uint32_t *gtab
 
 extern "C" int zs_launch_commit(const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream)
 {
-    if (d->commit == 2)
+    if (d->round_mode == 1 && d->commit == 2)
+        hipLaunchKernelGGL((zs::commit_kernel<true, true>), dim3(grid), dim3(768), 0, stream, *d, gtab);
+    else if (d->round_mode == 1)
+        hipLaunchKernelGGL((zs::commit_kernel<false, true>), dim3(grid), dim3(768), 0, stream, *d, gtab);
+    else if (d->commit == 2)
         hipLaunchKernelGGL(zs::commit_kernel<true>, dim3(grid), dim3(zs::BWG), 0, stream, *d, gtab);
     else
         hipLaunchKernelGGL(zs::commit_kernel<false>, dim3(grid), dim3(zs::BWG), 0, stream, *d, gtab);
