@@ -64,6 +64,8 @@ for step in "$@"; do
     cwaves)   timeout -k 10 600 python tools/commit_waves.py > gpurun_out/commit_waves.jsonl 2> gpurun_out/commit_waves.err ;;
     ab4split) AB_CASES=config4_verdict,config4_crcs,config4_write,config4_verify timeout -k 10 600 python tools/opt_ab.py \
                 0 536870912 > gpurun_out/ab4split.jsonl 2> gpurun_out/ab4split.err ;;
+    ab4ro)    AB_CASES=config4_verdict,config4_crcs,config4_write,config4_verify timeout -k 10 600 python tools/opt_ab.py \
+                0 2147483648 536870912 > gpurun_out/ab4ro.jsonl 2> gpurun_out/ab4ro.err ;;
     ab4)      AB_CASES=config4_verdict,config4_write,config4_crcs timeout -k 10 600 python tools/opt_ab.py 0 4194304 \
                 > gpurun_out/ab4.jsonl 2> gpurun_out/ab4.err ;;
     ab3)      AB_CASES=config3,fixed_16KiB,fixed_4KiB timeout -k 10 600 python tools/opt_ab.py 0 16777216 \

@@ -148,6 +148,7 @@ constexpr uint32_t OPT_XSTATIC = 1u << 26; /* tuning: spans on the static walk  
 constexpr uint32_t OPT_XDEAL_PARTS = 1u << 27; /* tuning: class-3 segment plans dealt too */
 constexpr uint32_t OPT_NO_ONLY3 = 1u << 28;    /* tuning: no fused class-3-only classify */
 constexpr uint32_t OPT_NO_RUNSPLIT = 1u << 29; /* tuning: bounded commit batches in one commit_kernel */
+constexpr uint32_t OPT_RO12 = 1u << 31;        /* tuning: the run-only commit_kernel at 12 waves per CU */
 constexpr uint32_t OPT_XDEAL = 1u << 30;   /* internal: this batch is a span's dealt segments */
 struct XMulti {
     uint32_t k;

@@ -3108,26 +3108,26 @@ __device__ __forceinline__ uint32_t deal_issue(const RoundSched &s, int lane)
 }
 
 /*
- * RO (BatchDesc::round_mode 1): the run rounds only, at 12 waves per CU.
+ * RO (BatchDesc::round_mode 1): the run rounds only, at 16 (or 12) waves per CU.
  * commit_kernel holds 232 VGPRs, so 8 waves per CU; its counters against
  * qteam_kernel's (profiles/r04/pmc_config4_box.json) put config 4's time
  * per byte at wave-cycles / resident waves -- occupancy.  Without the quad
- * bursts the kernel fits 168 VGPRs (three waves per SIMD); the run rounds'
- * scratch shrinks to 192 words per wave (run_hash_ro) so twelve fit beside
- * the tables.  Every round that is not a run round (file boundaries, odd
+ * bursts the kernel fits 127 VGPRs at 1,024 threads (four waves per SIMD;
+ * 140 at 768); the run rounds' scratch shrinks to 192 words per wave
+ * (run_hash_ro) so sixteen fit beside the tables.  Every round that is not a run round (file boundaries, odd
  * spans: ~1 % of config 4's) is listed for a second launch of commit_kernel
  * in round_mode 2, which takes its rounds from the list.
  */
-template <bool WR, bool RO = false>
-__global__ __launch_bounds__(RO ? 768 : BWG) void commit_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
+template <bool WR, bool RO = false, int RT = 1024>
+__global__ __launch_bounds__(RO ? RT : BWG) void commit_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
 {
-    constexpr int TPB = RO ? 768 : BWG;
+    constexpr int TPB = RO ? RT : BWG;
     constexpr uint32_t NWV = TPB / 64;
     constexpr uint32_t SW = RO ? RUN_WORDS_RO : RUN_WORDS;
     /* RO: the workgroup's leftover rounds gathered here and listed with one
      * global atomic at the end (an atomic per round on one address would
      * serialise a batch with few run rounds); past LB, one atomic each */
-    constexpr uint32_t LB = RO ? 1536 : 0;
+    constexpr uint32_t LB = RO ? (RT > 768 ? 512 : 1536) : 0;
     __shared__ __attribute__((aligned(16))) char L[OFF_RUN + 4 * SW * NWV + 4 * LB];
     __shared__ uint32_t lctr, lcnt;
     const uint64_t count = d.n;
@@ -4451,10 +4451,16 @@ extern "C" int zs_launch_cpass_post(const zs::CPassArgs *a, const uint32_t *gtab
 
 extern "C" int zs_launch_commit(const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream)
 {
-    if (d->round_mode == 1 && d->commit == 2)
-        hipLaunchKernelGGL((zs::commit_kernel<true, true>), dim3(grid), dim3(768), 0, stream, *d, gtab);
+    /* the run-only form: 16 waves per CU (127 VGPRs), or 12 (tuning bit 1 << 31) */
+    const bool w12 = (d->opt & zs::OPT_RO12) != 0;
+    if (d->round_mode == 1 && d->commit == 2 && w12)
+        hipLaunchKernelGGL((zs::commit_kernel<true, true, 768>), dim3(grid), dim3(768), 0, stream, *d, gtab);
+    else if (d->round_mode == 1 && w12)
+        hipLaunchKernelGGL((zs::commit_kernel<false, true, 768>), dim3(grid), dim3(768), 0, stream, *d, gtab);
+    else if (d->round_mode == 1 && d->commit == 2)
+        hipLaunchKernelGGL((zs::commit_kernel<true, true, 1024>), dim3(grid), dim3(1024), 0, stream, *d, gtab);
     else if (d->round_mode == 1)
-        hipLaunchKernelGGL((zs::commit_kernel<false, true>), dim3(grid), dim3(768), 0, stream, *d, gtab);
+        hipLaunchKernelGGL((zs::commit_kernel<false, true, 1024>), dim3(grid), dim3(1024), 0, stream, *d, gtab);
     else if (d->commit == 2)
         hipLaunchKernelGGL(zs::commit_kernel<true>, dim3(grid), dim3(zs::BWG), 0, stream, *d, gtab);
     else
