@@ -121,6 +121,7 @@ def test_fill_commits_host_million(batched):
 STATIC_ROUNDS = 1 << 22   # zs::BatchDesc::opt: commit_kernel's static schedule (rounds not dealt)
 NO_RUNSPLIT = 1 << 29     # opt: one commit_kernel (not the run-only kernel + the listed leftover rounds)
 RO12 = 1 << 31            # opt: the run-only commit_kernel at 12 waves per CU (default 16)
+RO_LIST = 1 << 14         # opt: its other rounds listed for a second commit_kernel launch (default: one lane per commit)
 
 
 def test_dealt_rounds_verdicts(batched):
@@ -144,7 +145,8 @@ def test_dealt_rounds_verdicts(batched):
         k = int(nbad.item())
         assert k == len(want) and set(bad[:k].cpu().tolist()) == want
     crc_d, st_d = zsfile.verify_commits(flat, offs, lens, max_len=312)
-    for opt in (STATIC_ROUNDS, NO_RUNSPLIT, STATIC_ROUNDS | NO_RUNSPLIT, RO12, STATIC_ROUNDS | RO12):
+    for opt in (STATIC_ROUNDS, NO_RUNSPLIT, STATIC_ROUNDS | NO_RUNSPLIT, RO12, STATIC_ROUNDS | RO12, RO_LIST,
+                RO_LIST | RO12):
         lib().zscrc_set_opt(opt)
         try:
             crc_s, st_s = zsfile.verify_commits(flat, offs, lens, max_len=312)
@@ -158,10 +160,10 @@ def test_dealt_rounds_verdicts(batched):
 
 
 def test_split_commit_batches_writer_and_crcs(batched):
-    """The split bounded commit batch (the run-only commit_kernel at 16 or 12
-    waves per CU + commit_kernel on the listed leftover rounds: file boundaries,
-    stale finalise commits, the last partial round) against one
-    commit_kernel: the writer's CRCs into a zeroed copy of the image byte for
+    """The run-only commit_kernel (16 or 12 waves per CU; its other rounds --
+    file boundaries, stale finalise commits, the last partial round -- hashed
+    one lane per commit, or listed for a second commit_kernel launch) against
+    one commit_kernel: the writer's CRCs into a zeroed copy of the image byte for
     byte, the CRC array, and the per-commit arrays."""
     from zeroskip_amd._lib import lib
     img, offs, lens, nfiles = batched
@@ -170,7 +172,7 @@ def test_split_commit_batches_writer_and_crcs(batched):
     ow, lw = offs[live].contiguous(), lens[live].contiguous()
     fields = (ow + lw + 4).view(-1, 1) + torch.arange(4, device=ow.device).view(1, -1)
     out = {}
-    for opt in (0, RO12, NO_RUNSPLIT):
+    for opt in (0, RO12, RO_LIST, NO_RUNSPLIT):
         lib().zscrc_set_opt(opt)
         try:
             z = flat.clone()
@@ -183,7 +185,7 @@ def test_split_commit_batches_writer_and_crcs(batched):
             lib().zscrc_set_opt(0)
         out[opt] = (z, crcs, arr)
     assert torch.equal(out[0][0], flat)                 # the split writer restores every CRC field
-    for opt in (RO12, NO_RUNSPLIT):
+    for opt in (RO12, RO_LIST, NO_RUNSPLIT):
         assert torch.equal(out[opt][0], flat), opt
         assert torch.equal(out[0][1], out[opt][1]), opt
         assert torch.equal(out[0][2][0], out[opt][2][0]) and torch.equal(out[0][2][1], out[opt][2][1]), opt

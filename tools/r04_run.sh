@@ -48,6 +48,8 @@ for step in "$@"; do
                 > gpurun_out/abonly3.jsonl 2> gpurun_out/abonly3.err ;;
     longtests) timeout -k 10 600 $T tests/test_gpu_longspans.py > gpurun_out/longtests.log 2>&1 ;;
     tracebench) bash tools/trace_bench.sh config3 config4 config2 config5 ;;
+    trace45)  bash tools/trace_bench.sh config4 config5 ;;
+    traffic45) bash tools/pmc_traffic.sh config4 5 && bash tools/pmc_traffic.sh config4w 5 && bash tools/pmc_traffic.sh config5 5 ;;
     spantests) timeout -k 10 600 $T tests/test_gpu_stream.py tests/test_gpu_parity.py -k "span" \
                 > gpurun_out/spantests.log 2>&1 ;;
     fillsweep) timeout -k 10 600 python tools/fill_sweep.py > gpurun_out/fill_sweep.jsonl 2> gpurun_out/fill_sweep.err ;;
@@ -64,6 +66,8 @@ for step in "$@"; do
     cwaves)   timeout -k 10 600 python tools/commit_waves.py > gpurun_out/commit_waves.jsonl 2> gpurun_out/commit_waves.err ;;
     ab4split) AB_CASES=config4_verdict,config4_crcs,config4_write,config4_verify timeout -k 10 600 python tools/opt_ab.py \
                 0 536870912 > gpurun_out/ab4split.jsonl 2> gpurun_out/ab4split.err ;;
+    ab4inl)   AB_CASES=config4_verdict,config4_crcs,config4_write,config4_verify timeout -k 10 600 python tools/opt_ab.py \
+                0 16384 536870912 > gpurun_out/ab4inl.jsonl 2> gpurun_out/ab4inl.err ;;
     ab4ro)    AB_CASES=config4_verdict,config4_crcs,config4_write,config4_verify timeout -k 10 600 python tools/opt_ab.py \
                 0 2147483648 536870912 > gpurun_out/ab4ro.jsonl 2> gpurun_out/ab4ro.err ;;
     ab4)      AB_CASES=config4_verdict,config4_write,config4_crcs timeout -k 10 600 python tools/opt_ab.py 0 4194304 \

@@ -495,13 +495,17 @@ int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1
 
 /* A bounded commit batch (every span within the one-lane bound): commit_kernel
  * -- run rounds, verdicts, rounds dealt per workgroup.  Batches of at least
- * 12 rounds per wave run split (zscrc_kernels.hip, commit_kernel RO): the
- * run-only kernel at 12 waves per CU lists every other round, then
- * commit_kernel takes those.  Tuning bit 1 << 29: one commit_kernel. */
+ * 12 rounds per wave run on the run-only form (zscrc_kernels.hip,
+ * commit_kernel RO: 16 waves per CU), which hashes its other rounds one lane
+ * per commit.  Tuning bits: 1 << 29 = commit_kernel alone, 16384 = the
+ * run-only kernel lists its other rounds and commit_kernel takes them in a
+ * second launch. */
 int launch_commit(DevCtx *c, zs::BatchDesc d, hipStream_t s)
 {
     const uint64_t nr = (d.n + 63) / 64;
-    if ((d.opt & zs::OPT_NO_RUNSPLIT) || nr < (uint64_t)c->ncu * 12 || nr >= (1ull << 32)) {
+    const bool split = !(d.opt & zs::OPT_NO_RUNSPLIT) && nr >= (uint64_t)c->ncu * 12 && nr < (1ull << 32);
+    if (!split || !(d.opt & zs::OPT_RO_LIST)) {
+        d.round_mode = split ? 3 : 0;
         if (zs_launch_commit(&d, c->gtab, c->ncu, s)) {
             set_err("commit kernel launch", hipGetLastError());
             return ZSCRC_EHIP;

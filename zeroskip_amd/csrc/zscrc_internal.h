@@ -92,7 +92,10 @@ struct BatchDesc {
                              plans dealt per workgroup too (g_xdeal segments per wave; default
                              one per wave, static), 1 << 28 = no fused class-3-only classify
                              (Classify::only3), 1 << 29 = bounded commit batches on one
-                             commit_kernel (not the run-only kernel + leftover rounds);
+                             commit_kernel (not the run-only kernel), 16384 = the run-only
+                             kernel lists its other rounds for a second commit_kernel launch
+                             (instead of hashing them one lane per commit), 1 << 31 = the
+                             run-only kernel at 12 waves per CU (not 16);
                              OPT_XDEAL (1 << 30) is set
                              by the span launches themselves, not a tuning bit */
     uint32_t *part_out;
@@ -109,10 +112,10 @@ struct BatchDesc {
      * class's bytes laid end to end (part_fold_kernel's last-part shift) */
     const uint64_t *rec_start;
     const uint32_t *seg_first; /* segment plans: first part of segment w */
-    /* commit_kernel's split form: round_mode 1 = the run-only kernel (12
-     * waves per CU) appends every round that is not a run round to
-     * round_list (*round_count, zeroed before); 2 = commit_kernel takes its
-     * rounds from that list */
+    /* commit_kernel's run-only form (16 waves per CU): round_mode 3 = every
+     * round that is not a run round hashed one lane per commit in the same
+     * launch; 1 = such rounds appended to round_list (*round_count, zeroed
+     * before) and 2 = commit_kernel takes its rounds from that list */
     int round_mode;
     uint32_t *round_list;
     uint32_t *round_count;
@@ -149,6 +152,7 @@ constexpr uint32_t OPT_XDEAL_PARTS = 1u << 27; /* tuning: class-3 segment plans 
 constexpr uint32_t OPT_NO_ONLY3 = 1u << 28;    /* tuning: no fused class-3-only classify */
 constexpr uint32_t OPT_NO_RUNSPLIT = 1u << 29; /* tuning: bounded commit batches in one commit_kernel */
 constexpr uint32_t OPT_RO12 = 1u << 31;        /* tuning: the run-only commit_kernel at 12 waves per CU */
+constexpr uint32_t OPT_RO_LIST = 1u << 14;     /* tuning: its other rounds listed for a second launch */
 constexpr uint32_t OPT_XDEAL = 1u << 30;   /* internal: this batch is a span's dealt segments */
 struct XMulti {
     uint32_t k;

@@ -2775,6 +2775,160 @@ __device__ __forceinline__ void run_hash_ro(const BatchDesc &d, BRec &b, uint32_
     emit(d, b.it, reg, L, c_lo, c_hi);
 }
 
+/* Piece p (< 2) of a grid whose record starts d0 bytes in (0..63): the
+ * bytes before the record zeroed, the initial register XOR-ed in at its
+ * first byte (which can spill into piece 1).  Per lane. */
+__device__ __forceinline__ void front_fix(uint32_t (&x)[16], int32_t d0, uint32_t p, uint32_t R0)
+{
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int32_t dk = d0 - 64 * (int32_t)p - 4 * k;
+        uint32_t v = x[k];
+        if (dk >= 4)
+            v = 0;
+        else if (dk > 0)
+            v &= 0xffffffffu << (8 * dk);
+        if (dk >= 0 && dk < 4)
+            v ^= R0 << (8 * dk);
+        else if (dk < 0 && dk > -4)
+            v ^= R0 >> (8 * -dk);
+        x[k] = v;
+    }
+}
+
+/* A record's np 64-byte grid pieces from V0 by one lane with clamped dword
+ * loads: the bytes before A zeroed, the initial register XOR-ed in at A. */
+__device__ __forceinline__ uint32_t clamped_pieces(const char *L, const Item &it, uintptr_t V0, uint64_t np,
+                                                   uintptr_t lo, uint32_t c_lo, uint32_t c_hi)
+{
+    uint32_t r = 0;
+    const int32_t d0 = (int32_t)(it.A - V0);
+    for (uint64_t p = 0; p < np; ++p) {
+        const uintptr_t q = V0 + 64 * p;
+        uint32_t x[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            x[k] = *(g32p)(q + 4 * k < lo ? lo : q + 4 * k);
+        if (p < 2)
+            front_fix(x, d0, (uint32_t)p, it.R0);
+        r = piece<false>(L, r, x, c_lo, c_hi);
+    }
+    return r;
+}
+
+/* One record hashed by its own lane without burst registers: spans under 8
+ * bytes byte by byte, others piece by piece over their 64-byte grid
+ * (clamped_pieces), then the tail bytes and the trailer -- burst_hash's
+ * paths for records without a burst.  The run-only commit_kernel's rounds
+ * that are not run rounds.
+ * Per lane: no cross-lane operations, so lanes may diverge. */
+__device__ __forceinline__ void lane_hash(const BatchDesc &d, BRec &b, const char *L, uintptr_t lo, uint32_t c_lo,
+                                          uint32_t c_hi)
+{
+    if (!b.ok || b.skip)
+        return;
+    Item &it = b.it;
+    const uintptr_t A = it.A, E = it.E;
+    uint32_t r;
+    if (b.np == 0) {
+        r = it.R0;
+        for (uint64_t k = 0; k < it.len; ++k)
+            r = byte_step(L, r, ((g8p)A)[k], c_hi);
+        emit(d, it, r, L, c_lo, c_hi);
+        return;
+    }
+    r = clamped_pieces(L, it, b.V0, b.np, lo, c_lo, c_hi);
+    const uint32_t tail = (uint32_t)((A + it.len) - E);
+    for (uint32_t k = 0; k < tail; ++k)
+        r = byte_step(L, r, ((g8p)E)[k], c_hi);
+    emit(d, it, r, L, c_lo, c_hi);
+}
+
+/* A round that is not a run round, in the run-only commit_kernel: its
+ * records in one-piece quad bursts.  For piece p, lane (g, c) loads bytes
+ * [16g, 16g+16) of piece p of the records of lanes (t, c), t = 0..3, and the
+ * row transpose (xpose_burst) hands each lane its own record's piece: 16-32
+ * cache lines per load instruction on 16 registers a piece, piece p + 1
+ * issued before piece p is hashed.  A lane's own dword loads (lane_hash)
+ * touch 64 lines an instruction: config 4's verdict measured 0.565 ms with
+ * those against 0.526 with these rounds listed for a second launch
+ * (profiles/r04/inline1).  Records without a burst (spans under 8 bytes,
+ * grids below the buffer) take lane_hash.  quad_round_issue issues piece 0
+ * (the caller then issues its next descriptors), quad_round_hash the rest.
+ * Every lane active. */
+struct QuadRound {
+    uintptr_t V[4]; /* grid bases of lanes (t, c) */
+    uint32_t np[4]; /* their burst pieces (0: no burst) */
+    uint32_t npw;   /* the wave's most pieces */
+    uint32_t w[1][16];
+};
+
+__device__ __forceinline__ void quad_piece(const QuadRound &Q, uint32_t p, uintptr_t dummy, int lane,
+                                           uint32_t (&w)[1][16])
+{
+    const uint32_t g = (uint32_t)lane >> 4;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const uintptr_t q = p < Q.np[t] ? Q.V[t] + 64u * p + 16u * g : dummy + 16u * g;
+        const u32x4 v = *(g4p)q;
+        w[0][4 * t + 0] = v.x;
+        w[0][4 * t + 1] = v.y;
+        w[0][4 * t + 2] = v.z;
+        w[0][4 * t + 3] = v.w;
+    }
+}
+
+__device__ __forceinline__ void quad_round_issue(const BRec &b, QuadRound &Q, uintptr_t dummy, int lane)
+{
+    const bool mine = b.ok && !b.skip && b.burst;
+    const uint32_t np = mine ? (uint32_t)b.np : 0u;
+    const uint32_t v_lo = (uint32_t)b.V0, v_hi = (uint32_t)((uint64_t)b.V0 >> 32);
+    const int c = lane & 15;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int src = 16 * t + c;
+        Q.V[t] = ((uintptr_t)__shfl(v_hi, src) << 32) | __shfl(v_lo, src);
+        Q.np[t] = __shfl(np, src);
+    }
+    uint32_t m = np;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1)
+        m = max(m, (uint32_t)__shfl_xor((int)m, o));
+    Q.npw = __builtin_amdgcn_readfirstlane(m);
+    quad_piece(Q, 0, dummy, lane, Q.w);
+}
+
+__device__ __forceinline__ void quad_round_hash(const BatchDesc &d, BRec &b, QuadRound &Q, const char *L,
+                                                uintptr_t lo, uintptr_t dummy, int lane, uint32_t c_lo,
+                                                uint32_t c_hi)
+{
+    const bool mine = b.ok && !b.skip && b.burst;
+    const uint32_t np = mine ? (uint32_t)b.np : 0u;
+    const int32_t d0 = (int32_t)(b.it.A - b.V0);
+    uint32_t r = 0;
+    for (uint32_t p = 0; p < Q.npw; ++p) {
+        if (p)
+            quad_piece(Q, p, dummy, lane, Q.w);
+        xpose_burst<1>(Q.w);
+        if (p == 0)
+            commit_take<1>(b, Q.w);
+        if (p < np) {
+            if (p < 2)
+                front_fix(Q.w[0], d0, p, b.it.R0);
+            r = piece<false>(L, r, Q.w[0], c_lo, c_hi);
+        }
+    }
+    if (mine) {
+        const uintptr_t E = b.it.E;
+        const uint32_t tail = (uint32_t)((b.it.A + b.it.len) - E);
+        for (uint32_t k = 0; k < tail; ++k)
+            r = byte_step(L, r, ((g8p)E)[k], c_hi);
+        emit(d, b.it, r, L, c_lo, c_hi);
+    } else {
+        lane_hash(d, b, L, lo, c_lo, c_hi);
+    }
+}
+
 /* FX: fixed-stride batch (the bitop3-folded chain measured faster there) */
 template <int NB, bool FX>
 __device__ __forceinline__ void burst_hash(const BatchDesc &d, BRec &b, uint32_t (&w)[NB][16], const char *L,
@@ -2868,32 +3022,7 @@ __device__ __forceinline__ void burst_hash(const BatchDesc &d, BRec &b, uint32_t
                     r = piece<false>(L, r, w[p], c_lo, c_hi);
         }
     } else {
-        r = 0;
-        const int32_t d0 = (int32_t)(A - V0);
-        for (uint64_t p = 0; p < b.np; ++p) {
-            const uintptr_t q = V0 + 64 * p;
-            uint32_t x[16];
-#pragma unroll
-            for (int k = 0; k < 16; ++k)
-                x[k] = *(g32p)(q + 4 * k < lo ? lo : q + 4 * k);
-            if (p < 2) {
-#pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                    const int32_t dk = d0 - 64 * (int32_t)p - 4 * k;
-                    uint32_t v = x[k];
-                    if (dk >= 4)
-                        v = 0;
-                    else if (dk > 0)
-                        v &= 0xffffffffu << (8 * dk);
-                    if (dk >= 0 && dk < 4)
-                        v ^= it.R0 << (8 * dk);
-                    else if (dk < 0 && dk > -4)
-                        v ^= it.R0 >> (8 * -dk);
-                    x[k] = v;
-                }
-            }
-            r = piece<false>(L, r, x, c_lo, c_hi);
-        }
+        r = clamped_pieces(L, it, V0, b.np, lo, c_lo, c_hi);
     }
     const uint32_t tail = (uint32_t)((A + it.len) - E);
     for (uint32_t k = 0; k < tail; ++k)
@@ -3108,15 +3237,20 @@ __device__ __forceinline__ uint32_t deal_issue(const RoundSched &s, int lane)
 }
 
 /*
- * RO (BatchDesc::round_mode 1): the run rounds only, at 16 (or 12) waves per CU.
+ * RO (BatchDesc::round_mode 3, or 1): the run rounds at 16 (or 12) waves per CU.
  * commit_kernel holds 232 VGPRs, so 8 waves per CU; its counters against
  * qteam_kernel's (profiles/r04/pmc_config4_box.json) put config 4's time
  * per byte at wave-cycles / resident waves -- occupancy.  Without the quad
  * bursts the kernel fits 127 VGPRs at 1,024 threads (four waves per SIMD;
  * 140 at 768); the run rounds' scratch shrinks to 192 words per wave
- * (run_hash_ro) so sixteen fit beside the tables.  Every round that is not a run round (file boundaries, odd
- * spans: ~1 % of config 4's) is listed for a second launch of commit_kernel
- * in round_mode 2, which takes its rounds from the list.
+ * (run_hash_ro) so sixteen fit beside the tables.  A round that is not a
+ * run round (file boundaries, odd spans: ~1 % of config 4's) is hashed in
+ * one-piece quad bursts (quad_round_hash: 16 registers a piece) in
+ * round_mode 3; in round_mode 1 it is listed for a second launch of
+ * commit_kernel in round_mode 2, which takes its rounds from the list --
+ * that launch measured 22.7 us per call (profiles/r04/trace45: ~1,500
+ * rounds, one per wave, at the latency of one quad-burst round plus the
+ * launch and table fill), ~4 % of config 4's verdict.
  */
 template <bool WR, bool RO = false, int RT = 1024>
 __global__ __launch_bounds__(RO ? RT : BWG) void commit_kernel(BatchDesc d, const uint32_t *__restrict__ gtab)
@@ -3191,6 +3325,19 @@ __global__ __launch_bounds__(RO ? RT : BWG) void commit_kernel(BatchDesc d, cons
         b.run = false;
         run_check(d, b, lane);
         const bool run = __builtin_amdgcn_readfirstlane((uint32_t)b.run) != 0;
+        if (RO && !run && d.round_mode == 3) { /* not a run round: one-piece quad bursts */
+            QuadRound Q;
+            quad_round_issue(b, Q, dummy, lane);
+            const uint64_t i_nxt = 64 * r_nxt + (uint64_t)lane;
+            bdesc_load(d, i_nxt, count, q);
+            commit_load(b);
+            const uint32_t f2 = deal_issue(rs, lane);
+            quad_round_hash(d, b, Q, L, lo, dummy, lane, c_lo, c_hi);
+            i = i_nxt;
+            r_cur = r_nxt;
+            r_nxt = round_at(rs, t + 2, f2);
+            continue;
+        }
         if (RO && !run) { /* not a run round: listed for the second launch */
             if (lane == 0) {
                 uint32_t *lbuf = reinterpret_cast<uint32_t *>(L + OFF_RUN + 4 * SW * NWV);
@@ -3235,7 +3382,7 @@ __global__ __launch_bounds__(RO ? RT : BWG) void commit_kernel(BatchDesc d, cons
         r_cur = r_nxt;
         r_nxt = round_at(rs, t + 2, f2);
     }
-    if (RO) { /* the workgroup's gathered leftover rounds to the list */
+    if (RO && d.round_mode == 1) { /* the workgroup's gathered leftover rounds to the list */
         __syncthreads();
         __shared__ uint32_t lbase;
         const uint32_t nl = lcnt < LB ? lcnt : LB;
@@ -4453,13 +4600,14 @@ extern "C" int zs_launch_commit(const zs::BatchDesc *d, const uint32_t *gtab, in
 {
     /* the run-only form: 16 waves per CU (127 VGPRs), or 12 (tuning bit 1 << 31) */
     const bool w12 = (d->opt & zs::OPT_RO12) != 0;
-    if (d->round_mode == 1 && d->commit == 2 && w12)
+    const bool ro = d->round_mode == 1 || d->round_mode == 3;
+    if (ro && d->commit == 2 && w12)
         hipLaunchKernelGGL((zs::commit_kernel<true, true, 768>), dim3(grid), dim3(768), 0, stream, *d, gtab);
-    else if (d->round_mode == 1 && w12)
+    else if (ro && w12)
         hipLaunchKernelGGL((zs::commit_kernel<false, true, 768>), dim3(grid), dim3(768), 0, stream, *d, gtab);
-    else if (d->round_mode == 1 && d->commit == 2)
+    else if (ro && d->commit == 2)
         hipLaunchKernelGGL((zs::commit_kernel<true, true, 1024>), dim3(grid), dim3(1024), 0, stream, *d, gtab);
-    else if (d->round_mode == 1)
+    else if (ro)
         hipLaunchKernelGGL((zs::commit_kernel<false, true, 1024>), dim3(grid), dim3(1024), 0, stream, *d, gtab);
     else if (d->commit == 2)
         hipLaunchKernelGGL(zs::commit_kernel<true>, dim3(grid), dim3(zs::BWG), 0, stream, *d, gtab);
