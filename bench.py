@@ -814,8 +814,9 @@ def run_config4(args, world, rank, dev, stream):
         del images, pinned, back
 
     nbytes = span_bytes + 8 * ncommit + 16 * ncommit   # spans + commit trailers + descriptors
-    r = roof(nbytes, kern_ms, "zs::commit_kernel<false> (verdict: run rounds of 64 back-to-back spans as coalesced "
-                              "1 KiB loads, quad bursts elsewhere)",
+    r = roof(nbytes, kern_ms, "zs::commit_kernel<false, true, 1024> (verdict, the run-only form at 16 waves per CU: "
+                              "run rounds of 64 back-to-back spans as coalesced 1 KiB loads, other rounds in "
+                              "one-piece quad bursts)",
              traffic_for("config4_bytes_per_launch"), read_peak)
     out_line = line(args, world, elapsed, span_bytes * world * args.steps,
                     {"workload": f"config4: zsbench writeseqtxn replay, {pairs_total} pairs per GPU, "

@@ -121,7 +121,7 @@ def test_fill_commits_host_million(batched):
 STATIC_ROUNDS = 1 << 22   # zs::BatchDesc::opt: commit_kernel's static schedule (rounds not dealt)
 NO_RUNSPLIT = 1 << 29     # opt: one commit_kernel (not the run-only kernel + the listed leftover rounds)
 RO12 = 1 << 31            # opt: the run-only commit_kernel at 12 waves per CU (default 16)
-RO_LIST = 1 << 14         # opt: its other rounds listed for a second commit_kernel launch (default: one lane per commit)
+RO_LIST = 1 << 14         # opt: its other rounds listed for a second commit_kernel launch (default: quad bursts)
 
 
 def test_dealt_rounds_verdicts(batched):
@@ -146,7 +146,7 @@ def test_dealt_rounds_verdicts(batched):
         assert k == len(want) and set(bad[:k].cpu().tolist()) == want
     crc_d, st_d = zsfile.verify_commits(flat, offs, lens, max_len=312)
     for opt in (STATIC_ROUNDS, NO_RUNSPLIT, STATIC_ROUNDS | NO_RUNSPLIT, RO12, STATIC_ROUNDS | RO12, RO_LIST,
-                RO_LIST | RO12):
+                RO_LIST | RO12, 0):
         lib().zscrc_set_opt(opt)
         try:
             crc_s, st_s = zsfile.verify_commits(flat, offs, lens, max_len=312)
@@ -162,8 +162,8 @@ def test_dealt_rounds_verdicts(batched):
 def test_split_commit_batches_writer_and_crcs(batched):
     """The run-only commit_kernel (16 or 12 waves per CU; its other rounds --
     file boundaries, stale finalise commits, the last partial round -- hashed
-    one lane per commit, or listed for a second commit_kernel launch) against
-    one commit_kernel: the writer's CRCs into a zeroed copy of the image byte for
+    in one-piece quad bursts, or listed for a second commit_kernel launch)
+    against one commit_kernel: the writer's CRCs into a zeroed copy of the image byte for
     byte, the CRC array, and the per-commit arrays."""
     from zeroskip_amd._lib import lib
     img, offs, lens, nfiles = batched
@@ -189,3 +189,24 @@ def test_split_commit_batches_writer_and_crcs(batched):
         assert torch.equal(out[opt][0], flat), opt
         assert torch.equal(out[0][1], out[opt][1]), opt
         assert torch.equal(out[0][2][0], out[opt][2][0]) and torch.equal(out[0][2][1], out[opt][2][1]), opt
+
+
+def test_verdicts_two_streams(batched):
+    """The run-only commit_kernel's verdicts alternating between two streams,
+    back to back, all find the same corrupt commits."""
+    img, offs, lens, nfiles = batched
+    flat = img.view(-1).clone()
+    live = torch.nonzero(lens > 0).flatten()
+    hit = live[torch.tensor([0, 5000, live.numel() // 2, live.numel() - 1], device=live.device)]
+    flat[offs[hit] + 37] ^= 0x5A
+    want = set(hit.cpu().tolist()) | set(torch.nonzero(lens == 0).flatten().cpu().tolist())
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = []
+    for k in range(6):
+        st = s1 if k % 2 == 0 else s2
+        with torch.cuda.stream(st):
+            outs.append(zsfile.verify_commits_verdict(flat, offs, lens, max_len=312, cap=8192))
+    torch.cuda.synchronize()
+    for nbad, bad in outs:
+        k = int(nbad.item())
+        assert k == len(want) and set(bad[:k].cpu().tolist()) == want

@@ -4,8 +4,10 @@ launch into table fill, run rounds and quad-burst rounds (file boundaries,
 stale finalise commits), and the tail (the spread of per-wave end times),
 with and without the per-record trailer + verdict (tuning bit 8192) and the
 chains (4096), so the gap between the verdict and the bare load + hash of
-tools/run_probe.hip can be named.
-usage (GPU box): python tools/commit_waves.py"""
+tools/run_probe.hip can be named.  The run-only form (default) runs 16 waves
+per workgroup, 12 with bit 1 << 31; commit_kernel alone (1 << 29) 8; the
+listed form (16384) is not timed here (its second launch reuses the wave slots).
+usage (GPU box): python tools/commit_waves.py [base|all]"""
 import json
 import os
 import sys
@@ -18,7 +20,10 @@ from tools import zsdb_gen as zg  # noqa: E402
 from zeroskip_amd import zsfile  # noqa: E402
 from zeroskip_amd._lib import check, lib  # noqa: E402
 
-BWG_WAVES = 8   # commit_kernel: 512-thread workgroups
+def block_waves(opt):
+    if opt & (1 << 29):
+        return 8    # commit_kernel: 512-thread workgroups
+    return 12 if opt & (1 << 31) else 16
 
 
 def waves(name, fn, nwaves, opt=0):
@@ -55,7 +60,7 @@ def waves(name, fn, nwaves, opt=0):
     # where the spread lives: inside a workgroup (its 8 waves) or between
     # workgroups (CUs), and between XCDs (blockIdx.x % 8)
     wid = np.nonzero(live)[0]
-    blk = wid // BWG_WAVES
+    blk = wid // block_waves(opt)
     ub = np.unique(blk)
     bmax = np.array([end[blk == b].max() for b in ub])
     bmin = np.array([end[blk == b].min() for b in ub])
@@ -80,7 +85,7 @@ def main():
     g = torch.Generator(device=dev)
     g.manual_seed(0x5EED)
     ncu = torch.cuda.get_device_properties(0).multi_processor_count
-    nw = ncu * BWG_WAVES
+    nw = ncu * 16
     ppf = zg.pairs_per_file(True)
     nfiles = -(-10_000_000 // ppf)
     img = zg.log_files(bytes(range(16)), 0, nfiles, ppf, 0, True, g, dev).view(-1)
@@ -88,8 +93,12 @@ def main():
     mx = int(lens.max().item())
     vout = (torch.empty(1, dtype=torch.int64, device=dev), torch.empty(4096, dtype=torch.int64, device=dev))
     fn = lambda: zsfile.verify_commits_verdict(img, offs, lens, max_len=mx, out=vout)  # noqa: E731
+    waves("config4 verdict (run-only kernel, other rounds in quad bursts)", fn, nw)
+    waves("config4 verdict, commit_kernel alone (1 << 29)", fn, nw, 1 << 29)
+    waves("config4 verdict, run-only at 12 waves (1 << 31)", fn, nw, 1 << 31)
+    if sys.argv[1:] == ["base"]:
+        return
     waves("config4 verdict, static rounds (1 << 22)", fn, nw, 1 << 22)
-    waves("config4 verdict (rounds dealt per workgroup)", fn, nw)
     waves("config4 verdict, no trailer / stores (diag 8192)", fn, nw, 8192)
     waves("config4 verdict, no chains (diag 4096)", fn, nw, 4096)
     waves("config4 verdict, no run rounds (2048)", fn, nw, 2048)

@@ -3267,7 +3267,10 @@ __global__ __launch_bounds__(RO ? RT : BWG) void commit_kernel(BatchDesc d, cons
     const uint64_t count = d.n;
     if ((uint64_t)blockIdx.x * TPB >= count)
         return;
-    const uint64_t t_entry = __builtin_amdgcn_s_memrealtime();
+    /* diagnostic (zscrc_diag_wave_times): each timestamp stored when taken
+     * (held across the loop, they cost the run-only form a spill) */
+    if (zs_wave_times && (threadIdx.x & 63) == 0)
+        zs_wave_times[4 * ((uint64_t)blockIdx.x * NWV + (threadIdx.x >> 6)) + 0] = __builtin_amdgcn_s_memrealtime();
     if (threadIdx.x == 0) {
         lctr = 0;
         lcnt = 0;
@@ -3313,7 +3316,8 @@ __global__ __launch_bounds__(RO ? RT : BWG) void commit_kernel(BatchDesc d, cons
     BDesc q;
     bdesc_load(d, i, count, q);
     uint32_t w[5][16];
-    const uint64_t t_fill = __builtin_amdgcn_s_memrealtime();
+    if (zs_wave_times && lane == 0)
+        zs_wave_times[4 * ((uint64_t)blockIdx.x * NWV + (threadIdx.x >> 6)) + 1] = __builtin_amdgcn_s_memrealtime();
     uint32_t rounds = 0, runs = 0;
     for (uint64_t t = 0;; ++t) {
         BRec b;
@@ -3396,12 +3400,11 @@ __global__ __launch_bounds__(RO ? RT : BWG) void commit_kernel(BatchDesc d, cons
     /* diagnostic (zscrc_diag_wave_times): entry, after the table fill, end,
      * rounds | run rounds << 32, per wave */
     uint64_t *wt = zs_wave_times;
-    if (!RO && wt && lane == 0) { /* (the tools size the buffer for 8 waves per CU) */
-        const uint64_t wave = (uint64_t)blockIdx.x * (BWG / 64) + (threadIdx.x >> 6);
-        wt[4 * wave + 0] = t_entry;
-        wt[4 * wave + 1] = t_fill;
+    if (wt && lane == 0) { /* (the tools size the buffer for 16 waves per CU) */
+        const uint64_t wave = rs.w;
         wt[4 * wave + 2] = __builtin_amdgcn_s_memrealtime();
-        wt[4 * wave + 3] = (uint64_t)rounds | ((uint64_t)runs << 32);
+        /* (the run-only form: no counts -- live across its loop, they spill) */
+        wt[4 * wave + 3] = RO ? 0u : (uint64_t)rounds | ((uint64_t)runs << 32);
     }
 }
 
