@@ -68,6 +68,8 @@ for step in "$@"; do
                 0 536870912 > gpurun_out/ab4split.jsonl 2> gpurun_out/ab4split.err ;;
     ab4inl)   AB_CASES=config4_verdict,config4_crcs,config4_write,config4_verify timeout -k 10 600 python tools/opt_ab.py \
                 0 16384 536870912 > gpurun_out/ab4inl.jsonl 2> gpurun_out/ab4inl.err ;;
+    ab4final) AB_CASES=config4_verdict,config4_crcs,config4_write,config4_verify timeout -k 10 600 python tools/opt_ab.py \
+                0 16384 2147483648 536870912 > gpurun_out/ab4final.jsonl 2> gpurun_out/ab4final.err ;;
     ab4steal) AB_CASES=config4_verdict,config4_crcs,config4_write,config4_verify timeout -k 10 600 python tools/opt_ab.py \
                 0 512 16384 > gpurun_out/ab4steal.jsonl 2> gpurun_out/ab4steal.err ;;
     cwavesb)  timeout -k 10 600 python tools/commit_waves.py base > gpurun_out/commit_waves_base.jsonl 2> gpurun_out/commit_waves.err ;;
