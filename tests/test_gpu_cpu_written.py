@@ -191,9 +191,12 @@ def test_split_commit_batches_writer_and_crcs(batched):
         assert torch.equal(out[0][2][0], out[opt][2][0]) and torch.equal(out[0][2][1], out[opt][2][1]), opt
 
 
-def test_verdicts_two_streams(batched):
-    """The run-only commit_kernel's verdicts alternating between two streams,
-    back to back, all find the same corrupt commits."""
+@pytest.mark.parametrize("opt", [0, RO12])
+def test_verdicts_two_streams(batched, opt):
+    """The run-only commit_kernel's verdicts (16 and 12 waves per CU)
+    alternating between two streams, back to back, all find the same corrupt
+    commits."""
+    from zeroskip_amd._lib import lib
     img, offs, lens, nfiles = batched
     flat = img.view(-1).clone()
     live = torch.nonzero(lens > 0).flatten()
@@ -202,11 +205,15 @@ def test_verdicts_two_streams(batched):
     want = set(hit.cpu().tolist()) | set(torch.nonzero(lens == 0).flatten().cpu().tolist())
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
     outs = []
-    for k in range(6):
-        st = s1 if k % 2 == 0 else s2
-        with torch.cuda.stream(st):
-            outs.append(zsfile.verify_commits_verdict(flat, offs, lens, max_len=312, cap=8192))
-    torch.cuda.synchronize()
+    lib().zscrc_set_opt(opt)
+    try:
+        for k in range(6):
+            st = s1 if k % 2 == 0 else s2
+            with torch.cuda.stream(st):
+                outs.append(zsfile.verify_commits_verdict(flat, offs, lens, max_len=312, cap=8192))
+        torch.cuda.synchronize()
+    finally:
+        lib().zscrc_set_opt(0)
     for nbad, bad in outs:
         k = int(nbad.item())
         assert k == len(want) and set(bad[:k].cpu().tolist()) == want

@@ -70,6 +70,16 @@ for step in "$@"; do
                 0 16384 536870912 > gpurun_out/ab4inl.jsonl 2> gpurun_out/ab4inl.err ;;
     ab4final) AB_CASES=config4_verdict,config4_crcs,config4_write,config4_verify timeout -k 10 600 python tools/opt_ab.py \
                 0 16384 2147483648 536870912 > gpurun_out/ab4final.jsonl 2> gpurun_out/ab4final.err ;;
+    ab4tail)  AB_CASES=config4_verdict,config4_crcs,config4_write,config4_verify timeout -k 10 600 python tools/opt_ab.py \
+                0 2147483648 2147484160 > gpurun_out/ab4tail.jsonl 2> gpurun_out/ab4tail.err ;;
+    bench4t)  ZSCRC_OPT=2147483648 timeout -k 10 600 python bench.py --workload config4 --no-e2e --no-cpu \
+                >> gpurun_out/bench4t.jsonl 2> gpurun_out/bench4t.err ;;
+    bench4u)  ZSCRC_OPT=2147484160 timeout -k 10 600 python bench.py --workload config4 --no-e2e --no-cpu \
+                >> gpurun_out/bench4u.jsonl 2> gpurun_out/bench4u.err ;;
+    bench4d)  timeout -k 10 600 python bench.py --workload config4 --no-e2e --no-cpu \
+                >> gpurun_out/bench4d.jsonl 2> gpurun_out/bench4d.err ;;
+    bench4h)  ZSCRC_LIB_PATH=$PWD/zeroskip_amd/libzscrc_head.so timeout -k 10 600 python bench.py --workload config4 \
+                --no-e2e --no-cpu >> gpurun_out/bench4h.jsonl 2> gpurun_out/bench4h.err ;;
     ab4steal) AB_CASES=config4_verdict,config4_crcs,config4_write,config4_verify timeout -k 10 600 python tools/opt_ab.py \
                 0 512 16384 > gpurun_out/ab4steal.jsonl 2> gpurun_out/ab4steal.err ;;
     cwavesb)  timeout -k 10 600 python tools/commit_waves.py base > gpurun_out/commit_waves_base.jsonl 2> gpurun_out/commit_waves.err ;;

@@ -3213,6 +3213,8 @@ __device__ __forceinline__ uint64_t slot_round(const RoundSched &s, uint64_t k)
 {
     if (k >= s.ns)
         return s.nr;
+    /* (readfirstlane returns int: widened directly it sign-extends past 2^31 --
+     * rounds and slots stay below 2^31 here, the host caps nr below 2^32) */
     return s.list ? (uint64_t)__builtin_amdgcn_readfirstlane(((g32p)s.list)[k]) : k;
 }
 
