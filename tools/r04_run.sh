@@ -80,6 +80,7 @@ for step in "$@"; do
                 >> gpurun_out/bench4d.jsonl 2> gpurun_out/bench4d.err ;;
     bench4l)  ZSCRC_OPT=16384 timeout -k 10 600 python bench.py --workload config4 --no-e2e --no-cpu \
                 >> gpurun_out/bench4l.jsonl 2> gpurun_out/bench4l.err ;;
+    benchdef) timeout -k 10 600 python bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err ;;
     bench4h)  ZSCRC_LIB_PATH=$PWD/zeroskip_amd/libzscrc_head.so timeout -k 10 600 python bench.py --workload config4 \
                 --no-e2e --no-cpu >> gpurun_out/bench4h.jsonl 2> gpurun_out/bench4h.err ;;
     ab4steal) AB_CASES=config4_verdict,config4_crcs,config4_write,config4_verify timeout -k 10 600 python tools/opt_ab.py \
