@@ -81,6 +81,12 @@ for step in "$@"; do
     bench4l)  ZSCRC_OPT=16384 timeout -k 10 600 python bench.py --workload config4 --no-e2e --no-cpu \
                 >> gpurun_out/bench4l.jsonl 2> gpurun_out/bench4l.err ;;
     benchdef) timeout -k 10 600 python bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err ;;
+    ab2nt)    AB_CASES=config2_multi32,config2_warm32 timeout -k 10 600 python tools/opt_ab.py 0 64 > gpurun_out/ab2nt.jsonl \
+                2> gpurun_out/ab2nt.err ;;
+    bench2nt) ZSCRC_OPT=64 timeout -k 10 600 python bench.py --workload config2 --no-cpu >> gpurun_out/bench2nt.jsonl \
+                2> gpurun_out/bench2nt.err ;;
+    bench2d)  timeout -k 10 600 python bench.py --workload config2 --no-cpu >> gpurun_out/bench2d.jsonl \
+                2> gpurun_out/bench2d.err ;;
     bench4h)  ZSCRC_LIB_PATH=$PWD/zeroskip_amd/libzscrc_head.so timeout -k 10 600 python bench.py --workload config4 \
                 --no-e2e --no-cpu >> gpurun_out/bench4h.jsonl 2> gpurun_out/bench4h.err ;;
     ab4steal) AB_CASES=config4_verdict,config4_crcs,config4_write,config4_verify timeout -k 10 600 python tools/opt_ab.py \
