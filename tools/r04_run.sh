@@ -90,6 +90,9 @@ for step in "$@"; do
     sustain45) PC_TIME=1 timeout -k 10 300 python tools/prof_case.py config4 200 > gpurun_out/sustain_config4.json \
                 2> gpurun_out/sustain.err && PC_TIME=1 timeout -k 10 300 python tools/prof_case.py config5 200 \
                 > gpurun_out/sustain_config5.json 2>> gpurun_out/sustain.err ;;
+    bench3d)  timeout -k 10 600 python bench.py --workload config3 --no-cpu >> gpurun_out/bench3d.jsonl 2> gpurun_out/bench3d.err ;;
+    bench3f)  ZSCRC_OPT=32 timeout -k 10 600 python bench.py --workload config3 --no-cpu >> gpurun_out/bench3f.jsonl \
+                2> gpurun_out/bench3f.err ;;
     bench4h)  ZSCRC_LIB_PATH=$PWD/zeroskip_amd/libzscrc_head.so timeout -k 10 600 python bench.py --workload config4 \
                 --no-e2e --no-cpu >> gpurun_out/bench4h.jsonl 2> gpurun_out/bench4h.err ;;
     ab4steal) AB_CASES=config4_verdict,config4_crcs,config4_write,config4_verify timeout -k 10 600 python tools/opt_ab.py \
