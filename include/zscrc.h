@@ -20,12 +20,16 @@
 extern "C" {
 #endif
 
-/* ABI version of this header.  3: round-3 ABI (zscrc_files_report.devices,
+/* ABI version of this header.  4: the drop-in symbols offload large calls to
+ * the GPU by default (32 MiB once a device context exists, 5 GiB before one;
+ * earlier versions never offloaded unless asked -- INTEGRATION.md 2), and
+ * zscrc_release_cache() also frees the fill and scalar-offload caches.
+ * 3: round-3 ABI (zscrc_files_report.devices,
  * the device-slot API); 2 added image_size / d_status to the commit entry
  * points.  A caller built against this header checks at startup that
  * zscrc_abi_version() == ZSCRC_ABI_VERSION: a library of another version
  * has other struct layouts or argument lists. */
-#define ZSCRC_ABI_VERSION 3
+#define ZSCRC_ABI_VERSION 4
 int zscrc_abi_version(void);
 
 /* zeroskip's string type (reference include/libzeroskip/cstring.h:23-29). */
@@ -364,7 +368,8 @@ int zscrc_device_commit_crcs_bounded(const void *d_image, uint64_t image_size, c
  * copied to the device once, pipelined in chunks (ZSCRC_FILL_CHUNK, default
  * 64 MiB) with host threads patching earlier chunks.  Span i is
  * [span_off[i], +span_len[i]) of the image; spans sorted and disjoint
- * (ZSCRC_EINVAL otherwise); the commit record's header words must already be
+ * (ZSCRC_EINVAL otherwise, with the image left unmodified: every span is
+ * checked before the first CRC is stored); the commit record's header words must already be
  * in the image (zscrc_device_write_commits' contract), a span without one is
  * counted in no_record and left alone.  max_len: a bound on the span lengths
  * or ZSCRC_LEN_UNBOUNDED; spans longer than a chunk are streamed through the
@@ -514,8 +519,10 @@ int zscrc_set_devices(const int *ids, int n);
 /* The slots a call would use now: writes up to cap ids, returns their count
  * (or a negative status). */
 int zscrc_files_devices(int *ids, int cap);
-/* Frees the pinned staging and device buffers the file APIs keep between
- * calls. */
+/* Frees the pinned staging, device buffers, streams and events the library
+ * keeps between calls: the file APIs', zscrc_zs_fill_commits' and the
+ * drop-in symbols' scalar offload (the next call that needs them allocates
+ * them again). */
 void zscrc_release_cache(void);
 
 /* Packed-file writer: the repack output path with its CRCs on the GPU.

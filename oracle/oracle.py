@@ -45,6 +45,9 @@ def lib() -> ctypes.CDLL:
         L.oracle_batch.argtypes = [vp, vp, vp, vp, vp, u64, u64, u64, ctypes.c_int, ctypes.c_int]
         L.oracle_batch.restype = ctypes.c_int
         L.oracle_now.restype = ctypes.c_double
+        L.oracle_batch_rate.argtypes = [vp, vp, vp, vp, vp, u64, u64, u64, ctypes.c_int, ctypes.c_int, vp,
+                                        ctypes.c_double, ctypes.POINTER(u64)]
+        L.oracle_batch_rate.restype = ctypes.c_double
         L.oracle_commit_crc.argtypes = [u32, u64, ctypes.c_int]
         L.oracle_commit_crc.restype = u32
         L.oracle_header_crc.argtypes = [u64, u32, ctypes.c_char_p, u32, u32]
@@ -121,6 +124,72 @@ def batch(base: np.ndarray, offs=None, lens=None, seeds=None, *, n=None, stride=
 
 def now() -> float:
     return lib().oracle_now()
+
+
+def pick_cpus(n: int) -> list:
+    """n logical CPUs of this process's affinity mask for the timing leg: one
+    per physical core, dealt round robin over the L3 domains (CCDs), so the
+    threads neither share a core's SMT siblings nor crowd one CCD's link to
+    memory.  Fewer physical cores than n: SMT siblings fill in."""
+    try:
+        allowed = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        return []
+
+    def rd(path, default):
+        try:
+            with open(path) as f:
+                return f.read().strip()
+        except OSError:
+            return default
+    doms, seen = {}, set()
+    spill = []
+    for c in allowed:
+        base = f"/sys/devices/system/cpu/cpu{c}"
+        core = (rd(base + "/topology/physical_package_id", "0"), rd(base + "/topology/core_id", str(c)))
+        l3 = rd(base + "/cache/index3/id", "0")
+        if core in seen:
+            spill.append(c)
+            continue
+        seen.add(core)
+        doms.setdefault((core[0], l3), []).append(c)
+    order, lists = [], [doms[k] for k in sorted(doms)]
+    while any(lists) and len(order) < n:
+        for li in lists:
+            if li and len(order) < n:
+                order.append(li.pop(0))
+    return (order + spill)[:n]
+
+
+def batch_rate(base: np.ndarray, offs=None, lens=None, seeds=None, *, n=None, stride=0, fixed_len=0,
+               impl: str = "hw", threads: int = 1, cpus=None, budget: float = 5.0):
+    """The bench's CPU timing leg (oracle_batch_rate): the batch's records laid
+    end to end and cut into equal byte ranges, one per persistent thread
+    (pinned to `cpus` if given), records cut by a range joined by the zero
+    shift; passes repeated for `budget` seconds.  impl "read" times a plain
+    read of the same bytes (the host memory bound).  Returns (crcs of the
+    last pass, seconds, passes)."""
+    base = np.ascontiguousarray(base).view(np.uint8)
+    if n is None:
+        n = len(offs) if offs is not None else len(lens)
+    out = np.zeros(n, dtype=np.uint32)
+    o = None if offs is None else np.ascontiguousarray(offs, dtype=np.uint64)
+    ln = None if lens is None else np.ascontiguousarray(lens, dtype=np.uint64)
+    s = None if seeds is None else np.ascontiguousarray(seeds, dtype=np.uint32)
+    cp = None
+    if cpus:
+        cp = np.full(threads, -1, dtype=np.int32)
+        cp[:min(threads, len(cpus))] = cpus[:threads]
+    passes = ctypes.c_uint64(0)
+    el = lib().oracle_batch_rate(base.ctypes.data,
+                                 None if o is None else o.ctypes.data,
+                                 None if ln is None else ln.ctypes.data,
+                                 None if s is None else s.ctypes.data,
+                                 out.ctypes.data, n, stride, fixed_len,
+                                 {"sw": 0, "hw": 1, "bitwise": 2, "read": 3}[impl], threads,
+                                 None if cp is None else cp.ctypes.data, budget, ctypes.byref(passes))
+    assert el >= 0, "oracle_batch_rate failed"
+    return out, el, int(passes.value)
 
 
 def commit_crc(span_crc: int, span_len: int, final: bool = False) -> int:

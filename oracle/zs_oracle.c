@@ -26,9 +26,15 @@
  * (tests/unit-crc32c.c:36, crc32c("lorem ipsum") = 0xdfb4e6c9, also chained)
  * and by the published CRC-32C check vectors (see tests/golden/).
  */
+#define _GNU_SOURCE /* pthread_setaffinity_np (the bench leg's pinned threads) */
 #include <stdint.h>
 #include <stddef.h>
+#include <stdlib.h>
 #include <string.h>
+#include <sched.h>
+#if defined(__x86_64__)
+#include <emmintrin.h>
+#endif
 #include <sys/uio.h>
 #include <pthread.h>
 #include <time.h>
@@ -328,4 +334,257 @@ double oracle_now(void)
     struct timespec ts;
     clock_gettime(CLOCK_MONOTONIC, &ts);
     return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+/* --------------------------------------------- the bench's all-core timing leg
+ * oracle_batch splits a batch by record count and starts its threads on every
+ * call: a sample holding one long span runs on one thread, and a small sample
+ * pays the thread starts each call.  This leg times the same batch as
+ * bench.py's cpu_baseline measures it: the records are laid end to end as one
+ * byte stream, each of nthreads persistent threads (optionally pinned to
+ * cpus[t]) owns an equal byte range of it, a record cut by a range boundary
+ * is hashed in pieces (the first from its seed, the others from 0) and the
+ * pieces joined by the zero shift (crc32c_shift, crc32c.c:363-367; combine
+ * as oracle_combine).  Passes repeat, a barrier between them, until `budget`
+ * seconds have gone; out[] holds the last pass's CRCs.  mode 0 = crc32c
+ * (impl as oracle_batch), 3 = read only (64-bit sums of the same bytes: the
+ * host memory's rate over this sample, the bound an all-core CRC cannot pass). */
+
+struct rate_piece {
+    uint64_t rec, skip, len;
+    uint32_t crc;
+};
+
+struct rate_pool {
+    const uint8_t *base;
+    const uint64_t *off, *len, *pos; /* pos: prefix sums of the lengths (n + 1) */
+    const uint32_t *seed;
+    uint32_t *out;
+    uint64_t n, stride, fixed_len, total;
+    int impl, nthreads;
+    const int *cpus;
+    pthread_barrier_t bar;
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+    int go;
+    volatile int stop;
+    double t0, budget;
+    uint64_t passes;
+    struct rate_piece piece[256][2];
+    int npiece[256];
+    volatile uint64_t sink[256 * 8];
+};
+
+struct rate_arg {
+    struct rate_pool *pool;
+    int t;
+};
+
+static inline uint64_t rp_pos(const struct rate_pool *P, uint64_t i)
+{
+    return P->pos ? P->pos[i] : i * P->fixed_len;
+}
+
+static inline uint64_t rp_len(const struct rate_pool *P, uint64_t i)
+{
+    return P->len ? P->len[i] : P->fixed_len;
+}
+
+/* first record of byte range start b: the smallest i with pos_i + max(len_i, 1)
+ * > b (a zero-length record at b belongs to the range that starts there) */
+static uint64_t rp_first(const struct rate_pool *P, uint64_t b)
+{
+    uint64_t lo = 0, hi = P->n;
+    while (lo < hi) {
+        const uint64_t m = lo + (hi - lo) / 2;
+        const uint64_t l = rp_len(P, m);
+        if (rp_pos(P, m) + (l ? l : 1) > b)
+            hi = m;
+        else
+            lo = m + 1;
+    }
+    return lo;
+}
+
+/* 64-bit lane sums of n bytes (the tail under 64 bytes ignored): four
+ * independent 128-bit chains, so the loads bound it, not the adds */
+static uint64_t read_sum(const uint8_t *p, uint64_t n)
+{
+#if defined(__x86_64__)
+    __m128i a0 = _mm_setzero_si128(), a1 = a0, a2 = a0, a3 = a0;
+    for (uint64_t k = 0; k + 64 <= n; k += 64) {
+        a0 = _mm_add_epi64(a0, _mm_loadu_si128((const __m128i *)(p + k)));
+        a1 = _mm_add_epi64(a1, _mm_loadu_si128((const __m128i *)(p + k + 16)));
+        a2 = _mm_add_epi64(a2, _mm_loadu_si128((const __m128i *)(p + k + 32)));
+        a3 = _mm_add_epi64(a3, _mm_loadu_si128((const __m128i *)(p + k + 48)));
+    }
+    a0 = _mm_xor_si128(_mm_xor_si128(a0, a1), _mm_xor_si128(a2, a3));
+    return (uint64_t)_mm_cvtsi128_si64(a0) ^ (uint64_t)_mm_cvtsi128_si64(_mm_unpackhi_epi64(a0, a0));
+#else
+    uint64_t s = 0;
+    for (uint64_t k = 0; k + 8 <= n; k += 8) {
+        uint64_t w;
+        memcpy(&w, p + k, 8);
+        s += w;
+    }
+    return s;
+#endif
+}
+
+static void rate_share(struct rate_pool *P, int t, int mode)
+{
+    const uint64_t b0 = P->total * (uint64_t)t / (uint64_t)P->nthreads;
+    const uint64_t b1 = P->total * (uint64_t)(t + 1) / (uint64_t)P->nthreads;
+    const int last = t == P->nthreads - 1;
+    uint64_t sum = 0;
+    int np = 0;
+    for (uint64_t i = rp_first(P, b0); i < P->n; ++i) {
+        const uint64_t pi = rp_pos(P, i), li = rp_len(P, i);
+        if (!(pi < b1 || (last && pi == b1)))
+            break;
+        const uint64_t s = pi < b0 ? b0 - pi : 0;
+        const uint64_t e = pi + li > b1 ? b1 - pi : li;
+        const uint8_t *p = P->base + (P->off ? P->off[i] : i * P->stride) + s;
+        if (mode == 3) {
+            sum += read_sum(p, e - s);
+            continue;
+        }
+        const uint32_t sd = s == 0 && P->seed ? P->seed[i] : 0;
+        const uint32_t c = P->impl == 1 ? oracle_crc32c_hw(sd, p, e - s)
+                         : P->impl == 2 ? oracle_crc32c_bitwise(sd, p, e - s)
+                                        : oracle_crc32c_sw(sd, p, e - s);
+        if (s == 0 && e == li)
+            P->out[i] = c;
+        else if (np < 2)
+            P->piece[t][np++] = (struct rate_piece){i, s, e - s, c};
+    }
+    P->npiece[t] = np;
+    P->sink[8 * t] = sum;
+}
+
+static void *rate_worker(void *arg)
+{
+    struct rate_arg *a = arg;
+    struct rate_pool *P = a->pool;
+    const int t = a->t;
+    const int mode = P->impl == 3 ? 3 : 0;
+    if (P->cpus && P->cpus[t] >= 0) {
+        cpu_set_t cs;
+        CPU_ZERO(&cs);
+        CPU_SET(P->cpus[t], &cs);
+        pthread_setaffinity_np(pthread_self(), sizeof cs, &cs);
+    }
+    /* the gate: the thread count (and so every range) is final once it opens */
+    pthread_mutex_lock(&P->mu);
+    while (!P->go)
+        pthread_cond_wait(&P->cv, &P->mu);
+    pthread_mutex_unlock(&P->mu);
+    for (;;) {
+        pthread_barrier_wait(&P->bar);
+        if (P->stop)
+            break;
+        rate_share(P, t, mode);
+        pthread_barrier_wait(&P->bar);
+        if (t == 0) {
+            ++P->passes;
+            if (oracle_now() - P->t0 >= P->budget)
+                P->stop = 1;
+        }
+    }
+    return NULL;
+}
+
+/* Returns the seconds the passes took (*passes of them), or -1. */
+double oracle_batch_rate(const uint8_t *base, const uint64_t *off, const uint64_t *len,
+                         const uint32_t *seed, uint32_t *out, uint64_t n, uint64_t stride,
+                         uint64_t fixed_len, int impl, int nthreads, const int *cpus,
+                         double budget, uint64_t *passes)
+{
+    oracle_init_tables();
+    if (nthreads < 1)
+        nthreads = 1;
+    if (nthreads > 256)
+        nthreads = 256;
+    static struct rate_pool P; /* one bench leg at a time */
+    memset(&P, 0, sizeof P);
+    uint64_t *pos = NULL;
+    if (len) {
+        pos = malloc((n + 1) * sizeof *pos);
+        if (!pos)
+            return -1;
+        pos[0] = 0;
+        for (uint64_t i = 0; i < n; ++i)
+            pos[i + 1] = pos[i] + len[i];
+    }
+    P.base = base;
+    P.off = off;
+    P.len = len;
+    P.pos = pos;
+    P.seed = seed;
+    P.out = out;
+    P.n = n;
+    P.stride = stride;
+    P.fixed_len = fixed_len;
+    P.total = len ? pos[n] : n * fixed_len;
+    P.impl = impl;
+    P.nthreads = nthreads;
+    P.cpus = cpus;
+    P.budget = budget;
+    pthread_mutex_init(&P.mu, NULL);
+    pthread_cond_init(&P.cv, NULL);
+    pthread_t th[256];
+    struct rate_arg args[256];
+    int started = 0;
+    for (int t = 1; t < nthreads; ++t) {
+        args[t] = (struct rate_arg){&P, t};
+        if (pthread_create(&th[t], NULL, rate_worker, &args[t]) != 0)
+            break;
+        started = t;
+    }
+    nthreads = P.nthreads = started + 1; /* the threads that exist */
+    if (pthread_barrier_init(&P.bar, NULL, (unsigned)nthreads) != 0) {
+        P.stop = 1; /* workers leave at their first look */
+        nthreads = 1;
+    }
+    pthread_mutex_lock(&P.mu);
+    P.go = 1;
+    pthread_cond_broadcast(&P.cv);
+    pthread_mutex_unlock(&P.mu);
+    if (P.stop) {
+        for (int t = 1; t <= started; ++t)
+            pthread_join(th[t], NULL);
+        free(pos);
+        return -1;
+    }
+    args[0] = (struct rate_arg){&P, 0};
+    cpu_set_t caller; /* thread 0 is the caller: its own mask comes back after */
+    const int have_mask = pthread_getaffinity_np(pthread_self(), sizeof caller, &caller) == 0;
+    P.t0 = oracle_now();
+    rate_worker(&args[0]);
+    const double el = oracle_now() - P.t0;
+    if (have_mask)
+        pthread_setaffinity_np(pthread_self(), sizeof caller, &caller);
+    for (int t = 1; t < nthreads; ++t)
+        pthread_join(th[t], NULL);
+    pthread_barrier_destroy(&P.bar);
+    /* join the pieces of the records the ranges cut, in byte order */
+    if (impl != 3) {
+        uint64_t cur = UINT64_MAX;
+        uint32_t crc = 0;
+        for (int t = 0; t < nthreads; ++t)
+            for (int k = 0; k < P.npiece[t]; ++k) {
+                const struct rate_piece *q = &P.piece[t][k];
+                if (q->rec != cur) {
+                    cur = q->rec;
+                    crc = q->crc;
+                } else {
+                    crc = oracle_shift(crc, q->len) ^ q->crc;
+                }
+                if (q->skip + q->len == rp_len(&P, q->rec))
+                    out[q->rec] = crc;
+            }
+    }
+    free(pos);
+    *passes = P.passes;
+    return el;
 }

@@ -143,11 +143,56 @@ def test_fill_commits_edges(gpu):
     rep = zsfile.fill_commits(out, o2, l2)
     assert rep["no_record"] == 1 and rep["commits"] == len(o)
     assert np.array_equal(out, img)
-    # unsorted spans are refused
-    bad = o.copy()
-    bad[[3, 4]] = bad[[4, 3]]
+    # unsorted spans are refused, and the image is left as it was (every
+    # span checked before the first store) -- a swap early, one
+    # late in the last chunk, and an overlap
+    for swap in ([3, 4], [len(o) - 2, len(o) - 1]):
+        bad = o.copy()
+        bad[swap] = bad[swap[::-1]]
+        blank = _blank(img, keep)
+        before = blank.copy()
+        with pytest.raises(ZscrcError):
+            zsfile.fill_commits(blank, bad, ln)
+        assert np.array_equal(blank, before)
+    over = ln.copy()
+    over[len(o) // 2] += 64
+    blank = _blank(img, keep)
+    before = blank.copy()
     with pytest.raises(ZscrcError):
-        zsfile.fill_commits(_blank(img, keep), bad, ln)
+        zsfile.fill_commits(blank, o, over)
+    assert np.array_equal(blank, before)
     # nothing to do
     assert zsfile.fill_commits(out, np.zeros(0, np.uint64), np.zeros(0, np.uint64))["commits"] == 0
     assert not os.environ.get("ZSCRC_FILL_CHUNK")
+
+
+def test_release_cache_frees_and_recovers(gpu):
+    """zscrc_release_cache() frees the fill pipeline's and the scalar
+    offload's cached buffers; the next calls allocate them again
+    and stay byte-exact."""
+    from zeroskip_amd import crc32c as zc
+    from zeroskip_amd._lib import lib, stats
+    img, commits = _log_images(3)
+    o, ln, keep = _writer_spans(commits)
+    out = _blank(img, keep)
+    zsfile.fill_commits(out, o, ln)
+    assert np.array_equal(out, img)
+    saved = (lib().zscrc_gpu_min(0), lib().zscrc_gpu_min(1))
+    lib().zscrc_set_gpu_min(1 << 20)
+    try:
+        d = np.random.default_rng(3).integers(0, 256, (9 << 20) + 5, dtype=np.uint8).tobytes()
+        assert zc.crc32c_hw(7, d) == oracle.crc32c_hw(7, d)
+        torch.cuda.synchronize()
+        free0 = torch.cuda.mem_get_info()[0]
+        lib().zscrc_release_cache()
+        free1 = torch.cuda.mem_get_info()[0]
+        assert free1 > free0   # device buffers went back
+        lib().zscrc_release_cache()   # twice is harmless
+        out = _blank(img, keep)
+        zsfile.fill_commits(out, o, ln)
+        assert np.array_equal(out, img)
+        before = stats()
+        assert zc.crc32c_hw(7, d) == oracle.crc32c_hw(7, d)
+        assert stats()[1] - before[1] == 1   # offloaded again after the release
+    finally:
+        lib().zscrc_set_gpu_min_pair(*saved)

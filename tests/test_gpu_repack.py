@@ -237,3 +237,24 @@ def test_repack_dir_lock_held(gpu, tmp_path):
     with pytest.raises(ZscrcError):
         repack.repack_dir(str(tmp_path))
     assert not (tmp_path / ".zsdb.lock").exists()
+
+
+def test_repack_dir_rename_failure_releases_lock(gpu, tmp_path, monkeypatch):
+    """a repack whose final .zsdb rename fails (fault injected,
+    ZSCRC_FAULT=dotzsdb_rename) reports an error and leaves no .zsdb.lock
+    behind, so the next update can take it; the old .zsdb is untouched."""
+    w = zf.FileWriter(UUID, idx=1)
+    w.add(b"k" * 16, b"v" * 40)
+    w.commit()
+    (tmp_path / f"zeroskip-{UUIDSTR}-1-1").write_bytes(w.image())
+    _dotzsdb(tmp_path, 2)
+    old = (tmp_path / ".zsdb").read_bytes()
+    monkeypatch.setenv("ZSCRC_FAULT", "dotzsdb_rename")
+    with pytest.raises(ZscrcError):
+        repack.repack_dir(str(tmp_path))
+    assert not (tmp_path / ".zsdb.lock").exists()
+    assert (tmp_path / ".zsdb").read_bytes() == old
+    monkeypatch.delenv("ZSCRC_FAULT")
+    # the lock is free: a later repack runs (nothing left to merge but the packed output)
+    rep = repack.repack_dir(str(tmp_path))
+    assert not (tmp_path / ".zsdb.lock").exists() and rep["branch"] in (0, 1)

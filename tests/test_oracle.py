@@ -82,3 +82,40 @@ def test_format_crcs_follow_writer():
     w2 = n.to_bytes(8, "little")
     w3 = (8 << 56).to_bytes(8, "little")
     assert oracle.commit_crc(sc, n) == oracle.crc32c_hw(oracle.crc32c_hw(oracle.crc32c_hw(sc, w1), w2), w3)
+
+
+def test_batch_rate_byte_split_matches_per_record():
+    """bench.py's all-core timing leg (oracle_batch_rate): records cut by the
+    threads' byte ranges -- long spans, zero-length records at range bounds,
+    seeds -- joined by the zero shift equal the per-record oracle."""
+    rng = np.random.default_rng(5)
+    data = rng.integers(0, 256, 1 << 23, dtype=np.uint8)
+    lens = np.array([0, 5, 1 << 21, 0, 0, 17, 3000, 1 << 20, 0, 64] + list(rng.integers(0, 5000, 300)),
+                    dtype=np.uint64)
+    offs = rng.integers(0, len(data) - (1 << 21) - 1, len(lens)).astype(np.uint64)
+    seeds = rng.integers(0, 1 << 32, len(lens), dtype=np.uint64).astype(np.uint32)
+    want = oracle.batch(data, offs, lens, seeds, impl="hw")
+    for t in (1, 2, 3, 7, 16, 33):
+        got, el, passes = oracle.batch_rate(data, offs, lens, seeds, impl="hw", threads=t, budget=0.01,
+                                            cpus=oracle.pick_cpus(t))
+        assert passes >= 1 and el > 0
+        assert np.array_equal(got, want), t
+    got, _, _ = oracle.batch_rate(data, n=2000, stride=4096, fixed_len=4093, impl="sw", threads=5, budget=0.01)
+    assert np.array_equal(got, oracle.batch(data, n=2000, stride=4096, fixed_len=4093, impl="sw"))
+    # the caller's own CPU mask is left as it was
+    import os
+    before = os.sched_getaffinity(0)
+    oracle.batch_rate(data, n=1, fixed_len=1 << 20, impl="read", threads=2, budget=0.01, cpus=oracle.pick_cpus(2))
+    assert os.sched_getaffinity(0) == before
+
+
+def test_bench_cpu_leg_small():
+    import bench
+    rng = np.random.default_rng(6)
+    data = rng.integers(0, 256, 1 << 22, dtype=np.uint8)
+    d = bench.cpu_leg(data, "test", n=64, stride=1 << 16, fixed_len=1 << 16, seconds=0.3, sw=True)
+    assert d["kind"] == "port" and d["value"] > 0 and d["value_1core"] > 0 and d["host_read_GiBs"] > 0
+    lens = np.array([1 << 21, 100, 0, 1 << 20], dtype=np.int64)
+    offs = np.array([0, 5, 9, 1 << 21], dtype=np.int64)
+    d = bench.cpu_leg(data, "spans", offs, lens, seconds=0.3)
+    assert d["cores"] >= 1 and "sw_value_1core" not in d

@@ -14,7 +14,13 @@
  *
  * build: gcc -O2 -Iinclude tools/crc32bench.c -Lzeroskip_amd -lzscrc -lz
  *        -Wl,-rpath,$PWD/zeroskip_amd -o tools/crc32bench_bin
- * usage: crc32bench [-r reps_1mib] [-g gpu_min_bytes]   (host CPU, 1 thread)
+ * usage: crc32bench [-r reps_1mib] [-g gpu_min_bytes] [-b route_bytes]
+ *
+ * -b N (N > 0): the drop-in's routing with a GPU present (tests/
+ * test_gpu_c_link.py): crc32c_hw over an N-byte xorshift64 buffer before any
+ * device context exists (the cold threshold, 5 GiB by default: the CPU), then
+ * zscrc_warmup() and the same call again (the warm threshold, 32 MiB: the
+ * GPU), each call's route read from zscrc_stats; both CRCs must agree.
  */
 #include <inttypes.h>
 #include <stdio.h>
@@ -88,13 +94,16 @@ static void run(const char *name, crc_fn f, const uint8_t *mib, int reps, struct
 int main(int argc, char **argv)
 {
     int reps = 2000, opt;
-    while ((opt = getopt(argc, argv, "r:g:")) != -1) {
+    size_t route = 0;
+    while ((opt = getopt(argc, argv, "r:g:b:")) != -1) {
         if (opt == 'r')
             reps = atoi(optarg);
+        else if (opt == 'b')
+            route = strtoull(optarg, NULL, 0);
         else if (opt == 'g')
             zscrc_set_gpu_min(strtoull(optarg, NULL, 0));
         else {
-            fprintf(stderr, "usage: %s [-r reps_1mib] [-g gpu_min_bytes]\n", argv[0]);
+            fprintf(stderr, "usage: %s [-r reps_1mib] [-g gpu_min_bytes] [-b route_bytes]\n", argv[0]);
             return 2;
         }
     }
@@ -128,6 +137,38 @@ int main(int argc, char **argv)
         printf(", \"%s\": {\"text_GBs\": %.3f, \"mib_GiBs\": %.3f}", r[i].name,
                (double)RUNS * strlen(TEXT) / r[i].text_us / 1e3,
                (double)rr * MIB / (r[i].mib_us * 1e-6) / (1 << 30));
+    }
+    if (route) {
+        /* routing: cold (no device context yet) then warm (after zscrc_warmup) */
+        uint8_t *big = malloc(route);
+        if (!big)
+            return 2;
+        for (size_t i = 0; i < route; i += MIB)
+            memcpy(big + i, mib, route - i < MIB ? route - i : MIB);
+        uint64_t s0[4], s1[4], s2[4];
+        zscrc_stats(s0);
+        double t0 = now_us();
+        const uint32_t cold = crc32c_hw(0, big, route);
+        double t1 = now_us();
+        zscrc_stats(s1);
+        const int wrc = zscrc_warmup();
+        crc32c_hw(0, big, route); /* the offload's buffers and tables warm */
+        zscrc_stats(s2);
+        const uint64_t off0 = s2[1];
+        double t2 = now_us();
+        const uint32_t warm = crc32c_hw(0, big, route);
+        double t3 = now_us();
+        zscrc_stats(s2);
+        const int cold_cpu = s1[0] == s0[0] + 1 && s1[1] == s0[1];
+        const int warm_gpu = wrc == 0 && s2[1] == off0 + 1;
+        bad |= cold != warm || !cold_cpu || !warm_gpu;
+        printf(", \"routing\": {\"bytes\": %zu, \"crc\": \"%08x\", \"cold_threshold\": %" PRIu64
+               ", \"warm_threshold\": %" PRIu64 ", \"cold_on_cpu\": %s, \"warm_on_gpu\": %s, "
+               "\"cold_GBs\": %.2f, \"warm_GBs\": %.2f, \"warmup_rc\": %d}",
+               route, warm, zscrc_gpu_min(1), zscrc_gpu_min(0), cold_cpu ? "true" : "false",
+               warm_gpu ? "true" : "false", route / (t1 - t0) / 1e3, route / (t3 - t2) / 1e3, wrc);
+        printf(", \"ok_all\": %s", bad ? "false" : "true");
+        free(big);
     }
     printf("}\n");
     free(mib);

@@ -1,0 +1,33 @@
+#!/bin/bash
+# One GPU session of round 5 (tools/r05_run.sh STEP...): each step is bounded
+# by its own timeout; an ordinary failure (rc 1) lets the next step run, a
+# time limit, abort, segfault or anything else ends the session there.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+R=$PWD
+mkdir -p gpurun_out
+T="python -u -m pytest --maxfail=10 -q --timeout 300 --timeout-method thread"
+for step in "$@"; do
+  case "$step" in
+    gputests) timeout -k 10 900 $T -m gpu tests > gpurun_out/gputests.log 2>&1 ;;
+    newtests) timeout -k 10 600 $T tests/test_gpu_c_link.py tests/test_gpu_fill.py tests/test_gpu_repack.py \
+                tests/test_gpu_mixed.py > gpurun_out/newtests.log 2>&1 ;;
+    smoke)    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
+    bench2|bench3|bench4|bench5)
+              timeout -k 10 900 python bench.py --workload config${step#bench} >> gpurun_out/$step.jsonl \
+                2>> gpurun_out/$step.err ;;
+    bench3q|bench2q|bench4q|bench5q)   # GPU part only
+              c=${step#bench}; c=${c%q}
+              timeout -k 10 600 python bench.py --workload config$c --no-cpu --no-e2e >> gpurun_out/$step.jsonl \
+                2>> gpurun_out/$step.err ;;
+    traffic2|traffic3|traffic4|traffic4w|traffic5)   # FETCH_SIZE and WRITE_SIZE passes, 5 passes each
+              c=config${step#traffic}
+              bash tools/pmc_traffic.sh $c 5 ;;
+    trace2|trace3|trace4|trace5) bash tools/trace_bench.sh config${step#trace} ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+  rc=$?
+  echo "step $step rc=$rc" | tee -a gpurun_out/steps.log
+  [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
+done
+exit 0

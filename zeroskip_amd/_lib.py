@@ -94,7 +94,7 @@ SIGNATURES = {
     "zscrc_device_verify_commits_verdict_range": (_int, [_vp, _u64, _vp, _vp, _vp, _sz, _u64, _u64, _vp, _vp, _sz,
                                                          _vp]),
 }
-ABI_VERSION = 3  # include/zscrc.h ZSCRC_ABI_VERSION
+ABI_VERSION = 4  # include/zscrc.h ZSCRC_ABI_VERSION
 
 ZSCRC_RAW = 1
 LEN_UNBOUNDED = (1 << 64) - 1  # ZSCRC_LEN_UNBOUNDED

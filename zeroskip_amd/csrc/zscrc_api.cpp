@@ -927,6 +927,25 @@ bool gpu_scalar(uint32_t crc, const void *buf, size_t len, uint32_t *res)
 
 } /* namespace */
 
+/* zscrc_release_cache(): the scalar offload's cached stream objects (three
+ * 64 MiB device buffers each), every device. */
+extern "C" void zs_scalar_release_cache(void)
+{
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    for (int d = 0; d < MAX_DEV; ++d) {
+        ScalarOffload &so = g_scalar[d];
+        std::lock_guard<std::mutex> lk(so.mu);
+        if (!so.s)
+            continue;
+        (void)hipSetDevice(d);
+        stream_free(so.s);
+        so.s = nullptr;
+    }
+    if (cur >= 0)
+        (void)hipSetDevice(cur);
+}
+
 /* ====================================================== Part 1: reference API */
 extern "C" {
 

@@ -823,6 +823,9 @@ extern "C" int zscrc_files_devices(int *ids, int cap)
     return (int)d.size();
 }
 
+extern "C" void zs_fill_release_cache(void);
+extern "C" void zs_scalar_release_cache(void);
+
 extern "C" void zscrc_release_cache(void)
 {
     int cur = -1;
@@ -833,6 +836,8 @@ extern "C" void zscrc_release_cache(void)
     }
     if (cur >= 0)
         (void)hipSetDevice(cur);
+    zs_fill_release_cache();   /* zscrc_zs_fill_commits' pipeline */
+    zs_scalar_release_cache(); /* the drop-in symbols' offload stream */
 }
 
 extern "C" int zscrc_zs_verify_files(const void *const *images, const uint64_t *sizes, const int *kinds, size_t n,

@@ -274,6 +274,8 @@ extern "C" int zscrc_zs_fill_commits(void *image, uint64_t size, const uint64_t 
         }
         const uint64_t i1 = a;
         const uint64_t last = span_end(i1 - 1);
+        if (span_off[i1 - 1] > size || span_len[i1 - 1] > size - span_off[i1 - 1] || last < lo)
+            return ZSCRC_EINVAL; /* unsorted: the plan's search met a span behind the chunk */
         const uint64_t hi = std::min(size, last + std::max<uint64_t>(rec_len(img, size, last), 8));
         chunks.push_back({i0, i1, lo, hi});
         max_commits = std::max(max_commits, i1 - i0);
@@ -300,11 +302,17 @@ extern "C" int zscrc_zs_fill_commits(void *image, uint64_t size, const uint64_t 
     /* tasks, in order: chunk k's descriptors and staging copies; chunk k's
      * patches after chunk k + LAG's copies (its D2H is queued by then) */
     struct Task {
-        int kind;      /* 0 descriptors, 1 staging copy, 2 patch */
+        int kind;      /* 0 descriptors, 1 staging copy, 2 patch, 3 validate */
         uint64_t k;    /* chunk */
         uint64_t a, b; /* copy: bytes [a, b) of the chunk; patch: commits [a, b) */
     };
     std::vector<Task> tasks;
+    /* first: every span's bounds and order, in slices over the workers; no
+     * patch touches the image before all slices passed, so invalid input
+     * fails with the image unmodified (the copies and kernels only read it) */
+    const uint64_t nval = std::min<uint64_t>((uint64_t)threads, n);
+    for (uint64_t v = 0; v < nval; ++v)
+        tasks.push_back({3, 0, n * v / nval, n * (v + 1) / nval});
     std::vector<std::atomic<int>> ready(nk); /* tasks left before chunk k can be issued */
     constexpr uint64_t PATCH_SUB = 1u << 16;
     const uint64_t LAG = NSLOT;
@@ -330,6 +338,7 @@ extern "C" int zscrc_zs_fill_commits(void *image, uint64_t size, const uint64_t 
     std::atomic<uint64_t> next{0};
     std::atomic<int64_t> issued{0};  /* chunks whose copies / kernel / D2H are queued */
     std::atomic<int> stop{0}, bad_order{0};
+    std::atomic<uint64_t> validated{0}; /* validation slices done */
     std::atomic<uint64_t> patched{0}, norec{0};
     auto wait_issued = [&](int64_t k) -> bool { /* chunk k queued (its events recorded) */
         while (issued.load(std::memory_order_acquire) <= k) {
@@ -345,6 +354,16 @@ extern "C" int zscrc_zs_fill_commits(void *image, uint64_t size, const uint64_t 
             if (t >= tasks.size())
                 return;
             const Task tk = tasks[t];
+            if (tk.kind == 3) {
+                bool ok = true;
+                for (uint64_t i = tk.a; ok && i < tk.b; ++i)
+                    ok = span_off[i] <= size && span_len[i] <= size - span_off[i] &&
+                         (i == 0 || span_off[i] >= span_end(i - 1));
+                if (!ok)
+                    bad_order = 1;
+                validated.fetch_add(1, std::memory_order_release);
+                continue;
+            }
             const Chunk &ch = chunks[tk.k];
             if (tk.kind == 0) {
                 uint32_t *p = c.hpairs + 2 * ch.i0;
@@ -373,7 +392,12 @@ extern "C" int zscrc_zs_fill_commits(void *image, uint64_t size, const uint64_t 
                 if (!wait_issued((int64_t)tk.k))
                     return;
                 (void)hipEventSynchronize(d2h[tk.k]);
-                if (!chunk_ok[tk.k])
+                while (validated.load(std::memory_order_acquire) < nval) {
+                    if (stop.load(std::memory_order_relaxed))
+                        return;
+                    std::this_thread::yield();
+                }
+                if (!chunk_ok[tk.k] || bad_order.load(std::memory_order_relaxed))
                     continue; /* unsorted / overlapping spans: nothing written, the call fails */
                 uint64_t done = 0, none = 0;
                 for (uint64_t i = tk.a; i < tk.b; ++i) {
@@ -459,7 +483,7 @@ extern "C" int zscrc_zs_fill_commits(void *image, uint64_t size, const uint64_t 
          hipStreamSynchronize(os) != hipSuccess) && !rc)
         rc = ZSCRC_EHIP;
     if (!rc && bad_order)
-        rc = ZSCRC_EINVAL; /* unsorted or overlapping spans: what was patched may be wrong */
+        rc = ZSCRC_EINVAL; /* unsorted or overlapping spans: the image was not patched */
 
     /* long commits: the span streamed through the GPU, trailer on the host
      * (zeroskip-file.c:266-302 / :303-328) */
@@ -501,4 +525,55 @@ extern "C" int zscrc_zs_fill_commits(void *image, uint64_t size, const uint64_t 
     rep->h2d_s = t_h2d - t0;
     rep->total_s = now_s() - t0;
     return rc;
+}
+
+/* zscrc_release_cache(): every device's staging slots, device ring, pinned
+ * per-commit arrays, streams and events (each cache under its own lock). */
+extern "C" void zs_fill_release_cache(void)
+{
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    for (int d = 0; d < MAX_DEV; ++d) {
+        Cache &c = g_cache[d];
+        std::lock_guard<std::mutex> lk(c.mu);
+        if (!c.cs && !c.slot_bytes && !c.ring_bytes && !c.ring_commits && !c.host_commits)
+            continue;
+        (void)hipSetDevice(d);
+        for (hipStream_t *st : {&c.cs, &c.ks, &c.os})
+            if (*st) {
+                (void)hipStreamSynchronize(*st);
+                (void)hipStreamDestroy(*st);
+                *st = nullptr;
+            }
+        for (auto *v : {&c.h2d, &c.kern, &c.d2h}) {
+            for (hipEvent_t e : *v)
+                (void)hipEventDestroy(e);
+            v->clear();
+        }
+        for (auto &p : c.slot) {
+            if (p)
+                (void)hipHostFree(p);
+            p = nullptr;
+        }
+        for (auto &p : c.dring) {
+            if (p)
+                (void)hipFree(p);
+            p = nullptr;
+        }
+        for (int r = 0; r < RING; ++r) {
+            if (c.dpairs[r])
+                (void)hipFree(c.dpairs[r]);
+            c.dpairs[r] = nullptr;
+            c.doff[r] = c.dlen[r] = nullptr;
+            c.dcrc[r] = nullptr;
+        }
+        if (c.hpairs)
+            (void)hipHostFree(c.hpairs);
+        if (c.hcrc)
+            (void)hipHostFree(c.hcrc);
+        c.hpairs = c.hcrc = nullptr;
+        c.slot_bytes = c.ring_bytes = c.ring_commits = c.host_commits = 0;
+    }
+    if (cur >= 0)
+        (void)hipSetDevice(cur);
 }

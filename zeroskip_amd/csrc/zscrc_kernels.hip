@@ -64,10 +64,25 @@ __device__ __forceinline__ void gstore32(const void *p, uint32_t v)
     *(gw32p)reinterpret_cast<uintptr_t>(p) = v;
 }
 
+/* The only readfirstlane / readlane in this file.  The builtins return int:
+ * widened straight into a 64-bit value they sign-extend from 2^31 (s_bfe_i64;
+ * round 4's faulting A/B build), so every use goes through
+ * these, which return uint32_t -- a 64-bit widening of the result is then a
+ * zero extension by construction (tests/test_kernel_source.py). */
+__device__ __forceinline__ uint32_t rfl_u32(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+
+__device__ __forceinline__ uint32_t rl_u32(uint32_t v, int lane)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
+}
+
 __device__ __forceinline__ uint64_t uni64(uint64_t v)
 {
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    const uint32_t lo = rfl_u32((uint32_t)v);
+    const uint32_t hi = rfl_u32((uint32_t)(v >> 32));
     return ((uint64_t)hi << 32) | lo;
 }
 
@@ -615,16 +630,16 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d_in, const uint32_t
     if (!FIXED) {
         uint32_t base = 0;
         for (uint32_t k = 0; k < d.klass; ++k)
-            base += __builtin_amdgcn_readfirstlane(((g32p)d.class_count)[k]);
-        count = __builtin_amdgcn_readfirstlane(((g32p)d.class_count)[d.klass]);
+            base += rfl_u32(((g32p)d.class_count)[k]);
+        count = rfl_u32(((g32p)d.class_count)[d.klass]);
         list = d.desc + base;
     }
     uint32_t sp = 0;
     uint64_t nitems = count;
     if (!FIXED && d.split) {
-        sp = __builtin_amdgcn_readfirstlane(((const volatile uint32_t *)&d.plan[d.klass].direct)[0]) ? 0u : 1u;
+        sp = rfl_u32(((const volatile uint32_t *)&d.plan[d.klass].direct)[0]) ? 0u : 1u;
         if (sp)
-            nitems = __builtin_amdgcn_readfirstlane(((const volatile uint32_t *)&d.plan[d.klass].parts)[0]);
+            nitems = rfl_u32(((const volatile uint32_t *)&d.plan[d.klass].parts)[0]);
     }
     if (!sp)
         d.part_out = nullptr; /* enough records: no split, results go out directly */
@@ -828,13 +843,13 @@ __device__ __forceinline__ void xgeom(const XDesc &d, const XMulti &m, const XPa
         return;
     }
     if (MODE == 2) { /* xp.first_rec / xp.U: read once per wave at kernel start */
-        const uint32_t idx = __builtin_amdgcn_readfirstlane(((g32p)xp.part_rec)[w]);
+        const uint32_t idx = rfl_u32(((g32p)xp.part_rec)[w]);
         const RecDesc *r = xp.desc + xp.first_rec + idx;
         typedef const __attribute__((address_space(1))) uint64_t *g64p;
         const uint64_t off = uni64(((g64p)r)[0]), rlen = uni64(((g64p)r)[1]);
-        const uint32_t seed = __builtin_amdgcn_readfirstlane(((g32p)r)[4]);
+        const uint32_t seed = rfl_u32(((g32p)r)[4]);
         const uint64_t U = xp.U;
-        const uint64_t part = w - __builtin_amdgcn_readfirstlane(((g32p)xp.part_base)[idx]);
+        const uint64_t part = w - rfl_u32(((g32p)xp.part_base)[idx]);
         uint64_t a;
         if (xp.seg) { /* the part is segment j0 + part's piece of the record */
             const uint64_t S = uni64(((g64p)xp.rec_start)[idx]);
@@ -1039,13 +1054,13 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp,
     static_assert(OFF_Z + 6 * 4096 + 4 <= LDS_BYTES, "no room for the LDS counter");
     uint32_t &lctr = *reinterpret_cast<uint32_t *>(L + OFF_Z + 6 * 4096);
     if (MODE == 2) { /* parts of a split class: their count is on the device */
-        d.n = __builtin_amdgcn_readfirstlane(((const volatile uint32_t *)&xp.plan[xp.klass].parts)[0]);
-        xp.seg = __builtin_amdgcn_readfirstlane(((const volatile uint32_t *)&xp.plan[xp.klass].seg)[0]);
+        d.n = rfl_u32(((const volatile uint32_t *)&xp.plan[xp.klass].parts)[0]);
+        xp.seg = rfl_u32(((const volatile uint32_t *)&xp.plan[xp.klass].seg)[0]);
         d.out = xp.part_out;
         d.xor_io = 0; /* raw part registers */
         uint32_t first = 0;
         for (uint32_t k = 0; k < xp.klass; ++k)
-            first += __builtin_amdgcn_readfirstlane(((g32p)xp.class_count)[k]);
+            first += rfl_u32(((g32p)xp.class_count)[k]);
         xp.first_rec = first;
         xp.U = uni64(((const __attribute__((address_space(1))) uint64_t *)(xp.plan + xp.klass))[0]);
     }
@@ -1071,8 +1086,8 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp,
     if (MODE == 2 && xp.seg) { /* segment w (of xp.seg) for wave w of this grid */
         wbeg = wend = 0;
         if (team < xp.seg) {
-            wbeg = __builtin_amdgcn_readfirstlane(((g32p)xp.seg_first)[team]);
-            wend = __builtin_amdgcn_readfirstlane(((g32p)xp.seg_first)[team + 1]);
+            wbeg = rfl_u32(((g32p)xp.seg_first)[team]);
+            wend = rfl_u32(((g32p)xp.seg_first)[team + 1]);
         }
     }
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(gtab);
@@ -1086,7 +1101,7 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp,
     };
     const uint64_t nitems = (MODE == 2 && xp.seg) ? xp.seg : d.n;
     auto deal_item = [&](uint32_t raw) -> uint64_t {
-        const uint32_t u = __builtin_amdgcn_readlane(raw, 0);
+        const uint32_t u = rl_u32(raw, 0);
         const uint64_t w = (uint64_t)blockIdx.x * WAVES + u % WAVES + (uint64_t)(u / WAVES) * nteams;
         return w < nitems ? w : nitems;
     };
@@ -1099,8 +1114,8 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp,
         if (j >= nitems)
             return false;
         if (MODE == 2 && xp.seg) {
-            const uint64_t a = __builtin_amdgcn_readfirstlane(((g32p)xp.seg_first)[j]);
-            const uint64_t b = __builtin_amdgcn_readfirstlane(((g32p)xp.seg_first)[j + 1]);
+            const uint64_t a = rfl_u32(((g32p)xp.seg_first)[j]);
+            const uint64_t b = rfl_u32(((g32p)xp.seg_first)[j + 1]);
             if (a >= b)
                 return false;
             ld.w = a;
@@ -1542,7 +1557,7 @@ __global__ __launch_bounds__(WG) void qteam_dyn_kernel(XDesc d, QDyn q, const ui
     uint32_t lp;
     /* slot u of this workgroup: part u % np of its (u / np)-th group */
     auto decode = [&](uint32_t raw, uint64_t &k, uint32_t &p) {
-        const uint32_t u = __builtin_amdgcn_readlane(raw, 0);
+        const uint32_t u = rl_u32(raw, 0);
         const uint32_t gi = u / np;
         const uint64_t grp = (uint64_t)blockIdx.x * WAVES + gi % WAVES + (uint64_t)(gi / WAVES) * nwaves;
         k = grp < ngroups ? grp : ngroups;
@@ -1643,7 +1658,7 @@ __device__ __forceinline__ uint32_t first_piece(const char *L, const Item &it, u
         return r;
     }
     const int32_t d0 = (int32_t)(A - V0); /* front padding, 0..63 */
-    const int32_t d0u = __builtin_amdgcn_readfirstlane(d0);
+    const int32_t d0u = (int32_t)rfl_u32((uint32_t)d0);
     if (__ballot(d0 != d0u || (A & 3) != 0) == 0) {
         /* every record of the wave starts at the same 4-aligned word f of its
          * first piece (fixed-stride batches, zsbench spans): skip the zero
@@ -1691,8 +1706,8 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
     if (!FIXED) {
         uint32_t base = 0;
         for (uint32_t k = 0; k < d.klass; ++k)
-            base += __builtin_amdgcn_readfirstlane(((g32p)d.class_count)[k]);
-        count = __builtin_amdgcn_readfirstlane(((g32p)d.class_count)[d.klass]);
+            base += rfl_u32(((g32p)d.class_count)[k]);
+        count = rfl_u32(((g32p)d.class_count)[d.klass]);
         list = d.desc + base;
     }
     /* every record of the batch in this (first) class: the classify scatter
@@ -1793,8 +1808,8 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
         __amdgpu_buffer_rsrc_t rsrc;
         bool inwin = true;
         if (PF >= 3) {
-            const uintptr_t first = __builtin_amdgcn_readfirstlane((uint32_t)V0) |
-                                    ((uintptr_t)__builtin_amdgcn_readfirstlane((uint32_t)(V0 >> 32)) << 32);
+            const uintptr_t first = rfl_u32((uint32_t)V0) |
+                                    ((uintptr_t)rfl_u32((uint32_t)(V0 >> 32)) << 32);
             W = first >= (1ull << 30) ? first - (1ull << 30) : 0;
             rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)W, (short)0, (int)RANGE, 0x00020000);
             inwin = V0 >= W && V0 + 64 * np - W < RANGE;
@@ -2042,7 +2057,7 @@ __device__ __forceinline__ void m64_issue(const MultiBatch &m, uint64_t n, const
      * bound on the 32-bit lane offset, no branch (a branchy clamp made the
      * compiler wait for the next chunk's loads before hashing this one) */
     const uint64_t room = ok ? base + n * 64 - 16 - sb : 0;
-    const uint32_t lim = __builtin_amdgcn_readfirstlane((uint32_t)(room < 0xffffffffull ? room : 0xffffffffull));
+    const uint32_t lim = rfl_u32((uint32_t)(room < 0xffffffffull ? room : 0xffffffffull));
 #pragma unroll
     for (int i = 0; i < 4 * K; ++i) {
         const uint32_t o = voff + 1024u * (uint32_t)i;
@@ -2116,11 +2131,11 @@ __global__ __launch_bounds__(WG) void multi64_kernel(BatchDesc d, MultiBatch m, 
             lslot = 0;
         __syncthreads();
         uint32_t s0 = lane == 0 ? atomicAdd(&lslot, 1u) : 0u;
-        item_pos(__builtin_amdgcn_readfirstlane(__shfl(s0, 0)), ph);
+        item_pos(rfl_u32(__shfl(s0, 0)), ph);
     }
     uint32_t snext = deal && lane == 0 ? atomicAdd(&lslot, 1u) : 0u; /* the item after the next */
     auto deal_advance = [&](M64Pos &p) {
-        item_pos(__builtin_amdgcn_readfirstlane(__shfl(snext, 0)), p);
+        item_pos(rfl_u32(__shfl(snext, 0)), p);
         snext = lane == 0 ? atomicAdd(&lslot, 1u) : 0u;
     };
     pl = ph;
@@ -2210,7 +2225,7 @@ __device__ __forceinline__ void m64d_issue(const MultiBatch &m, uint64_t n, uint
     const uintptr_t base = ok ? reinterpret_cast<uintptr_t>(m.base[b]) : dummy;
     const uintptr_t sb = uni64(base + (ok ? k * CHUNK : 0));
     const uint64_t room = ok ? base + n * 64 - 16 - sb : 0;
-    const uint32_t lim = __builtin_amdgcn_readfirstlane((uint32_t)(room < 0xffffffffull ? room : 0xffffffffull));
+    const uint32_t lim = rfl_u32((uint32_t)(room < 0xffffffffull ? room : 0xffffffffull));
 #pragma unroll
     for (int i = 0; i < 4 * K; ++i) {
         const uint32_t o = voff + 1024u * (uint32_t)i;
@@ -2592,7 +2607,7 @@ __device__ __forceinline__ void run_check(const BatchDesc &d, BRec &b, int lane)
     const uint64_t v0 = uni64((uint64_t)b.V0);
     const bool ok = b.ok && !b.skip && b.cfit && b.burst && b.it.len == RUN_SPAN && (b.it.A & 3) == 0 &&
                     (uint64_t)b.V0 == v0 + (uint64_t)RUN_GRID * (uint32_t)lane;
-    b.run = __builtin_amdgcn_readfirstlane((uint32_t)__all(ok)) != 0 && !(d.opt & 2048);
+    b.run = rfl_u32((uint32_t)__all(ok)) != 0 && !(d.opt & 2048);
 }
 
 /* NT: non-temporal loads (verification).  The writer reads with plain loads:
@@ -2894,7 +2909,7 @@ __device__ __forceinline__ void quad_round_issue(const BRec &b, QuadRound &Q, ui
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1)
         m = max(m, (uint32_t)__shfl_xor((int)m, o));
-    Q.npw = __builtin_amdgcn_readfirstlane(m);
+    Q.npw = rfl_u32(m);
     quad_piece(Q, 0, dummy, lane, Q.w);
 }
 
@@ -3044,8 +3059,8 @@ __global__ __launch_bounds__(NB == 1 ? 1024 : BWG) void burst_kernel(BatchDesc d
     if (!FIXED && d.class_count) { /* no classes: every record, caller's arrays */
         uint32_t base = 0;
         for (uint32_t k = 0; k < d.klass; ++k)
-            base += __builtin_amdgcn_readfirstlane(((g32p)d.class_count)[k]);
-        count = __builtin_amdgcn_readfirstlane(((g32p)d.class_count)[d.klass]);
+            base += rfl_u32(((g32p)d.class_count)[k]);
+        count = rfl_u32(((g32p)d.class_count)[d.klass]);
         list = d.desc + base;
         if (d.direct_max && count)
             count = d.n; /* walk every record, skip the other classes' */
@@ -3100,14 +3115,14 @@ __global__ __launch_bounds__(NB == 1 ? 1024 : BWG) void burst_kernel(BatchDesc d
             b.run = false;
             if (rr)
                 run_check(d, b, lane);
-            if (NB == 5 && __builtin_amdgcn_readfirstlane((uint32_t)b.run))
+            if (NB == 5 && rfl_u32((uint32_t)b.run))
                 run_issue(b, w, lane);
             else
                 burst_issue_x(b, dummy, w, lane);
         };
         auto hash = [&](BRec &b, uint32_t (&w)[NB][16]) {
             xpose_burst(w);
-            if (NB == 5 && __builtin_amdgcn_readfirstlane((uint32_t)b.run)) {
+            if (NB == 5 && rfl_u32((uint32_t)b.run)) {
                 if constexpr (NB == 5)
                     run_hash(d, b, w, L, S, lane, c_lo, c_hi);
                 return;
@@ -3213,9 +3228,7 @@ __device__ __forceinline__ uint64_t slot_round(const RoundSched &s, uint64_t k)
 {
     if (k >= s.ns)
         return s.nr;
-    /* (readfirstlane returns int: widened directly it sign-extends past 2^31 --
-     * rounds and slots stay below 2^31 here, the host caps nr below 2^32) */
-    return s.list ? (uint64_t)__builtin_amdgcn_readfirstlane(((g32p)s.list)[k]) : k;
+    return s.list ? (uint64_t)rfl_u32(((g32p)s.list)[k]) : k;
 }
 
 /* dealt slot k of this workgroup: slot wpb b + k % wpb + (k / wpb) nw */
@@ -3229,7 +3242,7 @@ __device__ __forceinline__ uint64_t deal_round(const RoundSched &s, uint64_t k)
 __device__ __forceinline__ uint64_t round_at(const RoundSched &s, uint64_t t, uint32_t fetched)
 {
     if (s.deal)
-        return deal_round(s, __builtin_amdgcn_readfirstlane(__shfl(fetched, 0)));
+        return deal_round(s, rfl_u32(__shfl(fetched, 0)));
     return slot_round(s, s.w + t * s.nw);
 }
 
@@ -3309,7 +3322,7 @@ __global__ __launch_bounds__(RO ? RT : BWG) void commit_kernel(BatchDesc d, cons
     rs.nr = (count + 63) / 64;
     rs.wpb = NWV;
     rs.list = !RO && d.round_mode == 2 ? d.round_list : nullptr;
-    rs.ns = rs.list ? __builtin_amdgcn_readfirstlane(((const volatile uint32_t *)d.round_count)[0]) : rs.nr;
+    rs.ns = rs.list ? rfl_u32(((const volatile uint32_t *)d.round_count)[0]) : rs.nr;
     rs.deal = !(d.opt & (1u << 22));
     rs.lctr = &lctr;
     uint64_t r_cur = round_at(rs, 0, deal_issue(rs, lane));
@@ -3330,7 +3343,7 @@ __global__ __launch_bounds__(RO ? RT : BWG) void commit_kernel(BatchDesc d, cons
         commit_next(b, lane);
         b.run = false;
         run_check(d, b, lane);
-        const bool run = __builtin_amdgcn_readfirstlane((uint32_t)b.run) != 0;
+        const bool run = rfl_u32((uint32_t)b.run) != 0;
         if (RO && !run && d.round_mode == 3) { /* not a run round: one-piece quad bursts */
             QuadRound Q;
             quad_round_issue(b, Q, dummy, lane);
@@ -3970,7 +3983,7 @@ __device__ __forceinline__ void fill_part_rec(uint32_t *part_rec, const uint32_t
     while (big) {
         const int i = __ffsll((unsigned long long)big) - 1;
         big &= big - 1;
-        const uint32_t a = __builtin_amdgcn_readlane(q0, i), b = __builtin_amdgcn_readlane(q1, i);
+        const uint32_t a = rl_u32(q0, i), b = rl_u32(q1, i);
         for (uint32_t q = a + (uint32_t)lane; q < b; q += 64)
             part_rec[q] = c0 + (uint32_t)(wv * 64 + i);
     }

@@ -568,11 +568,19 @@ extern "C" int zscrc_zs_repack(const char *dbdir, unsigned flags, int threads, z
         bool ok = write(lockfd, out, sizeof out) == (ssize_t)sizeof out;
         if (flags & ZSCRC_PACK_FSYNC)
             ok = ok && fsync(lockfd) == 0;
-        ok = ok && rename(lock_path.c_str(), dot_path.c_str()) == 0;
+        /* ZSCRC_FAULT=dotzsdb_rename: the rename fails (fault injection for
+         * tests/test_gpu_repack.py; nothing else reads it) */
+        const char *fault = getenv("ZSCRC_FAULT");
+        const bool renamed = ok && !(fault && !strcmp(fault, "dotzsdb_rename")) &&
+                             rename(lock_path.c_str(), dot_path.c_str()) == 0;
         close(lockfd);
         lockfd = -1;
-        if (!ok)
+        if (!renamed) {
+            /* the lock file was not renamed into place: it must not outlive
+             * the call (a stale .zsdb.lock refuses every later update) */
+            unlink(lock_path.c_str());
             rc = ZSCRC_EINVAL;
+        }
         rep->dotzsdb_crc = be64(out + 53) & 0xFFFFFFFFull;
     }
     unlock(rc);
