@@ -332,7 +332,7 @@ def test_scalar_offload_cached_and_pieces(gpu):
         lib().zscrc_set_gpu_min_pair(*saved)
 
 
-@pytest.mark.parametrize("mode", ["team16", "xteam", "qteam-static", "qteam"])
+@pytest.mark.parametrize("mode", ["team16", "xteam", "qteam-static", "qteam-qfold", "qteam"])
 def test_config3_headline_dispatch(gpu, mode):
     """BASELINE config 3 at full size through the exact call bench.py times:
     zscrc_device_fixed on 65,536 x 64 KiB chunks (4 GiB), seed 0, flags 0 --
@@ -345,11 +345,12 @@ def test_config3_headline_dispatch(gpu, mode):
     d = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=gpu, generator=g)
     lib().zscrc_set_xteam(1, 32768 if mode == "xteam" else 256 << 10)
     lib().zscrc_set_qteam(1 if mode.startswith("qteam") else 0)
-    lib().zscrc_set_opt(QSTATIC if mode == "qteam-static" else 0)
+    lib().zscrc_set_opt(QSTATIC if mode == "qteam-static" else QFOLD if mode == "qteam-qfold" else 0)
     try:
         name = lib().zscrc_fixed_kernel(d.data_ptr(), L, L, n).decode()
         assert name == {"team16": "team_kernel<16>", "xteam": "xteam_kernel",
-                        "qteam": "qteam_dyn_kernel+qfold_kernel", "qteam-static": "qteam_kernel"}[mode]
+                        "qteam": "qteam_dyn_kernel", "qteam-qfold": "qteam_dyn_kernel+qfold_kernel",
+                        "qteam-static": "qteam_kernel"}[mode]
         out = torch.empty(n, dtype=torch.int32, device=gpu)
         from zeroskip_amd._lib import check
         check(lib().zscrc_device_fixed(d.data_ptr(), L, L, 0, out.data_ptr(), n, 0,
@@ -394,10 +395,12 @@ def test_xteam_shapes(gpu):
 
 QDEAL = 1 << 25    # zs::BatchDesc::opt: qteam records cut into parts dealt per workgroup, at any size
 QSTATIC = 1 << 24  # qteam's static walk at any size
+QFOLD = 32         # qteam_dyn's part fold as a second launch (qfold_kernel), not in LDS
 
 
-@pytest.mark.parametrize("opt", [0, QDEAL], ids=["static", "dealt-parts"])
-def test_qteam_shapes(gpu, opt, monkeypatch):
+@pytest.mark.parametrize("opt,P", [(0, "3"), (QDEAL, "3"), (QDEAL, "1"), (QDEAL | QFOLD, "3")],
+                         ids=["static", "dealt-parts", "dealt-parts-P1", "dealt-parts-qfold"])
+def test_qteam_shapes(gpu, opt, P, monkeypatch):
     """qteam_kernel (coalesced 16-lane column-quad teams) on ragged shapes of
     equal-length records: a partial last group of four, unaligned bases (the
     first record's front-padded step clamped at the buffer start), ragged
@@ -407,7 +410,11 @@ def test_qteam_shapes(gpu, opt, monkeypatch):
     lib().zscrc_set_qteam(1)
     lib().zscrc_set_opt(opt)
     if opt:
-        monkeypatch.setenv("ZSCRC_QDYN_P", "3")     # parts of 3 KiB: ragged first parts, many per record
+        # parts of 3 KiB (1 KiB): ragged first parts, many per record; the
+        # part registers fit LDS (the in-kernel fold) on some shapes, not on
+        # others (qfold_kernel)
+        monkeypatch.setenv("ZSCRC_QDYN_P", P)
+    names = set()
     try:
         for stride, length, n, off in [(8192, 8192, 16385, 0), (8200, 8195, 16390, 1), (16384, 12000, 16387, 3),
                                        (65540, 65537, 16385, 2), (12288, 9000, 16400, 0), (2048, 2048, 16387, 0),
@@ -415,8 +422,10 @@ def test_qteam_shapes(gpu, opt, monkeypatch):
                                        (4096, 8192, 16384, 0), (0, 9000, 16386, 1)]:   # overlapping, stride 0
             data = rand_bytes(stride * (n - 1) + length + off, stride + length + n)
             dd = to_dev(data[off:], gpu)
-            assert lib().zscrc_fixed_kernel(dd.data_ptr(), stride, length, n).decode() == \
-                ("qteam_dyn_kernel+qfold_kernel" if opt else "qteam_kernel")
+            name = lib().zscrc_fixed_kernel(dd.data_ptr(), stride, length, n).decode()
+            names.add(name)
+            assert name == ("qteam_kernel" if not opt else "qteam_dyn_kernel+qfold_kernel" if opt & QFOLD
+                            else name if name in ("qteam_dyn_kernel", "qteam_dyn_kernel+qfold_kernel") else None)
             out = u32(zd.crc_fixed(dd, stride, length, n, seed=0xA5A5))
             ref = _oracle_seeded(data[off:], stride, length, n, 0xA5A5)
             bad = np.nonzero(out != ref)[0]
@@ -425,6 +434,8 @@ def test_qteam_shapes(gpu, opt, monkeypatch):
             want = (~oracle.crc32c_hw(~0x1234 & M32, data[off:off + length])) & M32
             assert raw[0] == want, (stride, length, "raw")
             del dd
+        if opt == QDEAL and P == "1":
+            assert names == {"qteam_dyn_kernel", "qteam_dyn_kernel+qfold_kernel"}, names
         d = torch.zeros(16, dtype=torch.uint8, device=gpu)
         assert lib().zscrc_fixed_kernel(d.data_ptr(), 8194, 8192, 16384).decode() == "team_kernel<16>"
     finally:

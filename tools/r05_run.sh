@@ -24,6 +24,12 @@ for step in "$@"; do
               c=config${step#traffic}
               bash tools/pmc_traffic.sh $c 5 ;;
     trace2|trace3|trace4|trace5) bash tools/trace_bench.sh config${step#trace} ;;
+    bench3f)  ZSCRC_OPT=32 timeout -k 10 600 python bench.py --workload config3 --no-cpu >> gpurun_out/bench3f.jsonl \
+                2>> gpurun_out/bench3f.err ;;
+    cputhreads) timeout -k 10 300 python tools/probes/cpu_threads.py > gpurun_out/cpu_threads.jsonl \
+                2> gpurun_out/cpu_threads.err ;;
+    ab3)      AB_CASES=config3,fixed_16KiB,fixed_4KiB,fixed_1MiB timeout -k 10 600 python tools/opt_ab.py 0 32 \
+                > gpurun_out/ab3.jsonl 2> gpurun_out/ab3.err ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   rc=$?

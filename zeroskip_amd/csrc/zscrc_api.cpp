@@ -404,26 +404,63 @@ bool qdeal_for(const DevCtx *c, const zs::BatchDesc &d)
     return (d.opt & (1u << 25)) || (d.n * d.fixed_len >= (1ull << 30) && ngroups >= 2ull * c->ncu * 16);
 }
 
-/* qteam with each workgroup's units dealt to its waves:
- * every record cut into parts of P 1 KiB steps (env ZSCRC_QDYN_P, default
- * 16), parts folded per record by a second launch. */
-int launch_qdyn(DevCtx *c, const zs::BatchDesc &d, hipStream_t s)
+/* qteam_dyn_kernel's parts: P 1 KiB steps each (env ZSCRC_QDYN_P, default
+ * 16), np per record; whether a workgroup's part registers fit its LDS (a
+ * workgroup's records -- 16 groups per ceil(ngroups / waves) -- x np), so
+ * it folds its own records at its end and no second launch runs. */
+struct QdynShape {
+    uint32_t P, np;
+    uint64_t tail, ngroups;
+    bool lds_fold;
+};
+
+QdynShape qdyn_shape(const DevCtx *c, const zs::BatchDesc &d)
 {
-    uint32_t P = 16;
+    QdynShape q;
+    q.P = 16;
     if (const char *e = getenv("ZSCRC_QDYN_P")) {
         const unsigned long v = strtoul(e, nullptr, 0);
         if (v >= 1 && v <= 4096)
-            P = (uint32_t)v;
+            q.P = (uint32_t)v;
     }
     const uint64_t ph = reinterpret_cast<uintptr_t>(d.base) & 3;
     const uint64_t span = ((ph + d.fixed_len) & ~uint64_t(3)) - ph;
     const uint64_t S = (span + 1023) / 1024;
-    const uint64_t tail = d.fixed_len - span;
-    const uint32_t np = (uint32_t)((S + P - 1) / P);
-    const uint64_t ngroups = (d.n + 3) / 4;
+    q.tail = d.fixed_len - span;
+    q.np = (uint32_t)((S + q.P - 1) / q.P);
+    q.ngroups = (d.n + 3) / 4;
+    const uint64_t nw = (uint64_t)c->ncu * 16;
+    q.lds_fold = !(d.opt & zs::OPT_QFOLD_LAUNCH) && 4 * 16 * ((q.ngroups + nw - 1) / nw) * q.np <= zs::QDYN_LDS_PARTS;
+    return q;
+}
+
+/* qteam with each workgroup's units dealt to its waves: every record cut
+ * into np parts, folded per record in the kernel (LDS) or by a second
+ * launch (qfold_kernel). */
+int launch_qdyn(DevCtx *c, const zs::BatchDesc &d, hipStream_t s)
+{
+    const QdynShape sh = qdyn_shape(c, d);
+    const uint32_t P = sh.P, np = sh.np;
+    const uint64_t tail = sh.tail, ngroups = sh.ngroups;
     /* a workgroup's slots: its groups x np (32-bit) */
     if (ngroups / ((uint64_t)c->ncu * 16) * np >= (1ull << 31))
         return ZSCRC_EINVAL;
+    const uint32_t K = zs_gf2_xpow8n(1024ull * P), K_last = zs_gf2_xpow8n(1024ull * P + tail);
+    if (sh.lds_fold) {
+        zs::QDyn q;
+        memset(&q, 0, sizeof q);
+        q.P = P;
+        q.np = np;
+        q.lds_fold = 1;
+        q.K = K;
+        q.K_last = K_last;
+        if (zs_launch_qdyn(&d, &q, K, K_last, c->gtab, c->ncu, s)) {
+            set_err("qteam dyn launch", hipGetLastError());
+            return ZSCRC_EHIP;
+        }
+        g_stat[2]++;
+        return ZSCRC_OK;
+    }
     std::lock_guard<std::recursive_mutex> lk(c->mu);
     int rc = scratch_acquire(c, s);
     if (rc)
@@ -431,10 +468,10 @@ int launch_qdyn(DevCtx *c, const zs::BatchDesc &d, hipStream_t s)
     rc = grow(&c->qparts, &c->qparts_bytes, (size_t)d.n * np * sizeof(uint32_t));
     if (!rc) {
         zs::QDyn q;
+        memset(&q, 0, sizeof q);
         q.part_out = static_cast<uint32_t *>(c->qparts);
         q.P = P;
         q.np = np;
-        const uint32_t K = zs_gf2_xpow8n(1024ull * P), K_last = zs_gf2_xpow8n(1024ull * P + tail);
         if (zs_launch_qdyn(&d, &q, K, K_last, c->gtab, c->ncu, s)) {
             set_err("qteam dyn launch", hipGetLastError());
             rc = ZSCRC_EHIP;
@@ -1535,7 +1572,8 @@ const char *zscrc_fixed_kernel(const void *d_base, uint64_t stride, uint64_t len
     if (g == 64 && g_xteam && g_depth[2] < 0 && len >= g_xteam_min)
         return "xteam_kernel";
     if (g == 16 && g_qteam && g_depth[1] < 0 && qteam_fits(d))
-        return qdeal_for(c, d) ? "qteam_dyn_kernel+qfold_kernel" : "qteam_kernel";
+        return !qdeal_for(c, d) ? "qteam_kernel"
+               : qdyn_shape(c, d).lds_fold ? "qteam_dyn_kernel" : "qteam_dyn_kernel+qfold_kernel";
     static const char *names[] = {"team_kernel<1>/short_kernel/burst_kernel", "team_kernel<2>",
                                   "team_kernel<16>", "team_kernel<64>"};
     return names[g == 1 ? 0 : g == 2 ? 1 : g == 16 ? 2 : 3];

@@ -140,7 +140,16 @@ struct QDyn {
     uint32_t *part_out; /* raw register of part p of record r at r * np + p */
     uint32_t P;         /* 1 KiB steps per part (part 0: the rest)          */
     uint32_t np;        /* parts per record                                */
+    /* lds_fold != 0: the part registers stay in LDS (a workgroup's records
+     * x np fit QDYN_LDS_PARTS) and each workgroup folds its own records at
+     * its end with K / K_last -- no part_out, no qfold_kernel launch */
+    uint32_t lds_fold;
+    uint32_t K, K_last;
 };
+/* part registers a qteam_dyn_kernel workgroup can hold in LDS: the 12 KiB
+ * after fill_lds<16>'s four Z tables, less the 16 bytes of its counter */
+constexpr uint32_t QDYN_LDS_PARTS = (163840u - (135168u + 4u * 4096u) - 16u) / 4u;
+constexpr uint32_t OPT_QFOLD_LAUNCH = 32u; /* tuning: qteam_dyn's fold as a second launch */
 
 /* Up to SPANS_MAX spans in one xteam_kernel launch (zscrc_device_spans):
  * span s is segments [first[s], first[s+1]) of the launch, seg[s] bytes each

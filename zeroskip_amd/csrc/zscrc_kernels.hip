@@ -1518,7 +1518,10 @@ __global__ __launch_bounds__(WG) void qteam_dyn_kernel(XDesc d, QDyn q, const ui
     };
 
     uint32_t acc = 0;
-    auto hash = [&](uint32_t (&w)[16], uint64_t k, uint32_t p, uint32_t s) {
+    /* in-LDS part registers (q.lds_fold): local record 4 gi + t of the
+     * workgroup's gi-th group, np registers each */
+    uint32_t *lparts = reinterpret_cast<uint32_t *>(L + OFF_Z + 4 * 4096 + 16);
+    auto hash = [&](uint32_t (&w)[16], uint64_t k, uint32_t p, uint32_t s, uint32_t gi) {
         xpose16(w);
         const uint64_t rec = 4 * k + (uint64_t)t;
         const uintptr_t A = base + rec * d.stride;
@@ -1545,7 +1548,10 @@ __global__ __launch_bounds__(WG) void qteam_dyn_kernel(XDesc d, QDyn q, const ui
                 for (uint32_t i = 0; i < tail; ++i)
                     acc = byte_step(L, acc, e[i], c_hi);
             }
-            q.part_out[rec * np + p] = acc;
+            if (q.lds_fold)
+                lparts[(4 * gi + (uint32_t)t) * np + p] = acc;
+            else
+                q.part_out[rec * np + p] = acc;
         }
         acc = 0;
         return true;
@@ -1554,23 +1560,23 @@ __global__ __launch_bounds__(WG) void qteam_dyn_kernel(XDesc d, QDyn q, const ui
     /* load cursor (lk, lp, ls) one step ahead of the hashing; the unit after
      * it (nk, np_) taken when it was */
     uint64_t lk;
-    uint32_t lp;
-    /* slot u of this workgroup: part u % np of its (u / np)-th group */
-    auto decode = [&](uint32_t raw, uint64_t &k, uint32_t &p) {
+    uint32_t lp, lg;
+    /* slot u of this workgroup: part u % np of its (u / np)-th group gi */
+    auto decode = [&](uint32_t raw, uint64_t &k, uint32_t &p, uint32_t &gi) {
         const uint32_t u = rl_u32(raw, 0);
-        const uint32_t gi = u / np;
+        gi = u / np;
         const uint64_t grp = (uint64_t)blockIdx.x * WAVES + gi % WAVES + (uint64_t)(gi / WAVES) * nwaves;
         k = grp < ngroups ? grp : ngroups;
         p = grp < ngroups ? u - gi * np : 0u;
     };
-    decode(fetch(), lk, lp);
+    decode(fetch(), lk, lp, lg);
     uint32_t pend = lk < ngroups ? fetch() : 0xffffffffu; /* the next unit, read when lk ends */
     uint32_t ls = lk < ngroups ? part_lo(lp) : 0u;
     auto advance_load = [&]() {
         if (lk >= ngroups)
             return;
         if (++ls == part_hi(lp)) {
-            decode(pend, lk, lp);
+            decode(pend, lk, lp, lg);
             if (lk < ngroups) {
                 ls = part_lo(lp);
                 pend = fetch();
@@ -1579,7 +1585,7 @@ __global__ __launch_bounds__(WG) void qteam_dyn_kernel(XDesc d, QDyn q, const ui
     };
     uint32_t b0[16], b1[16];
     uint64_t k0 = lk, k1;
-    uint32_t p0 = lp, p1, s0 = ls, s1;
+    uint32_t p0 = lp, p1, s0 = ls, s1, g0 = lg, g1;
     uint32_t units = 0;
     issue(lk, ls, b0);
     while (k0 < ngroups) {
@@ -1587,16 +1593,18 @@ __global__ __launch_bounds__(WG) void qteam_dyn_kernel(XDesc d, QDyn q, const ui
         k1 = lk;
         p1 = lp;
         s1 = ls;
+        g1 = lg;
         issue(k1, s1, b1);
-        units += hash(b0, k0, p0, s0) ? 1u : 0u;
+        units += hash(b0, k0, p0, s0, g0) ? 1u : 0u;
         if (k1 >= ngroups)
             break;
         advance_load();
         k0 = lk;
         p0 = lp;
         s0 = ls;
+        g0 = lg;
         issue(k0, s0, b0);
-        units += hash(b1, k1, p1, s1) ? 1u : 0u;
+        units += hash(b1, k1, p1, s1, g1) ? 1u : 0u;
     }
     uint64_t *wt = zs_wave_times; /* diagnostic (zscrc_diag_wave_times) */
     if (wt && lane == 0) {
@@ -1604,6 +1612,29 @@ __global__ __launch_bounds__(WG) void qteam_dyn_kernel(XDesc d, QDyn q, const ui
         wt[4 * wave + 1] = t_fill;
         wt[4 * wave + 2] = __builtin_amdgcn_s_memrealtime();
         wt[4 * wave + 3] = units;
+    }
+    if (!q.lds_fold)
+        return;
+    /* every part of the workgroup's records is in LDS once all its waves are
+     * here: Horner per record over its np registers (qfold_kernel's pass),
+     * the gmul table over the slice tables no wave reads any more */
+    __syncthreads();
+    load_gmul_table(L, gtab);
+    __syncthreads();
+    const uint32_t wgroups = (uint32_t)((ngroups - (uint64_t)blockIdx.x * WAVES + nwaves - 1) / nwaves) * WAVES;
+    for (uint32_t lr = threadIdx.x; lr < 4 * wgroups; lr += WG) {
+        const uint32_t gi = lr >> 2;
+        const uint64_t grp = (uint64_t)blockIdx.x * WAVES + gi % WAVES + (uint64_t)(gi / WAVES) * nwaves;
+        const uint64_t rec = 4 * grp + (lr & 3);
+        if (grp >= ngroups || rec >= d.n)
+            continue;
+        const uint32_t *pr = lparts + lr * np;
+        uint32_t reg = pr[0];
+        for (uint32_t p = 1; p + 1 < np; ++p)
+            reg = gmul_t(L, reg, q.K) ^ pr[p];
+        if (np > 1)
+            reg = gmul_t(L, reg, q.K_last) ^ pr[np - 1];
+        d.out[rec] = reg ^ d.xor_io;
     }
 }
 
@@ -4602,6 +4633,8 @@ extern "C" int zs_launch_qdyn(const zs::BatchDesc *bd, const zs::QDyn *q, uint32
     hipLaunchKernelGGL(zs::qteam_dyn_kernel<ZS_QTEAM_B3>, dim3(grid), dim3(zs::WG), 0, stream, x, *q, gtab);
     if (hipGetLastError() != hipSuccess)
         return -3;
+    if (q->lds_fold)
+        return 0; /* each workgroup folded its own records */
     const uint64_t fb = (bd->n + 255) / 256;
     hipLaunchKernelGGL(zs::qfold_kernel, dim3(fb < 1024 ? (unsigned)fb : 1024u), dim3(256), 0, stream, x, *q, K,
                        K_last, gtab);
