@@ -29,3 +29,19 @@ def test_gpus_without_launcher_spawns_torchrun():
 def test_world_size_mismatch_is_an_error():
     p = _run(["--gpus", "4"], WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
     assert p.returncode != 0 and "WORLD_SIZE=2" in (p.stderr + p.stdout)
+
+
+def test_traffic_only_for_its_own_kernel():
+    """a PMC traffic record is reported only on the line of the
+    kernel it was measured on (profiles/pmc_traffic.json is keyed by config
+    and names its kernel)."""
+    import json
+    import bench
+    rec = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+    for cfg in ("config2", "config3", "config4", "config5"):
+        assert cfg in rec and rec[cfg]["kernel"] and rec[cfg]["bytes_per_launch"] > 0, cfg
+        assert os.path.exists(os.path.join(ROOT, rec[cfg]["record"])), rec[cfg]["record"]
+        t, src = bench.traffic_for(cfg, rec[cfg]["kernel"])
+        assert t == rec[cfg]["bytes_per_launch"]
+        t, src = bench.traffic_for(cfg, rec[cfg]["kernel"] + "+another_kernel")
+        assert t is None and "not reported" in src
