@@ -117,7 +117,8 @@ def test_mixed_lengths_arrays_and_verdict(mixed, opt):
     assert k == len(m["bad"]) and set(badi[:k].cpu().tolist()) == m["bad"]
 
 
-@pytest.mark.parametrize("opt", [0, NO_RUNSPLIT, RO12, RO_LIST], ids=["default", "no_runsplit", "ro12", "ro_list"])
+@pytest.mark.parametrize("opt", [0, NO_RUNSPLIT, RO12, RO_LIST, 512],
+                         ids=["default", "no_runsplit", "ro12", "ro_list", "in_place"])
 def test_mixed_lengths_writer(mixed, opt):
     """The writer's CRC array and the in-place writer over the unseeded
     record spans of the clean image (the writer has no seeds): a copy with
@@ -140,3 +141,69 @@ def test_mixed_lengths_writer(mixed, opt):
         lib().zscrc_set_opt(0)
     assert np.array_equal(crcs.cpu().numpy().view(np.uint32), want)
     assert torch.equal(z, m["clean"])
+
+
+WRITE_INPLACE = 512   # opt: the bounded writer stores from inside its read pass (round 4's form)
+
+
+def _long_word_crc(host, off, ln, w0, w2):
+    c = oracle.crc32c_hw(0, host[off:off + ln])
+    words = w0.to_bytes(8, "little") + ln.to_bytes(8, "little") + (w2 & (0xFF << 56)).to_bytes(8, "little")
+    return oracle.crc32c_hw(c, words)
+
+
+@pytest.mark.parametrize("opt", [0, WRITE_INPLACE, RO12], ids=["two_pass", "in_place", "two_pass_ro12"])
+def test_writer_short_and_long_records(gpu, opt):
+    """The bounded writer over 250,000 short spans whose commit records are
+    short (8 bytes, CRC at +4) or -- every 40th -- long (24 bytes, CRC at +20:
+    the record form decides, src/zeroskip-file.c:266-302 / :303-328): the
+    two-pass writer's scatter (status 3 = long) and the in-place writer put
+    every CRC where the verifier finds it, the rest of the image untouched."""
+    rng = np.random.default_rng(0xB0B)
+    n = 250_000
+    lens = rng.integers(0, MAXLEN + 1, n)
+    long_rec = (np.arange(n) % 40) == 7
+    rl = np.where(long_rec, 24, 8)
+    offs = np.zeros(n, np.int64)
+    offs[0] = 41
+    offs[1:] = 41 + np.cumsum(lens + rl + rng.integers(0, 8, n))[:-1]
+    size = int(offs[-1] + lens[-1] + 24 + 64)
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    at = offs + lens
+    want = np.zeros(n, np.uint32)
+    short_i = np.nonzero(~long_rec)[0]
+    host[at[short_i]] = T_COMMIT
+    for i in np.nonzero(long_rec)[0]:
+        a, ln = int(at[i]), int(lens[i])
+        w0 = (36 << 56)                      # T_LONG_COMMIT
+        w2 = (8 << 56) | 0                   # T_2ND_HALF, CRC field zero
+        host[a:a + 8] = np.frombuffer(w0.to_bytes(8, "big"), np.uint8)
+        host[a + 8:a + 16] = np.frombuffer(ln.to_bytes(8, "big"), np.uint8)
+        host[a + 16:a + 24] = np.frombuffer(w2.to_bytes(8, "big"), np.uint8)
+        want[i] = _long_word_crc(host, int(offs[i]), ln, w0, w2)
+    # short records: the oracle writer on a copy gives the expected CRCs
+    ref = host.copy()
+    oracle.write_commits(ref, offs[short_i].astype(np.uint64), lens[short_i].astype(np.uint64), threads=8)
+    want[short_i] = ref[(at[short_i] + 4)[:, None] + np.arange(4)].view(">u4").reshape(-1)
+    # the fully written image expected: short records from the oracle, long CRC fields patched
+    full = ref.copy()
+    li = np.nonzero(long_rec)[0]
+    full[(at[li] + 20)[:, None] + np.arange(4)] = want[li].astype(">u4").view(np.uint8).reshape(-1, 4)
+    # the writer's input: short CRC fields zeroed (header words in place)
+    blank = full.copy()
+    blank[(at[short_i] + 4)[:, None] + np.arange(4)] = 0
+    blank[(at[li] + 20)[:, None] + np.arange(4)] = 0
+    img = torch.from_numpy(blank).to(gpu)
+    o = torch.from_numpy(offs).to(gpu)
+    ln = torch.from_numpy(lens.astype(np.int64)).to(gpu)
+    lib().zscrc_set_opt(opt)
+    try:
+        crc, st = zsfile.write_commits(img, o, ln, max_len=MAXLEN, status=True)
+        torch.cuda.synchronize()
+    finally:
+        lib().zscrc_set_opt(0)
+    assert np.array_equal(crc.cpu().numpy().view(np.uint32), want)
+    assert bool((st == 1).all())
+    assert np.array_equal(img.cpu().numpy(), full)
+    c2, s2 = zsfile.verify_commits(img, o, ln, max_len=MAXLEN)
+    assert bool((s2 == 1).all())

@@ -26,6 +26,12 @@ for step in "$@"; do
     trace2|trace3|trace4|trace5) bash tools/trace_bench.sh config${step#trace} ;;
     bench3f)  ZSCRC_OPT=32 timeout -k 10 600 python bench.py --workload config3 --no-cpu >> gpurun_out/bench3f.jsonl \
                 2>> gpurun_out/bench3f.err ;;
+    c2bound)  timeout -k 10 300 python tools/probes/config2_bound.py > gpurun_out/config2_bound.jsonl \
+                2> gpurun_out/config2_bound.err ;;
+    c2tests)  timeout -k 10 600 $T tests/test_gpu_parity.py -k "config2 or multi" > gpurun_out/c2tests.log 2>&1 ;;
+    ab4w)     AB_CASES=config4_write_nocrc,config4_write,config4_crcs timeout -k 10 600 python tools/opt_ab.py 0 512 \
+                > gpurun_out/ab4w.jsonl 2> gpurun_out/ab4w.err ;;
+    cwtests)  timeout -k 10 600 $T tests/test_gpu_cpu_written.py tests/test_gpu_fill.py > gpurun_out/cwtests.log 2>&1 ;;
     cputhreads) timeout -k 10 300 python tools/probes/cpu_threads.py > gpurun_out/cpu_threads.jsonl \
                 2> gpurun_out/cpu_threads.err ;;
     ab3)      AB_CASES=config3,fixed_16KiB,fixed_4KiB,fixed_1MiB timeout -k 10 600 python tools/opt_ab.py 0 32 \

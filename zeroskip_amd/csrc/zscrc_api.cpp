@@ -43,6 +43,8 @@ int zs_launch_multi(const zs::BatchDesc *d, const zs::MultiBatch *m, const uint3
                     hipStream_t stream);
 int zs_launch_xteam(int depth, const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
 int zs_launch_commit(const zs::BatchDesc *d, const uint32_t *gtab, int grid, hipStream_t stream);
+int zs_launch_commit_scatter(uint8_t *base, const uint64_t *off, const uint64_t *len, const uint32_t *crc,
+                             const uint32_t *status, uint64_t n, uint32_t *user_status, int ncu, hipStream_t stream);
 int zs_launch_qdyn(const zs::BatchDesc *bd, const zs::QDyn *q, uint32_t K, uint32_t K_last, const uint32_t *gtab,
                    int grid, hipStream_t stream);
 int zs_launch_xparts(const zs::BatchDesc *d, const uint32_t *gtab, int grid, int deal, hipStream_t stream);
@@ -138,6 +140,8 @@ struct DevCtx {
     size_t qparts_bytes = 0;
     void *rlist = nullptr;     /* split commit batches: leftover-round count + list */
     size_t rlist_bytes = 0;
+    void *wbuf = nullptr;      /* two-pass commit writer: statuses (+ CRCs) */
+    size_t wbuf_bytes = 0;
     size_t parts_bytes = 0;
     hipEvent_t last = nullptr; /* end of the last scratch user's work ... */
     hipStream_t last_stream = nullptr; /* ... enqueued on this stream */
@@ -537,10 +541,14 @@ int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1
  * per commit.  Tuning bits: 1 << 29 = commit_kernel alone, 16384 = the
  * run-only kernel lists its other rounds and commit_kernel takes them in a
  * second launch. */
+int launch_commit_two_pass(DevCtx *c, zs::BatchDesc d, hipStream_t s);
+
 int launch_commit(DevCtx *c, zs::BatchDesc d, hipStream_t s)
 {
     const uint64_t nr = (d.n + 63) / 64;
     const bool split = !(d.opt & zs::OPT_NO_RUNSPLIT) && nr >= (uint64_t)c->ncu * 12 && nr < (1ull << 32);
+    if (d.commit == 2 && split && !(d.opt & (zs::OPT_WRITE_INPLACE | zs::OPT_RO_LIST)))
+        return launch_commit_two_pass(c, d, s);
     if (!split || !(d.opt & zs::OPT_RO_LIST)) {
         d.round_mode = split ? 3 : 0;
         if (zs_launch_commit(&d, c->gtab, c->ncu, s)) {
@@ -571,6 +579,39 @@ int launch_commit(DevCtx *c, zs::BatchDesc d, hipStream_t s)
             } else {
                 g_stat[2]++;
             }
+        }
+    }
+    const int rc2 = scratch_release(c, s);
+    return rc ? rc : rc2;
+}
+
+/* The bounded commit writer in two passes: the run-only commit_kernel
+ * computes the CRCs (commit mode 4, the image only read) into the caller's
+ * d_crc or a scratch array, commit_scatter_kernel stores them into the
+ * image.  Tuning bit 512: stored from inside the read pass (round 4). */
+int launch_commit_two_pass(DevCtx *c, zs::BatchDesc d, hipStream_t s)
+{
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    int rc = scratch_acquire(c, s);
+    const size_t n = d.n;
+    if (!rc)
+        rc = grow(&c->wbuf, &c->wbuf_bytes, (d.out ? 4 : 8) * n);
+    if (!rc) {
+        uint32_t *st = static_cast<uint32_t *>(c->wbuf);
+        uint32_t *crc = d.out ? d.out : st + n;
+        uint32_t *user_status = d.status;
+        zs::BatchDesc dc = d;
+        dc.commit = 4;
+        dc.out = crc;
+        dc.status = st;
+        dc.round_mode = 3;
+        if (zs_launch_commit(&dc, c->gtab, c->ncu, s) ||
+            zs_launch_commit_scatter(const_cast<uint8_t *>(d.base), d.off, d.len, crc, st, n, user_status, c->ncu,
+                                     s)) {
+            set_err("commit writer launch", hipGetLastError());
+            rc = ZSCRC_EHIP;
+        } else {
+            g_stat[2] += 2;
         }
     }
     const int rc2 = scratch_release(c, s);

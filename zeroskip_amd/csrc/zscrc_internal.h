@@ -40,7 +40,8 @@ struct BatchDesc {
      * host-order trailer words); verify: status[i] 1 = matches the stored
      * CRC, 0 = mismatch, 2 = no commit record there; write: the CRC is stored
      * big-endian into the commit record; 3: out[] only (status 1 / 2 as the
-     * writer's), nothing stored into the image. */
+     * writer's), nothing stored into the image; 4: as 3 with status 3 for a
+     * long commit record (the two-pass writer's first pass). */
     uint32_t commit;
     uint32_t *status;     /* may be NULL */
     /* commit mode: bytes of the image at base.  A span whose commit word
@@ -150,6 +151,7 @@ struct QDyn {
  * after fill_lds<16>'s four Z tables, less the 16 bytes of its counter */
 constexpr uint32_t QDYN_LDS_PARTS = (163840u - (135168u + 4u * 4096u) - 16u) / 4u;
 constexpr uint32_t OPT_QFOLD_LAUNCH = 32u; /* tuning: qteam_dyn's fold as a second launch */
+constexpr uint32_t OPT_WRITE_INPLACE = 512u; /* tuning: bounded commit writer stores from inside its read pass */
 
 /* Up to SPANS_MAX spans in one xteam_kernel launch (zscrc_device_spans):
  * span s is segments [first[s], first[s+1]) of the launch, seg[s] bytes each
