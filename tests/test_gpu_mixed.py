@@ -118,7 +118,7 @@ def test_mixed_lengths_arrays_and_verdict(mixed, opt):
 
 
 @pytest.mark.parametrize("opt", [0, NO_RUNSPLIT, RO12, RO_LIST, 512],
-                         ids=["default", "no_runsplit", "ro12", "ro_list", "in_place"])
+                         ids=["default", "no_runsplit", "ro12", "ro_list", "two_pass"])
 def test_mixed_lengths_writer(mixed, opt):
     """The writer's CRC array and the in-place writer over the unseeded
     record spans of the clean image (the writer has no seeds): a copy with
@@ -143,7 +143,7 @@ def test_mixed_lengths_writer(mixed, opt):
     assert torch.equal(z, m["clean"])
 
 
-WRITE_INPLACE = 512   # opt: the bounded writer stores from inside its read pass (round 4's form)
+TWO_PASS = 512   # opt: the bounded writer as a CRC array + a scatter launch
 
 
 def _long_word_crc(host, off, ln, w0, w2):
@@ -152,7 +152,7 @@ def _long_word_crc(host, off, ln, w0, w2):
     return oracle.crc32c_hw(c, words)
 
 
-@pytest.mark.parametrize("opt", [0, WRITE_INPLACE, RO12], ids=["two_pass", "in_place", "two_pass_ro12"])
+@pytest.mark.parametrize("opt", [0, TWO_PASS, TWO_PASS | RO12], ids=["in_place", "two_pass", "two_pass_ro12"])
 def test_writer_short_and_long_records(gpu, opt):
     """The bounded writer over 250,000 short spans whose commit records are
     short (8 bytes, CRC at +4) or -- every 40th -- long (24 bytes, CRC at +20:

@@ -2,11 +2,14 @@
 1M x 64 B (4 GiB), forms and diagnostics interleaved block by block (10
 launches back to back between two events per block, 7 blocks, medians), beside
 the same-GPU streaming read of the same 4 GiB:
-  0            the shipped form (results stored after the next chunk's loads)
-  128          results stored right after their hash (round 4's form)
-  64           no result stores (diagnostic, wrong results)
+  0            the shipped form (unconditional result stores, lanes past the
+               batch's end to a sink word)
+  128          round 4's guarded stores (the compiler drained them with
+               vmcnt(0) before every other chunk's loads)
   1<<20        no hashing (diagnostic)
-  64|1<<20     loads only (diagnostic)
+  262144       result stores into one L2-resident window (diagnostic)
+(round 5's first probe also had bit 64: no result stores -- 0.609 ms against
+0.818 with them, the streaming read 0.618; profiles/r05/config2/bound_probe.jsonl)
 usage: python tools/probes/config2_bound.py [opt ...]"""
 import json
 import os
@@ -20,7 +23,7 @@ from zeroskip_amd._lib import check, lib  # noqa: E402
 
 
 def main():
-    opts = [int(x) for x in sys.argv[1:]] or [0, 128, 64, 1 << 20, 64 | (1 << 20)]
+    opts = [int(x) for x in sys.argv[1:]] or [0, 128, 1 << 20, 262144]
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev)
     g.manual_seed(0x64)

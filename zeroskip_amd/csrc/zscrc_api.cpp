@@ -129,6 +129,7 @@ struct DevCtx {
     bool ready = false;
     int ncu = 0;
     uint32_t *gtab = nullptr;
+    uint32_t *sink = nullptr;  /* 4 KiB a kernel's masked-off stores go to */
     void *scratch = nullptr;   /* span partials */
     size_t scratch_bytes = 0;
     void *stage = nullptr;     /* host-batch staging */
@@ -258,6 +259,11 @@ int get_ctx(DevCtx **out)
     if (e != hipSuccess) {
         set_err("hipMemcpy(tables)", e);
         return ZSCRC_EHIP;
+    }
+    e = hipMalloc(&c.sink, 4096);
+    if (e != hipSuccess) {
+        set_err("hipMalloc(sink)", e);
+        return ZSCRC_ENOMEM;
     }
     c.ncu = ncu;
     c.ready = true;
@@ -547,7 +553,7 @@ int launch_commit(DevCtx *c, zs::BatchDesc d, hipStream_t s)
 {
     const uint64_t nr = (d.n + 63) / 64;
     const bool split = !(d.opt & zs::OPT_NO_RUNSPLIT) && nr >= (uint64_t)c->ncu * 12 && nr < (1ull << 32);
-    if (d.commit == 2 && split && !(d.opt & (zs::OPT_WRITE_INPLACE | zs::OPT_RO_LIST)))
+    if (d.commit == 2 && split && (d.opt & zs::OPT_WRITE_TWO_PASS) && !(d.opt & zs::OPT_RO_LIST))
         return launch_commit_two_pass(c, d, s);
     if (!split || !(d.opt & zs::OPT_RO_LIST)) {
         d.round_mode = split ? 3 : 0;
@@ -585,10 +591,13 @@ int launch_commit(DevCtx *c, zs::BatchDesc d, hipStream_t s)
     return rc ? rc : rc2;
 }
 
-/* The bounded commit writer in two passes: the run-only commit_kernel
- * computes the CRCs (commit mode 4, the image only read) into the caller's
- * d_crc or a scratch array, commit_scatter_kernel stores them into the
- * image.  Tuning bit 512: stored from inside the read pass (round 4). */
+/* The bounded commit writer in two passes (tuning bit 512, measured and not
+ * the default): the run-only commit_kernel computes the CRCs (commit mode 4,
+ * the image only read) into the caller's d_crc or a scratch array,
+ * commit_scatter_kernel stores them into the image.  Config 4's 10 M fields:
+ * 1.025 ms (0.540 CRC array + ~0.485 scatter) against 0.977 for the stores
+ * from inside the read pass (interleaved, profiles/r05/writer_ab.jsonl): the
+ * scattered field writes cost the same wherever they are issued. */
 int launch_commit_two_pass(DevCtx *c, zs::BatchDesc d, hipStream_t s)
 {
     std::lock_guard<std::recursive_mutex> lk(c->mu);
@@ -1168,6 +1177,7 @@ int zscrc_device_fixed_multi(const void *const *d_bases, uint32_t *const *d_outs
     zs::MultiBatch m;
     memset(&m, 0, sizeof m);
     m.nb = (uint32_t)k;
+    m.sink = c->sink;
     for (size_t b = 0; b < k; ++b) {
         m.base[b] = static_cast<const uint8_t *>(d_bases[b]);
         m.out[b] = d_outs[b];

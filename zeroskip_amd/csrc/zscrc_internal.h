@@ -151,7 +151,7 @@ struct QDyn {
  * after fill_lds<16>'s four Z tables, less the 16 bytes of its counter */
 constexpr uint32_t QDYN_LDS_PARTS = (163840u - (135168u + 4u * 4096u) - 16u) / 4u;
 constexpr uint32_t OPT_QFOLD_LAUNCH = 32u; /* tuning: qteam_dyn's fold as a second launch */
-constexpr uint32_t OPT_WRITE_INPLACE = 512u; /* tuning: bounded commit writer stores from inside its read pass */
+constexpr uint32_t OPT_WRITE_TWO_PASS = 512u; /* tuning: bounded commit writer as CRC array + scatter launch */
 
 /* Up to SPANS_MAX spans in one xteam_kernel launch (zscrc_device_spans):
  * span s is segments [first[s], first[s+1]) of the launch, seg[s] bytes each
@@ -315,6 +315,9 @@ struct MultiBatch {
     uint32_t nb;
     const uint8_t *base[MULTI_MAX];
     uint32_t *out[MULTI_MAX];
+    /* a device word a store with nothing to write goes to (multi64_kernel's
+     * lanes past a batch's last record): the stores stay unconditional */
+    uint32_t *sink;
 };
 
 struct SpanFold {

@@ -2109,16 +2109,17 @@ __device__ __forceinline__ void m64_issue(const MultiBatch &m, uint64_t n, const
  * register ring (123 VGPRs) measured level with two (0.524 vs 0.522 ms per
  * 32 batches): the kernel hashes at ~4.7 TB/s from L3 as well, so the loads
  * are not what holds it back.
- * DEFER (round 5): a chunk's results are stored after the NEXT chunk's loads
- * are issued, from registers that stay live across that issue.  Stored right
- * after the hash, the compiler gave the result stores registers the next
- * load batch then overwrites, and guarded that with s_waitcnt vmcnt(0) ahead
- * of every other load batch (ISA of round 4's build): the wave sat with no
- * load in flight until its two result stores were acknowledged.
- * Diagnostics (wrong results): tuning bit 1 << 20 no hashing, 64 no result
- * stores (each lane's results XOR-ed into one word stored at the end) --
- * both: the load shape alone. */
-template <int K, bool DEFER>
+ * GUARD = false (round 5): the result stores are unconditional -- a lane past
+ * the batch's last record stores to m.sink.  Guarded by `if (record < n)`,
+ * each store sat in its own branch, and at the join the compiler's wait
+ * counting (one vmcnt for loads and stores on gfx950) could not tell how many
+ * stores were still in flight, so the next wait for load data became
+ * s_waitcnt vmcnt(0): every chunk drained the wave's result stores before its
+ * loads went out (ISA of round 4's build).  Without result stores the launch
+ * takes 0.609 against 0.818 ms (64 x 64 MiB, profiles/r05/config2/
+ * bound_probe.jsonl), the same-GPU streaming read 0.618.  GUARD = true
+ * (tuning bit 128): round 4's guarded stores. */
+template <int K, bool GUARD>
 __global__ __launch_bounds__(WG) void multi64_kernel(BatchDesc d, MultiBatch m, const uint32_t *__restrict__ gtab)
 {
     __shared__ __attribute__((aligned(16))) char L[OFF_U];
@@ -2138,8 +2139,6 @@ __global__ __launch_bounds__(WG) void multi64_kernel(BatchDesc d, MultiBatch m, 
     const uint32_t voff = 64u * (uint32_t)c + 16u * (uint32_t)g;
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(gtab);
     const uint32_t R0 = d.fixed_seed ^ d.xor_io;
-    const bool nostore = (d.opt & 64u) != 0;
-    uint32_t sink = 0;
     /* the walk's step in (batch, chunk) form, once */
     const uint64_t step_b = nw / cpb, step_k = nw - step_b * cpb;
     auto advance = [&](M64Pos &p) {
@@ -2186,7 +2185,8 @@ __global__ __launch_bounds__(WG) void multi64_kernel(BatchDesc d, MultiBatch m, 
     };
     pl = ph;
     m64_issue<K>(m, n, pl, voff, dummy, b0);
-    auto hash_r = [&](uint32_t (&w)[16 * K], uint32_t (&r)[K]) {
+    auto hash = [&](uint32_t (&w)[16 * K], const M64Pos &p) {
+        uint32_t r[K];
 #pragma unroll
         for (int q = 0; q < K; ++q) {
             xpose16(reinterpret_cast<uint32_t (&)[16]>(w[16 * q]));
@@ -2208,62 +2208,22 @@ __global__ __launch_bounds__(WG) void multi64_kernel(BatchDesc d, MultiBatch m, 
             for (int q = 0; q < K; ++q)
                 r[q] = m4(L, r[q], c_lo, c_hi);
         }
-        /* the stored value itself: no temporary between r and its store */
-#pragma unroll
-        for (int q = 0; q < K; ++q)
-            r[q] ^= d.xor_io;
-    };
-    auto store = [&](const uint32_t (&r)[K], const M64Pos &p) {
-        if (nostore) {
-#pragma unroll
-            for (int q = 0; q < K; ++q)
-                sink ^= r[q];
-            return;
-        }
         uint32_t *out = m.out[p.b];
         uint64_t r0 = p.k * RPC + (uint64_t)lane;
         if (d.opt & 262144) /* diagnostic: results into one L2-resident 64 KiB window (wrong results) */
             r0 &= 16383;
 #pragma unroll
-        for (int q = 0; q < K; ++q)
-            if (r0 + 64 * q < n)
-                out[r0 + 64 * q] = r[q];
-    };
-    auto hash = [&](uint32_t (&w)[16 * K], const M64Pos &p) {
-        uint32_t r[K];
-        hash_r(w, r);
-        store(r, p);
-    };
-    if (deal && DEFER) {
-        /* results of the chunk hashed last (ra / pa, rb / pb) stored after
-         * the next chunk's loads are issued */
-        M64Pos pn, pa, pb;
-        uint32_t ra[K], rb[K];
-        bool have_b = false;
-        while (ph.b < m.nb) {
-            deal_advance(pn);
-            m64_issue<K>(m, n, pn, voff, dummy, b1);
-            if (have_b)
-                store(rb, pb);
-            hash_r(b0, ra);
-            pa = ph;
-            ph = pn;
-            if (ph.b >= m.nb) {
-                store(ra, pa);
-                have_b = false;
-                break;
+        for (int q = 0; q < K; ++q) {
+            if (GUARD) {
+                if (r0 + 64 * q < n)
+                    out[r0 + 64 * q] = r[q] ^ d.xor_io;
+            } else {
+                uint32_t *at = r0 + 64 * q < n ? out + r0 + 64 * q : m.sink + lane;
+                *at = r[q] ^ d.xor_io;
             }
-            deal_advance(pn);
-            m64_issue<K>(m, n, pn, voff, dummy, b0);
-            store(ra, pa);
-            hash_r(b1, rb);
-            pb = ph;
-            have_b = true;
-            ph = pn;
         }
-        if (have_b)
-            store(rb, pb);
-    } else if (deal) {
+    };
+    if (deal) {
         M64Pos pn;
         while (ph.b < m.nb) {
             deal_advance(pn);
@@ -2277,22 +2237,20 @@ __global__ __launch_bounds__(WG) void multi64_kernel(BatchDesc d, MultiBatch m, 
             hash(b1, ph);
             ph = pn;
         }
-    } else {
-        while (ph.b < m.nb) {
-            advance(pl);
-            m64_issue<K>(m, n, pl, voff, dummy, b1);
-            hash(b0, ph);
-            advance(ph);
-            if (ph.b >= m.nb)
-                break;
-            advance(pl);
-            m64_issue<K>(m, n, pl, voff, dummy, b0);
-            hash(b1, ph);
-            advance(ph);
-        }
+        return;
     }
-    if (nostore)
-        m.out[0][(wave * 64 + (uint64_t)lane) % n] = sink;
+    while (ph.b < m.nb) {
+        advance(pl);
+        m64_issue<K>(m, n, pl, voff, dummy, b1);
+        hash(b0, ph);
+        advance(ph);
+        if (ph.b >= m.nb)
+            break;
+        advance(pl);
+        m64_issue<K>(m, n, pl, voff, dummy, b0);
+        hash(b1, ph);
+        advance(ph);
+    }
 }
 
 /*
@@ -4420,15 +4378,16 @@ __global__ __launch_bounds__(256) void part_fold_kernel(FoldPair fp, const uint3
 }
 
 /* ------------------------------------------------ the writer's second pass */
-/* The in-place commit writer as two passes (round 5): commit_kernel computes
- * every CRC into crc[] without touching the image (commit mode 4: status 1 a
- * short commit record, 3 a long one, 2 none), then this kernel stores each
- * one big-endian into its record's CRC field (+4 short, +20 long,
- * src/zeroskip-file.c:303-328 / :266-302).  Writing the fields from inside
- * the read stream cost 0.42 ms of config 4's writer (scattered
- * 4-byte stores, one 32-byte sector each, stalling the loads); here they come
- * after every read, from coalesced reads of the descriptors and CRCs.
- * user_status (may be NULL): the caller's status array, 1 written / 2 none. */
+/* The in-place commit writer as two passes (round 5, tuning bit 512):
+ * commit_kernel computes every CRC into crc[] without touching the image
+ * (commit mode 4: status 1 a short commit record, 3 a long one, 2 none),
+ * then this kernel stores each one big-endian into its record's CRC field
+ * (+4 short, +20 long, src/zeroskip-file.c:303-328 / :266-302), after every
+ * read, from coalesced reads of the descriptors and CRCs.  Measured against
+ * the stores from inside the read pass: 1.025 vs 0.977 ms on config 4 -- the
+ * scatter alone ~0.485 ms, the ten million partial-sector writes cost the
+ * same wherever they are issued.  user_status (may be
+ * NULL): the caller's status array, 1 written / 2 none. */
 __global__ __launch_bounds__(256) void commit_scatter_kernel(uint8_t *base, const uint64_t *__restrict__ off,
                                                              const uint64_t *__restrict__ len,
                                                              const uint32_t *__restrict__ crc,
@@ -4776,10 +4735,10 @@ extern "C" int zs_launch_multi(const zs::BatchDesc *d, const zs::MultiBatch *m, 
         packed64 = (reinterpret_cast<uintptr_t>(m->base[b]) & 15) == 0;
     if (packed64 && (d->opt & (1u << 21))) /* A/B: results staged per group of chunks */
         hipLaunchKernelGGL(zs::multi64d_kernel, dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
-    else if (packed64 && (d->opt & 128u)) /* A/B: results stored right after their hash (round 4) */
-        hipLaunchKernelGGL((zs::multi64_kernel<2, false>), dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
-    else if (packed64) /* two chains per lane (three measured slower: VGPR spills) */
+    else if (packed64 && (d->opt & 128u)) /* A/B: round 4's guarded result stores */
         hipLaunchKernelGGL((zs::multi64_kernel<2, true>), dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
+    else if (packed64) /* two chains per lane (three measured slower: VGPR spills) */
+        hipLaunchKernelGGL((zs::multi64_kernel<2, false>), dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
     else
         hipLaunchKernelGGL(zs::multi_kernel, dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
     return hipGetLastError() == hipSuccess ? 0 : -3;
