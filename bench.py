@@ -880,17 +880,34 @@ def run_config5(args, world, rank, dev, stream):
     t_open = time.perf_counter() - t0
     job.prepare()
 
+    # the native pass pipelined (zscrc_cpass_submit / _collect): step k
+    # enqueues pass k and reads pass k - 1's block while the device runs pass
+    # k, so the host's reading and the next launches stay off the device's
+    # critical path; every pass is collected and checked inside the timed
+    # region (drain).  BENCH_C5_SYNC=1: one synchronous pass per step.
+    pipelined = os.environ.get("BENCH_C5_SYNC") != "1"
+    reports = []
+
     def step(ev):
-        rep = job.run(events=ev)
-        step.rep = rep
+        if not pipelined or not job.submit(ev):
+            reports.append(job.run(events=ev))
+            return
+        if job.pending() > 1:
+            reports.append(job.collect())
+
+    def drain():
+        while job.pending():
+            reports.append(job.collect())
 
     probe = torch.empty(4 << 30, dtype=torch.uint8, device=dev)
     read_peak = read_ceiling(probe, probe.numel(), stream)   # also settles power (run_config3)
     del probe
     tm = Timer(world, dev)
-    elapsed = tm.run(step, args.steps, args.warmup)
-    rep = step.rep
-    assert rep.ok and rep.n_stale == args.finalised, (rep.ok, rep.n_bad, rep.n_stale, rep.walk_errors[:5])
+    elapsed = tm.run(step, args.steps, args.warmup, drain=drain)
+    assert len(reports) == args.steps + args.warmup, (len(reports), args.steps, args.warmup)
+    for rep in reports:
+        assert rep.ok and rep.n_stale == args.finalised, (rep.ok, rep.n_bad, rep.n_stale, rep.walk_errors[:5])
+    rep = reports[-1]
     # the checker over the whole DB (rank 0; every rank holds the same images)
     parity = oracle_check_db(job.db, args.finalised) if rank == 0 else None
     if parity and parity["mismatches"]:
@@ -914,6 +931,9 @@ def run_config5(args, world, rank, dev, stream):
                     device_pass={"verified_spans": len(job.c_off), "longest_verified_span": job.c_max,
                                  "raw_spans": [q[3] - q[2] for q in job.pieces][:16]},
                     run_timing={k: round(v, 5) for k, v in rep.timing.items()},
+                    passes={"checked": len(reports), "pipelined": bool(pipelined and job._cpass is not None),
+                            "note": "every pass's report collected and checked inside the timed region; "
+                                    "pipelined: pass k's copy back read while pass k + 1 runs"},
                     gen_s=round(t_gen, 2), open_s=round(t_open, 2))
     if rank == 0 and world == 1 and not args.no_cpu:
         # 64 finalised files' commit spans + 768 MiB of a packed records region

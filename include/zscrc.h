@@ -476,6 +476,14 @@ int zscrc_cpass_run(zscrc_cpass *p, void *stream, zscrc_cpass_result *res);
  * is enqueued -- the device's part of the pass, without the host's wait. */
 int zscrc_cpass_run_timed(zscrc_cpass *p, void *stream, void *start_event, void *end_event,
                           zscrc_cpass_result *res);
+/* The pass in two halves, so the host's reading of pass k overlaps the
+ * device's pass k + 1: submit enqueues everything on `stream` (events as
+ * zscrc_cpass_run_timed) with the copy back into host slot `slot` (0 or 1)
+ * and returns at once; collect waits for that slot's copy and fills `res`.
+ * A slot holds one submitted pass until it is collected (ZSCRC_EINVAL
+ * otherwise).  Passes on one stream run in order. */
+int zscrc_cpass_submit(zscrc_cpass *p, void *stream, void *start_event, void *end_event, int slot);
+int zscrc_cpass_collect(zscrc_cpass *p, int slot, zscrc_cpass_result *res);
 void zscrc_cpass_destroy(zscrc_cpass *p);
 
 /* End to end from host memory: every CRC of n zeroskip file images (mmap'd

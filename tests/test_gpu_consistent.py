@@ -261,3 +261,41 @@ def test_eight_slots_config5_shape(gpu, tmp_path):
 def oracle_region_len(img) -> int:
     from oracle import oracle
     return oracle.packed_image(img)["records"]["span_len"]
+
+
+def test_pipelined_passes(gpu):
+    """zscrc_cpass_submit / _collect (bench config 5's pipelined steps): up to
+    two passes in flight in two host slots, collected in order, each report
+    the same as a synchronous pass's -- and a corruption made on the device
+    between two submits shows in the second report only."""
+    db = small_db(long_region=True)
+    job = cs.Consistent(cs.open_db(db), 0, 1).prepare()
+    assert job._cpass is not None
+    want = job.run()
+    assert want.ok and len(want.stale_empty_commits) == 3
+    reps = []
+    for k in range(7):
+        assert job.submit()
+        if job.pending() > 1:
+            reps.append(job.collect())
+    while job.pending():
+        reps.append(job.collect())
+    assert len(reps) == 7 and all(same(r, want) for r in reps)
+    with pytest.raises(RuntimeError):
+        job.submit(), job.submit(), job.submit()
+    while job.pending():
+        job.collect()
+    # a commit span flipped on the device after pass 1 is submitted: pass 1
+    # clean (stream order: the flip runs after it), pass 2 reports it
+    f = name(7, 7)
+    fid = [i for i, x in enumerate(job.db.files) if x.name == f][0]
+    c = zf.walk(bytearray(db[f]))[0][9]
+    assert job.submit()
+    where = job.dev_offset(fid, c["span_off"] + 1)
+    job.buf[where] ^= 0x40
+    assert job.submit()
+    r1, r2 = job.collect(), job.collect()
+    assert r1.ok and same(r1, want)
+    assert not r2.ok and r2.bad_commits == [(f, c["commit_off"])]
+    job.buf[where] ^= 0x40
+    assert job.run().ok

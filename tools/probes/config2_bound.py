@@ -6,6 +6,7 @@ the same-GPU streaming read of the same 4 GiB:
                batch's end to a sink word)
   128          round 4's guarded stores (the compiler drained them with
                vmcnt(0) before every other chunk's loads)
+  64           unconditional non-temporal result stores
   1<<20        no hashing (diagnostic)
   262144       result stores into one L2-resident window (diagnostic)
 (round 5's first probe also had bit 64: no result stores -- 0.609 ms against
@@ -23,7 +24,7 @@ from zeroskip_amd._lib import check, lib  # noqa: E402
 
 
 def main():
-    opts = [int(x) for x in sys.argv[1:]] or [0, 128, 1 << 20, 262144]
+    opts = [int(x) for x in sys.argv[1:]] or [0, 128, 64, 1 << 20, 262144]
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev)
     g.manual_seed(0x64)

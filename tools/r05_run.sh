@@ -32,6 +32,9 @@ for step in "$@"; do
     ab4w)     AB_CASES=config4_write_nocrc,config4_write,config4_crcs timeout -k 10 600 python tools/opt_ab.py 0 512 \
                 > gpurun_out/ab4w.jsonl 2> gpurun_out/ab4w.err ;;
     cwtests)  timeout -k 10 600 $T tests/test_gpu_cpu_written.py tests/test_gpu_fill.py > gpurun_out/cwtests.log 2>&1 ;;
+    bench5sync) BENCH_C5_SYNC=1 timeout -k 10 600 python bench.py --workload config5 --no-cpu >> gpurun_out/bench5sync.jsonl \
+                2>> gpurun_out/bench5sync.err ;;
+    cstests)  timeout -k 10 600 $T tests/test_gpu_consistent.py > gpurun_out/cstests.log 2>&1 ;;
     cputhreads) timeout -k 10 300 python tools/probes/cpu_threads.py > gpurun_out/cpu_threads.jsonl \
                 2> gpurun_out/cpu_threads.err ;;
     ab3)      AB_CASES=config3,fixed_16KiB,fixed_4KiB,fixed_1MiB timeout -k 10 600 python tools/opt_ab.py 0 32 \

@@ -423,6 +423,7 @@ class Consistent:
             slots.append((u, u.lo, hi, pos))
             pos += -(-(hi - u.lo) // SLOT_ALIGN) * SLOT_ALIGN
         self.buf = be.empty(pos)
+        self._slots = slots
         pinned = None
         if any(db.files[u.fid].dev is None for u, *_ in slots) and self.buf.is_cuda:
             pinned = torch.empty(max(pos, 1), dtype=torch.uint8, pin_memory=True)
@@ -507,6 +508,14 @@ class Consistent:
                 and len(pieces) <= CPASS_SPANS:
             self._make_cpass(slots)
         return self
+
+    def dev_offset(self, fid: int, off: int) -> int:
+        """Where byte `off` of file `fid` sits in this rank's device buffer
+        (KeyError: not in this rank's share)."""
+        for u, lo, hi, p in self._slots:
+            if u.fid == fid and lo <= off < hi:
+                return p + off - lo
+        raise KeyError((fid, off))
 
     def _make_cpass(self, slots):
         """The device pass as one C call (zscrc_cpass): verdict batch, raw
@@ -593,13 +602,60 @@ class Consistent:
         # the events are that device's (zscrc_cpass_run_timed records the end
         # event before its host-side wait)
         with torch.cuda.device(dev):
-            ev = (None, None)
-            if events:
-                for e in events:          # torch creates its events lazily, on the first record
-                    e.record(stream)
-                ev = (ctypes.c_void_p(events[0].cuda_event), ctypes.c_void_p(events[1].cuda_event))
+            ev = self._c_events(events, stream)
             check(lib().zscrc_cpass_run_timed(self._cpass, ctypes.c_void_p(stream.cuda_stream), ev[0], ev[1],
                                               ctypes.byref(res)), "zscrc_cpass_run_timed")
+        return self._native_report(res, t0)
+
+    @staticmethod
+    def _c_events(events, stream):
+        if not events:
+            return (None, None)
+        for e in events:          # torch creates its events lazily, on the first record
+            e.record(stream)
+        return (ctypes.c_void_p(events[0].cuda_event), ctypes.c_void_p(events[1].cuda_event))
+
+    # ------------------------------------------------ pipelined native passes
+    def submit(self, events=None) -> bool:
+        """Enqueue one native pass (zscrc_cpass_submit) into the next of two
+        host slots and return at once, so the host reads pass k while the
+        device runs pass k + 1; collect() returns the passes' reports in
+        submission order.  False (nothing enqueued): no native pass here."""
+        from ._lib import check, lib
+        if self._cpass is None:
+            return False
+        if not hasattr(self, "_inflight"):
+            self._inflight, self._next_slot = [], 0
+            self._cres_slot = (CPassResult(), CPassResult())
+        slot = self._next_slot
+        if slot in self._inflight:
+            raise RuntimeError("both host slots hold uncollected passes")
+        dev = self.buf.device
+        stream = torch.cuda.current_stream(dev)
+        with torch.cuda.device(dev):
+            ev = self._c_events(events, stream)
+            check(lib().zscrc_cpass_submit(self._cpass, ctypes.c_void_p(stream.cuda_stream), ev[0], ev[1], slot),
+                  "zscrc_cpass_submit")
+        self._inflight.append((slot, time.perf_counter()))
+        self._next_slot ^= 1
+        return True
+
+    def pending(self) -> int:
+        return len(getattr(self, "_inflight", []))
+
+    def collect(self) -> Report:
+        """The report of the oldest submitted pass (waits for its copy back).
+        A pass that left commits undecided is decided by the torch path (a
+        synchronous pass of its own)."""
+        from ._lib import check, lib
+        slot, t0 = self._inflight.pop(0)
+        res = self._cres_slot[slot]
+        with torch.cuda.device(self.buf.device):
+            check(lib().zscrc_cpass_collect(self._cpass, slot, ctypes.byref(res)), "zscrc_cpass_collect")
+        rep = self._native_report(res, t0)
+        return rep if rep is not None else self._run_torch()
+
+    def _native_report(self, res, t0):
         if res.n_undecided or not res.complete:
             return None
         t_dev = time.perf_counter()

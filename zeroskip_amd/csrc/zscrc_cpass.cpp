@@ -46,7 +46,9 @@ struct zscrc_cpass {
      * (written by the post kernel) -- the block goes back to the host every
      * pass */
     uint8_t *dblk = nullptr;
-    uint8_t *hblk = nullptr;
+    uint8_t *hblk = nullptr;   /* NSLOT host blocks (zscrc_cpass_submit / _collect) */
+    hipEvent_t done[2] = {};   /* each slot's copy back */
+    bool pending[2] = {};
     uint64_t *dbad_full = nullptr; /* the verdict's list (cap entries) */
     uint64_t cap = 0;
     int64_t *dspan_commit = nullptr;
@@ -61,8 +63,15 @@ namespace {
 constexpr size_t OFF_RAW = 16, OFF_ST = OFF_RAW + 4 * zs::CPASS_SPANS, OFF_FLAGS = OFF_ST + 4 * zs::CPASS_SPANS,
                  OFF_BAD = OFF_FLAGS + 4 * LIST_CAP, BLK = OFF_BAD + 8 * LIST_CAP;
 
+constexpr int NSLOT = 2;
+
 void cpass_free(zscrc_cpass *p)
 {
+    for (hipEvent_t &e : p->done)
+        if (e) {
+            (void)hipEventSynchronize(e);
+            (void)hipEventDestroy(e);
+        }
     if (p->dblk)
         (void)hipFree(p->dblk);
     if (p->hblk)
@@ -108,7 +117,9 @@ extern "C" int zscrc_cpass_create(zscrc_cpass **out, const zscrc_cpass_spec *spe
         init[k] = zs_gf2_mul(0xFFFFFFFFu, zs_gf2_xpow8n(p->span_len[k]));
     hipError_t e = hipMalloc(&p->dblk, BLK);
     if (e == hipSuccess)
-        e = hipHostMalloc(reinterpret_cast<void **>(&p->hblk), BLK, hipHostMallocDefault);
+        e = hipHostMalloc(reinterpret_cast<void **>(&p->hblk), NSLOT * BLK, hipHostMallocDefault);
+    for (int k = 0; k < NSLOT && e == hipSuccess; ++k)
+        e = hipEventCreateWithFlags(&p->done[k], hipEventDisableTiming);
     if (e == hipSuccess)
         e = hipMalloc(&p->dbad_full, 8 * p->cap);
     if (e == hipSuccess)
@@ -130,7 +141,26 @@ extern "C" int zscrc_cpass_create(zscrc_cpass **out, const zscrc_cpass_spec *spe
 
 namespace {
 
-int cpass_run(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1, zscrc_cpass_result *res);
+int cpass_submit(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1, int slot);
+int cpass_collect(zscrc_cpass *p, int slot, zscrc_cpass_result *res);
+
+/* the pass runs on the device it was created on (its buffers and the
+ * operator table the kernels read are that device's), whatever device the
+ * caller has current; the caller's device is restored */
+struct OnDevice {
+    int cur = -1;
+    int dev;
+    bool ok;
+    explicit OnDevice(int d) : dev(d)
+    {
+        ok = hipGetDevice(&cur) == hipSuccess && (cur == dev || hipSetDevice(dev) == hipSuccess);
+    }
+    ~OnDevice()
+    {
+        if (ok && cur != dev)
+            (void)hipSetDevice(cur);
+    }
+};
 
 } /* namespace */
 
@@ -144,22 +174,46 @@ extern "C" int zscrc_cpass_run_timed(zscrc_cpass *p, void *stream, void *start_e
 {
     if (!p || !res)
         return ZSCRC_EINVAL;
-    /* the pass runs on the device it was created on (its buffers and the
-     * operator table the kernels read are that device's), whatever device
-     * the caller has current; the caller's device is restored */
-    int cur = -1;
-    if (hipGetDevice(&cur) != hipSuccess || (cur != p->dev && hipSetDevice(p->dev) != hipSuccess))
+    OnDevice od(p->dev);
+    if (!od.ok)
         return ZSCRC_EHIP;
-    const int rc = cpass_run(p, static_cast<hipStream_t>(stream), static_cast<hipEvent_t>(start_event),
-                             static_cast<hipEvent_t>(end_event), res);
-    if (cur != p->dev)
-        (void)hipSetDevice(cur);
-    return rc;
+    /* a synchronous pass takes a free slot; one still holding an uncollected
+     * pass is collected first (its result dropped) */
+    const int slot = p->pending[0] && !p->pending[1] ? 1 : 0;
+    zscrc_cpass_result tmp;
+    if (p->pending[slot])
+        (void)cpass_collect(p, slot, &tmp);
+    const int rc = cpass_submit(p, static_cast<hipStream_t>(stream), static_cast<hipEvent_t>(start_event),
+                                static_cast<hipEvent_t>(end_event), slot);
+    return rc ? rc : cpass_collect(p, slot, res);
+}
+
+extern "C" int zscrc_cpass_submit(zscrc_cpass *p, void *stream, void *start_event, void *end_event, int slot)
+{
+    if (!p || slot < 0 || slot >= NSLOT || p->pending[slot])
+        return ZSCRC_EINVAL;
+    OnDevice od(p->dev);
+    if (!od.ok)
+        return ZSCRC_EHIP;
+    return cpass_submit(p, static_cast<hipStream_t>(stream), static_cast<hipEvent_t>(start_event),
+                        static_cast<hipEvent_t>(end_event), slot);
+}
+
+extern "C" int zscrc_cpass_collect(zscrc_cpass *p, int slot, zscrc_cpass_result *res)
+{
+    if (!p || !res || slot < 0 || slot >= NSLOT || !p->pending[slot])
+        return ZSCRC_EINVAL;
+    OnDevice od(p->dev);
+    if (!od.ok)
+        return ZSCRC_EHIP;
+    return cpass_collect(p, slot, res);
 }
 
 namespace {
 
-int cpass_run(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1, zscrc_cpass_result *res)
+/* Enqueue one pass on s: the verdict batch, the raw spans, the post kernel
+ * and the copy of the small block into host slot `slot`; nothing waits. */
+int cpass_submit(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1, int slot)
 {
     if (ev0 && hipEventRecord(ev0, s) != hipSuccess)
         return ZSCRC_EHIP;
@@ -214,21 +268,34 @@ int cpass_run(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1, zsc
     }
     /* the post kernel wrote the listed part of the verdict next to the
      * counters: one copy back (two device-to-device copies of the lists
-     * before it cost a launch each) */
-    if (!rc && hipMemcpyAsync(p->hblk, p->dblk, BLK, hipMemcpyDeviceToHost, s) != hipSuccess)
+     * before it cost a launch each).  The next pass on this stream rewrites
+     * the device block only after this copy (stream order), so two passes
+     * can be in flight with their host slots apart. */
+    if (!rc && hipMemcpyAsync(p->hblk + slot * BLK, p->dblk, BLK, hipMemcpyDeviceToHost, s) != hipSuccess)
         rc = ZSCRC_EHIP;
     /* the end event right behind the copy back: the device's part of the
-     * pass, without the host's wait and the list sorting below */
+     * pass, without the host's wait and the list sorting */
     if (!rc && ev1 && hipEventRecord(ev1, s) != hipSuccess)
         rc = ZSCRC_EHIP;
-    if (!rc && hipStreamSynchronize(s) != hipSuccess)
+    if (!rc && hipEventRecord(p->done[slot], s) != hipSuccess)
         rc = ZSCRC_EHIP;
-    if (rc)
-        return rc;
-    const uint64_t nbad = reinterpret_cast<const uint64_t *>(p->hblk)[0];
-    const uint64_t nstale = reinterpret_cast<const uint64_t *>(p->hblk)[1];
-    const uint32_t *flags = reinterpret_cast<const uint32_t *>(p->hblk + OFF_FLAGS);
-    const uint64_t *bad = reinterpret_cast<const uint64_t *>(p->hblk + OFF_BAD);
+    if (!rc)
+        p->pending[slot] = true;
+    return rc;
+}
+
+/* Wait for slot's copy back and read its block. */
+int cpass_collect(zscrc_cpass *p, int slot, zscrc_cpass_result *res)
+{
+    p->pending[slot] = false;
+    if (hipEventSynchronize(p->done[slot]) != hipSuccess)
+        return ZSCRC_EHIP;
+    const zscrc_cpass_spec &sp = p->spec;
+    const uint8_t *blk = p->hblk + slot * BLK;
+    const uint64_t nbad = reinterpret_cast<const uint64_t *>(blk)[0];
+    const uint64_t nstale = reinterpret_cast<const uint64_t *>(blk)[1];
+    const uint32_t *flags = reinterpret_cast<const uint32_t *>(blk + OFF_FLAGS);
+    const uint64_t *bad = reinterpret_cast<const uint64_t *>(blk + OFF_BAD);
     memset(res, 0, sizeof *res);
     const uint64_t nl = std::min<uint64_t>(nbad, LIST_CAP);
     res->complete = nbad <= LIST_CAP;
@@ -247,8 +314,8 @@ int cpass_run(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1, zsc
     std::copy(st.begin(), st.begin() + res->n_listed_stale, res->stale);
     for (size_t k = 0; k < und.size() && k < ZSCRC_CPASS_SPANS; ++k)
         res->undecided[k] = und[k];
-    memcpy(res->span_raw, p->hblk + OFF_RAW, 4 * sp.nspans);
-    memcpy(res->span_status, p->hblk + OFF_ST, 4 * sp.nspans);
+    memcpy(res->span_raw, blk + OFF_RAW, 4 * sp.nspans);
+    memcpy(res->span_status, blk + OFF_ST, 4 * sp.nspans);
     return ZSCRC_OK;
 }
 

@@ -2117,9 +2117,10 @@ __device__ __forceinline__ void m64_issue(const MultiBatch &m, uint64_t n, const
  * s_waitcnt vmcnt(0): every chunk drained the wave's result stores before its
  * loads went out (ISA of round 4's build).  Without result stores the launch
  * takes 0.609 against 0.818 ms (64 x 64 MiB, profiles/r05/config2/
- * bound_probe.jsonl), the same-GPU streaming read 0.618.  GUARD = true
- * (tuning bit 128): round 4's guarded stores. */
-template <int K, bool GUARD>
+ * bound_probe.jsonl), the same-GPU streaming read 0.618.  GUARD = 1
+ * (tuning bit 128): round 4's guarded stores; 2 (bit 64): unconditional
+ * non-temporal stores. */
+template <int K, int GUARD>
 __global__ __launch_bounds__(WG) void multi64_kernel(BatchDesc d, MultiBatch m, const uint32_t *__restrict__ gtab)
 {
     __shared__ __attribute__((aligned(16))) char L[OFF_U];
@@ -2214,12 +2215,15 @@ __global__ __launch_bounds__(WG) void multi64_kernel(BatchDesc d, MultiBatch m, 
             r0 &= 16383;
 #pragma unroll
         for (int q = 0; q < K; ++q) {
-            if (GUARD) {
+            if (GUARD == 1) {
                 if (r0 + 64 * q < n)
                     out[r0 + 64 * q] = r[q] ^ d.xor_io;
             } else {
                 uint32_t *at = r0 + 64 * q < n ? out + r0 + 64 * q : m.sink + lane;
-                *at = r[q] ^ d.xor_io;
+                if (GUARD == 2)
+                    __builtin_nontemporal_store(r[q] ^ d.xor_io, at);
+                else
+                    *at = r[q] ^ d.xor_io;
             }
         }
     };
@@ -4736,9 +4740,11 @@ extern "C" int zs_launch_multi(const zs::BatchDesc *d, const zs::MultiBatch *m, 
     if (packed64 && (d->opt & (1u << 21))) /* A/B: results staged per group of chunks */
         hipLaunchKernelGGL(zs::multi64d_kernel, dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
     else if (packed64 && (d->opt & 128u)) /* A/B: round 4's guarded result stores */
-        hipLaunchKernelGGL((zs::multi64_kernel<2, true>), dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
+        hipLaunchKernelGGL((zs::multi64_kernel<2, 1>), dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
+    else if (packed64 && (d->opt & 64u)) /* A/B: non-temporal result stores */
+        hipLaunchKernelGGL((zs::multi64_kernel<2, 2>), dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
     else if (packed64) /* two chains per lane (three measured slower: VGPR spills) */
-        hipLaunchKernelGGL((zs::multi64_kernel<2, false>), dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
+        hipLaunchKernelGGL((zs::multi64_kernel<2, 0>), dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
     else
         hipLaunchKernelGGL(zs::multi_kernel, dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
     return hipGetLastError() == hipSuccess ? 0 : -3;
