@@ -686,7 +686,7 @@ def run_config4(args, world, rank, dev, stream):
         nb_arr["crc"], nb_arr["st"] = zsfile.verify_commits(img_nb.view(-1), o_nb, l_nb)
     # interleaved, so no form sees a different power / clock state; blocks of
     # 20 calls (6 could not resolve the forms' ~13 us difference,
-    # tools/nb_forms.py)
+    # tools/probes/nb_forms.py)
     nb_ms, nb_unranged_ms, nb_arrays_ms = _timed_ab([nb_verdict, nb_verdict_unranged, nb_arrays], 20, stream,
                                                     rounds=5)
     nb_verdict()

@@ -31,16 +31,16 @@ for step in "$@"; do
                 2> gpurun_out/box4.err && bash tools/pmc_case.sh config4 ;;
     pmc2box)  timeout -k 10 180 python -c "import json, bench; print(json.dumps(bench.box_info(0)))" > gpurun_out/box.json \
                 2> gpurun_out/box.err && bash tools/pmc_case.sh config2 && bash tools/pmc_case.sh config3 ;;
-    nbseq)    bash tools/nb_seq.sh ;;
-    nbforms)  timeout -k 10 300 python tools/nb_forms.py > gpurun_out/nb_forms.json 2> gpurun_out/nb_forms.err ;;
+    nbseq)    bash tools/probes/nb_seq.sh ;;
+    nbforms)  timeout -k 10 300 python tools/probes/nb_forms.py > gpurun_out/nb_forms.json 2> gpurun_out/nb_forms.err ;;
     nbmix)    ( cd /tmp && export TMPDIR=/tmp && C4NB_MODE=mixed timeout -k 10 300 rocprofv3 --kernel-trace --stats \
                 --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/nbmix -o run -- \
                 python3 $GRAFT_REPO_ROOT/tools/prof_case.py config4nb 90 > $GRAFT_REPO_ROOT/gpurun_out/nbmix.log 2>&1 ) && \
-              python tools/nb_mixed_summary.py gpurun_out/nbmix 15 > gpurun_out/nbmix.json ;;
-    cphases)  timeout -k 10 300 python tools/classify_phases.py > gpurun_out/classify_phases.jsonl \
+              python tools/probes/nb_mixed_summary.py gpurun_out/nbmix 15 > gpurun_out/nbmix.json ;;
+    cphases)  timeout -k 10 300 python tools/probes/classify_phases.py > gpurun_out/classify_phases.jsonl \
                 2> gpurun_out/classify_phases.err ;;
-    xdeal)    timeout -k 10 600 python tools/xdeal_ab.py > gpurun_out/xdeal_ab.jsonl 2> gpurun_out/xdeal_ab.err ;;
-    xdealnb)  XD_NB=1 timeout -k 10 600 python tools/xdeal_ab.py 0 2 4 8 16 > gpurun_out/xdeal_nb.jsonl \
+    xdeal)    timeout -k 10 600 python tools/probes/xdeal_ab.py > gpurun_out/xdeal_ab.jsonl 2> gpurun_out/xdeal_ab.err ;;
+    xdealnb)  XD_NB=1 timeout -k 10 600 python tools/probes/xdeal_ab.py 0 2 4 8 16 > gpurun_out/xdeal_nb.jsonl \
                 2> gpurun_out/xdeal_nb.err ;;
     abnb)     AB_CASES=config4_nb timeout -k 10 600 python tools/opt_ab.py 0 67108864 \
                 > gpurun_out/abnb.jsonl 2> gpurun_out/abnb.err ;;
@@ -52,7 +52,7 @@ for step in "$@"; do
     traffic45) bash tools/pmc_traffic.sh config4 5 && bash tools/pmc_traffic.sh config4w 5 && bash tools/pmc_traffic.sh config5 5 ;;
     spantests) timeout -k 10 600 $T tests/test_gpu_stream.py tests/test_gpu_parity.py -k "span" \
                 > gpurun_out/spantests.log 2>&1 ;;
-    fillsweep) timeout -k 10 600 python tools/fill_sweep.py > gpurun_out/fill_sweep.jsonl 2> gpurun_out/fill_sweep.err ;;
+    fillsweep) timeout -k 10 600 python tools/probes/fill_sweep.py > gpurun_out/fill_sweep.jsonl 2> gpurun_out/fill_sweep.err ;;
     rehearse3)
               BENCH_SHARE_GPU=1 BENCH_DIST=gloo timeout -k 10 600 python bench.py --gpus 2 --workload config3 \
                 --no-cpu > gpurun_out/rehearse3_n2.json 2> gpurun_out/rehearse3_n2.err ;;
@@ -63,7 +63,7 @@ for step in "$@"; do
               BENCH_SHARE_GPU=1 BENCH_DIST=gloo timeout -k 10 900 python bench.py --gpus 8 --workload config5 \
                 --no-cpu --packed-mib 1024 --finalised 256 > gpurun_out/rehearse5_n8.json \
                 2> gpurun_out/rehearse5_n8.err ;;
-    cwaves)   timeout -k 10 600 python tools/commit_waves.py > gpurun_out/commit_waves.jsonl 2> gpurun_out/commit_waves.err ;;
+    cwaves)   timeout -k 10 600 python tools/probes/commit_waves.py > gpurun_out/commit_waves.jsonl 2> gpurun_out/commit_waves.err ;;
     ab4split) AB_CASES=config4_verdict,config4_crcs,config4_write,config4_verify timeout -k 10 600 python tools/opt_ab.py \
                 0 536870912 > gpurun_out/ab4split.jsonl 2> gpurun_out/ab4split.err ;;
     ab4inl)   AB_CASES=config4_verdict,config4_crcs,config4_write,config4_verify timeout -k 10 600 python tools/opt_ab.py \
@@ -97,7 +97,7 @@ for step in "$@"; do
                 --no-e2e --no-cpu >> gpurun_out/bench4h.jsonl 2> gpurun_out/bench4h.err ;;
     ab4steal) AB_CASES=config4_verdict,config4_crcs,config4_write,config4_verify timeout -k 10 600 python tools/opt_ab.py \
                 0 512 16384 > gpurun_out/ab4steal.jsonl 2> gpurun_out/ab4steal.err ;;
-    cwavesb)  timeout -k 10 600 python tools/commit_waves.py base > gpurun_out/commit_waves_base.jsonl 2> gpurun_out/commit_waves.err ;;
+    cwavesb)  timeout -k 10 600 python tools/probes/commit_waves.py base > gpurun_out/commit_waves_base.jsonl 2> gpurun_out/commit_waves.err ;;
     ab4ro)    AB_CASES=config4_verdict,config4_crcs,config4_write,config4_verify timeout -k 10 600 python tools/opt_ab.py \
                 0 2147483648 536870912 > gpurun_out/ab4ro.jsonl 2> gpurun_out/ab4ro.err ;;
     ab4)      AB_CASES=config4_verdict,config4_write,config4_crcs timeout -k 10 600 python tools/opt_ab.py 0 4194304 \
@@ -106,13 +106,13 @@ for step in "$@"; do
                 > gpurun_out/ab3.jsonl 2> gpurun_out/ab3.err ;;
     ab3p)     for P in 8 32; do ZSCRC_QDYN_P=$P AB_CASES=config3 timeout -k 10 300 python tools/opt_ab.py 0 16777216 \
                 || exit $?; done > gpurun_out/ab3p.jsonl 2> gpurun_out/ab3p.err ;;
-    spreadq)  WS_OPT=16777216 timeout -k 10 600 python tools/wave_spread.py > gpurun_out/wave_spread_q.jsonl \
+    spreadq)  WS_OPT=16777216 timeout -k 10 600 python tools/probes/wave_spread.py > gpurun_out/wave_spread_q.jsonl \
                 2> gpurun_out/wave_spread_q.err ;;
     ab2)      AB_CASES=config2_multi32 timeout -k 10 600 python tools/opt_ab.py 0 8388608 2097152 \
                 > gpurun_out/ab2.jsonl 2> gpurun_out/ab2.err ;;
     pmc4crcs) C4_CRCS=1 bash tools/pmc_traffic.sh config4w 5 ;;
-    spread)   timeout -k 10 600 python tools/wave_spread.py > gpurun_out/wave_spread.jsonl 2> gpurun_out/wave_spread.err ;;
-    crossover) timeout -k 10 600 python tools/crossover.py > gpurun_out/crossover.jsonl 2> gpurun_out/crossover.err ;;
+    spread)   timeout -k 10 600 python tools/probes/wave_spread.py > gpurun_out/wave_spread.jsonl 2> gpurun_out/wave_spread.err ;;
+    crossover) timeout -k 10 600 python tools/probes/crossover.py > gpurun_out/crossover.jsonl 2> gpurun_out/crossover.err ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   rc=$?

@@ -70,7 +70,7 @@ std::atomic<uint64_t> g_stat[4];
  * of at least g_gpu_min bytes goes to the GPU once this process has a device
  * context (warm), at least g_gpu_min_cold before (the first offloaded call
  * pays HIP init, ~0.1-0.2 s).  Defaults are the crossovers measured against
- * one CPU core on a pageable buffer (tools/crossover.py,
+ * one CPU core on a pageable buffer (tools/probes/crossover.py,
  * profiles/r04/crossover.jsonl); env ZSCRC_GPU_MIN sets both (0 = never),
  * ZSCRC_GPU_MIN_COLD the cold one alone. */
 /* measured: warm, the GPU wins from 32 MiB (0.85 vs 1.26 ms; 16 MiB level,
@@ -110,7 +110,7 @@ uint32_t xdeal_for(uint32_t opt)
  * team_kernel<16>'s two-level walk on equal-length fixed-stride records of
  * >= g_qteam_min bytes: 0 = off, 1 = on */
 std::atomic<int> g_qteam{1};
-/* qteam from 2 KiB records (tools/qteam_ab.py, profiles/r02/qteam_ab_small.jsonl:
+/* qteam from 2 KiB records (tools/probes/qteam_ab.py, profiles/r02/qteam_ab_small.jsonl:
  * 2 KiB 0.789 vs 0.824 ms per 4 GiB, 4 KiB 0.665 vs 0.756, 8 KiB 0.661 vs
  * 0.736; ~1 KiB loses, 1.53 vs 1.32); env ZSCRC_QTEAM_MIN */
 std::atomic<uint64_t> g_qteam_min{2048};
@@ -383,7 +383,7 @@ int walk_for(int g, int fixed, uint64_t len)
     if (g == 1) /* record bursts with quad-cooperative loads (burst_kernel,
                  * walk 10) for records over 64 bytes and variable batches;
                  * one-piece fixed-stride records: the piece walk
-                 * (tools/g1_sweep.py, profiles/r01/mid_sweep.jsonl) */
+                 * (tools/probes/g1_sweep.py, profiles/r01/mid_sweep.jsonl) */
         return fixed && len <= 64 ? 3 : 10;
     if (len >= 8192)
         return 0;

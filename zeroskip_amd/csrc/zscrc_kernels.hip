@@ -111,7 +111,7 @@ __device__ __forceinline__ uint32_t m4(const char *L, uint32_t x, uint32_t c_lo,
 
 /* m4(x) ^ w.  B3: the four lookups and the data word folded by two
  * v_bitop3_b32 (4 v_perm + 2 XOR ops per word instead of 4 + 4).  Same-box
- * A/B of two builds (tools/lib_ab.sh, profiles/r02/bitop3_ab.jsonl):
+ * A/B of two builds (tools/probes/lib_ab.sh, profiles/r02/bitop3_ab.jsonl):
  * fixed-stride 312-byte bursts -5.5 %, config 2 chunks -2..-5 %, but the
  * commit-batch bursts +3.5 % and team<16> +0.8 % (the chain then waits for
  * two lookups at a time) -- so those keep the plain XOR chain. */
@@ -348,7 +348,7 @@ __device__ __forceinline__ bool fetch_record(const BatchDesc &d, const RecDesc *
 }
 
 /* Issue the loads of lane j's piece of step s: always exactly four 16-byte
- * loads (gfx950 serves 4-byte-aligned dwordx4 loads; tools/unaligned_probe),
+ * loads (gfx950 serves 4-byte-aligned dwordx4 loads; tools/probes/unaligned_probe),
  * so the compiler can count the prefetch ring with partial vmcnt waits.  A
  * front-padded step 0 may read caller bytes before the record (fixup zeroes
  * them) but never before `lo`, the batch buffer's first aligned dword: block
@@ -802,12 +802,12 @@ __global__ __launch_bounds__(WG) void team_kernel(BatchDesc d_in, const uint32_t
  * by the instruction that fetched it and the nt policy costs no L1 re-fetch;
  * a row transpose (v_permlane32/16_swap: block i of lane (g, c) <-> block g
  * of lane (i, c)) then hands lane 16g + c its whole piece.
- * tools/ceiling_probe.hip: nt coalesced reads 6.9-7.2 TB/s against 6.4-6.6
+ * tools/probes/ceiling_probe.hip: nt coalesced reads 6.9-7.2 TB/s against 6.4-6.6
  * for per-lane 64-byte piece loads (team<16>), which lose half their rate
  * with nt.  The next step's loads are in flight while a step is hashed (two
  * register buffers; the loop is unrolled twice so that no buffer copy makes
  * the compiler wait on them).  Each wave walks a contiguous block of records.
- * Same-box interleaved A/B (tools/xteam_ab.py, profiles/r02/xteam_ab.jsonl,
+ * Same-box interleaved A/B (tools/probes/xteam_ab.py, profiles/r02/xteam_ab.jsonl,
  * four boxes): 1 MiB x 4,096 records 0.635-0.676 ms against team<64>'s
  * 0.726-0.771 (4 GiB: 6.4-6.8 TB/s); on 64 KiB x 65,536 (config 3) 0.646-0.72
  * against team<16>'s 0.663-0.673, and slower on 4-16 KiB records: the
@@ -1284,7 +1284,7 @@ extern "C" int zs_set_classify_times(uint64_t *p)
  * by the instruction that fetched it, so the loads can be non-temporal --
  * and the row transpose of xteam (v_permlane32/16_swap: block i of lane
  * (g, c) <-> block g of lane (i, c)) hands lane (g, c) bytes
- * [256g + 64h, +64) = piece 4g+h.  tools/ceiling_probe.hip: this load shape
+ * [256g + 64h, +64) = piece 4g+h.  tools/probes/ceiling_probe.hip: this load shape
  * ("teamq S1 nt") reads at 6.77-6.88 TB/s against 6.44-6.57 for team<16>'s
  * per-lane 64-byte piece loads, which cannot be non-temporal (4.4 TB/s:
  * each 16-byte load re-fetches a line L1 no longer holds).
@@ -1669,7 +1669,7 @@ __global__ __launch_bounds__(256) void qfold_kernel(XDesc d, QDyn q, uint32_t K,
  * piece with the next piece's loads in flight, nothing carried across
  * records.  Same end-aligned 64-byte piece grid, fix-ups, tail and emit() as
  * team_kernel<1>, without the generic (record, step) cursor: the per-record
- * overhead is a handful of scalar/vector ops.  (tools/short_probe: this
+ * overhead is a handful of scalar/vector ops.  (tools/probes/short_probe: this
  * shape reads at the streaming ceiling on 64 B and 320 B records.)
  * PF: 0 = next piece loaded only if it exists; 1 = always four loads (past
  * the record: the record's own first piece again) so the wait counts stay
@@ -1776,7 +1776,7 @@ __global__ __launch_bounds__(WG) void short_kernel(BatchDesc d, const uint32_t *
     bool have = false;
     /* Plain results of batches with at most STASH records per thread wait in
      * LDS and go out after the thread's last record: stores interleaved with
-     * the read stream cost ~20 % of the read rate (tools/short_probe: any
+     * the read stream cost ~20 % of the read rate (tools/probes/short_probe: any
      * store stream that leaves the L2), one burst at the end does not. */
     const uint64_t first = (uint64_t)blockIdx.x * WG + threadIdx.x;
     const bool stash = (FIXED || direct) && !d.commit && !d.part_out && !d.status && count <= STASH * nthr;
@@ -2565,7 +2565,7 @@ __device__ __forceinline__ void burst_issue(const BRec &b, uintptr_t dummy, uint
  * (t, c), t = 0..3 -- each load instruction reads 16 pieces of 64 contiguous
  * bytes (16-32 cache lines) instead of 64 scattered 16-byte pieces (64 lines,
  * the TA-bound shape of the plain burst).  xpose_burst then
- * hands every lane its own record's pieces (tools/xpose_probe.hip).  The
+ * hands every lane its own record's pieces (tools/probes/xpose_probe.hip).  The
  * owners' grid base, piece count and burst flag come over ds_bpermute.  Call
  * with every lane of the wave active. */
 template <int NB>
@@ -3239,7 +3239,7 @@ __global__ __launch_bounds__(NB == 1 ? 1024 : BWG) void burst_kernel(BatchDesc d
  * single-buffered.  Per round: the descriptors (loaded during the previous
  * round's hash), then the round's loads -- a run round's 20 coalesced nt
  * loads or the quad bursts -- then the next round's descriptors, then the
- * hash.  Measured with tools/run_probe.hip: the run shape with hashing reads
+ * hash.  Measured with tools/probes/run_probe.hip: the run shape with hashing reads
  * at 6.6-6.8 TB/s single-buffered at 8 waves per CU, level with two
  * buffers; burst_kernel's double buffer waits on vmcnt(0) at the top of
  * every round (its descriptor prefetch is younger than the round's data), so
@@ -3802,7 +3802,7 @@ __device__ void classify_single(const Classify &c, uint32_t *cnt, const unsigned
  * it), writes the descriptor and sums the lengths, which stay in registers
  * (<= 16 records per thread) for the plan -- the count pass, the scatter and
  * the plan's reload of the list are gone
- * (tools/classify_phases.py: 5.7 + 5.9 us of the 23 us launch). */
+ * (tools/probes/classify_phases.py: 5.7 + 5.9 us of the 23 us launch). */
 constexpr uint32_t ONLY3_MAX = 16 * CWG;
 __device__ __forceinline__ uint64_t block_scan64(uint64_t v, unsigned long long *ws, uint64_t *tot);
 __device__ __forceinline__ uint64_t seg_unit(const PlanArgs &a, uint64_t bytes);
@@ -4413,7 +4413,7 @@ __global__ __launch_bounds__(256) void commit_scatter_kernel(uint8_t *base, cons
  * same GPU (bench.py reports both): a fully coalesced non-temporal streaming
  * read, each wave sweeping blocks of 4 x 1 KiB (lane l: 16 B at 16*l + 1024*i)
  * with the next block's loads in flight while one is XOR-reduced -- the
- * fastest read shape found (tools/ceiling_probe.hip: 6.9-7.2 TB/s, against
+ * fastest read shape found (tools/probes/ceiling_probe.hip: 6.9-7.2 TB/s, against
  * 6.1-6.3 for plain loads and 6.4-6.6 for per-lane 64-byte pieces). */
 __global__ __launch_bounds__(1024) void stream_read_kernel(const uint8_t *buf, uint64_t n, uint32_t *out)
 {
