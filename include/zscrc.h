@@ -484,6 +484,29 @@ int zscrc_cpass_run_timed(zscrc_cpass *p, void *stream, void *start_event, void 
  * otherwise).  Passes on one stream run in order. */
 int zscrc_cpass_submit(zscrc_cpass *p, void *stream, void *start_event, void *end_event, int slot);
 int zscrc_cpass_collect(zscrc_cpass *p, int slot, zscrc_cpass_result *res);
+/* The pass's digest as a fixed-shape int64 row in DEVICE memory, for ranks
+ * that all-gather their digests over RCCL (one collective, one copy to the
+ * host, no host round trip inside the pass): [commits, n_bad, n_stale,
+ * listed bad, listed stale, pieces, flags (1 more mismatches than the pass
+ * lists, 2 commits left undecided: the caller decides them itself)], then
+ * `listed` (file id, record offset) pairs of bad commits in ascending commit
+ * order, `listed` pairs of stale finalise commits, and `pmax` (file id, piece
+ * code, length, raw register) quadruples -- the span's own piece code and
+ * raw register when span_commit was -1, else checked[0..3] (ok, bad, tail
+ * ok, tail bad; a tail = piece code -1) and 0.  Row length: 7 + 4 listed +
+ * 4 pmax. */
+typedef struct zscrc_cpass_row_spec {
+    const int64_t *d_rec;      /* device, n: each commit's record offset in its file */
+    const int64_t *piece_fid;  /* host, nspans: file id of each span              */
+    const int64_t *piece_code; /* host, nspans: piece index (>= 0) or -1 (tail)   */
+    uint32_t listed;           /* pairs per list (<= ZSCRC_CPASS_LIST is what the pass keeps) */
+    uint32_t pmax;             /* piece slots (>= nspans)                          */
+    int64_t checked[4];
+} zscrc_cpass_row_spec;
+int zscrc_cpass_set_row(zscrc_cpass *p, const zscrc_cpass_row_spec *spec);
+/* Enqueue one pass and its row into d_row (device, row length int64);
+ * nothing is copied to the host and nothing waits. */
+int zscrc_cpass_submit_row(zscrc_cpass *p, void *stream, void *start_event, void *end_event, int64_t *d_row);
 void zscrc_cpass_destroy(zscrc_cpass *p);
 
 /* End to end from host memory: every CRC of n zeroskip file images (mmap'd

@@ -154,6 +154,8 @@ def _rank_worker(rank, world, port, q):
         img[c["span_off"] + 7] ^= 1
         db[name(4, 5)] = bytes(img)
         rep = gpu_report(db, world, rank)
+        # the digest rows' exchange: one host round trip per pass
+        assert rep.timing.get("host_round_trips") == 1, rep.timing
         q.put((rank, rep.ok, rep.commits, rep.bad_commits, len(rep.stale_empty_commits), c["commit_off"]))
     finally:
         dist.destroy_process_group()
@@ -299,3 +301,55 @@ def test_pipelined_passes(gpu):
     assert not r2.ok and r2.bad_commits == [(f, c["commit_off"])]
     job.buf[where] ^= 0x40
     assert job.run().ok
+
+
+@pytest.mark.parametrize("case", ["clean", "corrupt", "bad_2000", "bad_5000"])
+def test_device_row_matches_host_digest(gpu, case):
+    """zscrc_cpass_submit_row's digest row (cpass_row_kernel: the listed
+    verdict sorted on the device) equals the row the host builds from the same
+    pass's copied-back block (Consistent._pack of the native digest), int64
+    for int64 -- clean, with a bad commit, a bad records region and stale
+    commits, with more bad commits than a row lists (2,000 > 1,000) and more
+    than the pass keeps (5,000 > 4,096: flag 1, the caller takes the torch
+    path)."""
+    import ctypes
+    from zeroskip_amd._lib import check, lib
+    if case.startswith("bad_"):
+        from tools import zsdb_gen
+        db = zsdb_gen.make_db(device=gpu, packed=2, packed_region_bytes=8 << 20, packed_vlen=1000,
+                              finalised=3, active_pairs=100)
+    else:
+        db = small_db(long_region=True)
+    if case == "corrupt":
+        for f, what in ((name(7, 7), None), (name(4, 5), "records")):
+            img = bytearray(db[f])
+            if what is None:
+                c = zf.walk(img)[0][3]
+                img[c["span_off"]] ^= 0x21
+            else:
+                c = {c["kind"]: c for c in zf.packed_check(img)}[what]
+                img[c["span_off"] + 99] ^= 2
+            db[f] = bytes(img)
+    job = cs.Consistent(cs.open_db(db), 0, 1).prepare()
+    assert job._cpass is not None
+    if case.startswith("bad_"):
+        k = int(case[4:])
+        live = torch.nonzero(job.d_len > 0).flatten()[:k]
+        assert live.numel() == k
+        job.buf[job.d_off[live]] ^= 0x5A
+    row = job.device_row().cpu().numpy()
+    res = cs.CPassResult()
+    with torch.cuda.device(job.buf.device):
+        check(lib().zscrc_cpass_run(job._cpass, None, ctypes.byref(res)), "zscrc_cpass_run")
+    want = job._pack(job._native_digest(res))
+    assert row.shape == want.shape
+    if case == "bad_5000":
+        assert not res.complete and row[6] == 1 and row[1] >= 5000
+        want[6] = 1
+    else:
+        assert row[6] == 0
+    if case.startswith("bad_"):
+        assert row[3] == job.MAX_LISTED
+    assert np.array_equal(row, want), np.nonzero(row != want)[0][:10]
+    if case == "corrupt":
+        assert row[1] >= 1 and row[2] == 3

@@ -82,6 +82,8 @@ SIGNATURES = {
     "zscrc_cpass_run_timed": (_int, [_vp, _vp, _vp, _vp, _vp]),
     "zscrc_cpass_submit": (_int, [_vp, _vp, _vp, _vp, ctypes.c_int]),
     "zscrc_cpass_collect": (_int, [_vp, ctypes.c_int, _vp]),
+    "zscrc_cpass_set_row": (_int, [_vp, _vp]),
+    "zscrc_cpass_submit_row": (_int, [_vp, _vp, _vp, _vp, _vp]),
     "zscrc_cpass_destroy": (None, [_vp]),
     "zscrc_device_verify_commits_verdict": (_int, [_vp, _u64, _vp, _vp, _vp, _sz, _u64, _vp, _vp, _sz, _vp]),
     "zscrc_pack_abort": (_int, [_vp]),

@@ -153,6 +153,12 @@ class CPassSpec(ctypes.Structure):
                 ("span_len", ctypes.c_void_p), ("span_commit", ctypes.c_void_p)]
 
 
+class CPassRowSpec(ctypes.Structure):
+    """zscrc_cpass_row_spec (include/zscrc.h)."""
+    _fields_ = [("d_rec", ctypes.c_void_p), ("piece_fid", ctypes.c_void_p), ("piece_code", ctypes.c_void_p),
+                ("listed", ctypes.c_uint32), ("pmax", ctypes.c_uint32), ("checked", ctypes.c_int64 * 4)]
+
+
 class CPassResult(ctypes.Structure):
     """zscrc_cpass_result (include/zscrc.h)."""
     _fields_ = [("n_bad", ctypes.c_uint64), ("n_stale", ctypes.c_uint64), ("n_undecided", ctypes.c_uint64),
@@ -493,9 +499,11 @@ class Consistent:
         self._pmax = max([sum(1 for u in self.plan.units if u.rank == r and u.what in ("piece", "tail"))
                           for r in range(self.world)] + [0])
         # host-side findings do not change between runs: exchanged once, here
+        native_ok = bool(getattr(be, "native_pass", False) and os.environ.get("ZS_POSTPASS", "native") == "native"
+                         and len(pieces) <= CPASS_SPANS)
         host = dict(files=self.local.files, bytes=self.local.bytes_checked,
                     header_errors=self.local.header_errors, walk_errors=self.local.walk_errors,
-                    issues=self.local.issues)
+                    issues=self.local.issues, native_ok=native_ok)
         if self.world == 1:
             self._host_all = [host]
         else:
@@ -504,8 +512,8 @@ class Consistent:
             dist.all_gather_object(self._host_all, host, group=self.group)
         self._dotzsdb = self._check_dotzsdb()    # the .zsdb does not change between passes
         self._cpass = None
-        if getattr(be, "native_pass", False) and os.environ.get("ZS_POSTPASS", "native") == "native" \
-                and len(pieces) <= CPASS_SPANS:
+        # every rank takes the same path, so their collectives pair up
+        if all(h.get("native_ok", False) for h in self._host_all):
             self._make_cpass(slots)
         return self
 
@@ -546,6 +554,19 @@ class Consistent:
             check(lib().zscrc_cpass_create(ctypes.byref(h), ctypes.byref(spec)), "zscrc_cpass_create")
         self._cpass = h
         self._cres = CPassResult()
+        # the digest row on the device (zscrc_cpass_submit_row): the exchange
+        # of world > 1 all-gathers it without a host round trip
+        self.d_rec = torch.from_numpy(self.c_rec.astype(np.int64)).to(dev)
+        self._piece_fid = np.array([q[0] for q in self.pieces], np.int64)
+        self._piece_code = np.array([q[1] for q in self.pieces], np.int64)
+        rs = CPassRowSpec(self.d_rec.data_ptr(), self._piece_fid.ctypes.data, self._piece_code.ctypes.data,
+                          self.MAX_LISTED, max(self._pmax, len(self.pieces)),
+                          (ctypes.c_int64 * 4)(CHECKED_OK, CHECKED_BAD, CHECKED_TAIL_OK, CHECKED_TAIL_BAD))
+        with torch.cuda.device(dev):
+            check(lib().zscrc_cpass_set_row(h, ctypes.byref(rs)), "zscrc_cpass_set_row")
+        self._row_len = self.HEAD + 4 * self.MAX_LISTED + 4 * max(self._pmax, len(self.pieces))
+        self._row = torch.zeros(self._row_len, dtype=torch.int64, device=dev)
+        self._rows = None
 
     def __del__(self):
         h = getattr(self, "_cpass", None)
@@ -583,10 +604,47 @@ class Consistent:
         """events: optional (start, end) device events recorded around the
         device pass (bench.py's kernel timing)."""
         if self._cpass is not None:
-            rep = self._run_native(events)
+            rep = self._run_native_rows(events) if self.world > 1 else self._run_native(events)
             if rep is not None:
                 return rep
         return self._run_torch(events)
+
+    def device_row(self, events=None) -> torch.Tensor:
+        """Enqueue one native pass whose digest row (include/zscrc.h,
+        zscrc_cpass_submit_row) lands in a device tensor; nothing waits."""
+        from ._lib import check, lib
+        dev = self.buf.device
+        stream = torch.cuda.current_stream(dev)
+        with torch.cuda.device(dev):
+            ev = self._c_events(events, stream)
+            check(lib().zscrc_cpass_submit_row(self._cpass, ctypes.c_void_p(stream.cuda_stream), ev[0], ev[1],
+                                               ctypes.c_void_p(self._row.data_ptr())), "zscrc_cpass_submit_row")
+        return self._row
+
+    def _run_native_rows(self, events):
+        """world > 1: the pass and its digest row on the device, one
+        all-gather of the rows (RCCL under nccl: device to device), one copy of
+        all rows to the host -- the step's only host round trip.  None (every
+        rank takes the torch path, the same rows tell each the same) when a
+        rank's pass left commits undecided or listed only part of them."""
+        import torch.distributed as dist
+        t0 = time.perf_counter()
+        row = self.device_row(events)
+        nccl = dist.get_backend(self.group) == "nccl"
+        if self._rows is None:
+            self._rows = torch.empty(self.world * self._row_len, dtype=torch.int64,
+                                     device=row.device if nccl else "cpu")
+        dist.all_gather_into_tensor(self._rows, row if nccl else row.cpu(), group=self.group)
+        rows = self._rows.cpu().numpy().reshape(self.world, -1)
+        t_x = time.perf_counter()
+        if (rows[:, self.HEAD - 1] != 0).any():
+            return None
+        allsum = [self._unpack(r, rows[r]) for r in range(self.world)]
+        rep = self._merge(allsum)
+        t1 = time.perf_counter()
+        rep.timing = dict(device_s=0.0, exchange_s=t_x - t0, fold_s=t1 - t_x, total_s=t1 - t0,
+                          host_round_trips=1)
+        return rep
 
     def _run_native(self, events):
         """One C call: the verdict batch, the raw spans, the post kernel and
@@ -659,6 +717,16 @@ class Consistent:
         if res.n_undecided or not res.complete:
             return None
         t_dev = time.perf_counter()
+        digest = self._native_digest(res)
+        allsum = self._gather(digest)
+        t_x = time.perf_counter()
+        rep = self._merge(allsum)
+        t1 = time.perf_counter()
+        rep.timing = dict(device_s=t_dev - t0, exchange_s=t_x - t_dev, fold_s=t1 - t_x, total_s=t1 - t0)
+        return rep
+
+    def _native_digest(self, res) -> dict:
+        """A native pass's host block (zscrc_cpass_result) as this rank's digest."""
         L = self.MAX_LISTED
         bad_i = np.ctypeslib.as_array(res.bad)[:res.n_listed_bad].astype(np.int64)
         stale_i = np.ctypeslib.as_array(res.stale)[:res.n_listed_stale].astype(np.int64)
@@ -671,16 +739,10 @@ class Consistent:
             else:
                 pieces.append((fid, (CHECKED_TAIL_OK if st == 1 else CHECKED_TAIL_BAD) if pc < 0 else
                                (CHECKED_OK if st == 1 else CHECKED_BAD), hi - lo, 0))
-        digest = dict(commits=len(self.c_off), n_bad=n_bad, n_stale=int(res.n_stale),
-                      bad=np.stack([self.c_file[bad_i[:L]], self.c_rec[bad_i[:L]]], 1),
-                      stale=np.stack([self.c_file[stale_i[:L]], self.c_rec[stale_i[:L]]], 1),
-                      pieces=np.array(pieces, np.int64).reshape(-1, 4))
-        allsum = self._gather(digest)
-        t_x = time.perf_counter()
-        rep = self._merge(allsum)
-        t1 = time.perf_counter()
-        rep.timing = dict(device_s=t_dev - t0, exchange_s=t_x - t_dev, fold_s=t1 - t_x, total_s=t1 - t0)
-        return rep
+        return dict(commits=len(self.c_off), n_bad=n_bad, n_stale=int(res.n_stale),
+                    bad=np.stack([self.c_file[bad_i[:L]], self.c_rec[bad_i[:L]]], 1),
+                    stale=np.stack([self.c_file[stale_i[:L]], self.c_rec[stale_i[:L]]], 1),
+                    pieces=np.array(pieces, np.int64).reshape(-1, 4))
 
     def _run_torch(self, events=None) -> Report:
         be = self.backend
@@ -782,7 +844,7 @@ class Consistent:
         return rep
 
     # ------------------------------------------------------------- exchange
-    HEAD = 6   # commits, n_bad, n_stale, listed bad, listed stale, pieces
+    HEAD = 7   # commits, n_bad, n_stale, listed bad, listed stale, pieces, flags (include/zscrc.h row)
 
     def _pack(self, d) -> np.ndarray:
         """One rank's digest as a fixed-shape int64 row: the head, then
@@ -792,7 +854,7 @@ class Consistent:
         L = self.MAX_LISTED
         row = np.zeros(self.HEAD + 4 * L + 4 * self._pmax, np.int64)
         row[:self.HEAD] = (d["commits"], d["n_bad"], d["n_stale"], len(d["bad"]), len(d["stale"]),
-                           len(d["pieces"]))
+                           len(d["pieces"]), 0)
         o = self.HEAD
         row[o:o + 2 * len(d["bad"])] = d["bad"].reshape(-1)
         o += 2 * L
@@ -803,7 +865,7 @@ class Consistent:
 
     def _unpack(self, r: int, row: np.ndarray) -> dict:
         L = self.MAX_LISTED
-        commits, n_bad, n_stale, nb, ns, npc = (int(v) for v in row[:self.HEAD])
+        commits, n_bad, n_stale, nb, ns, npc, _flags = (int(v) for v in row[:self.HEAD])
         o = self.HEAD
         bad = row[o:o + 2 * nb].reshape(-1, 2)
         o += 2 * L

@@ -26,6 +26,7 @@
 extern "C" {
 const uint32_t *zscrc_internal_gtab(void);
 int zs_launch_cpass_post(const zs::CPassArgs *a, const uint32_t *gtab, hipStream_t stream);
+int zs_launch_cpass_row(const zs::CPassRowArgs *a, hipStream_t stream);
 uint32_t zs_gf2_xpow8n(uint64_t n);
 uint32_t zs_gf2_mul(uint32_t a, uint32_t b);
 }
@@ -49,6 +50,10 @@ struct zscrc_cpass {
     uint8_t *hblk = nullptr;   /* NSLOT host blocks (zscrc_cpass_submit / _collect) */
     hipEvent_t done[2] = {};   /* each slot's copy back */
     bool pending[2] = {};
+    /* the digest row (zscrc_cpass_set_row / _submit_row) */
+    bool have_row = false;
+    zs::CPassRowArgs row = {};
+    int64_t *dpiece = nullptr;
     uint64_t *dbad_full = nullptr; /* the verdict's list (cap entries) */
     uint64_t cap = 0;
     int64_t *dspan_commit = nullptr;
@@ -80,6 +85,8 @@ void cpass_free(zscrc_cpass *p)
         (void)hipFree(p->dbad_full);
     if (p->dspan_commit)
         (void)hipFree(p->dspan_commit);
+    if (p->dpiece)
+        (void)hipFree(p->dpiece);
     delete p;
 }
 
@@ -209,11 +216,97 @@ extern "C" int zscrc_cpass_collect(zscrc_cpass *p, int slot, zscrc_cpass_result 
     return cpass_collect(p, slot, res);
 }
 
+extern "C" int zscrc_cpass_set_row(zscrc_cpass *p, const zscrc_cpass_row_spec *rs)
+{
+    if (!p || !rs || (p->spec.n && !rs->d_rec) || (p->spec.nspans && (!rs->piece_fid || !rs->piece_code)) ||
+        rs->pmax < p->spec.nspans || rs->listed == 0)
+        return ZSCRC_EINVAL;
+    OnDevice od(p->dev);
+    if (!od.ok)
+        return ZSCRC_EHIP;
+    std::vector<int64_t> meta(3 * std::max<size_t>(p->spec.nspans, 1));
+    for (size_t k = 0; k < p->spec.nspans; ++k) {
+        meta[3 * k] = rs->piece_fid[k];
+        meta[3 * k + 1] = rs->piece_code[k];
+        meta[3 * k + 2] = (int64_t)p->span_len[k];
+    }
+    if (!p->dpiece && hipMalloc(&p->dpiece, 3 * 8 * zs::CPASS_SPANS) != hipSuccess)
+        return ZSCRC_ENOMEM;
+    if (hipMemcpy(p->dpiece, meta.data(), 8 * meta.size(), hipMemcpyHostToDevice) != hipSuccess)
+        return ZSCRC_EHIP;
+    zs::CPassRowArgs &a = p->row;
+    memset(&a, 0, sizeof a);
+    a.blk = p->dblk;
+    a.off_raw = OFF_RAW;
+    a.off_st = OFF_ST;
+    a.off_flags = OFF_FLAGS;
+    a.off_bad = OFF_BAD;
+    a.list_cap = (uint32_t)LIST_CAP;
+    a.commits = p->spec.n;
+    a.file = p->spec.d_file;
+    a.rec = rs->d_rec;
+    a.piece = p->dpiece;
+    a.nspans = (uint32_t)p->spec.nspans;
+    a.listed = rs->listed;
+    a.pmax = rs->pmax;
+    for (int k = 0; k < 4; ++k)
+        a.checked[k] = rs->checked[k];
+    p->have_row = true;
+    return ZSCRC_OK;
+}
+
+namespace {
+int cpass_enqueue(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0);
+}
+
+extern "C" int zscrc_cpass_submit_row(zscrc_cpass *p, void *stream, void *start_event, void *end_event,
+                                      int64_t *d_row)
+{
+    if (!p || !d_row || !p->have_row)
+        return ZSCRC_EINVAL;
+    OnDevice od(p->dev);
+    if (!od.ok)
+        return ZSCRC_EHIP;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int rc = cpass_enqueue(p, s, static_cast<hipEvent_t>(start_event));
+    if (!rc) {
+        zs::CPassRowArgs a = p->row;
+        a.row = d_row;
+        if (zs_launch_cpass_row(&a, s))
+            rc = ZSCRC_EHIP;
+    }
+    if (!rc && end_event && hipEventRecord(static_cast<hipEvent_t>(end_event), s) != hipSuccess)
+        rc = ZSCRC_EHIP;
+    return rc;
+}
+
 namespace {
 
 /* Enqueue one pass on s: the verdict batch, the raw spans, the post kernel
  * and the copy of the small block into host slot `slot`; nothing waits. */
 int cpass_submit(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1, int slot)
+{
+    int rc = cpass_enqueue(p, s, ev0);
+    /* the post kernel wrote the listed part of the verdict next to the
+     * counters: one copy back (two device-to-device copies of the lists
+     * before it cost a launch each).  The next pass on this stream rewrites
+     * the device block only after this copy (stream order), so two passes
+     * can be in flight with their host slots apart. */
+    if (!rc && hipMemcpyAsync(p->hblk + slot * BLK, p->dblk, BLK, hipMemcpyDeviceToHost, s) != hipSuccess)
+        rc = ZSCRC_EHIP;
+    /* the end event right behind the copy back: the device's part of the
+     * pass, without the host's wait and the list sorting */
+    if (!rc && ev1 && hipEventRecord(ev1, s) != hipSuccess)
+        rc = ZSCRC_EHIP;
+    if (!rc && hipEventRecord(p->done[slot], s) != hipSuccess)
+        rc = ZSCRC_EHIP;
+    if (!rc)
+        p->pending[slot] = true;
+    return rc;
+}
+
+/* The pass's kernels: verdict batch, raw spans, post kernel (into dblk). */
+int cpass_enqueue(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0)
 {
     if (ev0 && hipEventRecord(ev0, s) != hipSuccess)
         return ZSCRC_EHIP;
@@ -266,21 +359,6 @@ int cpass_submit(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1, 
         if (zs_launch_cpass_post(&a, zscrc_internal_gtab(), s))
             rc = ZSCRC_EHIP;
     }
-    /* the post kernel wrote the listed part of the verdict next to the
-     * counters: one copy back (two device-to-device copies of the lists
-     * before it cost a launch each).  The next pass on this stream rewrites
-     * the device block only after this copy (stream order), so two passes
-     * can be in flight with their host slots apart. */
-    if (!rc && hipMemcpyAsync(p->hblk + slot * BLK, p->dblk, BLK, hipMemcpyDeviceToHost, s) != hipSuccess)
-        rc = ZSCRC_EHIP;
-    /* the end event right behind the copy back: the device's part of the
-     * pass, without the host's wait and the list sorting */
-    if (!rc && ev1 && hipEventRecord(ev1, s) != hipSuccess)
-        rc = ZSCRC_EHIP;
-    if (!rc && hipEventRecord(p->done[slot], s) != hipSuccess)
-        rc = ZSCRC_EHIP;
-    if (!rc)
-        p->pending[slot] = true;
     return rc;
 }
 

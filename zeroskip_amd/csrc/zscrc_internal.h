@@ -219,6 +219,28 @@ struct CPassArgs {
     int32_t *span_status;        /* 1 ok, 0 mismatch, 2 no commit record, -1 not checked */
 };
 
+/* cpass_row_kernel: one rank's digest of a consistent pass as the fixed-shape
+ * int64 row the ranks all-gather (zeroskip_amd/consistent.py Consistent._pack):
+ * [commits, n_bad, n_stale, listed bad, listed stale, pieces, flags]
+ * + listed x (file, record offset) of bad commits, ascending commit index
+ * + listed x (file, record offset) of stale finalise commits
+ * + pmax x (file, piece, length, raw register). */
+constexpr uint32_t ROW_HEAD = 7;
+constexpr uint32_t ROW_FLAG_INCOMPLETE = 1, ROW_FLAG_UNDECIDED = 2;
+struct CPassRowArgs {
+    const uint8_t *blk;          /* the pass's device block (cpass_post_kernel's output) */
+    uint64_t off_raw, off_st, off_flags, off_bad; /* its layout */
+    uint32_t list_cap;           /* entries the block lists */
+    uint64_t commits;
+    const uint32_t *file;        /* file id per commit */
+    const int64_t *rec;          /* record offset in its file per commit */
+    const int64_t *piece;        /* nspans x (file, piece code, length) */
+    uint32_t nspans;
+    uint32_t listed, pmax;
+    int64_t checked[4];          /* piece codes of checked spans: ok, bad, tail ok, tail bad */
+    int64_t *row;
+};
+
 struct RecDesc {
     uint64_t off;
     uint64_t len;

@@ -4381,6 +4381,105 @@ __global__ __launch_bounds__(256) void part_fold_kernel(FoldPair fp, const uint3
     }
 }
 
+/* ------------------------------------------------ consistent: the digest row */
+/* One workgroup: the pass's listed verdict entries (flag 0 bad, 1 stale, 2
+ * undecided) sorted by (flag, commit index) in LDS -- bitonic over
+ * ROW_SORT keys -- then written as the rank's digest row in the layout of
+ * consistent.py's Consistent._pack, so the ranks all-gather it straight from
+ * the device (one RCCL all-gather, one copy to the host) instead of copying
+ * the block back, building the row in numpy and copying it up again. */
+constexpr uint32_t ROW_SORT = 4096;
+
+__global__ __launch_bounds__(1024) void cpass_row_kernel(CPassRowArgs a)
+{
+    __shared__ uint64_t key[ROW_SORT];
+    __shared__ uint32_t cnt[3];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t nbad = reinterpret_cast<const uint64_t *>(a.blk)[0];
+    const uint64_t nstale = reinterpret_cast<const uint64_t *>(a.blk)[1];
+    const uint32_t nl = (uint32_t)(nbad < a.list_cap ? nbad : a.list_cap);
+    const uint32_t *flags = reinterpret_cast<const uint32_t *>(a.blk + a.off_flags);
+    const uint64_t *bad = reinterpret_cast<const uint64_t *>(a.blk + a.off_bad);
+    if (tid < 3)
+        cnt[tid] = 0;
+    __syncthreads();
+    for (uint32_t k = tid; k < ROW_SORT; k += blockDim.x) {
+        uint64_t v = ~0ull;
+        if (k < nl) {
+            const uint32_t f = flags[k] > 2 ? 2u : flags[k];
+            v = ((uint64_t)f << 56) | bad[k];
+            atomicAdd(&cnt[f], 1u);
+        }
+        key[k] = v;
+    }
+    __syncthreads();
+    for (uint32_t size = 2; size <= ROW_SORT; size <<= 1)
+        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+            for (uint32_t k = tid; k < ROW_SORT; k += blockDim.x) {
+                const uint32_t j = k ^ stride;
+                if (j > k) {
+                    const bool up = (k & size) == 0;
+                    const uint64_t x = key[k], y = key[j];
+                    if ((x > y) == up) {
+                        key[k] = y;
+                        key[j] = x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    const uint32_t nb = cnt[0], ns = cnt[1], nu = cnt[2];
+    const uint32_t lb = nb < a.listed ? nb : a.listed, ls = ns < a.listed ? ns : a.listed;
+    int64_t *row = a.row;
+    if (tid == 0) {
+        row[0] = (int64_t)a.commits;
+        row[1] = (int64_t)(nbad - nstale); /* undecided ones included, as the host report */
+        row[2] = (int64_t)nstale;
+        row[3] = lb;
+        row[4] = ls;
+        row[5] = a.nspans;
+        row[6] = (nbad > a.list_cap ? (int64_t)ROW_FLAG_INCOMPLETE : 0) | (nu ? (int64_t)ROW_FLAG_UNDECIDED : 0);
+    }
+    int64_t *rb = row + ROW_HEAD, *rs = rb + 2 * a.listed, *rp = rs + 2 * a.listed;
+    const uint64_t IDX = (1ull << 56) - 1;
+    for (uint32_t k = tid; k < a.listed; k += blockDim.x) {
+        int64_t f = 0, r = 0;
+        if (k < lb) {
+            const uint64_t i = key[k] & IDX;
+            f = a.file[i];
+            r = a.rec[i];
+        }
+        rb[2 * k] = f;
+        rb[2 * k + 1] = r;
+        f = r = 0;
+        if (k < ls) {
+            const uint64_t i = key[nb + k] & IDX;
+            f = a.file[i];
+            r = a.rec[i];
+        }
+        rs[2 * k] = f;
+        rs[2 * k + 1] = r;
+    }
+    const uint32_t *raw = reinterpret_cast<const uint32_t *>(a.blk + a.off_raw);
+    const int32_t *st = reinterpret_cast<const int32_t *>(a.blk + a.off_st);
+    for (uint32_t k = tid; k < a.pmax; k += blockDim.x) {
+        int64_t q[4] = {0, 0, 0, 0};
+        if (k < a.nspans) {
+            const int64_t fid = a.piece[3 * k], pc = a.piece[3 * k + 1], len = a.piece[3 * k + 2];
+            q[0] = fid;
+            q[2] = len;
+            if (st[k] < 0) {
+                q[1] = pc;
+                q[3] = raw[k];
+            } else {
+                q[1] = pc < 0 ? (st[k] == 1 ? a.checked[2] : a.checked[3]) : (st[k] == 1 ? a.checked[0] : a.checked[1]);
+            }
+        }
+        for (int j = 0; j < 4; ++j)
+            rp[4 * k + j] = q[j];
+    }
+}
+
 /* ------------------------------------------------ the writer's second pass */
 /* The in-place commit writer as two passes (round 5, tuning bit 512):
  * commit_kernel computes every CRC into crc[] without touching the image
@@ -4700,6 +4799,14 @@ extern "C" int zs_launch_commit_scatter(uint8_t *base, const uint64_t *off, cons
     const uint64_t blocks = (n + 255) / 256, cap = (uint64_t)ncu * 16;
     hipLaunchKernelGGL(zs::commit_scatter_kernel, dim3((unsigned)(blocks < cap ? blocks : cap)), dim3(256), 0, stream,
                        base, off, len, crc, status, n, user_status);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int zs_launch_cpass_row(const zs::CPassRowArgs *a, hipStream_t stream)
+{
+    if (a->list_cap > zs::ROW_SORT)
+        return -1;
+    hipLaunchKernelGGL(zs::cpass_row_kernel, dim3(1), dim3(1024), 0, stream, *a);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
