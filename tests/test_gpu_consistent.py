@@ -324,8 +324,9 @@ def test_device_row_matches_host_digest(gpu, case):
         for f, what in ((name(7, 7), None), (name(4, 5), "records")):
             img = bytearray(db[f])
             if what is None:
-                c = zf.walk(img)[0][3]
-                img[c["span_off"]] ^= 0x21
+                c = zf.walk(img)[0][5]
+                assert c["span_len"] > 3
+                img[c["span_off"] + 3] ^= 0x10
             else:
                 c = {c["kind"]: c for c in zf.packed_check(img)}[what]
                 img[c["span_off"] + 99] ^= 2
@@ -344,10 +345,14 @@ def test_device_row_matches_host_digest(gpu, case):
     want = job._pack(job._native_digest(res))
     assert row.shape == want.shape
     if case == "bad_5000":
+        # more mismatches than the pass keeps: WHICH 4,096 a pass lists depends
+        # on the order its waves found them, so two passes list different
+        # subsets -- the counts agree and the row says incomplete (the caller
+        # then decides on the torch path)
         assert not res.complete and row[6] == 1 and row[1] >= 5000
-        want[6] = 1
-    else:
-        assert row[6] == 0
+        assert np.array_equal(row[:3], want[:3]) and row[3] == job.MAX_LISTED
+        return
+    assert row[6] == 0
     if case.startswith("bad_"):
         assert row[3] == job.MAX_LISTED
     assert np.array_equal(row, want), np.nonzero(row != want)[0][:10]
