@@ -153,9 +153,21 @@ def _rank_worker(rank, world, port, q):
         c = {c["kind"]: c for c in zf.packed_check(img)}["records"]
         img[c["span_off"] + 7] ^= 1
         db[name(4, 5)] = bytes(img)
-        rep = gpu_report(db, world, rank)
+        job = cs.Consistent(cs.open_db(db), rank, world).prepare()
+        rep = job.run()
         # the digest rows' exchange: one host round trip per pass
         assert rep.timing.get("host_round_trips") == 1, rep.timing
+        # pipelined: two passes' rows in flight, collected in order, the same reports
+        reps = []
+        for _ in range(4):
+            assert job.submit()
+            if job.pending() > 1:
+                reps.append(job.collect())
+        while job.pending():
+            reps.append(job.collect())
+        assert len(reps) == 4
+        assert all((r.ok, r.commits, r.bad_commits, r.stale_empty_commits) ==
+                   (rep.ok, rep.commits, rep.bad_commits, rep.stale_empty_commits) for r in reps)
         q.put((rank, rep.ok, rep.commits, rep.bad_commits, len(rep.stale_empty_commits), c["commit_off"]))
     finally:
         dist.destroy_process_group()

@@ -35,6 +35,9 @@ for step in "$@"; do
     bench5sync) BENCH_C5_SYNC=1 timeout -k 10 600 python bench.py --workload config5 --no-cpu >> gpurun_out/bench5sync.jsonl \
                 2>> gpurun_out/bench5sync.err ;;
     cstests)  timeout -k 10 600 $T tests/test_gpu_consistent.py > gpurun_out/cstests.log 2>&1 ;;
+    rowtail)  ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+                -d $R/gpurun_out/rowtail -o run -- python3 $R/tools/probes/c5_row_tail.py 8 > $R/gpurun_out/rowtail.json \
+                2> $R/gpurun_out/rowtail.err ) ;;
     cputhreads) timeout -k 10 300 python tools/probes/cpu_threads.py > gpurun_out/cpu_threads.jsonl \
                 2> gpurun_out/cpu_threads.err ;;
     ab3)      AB_CASES=config3,fixed_16KiB,fixed_4KiB,fixed_1MiB timeout -k 10 600 python tools/opt_ab.py 0 32 \

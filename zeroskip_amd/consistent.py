@@ -621,6 +621,61 @@ class Consistent:
                                                ctypes.c_void_p(self._row.data_ptr())), "zscrc_cpass_submit_row")
         return self._row
 
+    def _row_buffers(self, nccl: bool, slot: int):
+        """Per host slot: the device row, the gathered rows (device under nccl,
+        host under gloo) and pinned host rows."""
+        if getattr(self, "_rowbuf", None) is None:
+            dev = self.buf.device
+            n = self.world * self._row_len
+            self._rowbuf = [dict(row=torch.zeros(self._row_len, dtype=torch.int64, device=dev),
+                                 rows=torch.empty(n, dtype=torch.int64, device=dev if nccl else "cpu"),
+                                 host=torch.empty(n, dtype=torch.int64, pin_memory=True))
+                            for _ in range(2)]
+        return self._rowbuf[slot]
+
+    def _submit_rows(self, events, slot: int) -> bool:
+        """world > 1, pipelined: pass k's row on the device, its all-gather
+        queued (async) and the gathered rows' copy into pinned host memory
+        queued behind it; collect() waits for the copy and merges -- while pass
+        k + 1 already runs."""
+        import torch.distributed as dist
+        from ._lib import check, lib
+        nccl = dist.get_backend(self.group) == "nccl"
+        b = self._row_buffers(nccl, slot)
+        dev = self.buf.device
+        stream = torch.cuda.current_stream(dev)
+        with torch.cuda.device(dev):
+            ev = self._c_events(events, stream)
+            check(lib().zscrc_cpass_submit_row(self._cpass, ctypes.c_void_p(stream.cuda_stream), ev[0], ev[1],
+                                               ctypes.c_void_p(b["row"].data_ptr())), "zscrc_cpass_submit_row")
+        t0 = time.perf_counter()
+        if nccl:
+            work = dist.all_gather_into_tensor(b["rows"], b["row"], group=self.group, async_op=True)
+            work.wait()   # the current stream waits for the collective (the host does not)
+            b["host"].copy_(b["rows"], non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(stream)
+        else:
+            dist.all_gather_into_tensor(b["rows"], b["row"].cpu(), group=self.group)
+            b["host"].copy_(b["rows"])
+            done = None
+        self._inflight.append((slot, t0, done))
+        self._next_slot ^= 1
+        return True
+
+    def _collect_rows(self) -> Report:
+        slot, t0, done = self._inflight.pop(0)
+        if done is not None:
+            done.synchronize()
+        rows = self._rowbuf[slot]["host"].numpy().reshape(self.world, -1)
+        t_x = time.perf_counter()
+        if (rows[:, self.HEAD - 1] != 0).any():
+            return self._run_torch()
+        rep = self._merge([self._unpack(r, rows[r]) for r in range(self.world)])
+        t1 = time.perf_counter()
+        rep.timing = dict(device_s=0.0, exchange_s=t_x - t0, fold_s=t1 - t_x, total_s=t1 - t0, host_round_trips=1)
+        return rep
+
     def _run_native_rows(self, events):
         """world > 1: the pass and its digest row on the device, one
         all-gather of the rows (RCCL under nccl: device to device), one copy of
@@ -634,8 +689,11 @@ class Consistent:
         if self._rows is None:
             self._rows = torch.empty(self.world * self._row_len, dtype=torch.int64,
                                      device=row.device if nccl else "cpu")
+            self._rows_h = torch.empty(self.world * self._row_len, dtype=torch.int64, pin_memory=True)
         dist.all_gather_into_tensor(self._rows, row if nccl else row.cpu(), group=self.group)
-        rows = self._rows.cpu().numpy().reshape(self.world, -1)
+        self._rows_h.copy_(self._rows, non_blocking=True)
+        torch.cuda.current_stream(row.device).synchronize()
+        rows = self._rows_h.numpy().reshape(self.world, -1)
         t_x = time.perf_counter()
         if (rows[:, self.HEAD - 1] != 0).any():
             return None
@@ -686,15 +744,17 @@ class Consistent:
             self._inflight, self._next_slot = [], 0
             self._cres_slot = (CPassResult(), CPassResult())
         slot = self._next_slot
-        if slot in self._inflight:
+        if slot in [q[0] for q in self._inflight]:
             raise RuntimeError("both host slots hold uncollected passes")
+        if self.world > 1:
+            return self._submit_rows(events, slot)
         dev = self.buf.device
         stream = torch.cuda.current_stream(dev)
         with torch.cuda.device(dev):
             ev = self._c_events(events, stream)
             check(lib().zscrc_cpass_submit(self._cpass, ctypes.c_void_p(stream.cuda_stream), ev[0], ev[1], slot),
                   "zscrc_cpass_submit")
-        self._inflight.append((slot, time.perf_counter()))
+        self._inflight.append((slot, time.perf_counter(), None))
         self._next_slot ^= 1
         return True
 
@@ -706,7 +766,9 @@ class Consistent:
         A pass that left commits undecided is decided by the torch path (a
         synchronous pass of its own)."""
         from ._lib import check, lib
-        slot, t0 = self._inflight.pop(0)
+        if self.world > 1:
+            return self._collect_rows()
+        slot, t0, _ = self._inflight.pop(0)
         res = self._cres_slot[slot]
         with torch.cuda.device(self.buf.device):
             check(lib().zscrc_cpass_collect(self._cpass, slot, ctypes.byref(res)), "zscrc_cpass_collect")
