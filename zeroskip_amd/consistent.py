@@ -650,11 +650,17 @@ class Consistent:
                                                ctypes.c_void_p(b["row"].data_ptr())), "zscrc_cpass_submit_row")
         t0 = time.perf_counter()
         if nccl:
+            # the gather (RCCL's own stream) and the copy to the host (a side
+            # stream waiting for it) run beside the next pass's kernels: the
+            # compute stream never waits for the exchange
             work = dist.all_gather_into_tensor(b["rows"], b["row"], group=self.group, async_op=True)
-            work.wait()   # the current stream waits for the collective (the host does not)
-            b["host"].copy_(b["rows"], non_blocking=True)
-            done = torch.cuda.Event()
-            done.record(stream)
+            if getattr(self, "_xstream", None) is None:
+                self._xstream = torch.cuda.Stream(dev)
+            with torch.cuda.stream(self._xstream):
+                work.wait()   # the side stream waits for the collective (the host does not)
+                b["host"].copy_(b["rows"], non_blocking=True)
+                done = torch.cuda.Event()
+                done.record(self._xstream)
         else:
             dist.all_gather_into_tensor(b["rows"], b["row"].cpu(), group=self.group)
             b["host"].copy_(b["rows"])

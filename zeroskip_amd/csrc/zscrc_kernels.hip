@@ -4387,16 +4387,14 @@ __global__ __launch_bounds__(256) void part_fold_kernel(FoldPair fp, const uint3
  * rank's digest row in the layout of consistent.py's Consistent._pack, so the
  * ranks all-gather it straight from the device (one RCCL all-gather, one copy
  * to the host) instead of copying the block back, building the row in numpy
- * and copying it up again.  The order is a rank by counting: the keys are
- * distinct, each entry's position is the number of keys below it, every
- * thread reading the same key at once (an LDS broadcast) -- a 4,096-key
- * bitonic sort (78 barriers) took 60 us of a 1.4 ms pass, the counting takes
- * a few for config 5's 1,024 entries. */
+ * and copying it up again.  (A fixed 4,096-key bitonic sort with four
+ * guarded pairs per thread took 60 us; a rank by counting 28 -- 16 waves x
+ * nl broadcast LDS reads.) */
 constexpr uint32_t ROW_SORT = 4096;
 
 __global__ __launch_bounds__(1024) void cpass_row_kernel(CPassRowArgs a)
 {
-    __shared__ uint64_t key[ROW_SORT], sorted[ROW_SORT];
+    __shared__ uint64_t key[ROW_SORT];
     __shared__ uint32_t cnt[3];
     const uint32_t tid = threadIdx.x;
     const uint64_t nbad = reinterpret_cast<const uint64_t *>(a.blk)[0];
@@ -4413,14 +4411,53 @@ __global__ __launch_bounds__(1024) void cpass_row_kernel(CPassRowArgs a)
         atomicAdd(&cnt[f], 1u);
     }
     __syncthreads();
-    for (uint32_t k = tid; k < nl; k += blockDim.x) {
-        const uint64_t x = key[k];
-        uint32_t rank = 0;
-        for (uint32_t j = 0; j < nl; ++j)
-            rank += key[j] < x ? 1u : 0u;
-        sorted[rank] = x;
+    /* bitonic over the next power of two >= nl (padded with ~0).  Up to
+     * 1,024 entries (config 5 lists 1,024 stale commits): one key per
+     * thread in a register, strides below 64 exchanged inside the wave
+     * (__shfl_xor, no barrier), only strides of 64 and up through LDS --
+     * 10 of config 5's 55 stages.  More: the same network on LDS, one
+     * compare-exchange pair per thread per stage. */
+    uint32_t n2 = 2;
+    while (n2 < nl)
+        n2 <<= 1;
+    if (n2 <= blockDim.x) {
+        uint64_t x = tid < nl ? key[tid] : ~0ull;
+        for (uint32_t size = 2; size <= n2; size <<= 1)
+            for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+                uint64_t y;
+                if (stride >= 64) {
+                    __syncthreads();
+                    key[tid] = x;
+                    __syncthreads();
+                    y = key[tid ^ stride];
+                } else {
+                    const uint32_t lo = __shfl_xor((uint32_t)x, (int)stride);
+                    const uint32_t hi = __shfl_xor((uint32_t)(x >> 32), (int)stride);
+                    y = ((uint64_t)hi << 32) | lo;
+                }
+                const bool up = (tid & size) == 0, lower = (tid & stride) == 0;
+                x = (lower == up) ? (x < y ? x : y) : (x < y ? y : x);
+            }
+        __syncthreads();
+        key[tid] = x;
+        __syncthreads();
+    } else {
+        for (uint32_t k = nl + tid; k < n2; k += blockDim.x)
+            key[k] = ~0ull;
+        __syncthreads();
+        for (uint32_t size = 2; size <= n2; size <<= 1)
+            for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+                for (uint32_t q = tid; q < n2 / 2; q += blockDim.x) {
+                    const uint32_t k = 2 * q - (q & (stride - 1)), j = k + stride;
+                    const uint64_t x = key[k], y = key[j];
+                    if ((x > y) == ((k & size) == 0)) {
+                        key[k] = y;
+                        key[j] = x;
+                    }
+                }
+                __syncthreads();
+            }
     }
-    __syncthreads();
     const uint32_t nb = cnt[0], ns = cnt[1], nu = cnt[2];
     const uint32_t lb = nb < a.listed ? nb : a.listed, ls = ns < a.listed ? ns : a.listed;
     int64_t *row = a.row;
@@ -4438,7 +4475,7 @@ __global__ __launch_bounds__(1024) void cpass_row_kernel(CPassRowArgs a)
     for (uint32_t k = tid; k < a.listed; k += blockDim.x) {
         int64_t f = 0, r = 0;
         if (k < lb) {
-            const uint64_t i = sorted[k] & IDX;
+            const uint64_t i = key[k] & IDX;
             f = a.file[i];
             r = a.rec[i];
         }
@@ -4446,7 +4483,7 @@ __global__ __launch_bounds__(1024) void cpass_row_kernel(CPassRowArgs a)
         rb[2 * k + 1] = r;
         f = r = 0;
         if (k < ls) {
-            const uint64_t i = sorted[nb + k] & IDX;
+            const uint64_t i = key[nb + k] & IDX;
             f = a.file[i];
             r = a.rec[i];
         }
