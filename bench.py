@@ -139,8 +139,9 @@ def cpu_leg(host: np.ndarray, what: str, offs=None, lens=None, *, n=None, stride
     # all cores pinned (one thread per physical core) and left to the
     # scheduler: the box's other tenants share its cores, and either can be
     # the faster on a given box (profiles/r05/cpu_threads.jsonl)
-    legs = [("all", "hw", cores, 0.3, True), ("all_unpinned", "hw", cores, 0.2, False), ("hw", "hw", 1, 0.2, True),
-            ("read", "read", cores, 0.15, True)]
+    legs = [("all", "hw", cores, 0.15, True), ("all_unpinned", "hw", cores, 0.15, False), ("hw", "hw", 1, 0.2, True),
+            ("all2", "hw", cores, 0.15, True), ("read", "read", cores, 0.1, True),
+            ("read_unpinned", "read", cores, 0.05, False)]
     if sw:
         legs.append(("sw", "sw", 1, 0.15, True))
     res, out_all = {}, None
@@ -150,8 +151,9 @@ def cpu_leg(host: np.ndarray, what: str, offs=None, lens=None, *, n=None, stride
         res[key] = passes * nbytes / el / GIB
         if key == "all":
             out_all = got
-    pinned, unpinned = res["all"], res["all_unpinned"]
+    pinned, unpinned = max(res["all"], res["all2"]), res["all_unpinned"]
     res["all"] = max(pinned, unpinned)
+    res["read"] = max(res["read"], res["read_unpinned"])
     want = oracle.batch(host, offs, lens, impl="hw", threads=cores, **kw)
     if not np.array_equal(out_all, want):
         raise SystemExit("cpu_baseline: the byte-split all-core pass differs from the per-record oracle")
@@ -160,8 +162,8 @@ def cpu_leg(host: np.ndarray, what: str, offs=None, lens=None, *, n=None, stride
          "value_1core": round(res["hw"], 3), "host_read_GiBs": round(res["read"], 3),
          "all_pinned": round(pinned, 3), "all_unpinned": round(unpinned, 3),
          "sample": (f"{what}: {nbytes / 2**20:.0f} MiB, repeated on {cores} threads pinned one per physical "
-                    f"core ({cpus[:cores]}, ~{seconds * 0.3:.0f} s) and unpinned (~{seconds * 0.2:.0f} s; value "
-                    f"= the faster) and ~{seconds * 0.2:.0f} s on 1 core of "
+                    f"core ({cpus[:cores]}, two legs of ~{seconds * 0.15:.0f} s) and unpinned (~{seconds * 0.15:.0f} "
+                    f"s; value = the fastest leg) and ~{seconds * 0.2:.0f} s on 1 core of "
                     f"{cpu_model()} ({os.cpu_count()} threads visible, {cores} usable); byte-balanced "
                     "persistent threads, records cut by a range joined by the zero shift; oracle SSE4.2 "
                     "crc32c_hw class (src/crc32c.c:370-453)")}

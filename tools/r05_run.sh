@@ -38,6 +38,12 @@ for step in "$@"; do
     rowtail)  ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
                 -d $R/gpurun_out/rowtail -o run -- python3 $R/tools/probes/c5_row_tail.py 8 > $R/gpurun_out/rowtail.json \
                 2> $R/gpurun_out/rowtail.err ) ;;
+    rehearse5)
+              BENCH_SHARE_GPU=1 BENCH_DIST=gloo timeout -k 10 900 python bench.py --gpus 2 --workload config5 \
+                --no-cpu > gpurun_out/rehearse5_n2.json 2> gpurun_out/rehearse5_n2.err ;;
+    rehearse3)
+              BENCH_SHARE_GPU=1 BENCH_DIST=gloo timeout -k 10 600 python bench.py --gpus 2 --workload config3 \
+                --no-cpu > gpurun_out/rehearse3_n2.json 2> gpurun_out/rehearse3_n2.err ;;
     cputhreads) timeout -k 10 300 python tools/probes/cpu_threads.py > gpurun_out/cpu_threads.jsonl \
                 2> gpurun_out/cpu_threads.err ;;
     ab3)      AB_CASES=config3,fixed_16KiB,fixed_4KiB,fixed_1MiB timeout -k 10 600 python tools/opt_ab.py 0 32 \
