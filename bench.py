@@ -67,7 +67,7 @@ def box_info(index: int | None = None) -> dict:
     """What tells one GPU box from another (read-only sysfs of the device
     this rank runs on, taken after the timed region): clock levels, power
     cap, firmware, the card's id.  Config 2 and 4's rates move 10-15 % from
-    box to box while the streaming read and config 3 stay level (DESIGN.md
+    box to box while the streaming read and config 3 stay level (DESIGN_LOG.md
     1.8), so every line records the box it was measured on."""
     info = {}
     try:
@@ -409,7 +409,7 @@ def run_config3(args, world, rank, dev, stream):
     # The same-GPU read ceiling is measured first, right before the warmup:
     # config 3 runs at the package's 1400 W cap, and the power controller's
     # settling after idle (~20-30 ms, longer than 5 warmup steps) would
-    # otherwise land in the timed steps (DESIGN.md 1.6,
+    # otherwise land in the timed steps (DESIGN_LOG.md 1.6,
     # profiles/r02/sustain*.jsonl); the streaming probe brings the package to
     # its loaded operating point as a sustained checksum job finds it.
     read_peak = read_ceiling(data, NCHUNK * CHUNK, stream)
@@ -433,7 +433,7 @@ def run_config3(args, world, rank, dev, stream):
     sustained = {"kernel_ms_median": round(sus_ms[len(sus_ms) // 2], 4),
                  "kernel_ms_mean": round(float(np.mean(sus_ms)), 4), "calls": len(sus_ms),
                  "note": "200 back-to-back calls after the timed steps (the package at its 1400 W cap; "
-                         "DESIGN.md 1.6); reported only"}
+                         "DESIGN_LOG.md 1.6); reported only"}
     # the timed call's own outputs: 256 sampled chunks against the oracle
     torch.cuda.synchronize()
     host_out = out.cpu().numpy().view(np.uint32)

@@ -163,7 +163,7 @@ void zscrc_stats(uint64_t out[4]);
  * (falling back to the CPU silently if that fails, unless ZSCRC_STRICT=1).
  * Two thresholds: the warm one once this process has a device context, the
  * cold one before (the first GPU call pays HIP init).  Defaults: the
- * crossovers against one CPU core measured on MI355X (DESIGN.md §5,
+ * crossovers against one CPU core measured on MI355X (DESIGN.md §8,
  * profiles/r04/crossover.jsonl); env ZSCRC_GPU_MIN sets both, 0 = never;
  * ZSCRC_GPU_MIN_COLD the cold one alone.  zscrc_set_gpu_min sets both. */
 void zscrc_set_gpu_min(uint64_t min_bytes);

@@ -2,7 +2,7 @@
 
 Round 4's faulting A/B build widened ``__builtin_amdgcn_readfirstlane``'s
 ``int`` result straight into a 64-bit address, which sign-extends from 2^31
-(DESIGN.md 1.8).  The kernels now read lanes only through ``rfl_u32`` /
+(DESIGN_LOG.md 1.8).  The kernels now read lanes only through ``rfl_u32`` /
 ``rl_u32``, which return ``uint32_t``; this test keeps it that way."""
 import os
 import re

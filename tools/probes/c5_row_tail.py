@@ -1,4 +1,4 @@
-"""The parts of config 5's fixed per-step tail at N ranks (DESIGN.md 3.1),
+"""The parts of config 5's fixed per-step tail at N ranks (DESIGN.md §4.1),
 measured on one GPU: the device pass with its digest row vs with the block
 copy back (event-timed, 20 passes each, medians), the copy of N rows to the
 host, and the host's unpack + merge of N rows.  Run under rocprofv3

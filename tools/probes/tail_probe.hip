@@ -1,5 +1,5 @@
 // tail_probe: is the last ~10 % of a persistent streaming launch (waves
-// ending between p10 and max) recoverable by handing the work
+// ending between p10 and max, DESIGN_LOG.md 1.7) recoverable by handing the work
 // out dynamically?  4 GiB of non-temporal coalesced reads (stream_read_kernel's
 // shape: 4 KiB blocks, a wave's next block in flight), one 1024-thread block
 // per CU; static = blocks strided over the waves (the product's walk),

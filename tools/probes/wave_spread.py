@@ -18,7 +18,7 @@ from zeroskip_amd._lib import check, lib  # noqa: E402
 
 def waves(name, fn, nwaves, per_block):
     buf = torch.zeros(nwaves * 4, dtype=torch.int64, device="cuda")
-    for _ in range(30):            # the power controller settles under load
+    for _ in range(30):            # the power controller settles under load (DESIGN_LOG.md 1.6)
         fn()
     torch.cuda.synchronize()
     check(lib().zscrc_diag_wave_times(buf.data_ptr()), "wave times")

@@ -66,7 +66,7 @@ __device__ __forceinline__ void gstore32(const void *p, uint32_t v)
 
 /* The only readfirstlane / readlane in this file.  The builtins return int:
  * widened straight into a 64-bit value they sign-extend from 2^31 (s_bfe_i64;
- * round 4's faulting A/B build), so every use goes through
+ * round 4's faulting A/B build, DESIGN_LOG.md 1.8), so every use goes through
  * these, which return uint32_t -- a 64-bit widening of the result is then a
  * zero extension by construction (tests/test_kernel_source.py). */
 __device__ __forceinline__ uint32_t rfl_u32(uint32_t v)
@@ -2265,7 +2265,7 @@ __global__ __launch_bounds__(WG) void multi64_kernel(BatchDesc d, MultiBatch m, 
  * one contiguous 2 KiB block after the group's reads -- eight coalesced
  * 256-byte stores back to back instead of two after every chunk.  Config 2's
  * counters put its stall on load latency under the mix of reads and result
- * writes; this tests whether fewer, larger write bursts shorten
+ * writes (DESIGN_LOG.md 1.7); this tests whether fewer, larger write bursts shorten
  * it.  Tuning bit 1 << 20 (both forms, diagnostic): no hashing -- each result
  * is the XOR of its record's words (wrong results), the load + store shape
  * alone.
@@ -2564,7 +2564,7 @@ __device__ __forceinline__ void burst_issue(const BRec &b, uintptr_t dummy, uint
  * loads bytes [16g, 16g+16) of every piece of the records owned by lanes
  * (t, c), t = 0..3 -- each load instruction reads 16 pieces of 64 contiguous
  * bytes (16-32 cache lines) instead of 64 scattered 16-byte pieces (64 lines,
- * the TA-bound shape of the plain burst).  xpose_burst then
+ * the TA-bound shape of the plain burst, DESIGN_LOG.md 1.3).  xpose_burst then
  * hands every lane its own record's pieces (tools/probes/xpose_probe.hip).  The
  * owners' grid base, piece count and burst flag come over ds_bpermute.  Call
  * with every lane of the wave active. */
@@ -4519,7 +4519,7 @@ __global__ __launch_bounds__(1024) void cpass_row_kernel(CPassRowArgs a)
  * read, from coalesced reads of the descriptors and CRCs.  Measured against
  * the stores from inside the read pass: 1.025 vs 0.977 ms on config 4 -- the
  * scatter alone ~0.485 ms, the ten million partial-sector writes cost the
- * same wherever they are issued (DESIGN.md 1.9).  user_status (may be
+ * same wherever they are issued (DESIGN.md §5).  user_status (may be
  * NULL): the caller's status array, 1 written / 2 none. */
 __global__ __launch_bounds__(256) void commit_scatter_kernel(uint8_t *base, const uint64_t *__restrict__ off,
                                                              const uint64_t *__restrict__ len,
