@@ -27,6 +27,9 @@ extern "C" {
 const uint32_t *zscrc_internal_gtab(void);
 int zs_launch_cpass_post(const zs::CPassArgs *a, const uint32_t *gtab, hipStream_t stream);
 int zs_launch_cpass_row(const zs::CPassRowArgs *a, hipStream_t stream);
+int zscrc_internal_verdict_prezeroed(const void *d_image, uint64_t image_size, const uint64_t *d_span_off,
+                                     const uint64_t *d_span_len, size_t n, uint64_t max_len, uint64_t *d_nbad,
+                                     uint64_t *d_bad, size_t cap, void *stream);
 uint32_t zs_gf2_xpow8n(uint64_t n);
 uint32_t zs_gf2_mul(uint32_t a, uint32_t b);
 }
@@ -46,7 +49,12 @@ struct zscrc_cpass {
      * span_status[64] (i32), flags[LIST_CAP] (u32), bad[LIST_CAP] (u64)
      * (written by the post kernel) -- the block goes back to the host every
      * pass */
-    uint8_t *dblk = nullptr;
+    /* two device blocks, used by consecutive passes in turn: a pass's post
+     * kernel zeroes the other block's counters for the next pass, so no
+     * memset launch precedes a pass (two fill kernels of ~4.5 us and their
+     * gaps per pass until then) */
+    uint8_t *dblk = nullptr;   /* 2 x BLK */
+    int blk_next = 0;
     uint8_t *hblk = nullptr;   /* NSLOT host blocks (zscrc_cpass_submit / _collect) */
     hipEvent_t done[2] = {};   /* each slot's copy back */
     bool pending[2] = {};
@@ -122,7 +130,9 @@ extern "C" int zscrc_cpass_create(zscrc_cpass **out, const zscrc_cpass_spec *spe
     std::vector<uint32_t> init(spec->nspans);
     for (size_t k = 0; k < spec->nspans; ++k)
         init[k] = zs_gf2_mul(0xFFFFFFFFu, zs_gf2_xpow8n(p->span_len[k]));
-    hipError_t e = hipMalloc(&p->dblk, BLK);
+    hipError_t e = hipMalloc(&p->dblk, 2 * BLK);
+    if (e == hipSuccess)
+        e = hipMemset(p->dblk, 0, 2 * BLK); /* both blocks' counters start at 0 */
     if (e == hipSuccess)
         e = hipHostMalloc(reinterpret_cast<void **>(&p->hblk), NSLOT * BLK, hipHostMallocDefault);
     for (int k = 0; k < NSLOT && e == hipSuccess; ++k)
@@ -236,7 +246,7 @@ extern "C" int zscrc_cpass_set_row(zscrc_cpass *p, const zscrc_cpass_row_spec *r
         return ZSCRC_EHIP;
     zs::CPassRowArgs &a = p->row;
     memset(&a, 0, sizeof a);
-    a.blk = p->dblk;
+    a.blk = p->dblk; /* set per pass: the block it used */
     a.off_raw = OFF_RAW;
     a.off_st = OFF_ST;
     a.off_flags = OFF_FLAGS;
@@ -256,7 +266,7 @@ extern "C" int zscrc_cpass_set_row(zscrc_cpass *p, const zscrc_cpass_row_spec *r
 }
 
 namespace {
-int cpass_enqueue(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0);
+int cpass_enqueue(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, uint8_t **blk);
 }
 
 extern "C" int zscrc_cpass_submit_row(zscrc_cpass *p, void *stream, void *start_event, void *end_event,
@@ -268,9 +278,11 @@ extern "C" int zscrc_cpass_submit_row(zscrc_cpass *p, void *stream, void *start_
     if (!od.ok)
         return ZSCRC_EHIP;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    int rc = cpass_enqueue(p, s, static_cast<hipEvent_t>(start_event));
+    uint8_t *blk = nullptr;
+    int rc = cpass_enqueue(p, s, static_cast<hipEvent_t>(start_event), &blk);
     if (!rc) {
         zs::CPassRowArgs a = p->row;
+        a.blk = blk;
         a.row = d_row;
         if (zs_launch_cpass_row(&a, s))
             rc = ZSCRC_EHIP;
@@ -286,13 +298,14 @@ namespace {
  * and the copy of the small block into host slot `slot`; nothing waits. */
 int cpass_submit(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1, int slot)
 {
-    int rc = cpass_enqueue(p, s, ev0);
+    uint8_t *blk = nullptr;
+    int rc = cpass_enqueue(p, s, ev0, &blk);
     /* the post kernel wrote the listed part of the verdict next to the
      * counters: one copy back (two device-to-device copies of the lists
      * before it cost a launch each).  The next pass on this stream rewrites
      * the device block only after this copy (stream order), so two passes
      * can be in flight with their host slots apart. */
-    if (!rc && hipMemcpyAsync(p->hblk + slot * BLK, p->dblk, BLK, hipMemcpyDeviceToHost, s) != hipSuccess)
+    if (!rc && hipMemcpyAsync(p->hblk + slot * BLK, blk, BLK, hipMemcpyDeviceToHost, s) != hipSuccess)
         rc = ZSCRC_EHIP;
     /* the end event right behind the copy back: the device's part of the
      * pass, without the host's wait and the list sorting */
@@ -305,18 +318,22 @@ int cpass_submit(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1, 
     return rc;
 }
 
-/* The pass's kernels: verdict batch, raw spans, post kernel (into dblk). */
-int cpass_enqueue(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0)
+/* The pass's kernels: verdict batch, raw spans, post kernel, into the next
+ * of the two device blocks (*blk).  Passes must follow one another in
+ * stream order (one stream, or the caller's own ordering): the blocks'
+ * counters are zeroed by the previous pass. */
+int cpass_enqueue(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, uint8_t **blk)
 {
     if (ev0 && hipEventRecord(ev0, s) != hipSuccess)
         return ZSCRC_EHIP;
     const zscrc_cpass_spec &sp = p->spec;
-    uint64_t *d_nbad = reinterpret_cast<uint64_t *>(p->dblk);
-    uint32_t *d_raw = reinterpret_cast<uint32_t *>(p->dblk + OFF_RAW);
-    int rc = zscrc_device_verify_commits_verdict(sp.d_image, sp.image_size, sp.d_off, sp.d_len, nullptr, sp.n,
-                                                 sp.max_len, d_nbad, p->dbad_full, p->cap, s);
-    if (!rc && hipMemsetAsync(p->dblk + 8, 0, 8, s) != hipSuccess)
-        rc = ZSCRC_EHIP;
+    uint8_t *b = p->dblk + p->blk_next * BLK, *other = p->dblk + (p->blk_next ^ 1) * BLK;
+    p->blk_next ^= 1;
+    *blk = b;
+    uint64_t *d_nbad = reinterpret_cast<uint64_t *>(b);
+    uint32_t *d_raw = reinterpret_cast<uint32_t *>(b + OFF_RAW);
+    int rc = zscrc_internal_verdict_prezeroed(sp.d_image, sp.image_size, sp.d_off, sp.d_len, sp.n, sp.max_len,
+                                              d_nbad, p->dbad_full, p->cap, s);
     /* raw spans: up to 8 of >= 16 KiB per launch pair, else one by one */
     const uint8_t *img = static_cast<const uint8_t *>(sp.d_image);
     for (size_t i = 0; !rc && i < sp.nspans;) {
@@ -347,17 +364,22 @@ int cpass_enqueue(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0)
         a.nbad = reinterpret_cast<const unsigned long long *>(d_nbad);
         a.bad = p->dbad_full;
         a.cap = p->cap;
-        a.flags = reinterpret_cast<uint32_t *>(p->dblk + OFF_FLAGS);
-        a.bad_out = reinterpret_cast<uint64_t *>(p->dblk + OFF_BAD);
+        a.flags = reinterpret_cast<uint32_t *>(b + OFF_FLAGS);
+        a.bad_out = reinterpret_cast<uint64_t *>(b + OFF_BAD);
         a.out_cap = LIST_CAP;
-        a.nstale = reinterpret_cast<unsigned long long *>(p->dblk + 8);
+        a.nstale = reinterpret_cast<unsigned long long *>(b + 8);
+        a.next_counters = reinterpret_cast<unsigned long long *>(other);
         a.nspans = (uint32_t)sp.nspans;
         a.span_raw = d_raw;
         a.span_commit = p->dspan_commit;
         a.span_init = p->dspan_init;
-        a.span_status = reinterpret_cast<int32_t *>(p->dblk + OFF_ST);
+        a.span_status = reinterpret_cast<int32_t *>(b + OFF_ST);
         if (zs_launch_cpass_post(&a, zscrc_internal_gtab(), s))
             rc = ZSCRC_EHIP;
+    }
+    if (rc) { /* a pass cut short did not zero the next block: start both over */
+        (void)hipMemsetAsync(b, 0, 16, s);
+        (void)hipMemsetAsync(other, 0, 16, s);
     }
     return rc;
 }

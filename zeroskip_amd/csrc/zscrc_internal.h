@@ -104,6 +104,7 @@ struct BatchDesc {
      * every commit whose status is not 1 is counted in *bad_count and its
      * index stored in bad_idx[<bad_cap] (any order) */
     unsigned long long *bad_count;
+    uint32_t bad_prezeroed;  /* verdict: *bad_count already 0 on the stream (no memset launch) */
     uint64_t *bad_idx;
     uint64_t bad_cap;
     const struct SplitPlan *plan;
@@ -217,6 +218,7 @@ struct CPassArgs {
     const int64_t *span_commit;  /* image offset of the span's commit record, -1 = none here */
     const uint32_t *span_init;   /* shift(~0, span length): the register of ~0 after the span */
     int32_t *span_status;        /* 1 ok, 0 mismatch, 2 no commit record, -1 not checked */
+    unsigned long long *next_counters; /* the next pass's [nbad, nstale]: zeroed here */
 };
 
 /* cpass_row_kernel: one rank's digest of a consistent pass as the fixed-shape

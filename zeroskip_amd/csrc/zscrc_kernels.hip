@@ -3535,6 +3535,11 @@ __device__ __forceinline__ uint32_t crc_word(const char *T, uint32_t r, uint64_t
 __global__ __launch_bounds__(256) void cpass_post_kernel(CPassArgs a, const uint32_t *__restrict__ gtab)
 {
     __shared__ __attribute__((aligned(16))) char T[4096];
+    /* the next pass's block: nothing reads it during this pass (its last
+     * copy back ran before this pass's kernels), so its counters are zeroed
+     * here instead of by a memset launch ahead of the next pass */
+    if (a.next_counters && blockIdx.x == 0 && threadIdx.x < 2)
+        a.next_counters[threadIdx.x] = 0ull;
     load_gmul_table(T, gtab); /* GT_S4, compact: table j at 1024 j */
     __syncthreads();
     const uint64_t nbad = *a.nbad, nl = nbad < a.cap ? nbad : a.cap;
