@@ -453,7 +453,8 @@ typedef struct zscrc_cpass_spec {
 } zscrc_cpass_spec;
 typedef struct zscrc_cpass_result {
     uint64_t n_bad;               /* commits that do not verify (undecided incl.) */
-    uint64_t n_stale;             /* finalise-quirk commits                       */
+    uint64_t n_stale;             /* finalise-quirk commits (among the listed ones
+                                   * when the pass is not complete)                */
     uint64_t n_undecided;         /* zero-length commits after a long span or with a
                                    * long trailer: the caller decides (indices below) */
     int32_t complete;             /* 0: more mismatches than one pass lists       */

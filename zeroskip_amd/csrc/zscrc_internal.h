@@ -219,6 +219,11 @@ struct CPassArgs {
     const uint32_t *span_init;   /* shift(~0, span length): the register of ~0 after the span */
     int32_t *span_status;        /* 1 ok, 0 mismatch, 2 no commit record, -1 not checked */
     unsigned long long *next_counters; /* the next pass's [nbad, nstale]: zeroed here */
+    /* host_nbad != NULL: flags / bad_out / span_status point into a pinned
+     * host block, and the kernel also writes *nbad and the span registers
+     * there (host_raw) -- no copy back after it */
+    uint64_t *host_nbad;
+    uint32_t *host_raw;
 };
 
 /* cpass_row_kernel: one rank's digest of a consistent pass as the fixed-shape

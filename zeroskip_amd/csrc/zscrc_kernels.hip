@@ -3540,6 +3540,12 @@ __global__ __launch_bounds__(256) void cpass_post_kernel(CPassArgs a, const uint
      * here instead of by a memset launch ahead of the next pass */
     if (a.next_counters && blockIdx.x == 0 && threadIdx.x < 2)
         a.next_counters[threadIdx.x] = 0ull;
+    if (a.host_nbad && blockIdx.x == 0) { /* the pass's count and span registers, straight to the host */
+        if (threadIdx.x == 0)
+            *a.host_nbad = *a.nbad;
+        for (uint32_t k = threadIdx.x; k < a.nspans; k += blockDim.x)
+            a.host_raw[k] = a.span_raw[k];
+    }
     load_gmul_table(T, gtab); /* GT_S4, compact: table j at 1024 j */
     __syncthreads();
     const uint64_t nbad = *a.nbad, nl = nbad < a.cap ? nbad : a.cap;
