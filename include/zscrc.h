@@ -482,7 +482,9 @@ int zscrc_cpass_run_timed(zscrc_cpass *p, void *stream, void *start_event, void 
  * zscrc_cpass_run_timed) with the copy back into host slot `slot` (0 or 1)
  * and returns at once; collect waits for that slot's copy and fills `res`.
  * A slot holds one submitted pass until it is collected (ZSCRC_EINVAL
- * otherwise).  Passes on one stream run in order. */
+ * otherwise).  Passes on one stream run in order.  A submit's end_event
+ * (may be NULL) is also what its collect waits on: record it again only
+ * after that collect. */
 int zscrc_cpass_submit(zscrc_cpass *p, void *stream, void *start_event, void *end_event, int slot);
 int zscrc_cpass_collect(zscrc_cpass *p, int slot, zscrc_cpass_result *res);
 /* The pass's digest as a fixed-shape int64 row in DEVICE memory, for ranks

@@ -56,7 +56,8 @@ struct zscrc_cpass {
     uint8_t *dblk = nullptr;   /* 2 x BLK */
     int blk_next = 0;
     uint8_t *hblk = nullptr;   /* NSLOT host blocks (zscrc_cpass_submit / _collect) */
-    hipEvent_t done[2] = {};   /* each slot's copy back */
+    hipEvent_t done[2] = {};   /* each slot's completion */
+    hipEvent_t wait[2] = {};   /* what collect waits on: done[], or the caller's end event */
     bool pending[2] = {};
     /* the digest row (zscrc_cpass_set_row / _submit_row) */
     bool have_row = false;
@@ -307,7 +308,10 @@ int cpass_submit(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1, 
      * pass, without the host's wait and the list sorting */
     if (!rc && ev1 && hipEventRecord(ev1, s) != hipSuccess)
         rc = ZSCRC_EHIP;
-    if (!rc && hipEventRecord(p->done[slot], s) != hipSuccess)
+    /* the caller's end event doubles as the slot's completion (one event
+     * record less between passes); otherwise the slot's own */
+    p->wait[slot] = ev1 ? ev1 : p->done[slot];
+    if (!rc && !ev1 && hipEventRecord(p->done[slot], s) != hipSuccess)
         rc = ZSCRC_EHIP;
     if (!rc)
         p->pending[slot] = true;
@@ -389,7 +393,7 @@ int cpass_enqueue(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, uint8_t **blk, 
 int cpass_collect(zscrc_cpass *p, int slot, zscrc_cpass_result *res)
 {
     p->pending[slot] = false;
-    if (hipEventSynchronize(p->done[slot]) != hipSuccess)
+    if (hipEventSynchronize(p->wait[slot]) != hipSuccess)
         return ZSCRC_EHIP;
     const zscrc_cpass_spec &sp = p->spec;
     const uint8_t *blk = p->hblk + slot * BLK;
