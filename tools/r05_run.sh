@@ -44,6 +44,10 @@ for step in "$@"; do
     rehearse3)
               BENCH_SHARE_GPU=1 BENCH_DIST=gloo timeout -k 10 600 python bench.py --gpus 2 --workload config3 \
                 --no-cpu > gpurun_out/rehearse3_n2.json 2> gpurun_out/rehearse3_n2.err ;;
+    tracenb)  ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+                -d $R/gpurun_out/tracenb -o run -- python3 $R/tools/prof_case.py config4nb 20 > $R/gpurun_out/tracenb.log 2>&1 ) ;;
+    ab4em)    AB_CASES=config4_verify,config4_crcs,config4_write_nocrc,config4_write,config4_verdict timeout -k 10 600 \
+                python tools/opt_ab.py 0 128 > gpurun_out/ab4em.jsonl 2> gpurun_out/ab4em.err ;;
     cputhreads) timeout -k 10 300 python tools/probes/cpu_threads.py > gpurun_out/cpu_threads.jsonl \
                 2> gpurun_out/cpu_threads.err ;;
     ab3)      AB_CASES=config3,fixed_16KiB,fixed_4KiB,fixed_1MiB timeout -k 10 600 python tools/opt_ab.py 0 32 \
