@@ -1,0 +1,210 @@
+/*
+ * Format-layer demonstrator (TEST INFRASTRUCTURE ONLY): the reference's OWN
+ * writer and verifier -- src/zeroskip-file.c, zeroskip-record.c,
+ * zeroskip-header.c and mfile.c (with util.c, log.c, cstring.c), compiled
+ * unmodified from /root/reference by oracle/Makefile's `ref-format` target --
+ * linked against libzscrc.so instead of src/crc32c.c.  Every CRC these
+ * sources compute goes through the drop-in crc32c / crc32c_hw symbols.
+ * tests/test_reference_format.py drives it and holds oracle/zs_format.py and
+ * the product's walk / GPU verifier to what it writes and what it accepts.
+ *
+ * usage: format_demo write OUT BLOB < OPS
+ *   one op per line; key/value bytes are slices of the file BLOB:
+ *     H <uuid hex32> <startidx> <endidx>  zs_header_write (zeroskip-header.c:30)
+ *     A <koff> <klen> <voff> <vlen>       zsdb_add's file half (zeroskip.c:930-936):
+ *                                         crc32_begin unless one is running,
+ *                                         zs_file_write_keyval_record
+ *     D <koff> <klen>                     zsdb_remove's file half (zeroskip.c:985-987):
+ *                                         crc32_begin always, zs_file_write_delete_record
+ *     a <koff> <klen> <voff> <vlen>       zs_file_write_keyval_record alone (the packed
+ *                                         writer, zeroskip-packed.c:163-176)
+ *     d <koff> <klen>                     zs_file_write_delete_record alone
+ *     C                                   zs_file_write_commit_record(f, 0)
+ *     F                                   zs_file_write_commit_record(f, 1)
+ *     B                                   crc32_begin alone (zeroskip-packed.c:424, :449)
+ *     P <count> <off>...                  the packed pointer section's words, big-endian
+ *   prints {"size": N}
+ *
+ * usage: format_demo verify FILE
+ *   zs_header_validate (zeroskip-header.c:105), then zs_record_read_from_file
+ *   (zeroskip-record.c:283) from offset 40 until the offset stops moving.
+ *   Prints one JSON line: the header rc, each short commit's offset and rc,
+ *   the long commits met (listed, not verified: zeroskip-record.c:258 hands
+ *   the length VALUE to crc32c_hw as a pointer, so the reference's own
+ *   verifier cannot run on them), and the offset the walk stopped at.
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <libzeroskip/mfile.h>
+#include <libzeroskip/zeroskip.h>
+
+#include "zeroskip-priv.h"
+
+static int hexbyte(const char *s)
+{
+    unsigned v;
+    return sscanf(s, "%2x", &v) == 1 ? (int)v : -1;
+}
+
+static unsigned char *load(const char *path, size_t *n)
+{
+    FILE *fp = fopen(path, "rb");
+    if (!fp)
+        return NULL;
+    fseek(fp, 0, SEEK_END);
+    *n = (size_t)ftell(fp);
+    fseek(fp, 0, SEEK_SET);
+    unsigned char *p = malloc(*n ? *n : 1);
+    if (p && fread(p, 1, *n, fp) != *n) {
+        free(p);
+        p = NULL;
+    }
+    fclose(fp);
+    return p;
+}
+
+static int do_write(const char *out, const char *blobpath)
+{
+    size_t nblob = 0;
+    unsigned char *blob = load(blobpath, &nblob);
+    if (!blob) {
+        perror("blob");
+        return 1;
+    }
+    struct zsdb_file f;
+    memset(&f, 0, sizeof f);
+    f.type = DB_FTYPE_ACTIVE;
+    if (mfile_open(out, MFILE_RW_CR, &f.mf) != 0) {
+        perror("mfile_open");
+        return 1;
+    }
+    f.is_open = 1;
+    char line[1 << 16];
+    int rc = 0;
+    while (!rc && fgets(line, sizeof line, stdin)) {
+        unsigned long long a, b, c, d;
+        char hex[64];
+        switch (line[0]) {
+        case 'H':
+            if (sscanf(line + 1, "%32s %llu %llu", hex, &a, &b) != 3 || strlen(hex) != 32)
+                return 2;
+            f.header.signature = ZS_SIGNATURE;
+            f.header.version = ZS_VERSION;
+            for (int i = 0; i < 16; ++i)
+                f.header.uuid[i] = (unsigned char)hexbyte(hex + 2 * i);
+            f.header.startidx = (uint32_t)a;
+            f.header.endidx = (uint32_t)b;
+            rc = zs_header_write(&f);
+            break;
+        case 'A':
+        case 'a':
+            if (sscanf(line + 1, "%llu %llu %llu %llu", &a, &b, &c, &d) != 4 || a + b > nblob ||
+                c + d > nblob)
+                return 2;
+            if (line[0] == 'A' && !f.mf->compute_crc)
+                crc32_begin(&f.mf);
+            rc = zs_file_write_keyval_record(&f, blob + a, b, blob + c, d);
+            break;
+        case 'D':
+        case 'd':
+            if (sscanf(line + 1, "%llu %llu", &a, &b) != 2 || a + b > nblob)
+                return 2;
+            if (line[0] == 'D')
+                crc32_begin(&f.mf);
+            rc = zs_file_write_delete_record(&f, blob + a, b);
+            break;
+        case 'C':
+        case 'F':
+            rc = zs_file_write_commit_record(&f, line[0] == 'F');
+            break;
+        case 'B':
+            crc32_begin(&f.mf);
+            break;
+        case 'P': {
+            char *s = line + 1;
+            while (!rc && *s && *s != '\n') {
+                char *e;
+                unsigned long long v = strtoull(s, &e, 10);
+                if (e == s)
+                    break;
+                s = e;
+                unsigned char w[8];
+                for (int i = 0; i < 8; ++i)
+                    w[i] = (unsigned char)(v >> (56 - 8 * i));
+                uint64_t nb;
+                rc = mfile_write(&f.mf, w, 8, &nb);
+            }
+            break;
+        }
+        default:
+            return 2;
+        }
+    }
+    if (rc) {
+        fprintf(stderr, "reference writer returned %d\n", rc);
+        return 1;
+    }
+    uint64_t size = f.mf->offset;
+    if (mfile_flush(&f.mf) != 0 || mfile_close(&f.mf) != 0)
+        return 1;
+    free(blob);
+    printf("{\"size\": %llu}\n", (unsigned long long)size);
+    return 0;
+}
+
+static int do_verify(const char *path)
+{
+    struct zsdb_file f;
+    memset(&f, 0, sizeof f);
+    f.type = DB_FTYPE_ACTIVE;
+    if (mfile_open(path, MFILE_RD, &f.mf) != 0) {
+        perror("mfile_open");
+        return 1;
+    }
+    f.is_open = 1;
+    size_t size = 0;
+    mfile_size(&f.mf, &size);
+    printf("{\"header\": %d, \"commits\": [", zs_header_validate(&f));
+    uint64_t off = ZS_HDR_SIZE;
+    const char *sep = "", *why = "end";
+    char longs[1 << 14] = "";
+    size_t nl = 0;
+    while (off + 8 <= size) {
+        const unsigned char t = f.mf->ptr[off];
+        if (t == REC_TYPE_LONG_COMMIT) {
+            nl += (size_t)snprintf(longs + nl, sizeof longs - nl, "%s%llu", nl ? ", " : "",
+                                   (unsigned long long)off);
+            if (nl >= sizeof longs)
+                return 1;
+            off += ZS_LONG_COMMIT_REC_SIZE;
+            continue;
+        }
+        const uint64_t before = off;
+        const int rc = zs_record_read_from_file(&f, &off, NULL, NULL, NULL);
+        if (t == REC_TYPE_COMMIT) {
+            printf("%s[%llu, %d]", sep, (unsigned long long)before, rc);
+            sep = ", ";
+        }
+        if (off == before) {
+            why = "stopped";
+            break;
+        }
+    }
+    printf("], \"long_commits\": [%s], \"stop\": %llu, \"why\": \"%s\"}\n", longs,
+           (unsigned long long)off, why);
+    mfile_close(&f.mf);
+    return 0;
+}
+
+int main(int argc, char **argv)
+{
+    if (argc == 4 && strcmp(argv[1], "write") == 0)
+        return do_write(argv[2], argv[3]);
+    if (argc == 3 && strcmp(argv[1], "verify") == 0)
+        return do_verify(argv[2]);
+    fprintf(stderr, "usage: %s write OUT BLOB < OPS | verify FILE\n", argv[0]);
+    return 2;
+}

@@ -1,0 +1,178 @@
+"""Zeroskip file images written by the reference's OWN format code, and what
+the reference's OWN verifier says about them (TEST INFRASTRUCTURE ONLY).
+
+oracle/_ref/format_demo (tests/c/format_demo.c; oracle/Makefile `ref-format`)
+runs src/zeroskip-file.c, -record.c, -header.c and mfile.c compiled unmodified
+from /root/reference.  `Script` feeds it a sequence of zsdb_add / zsdb_remove
+/ commit steps and mirrors each step into oracle/zs_format.FileWriter, so a
+test can hold the oracle to the reference byte for byte.
+
+Run as a script (where /root/reference exists) it regenerates
+tests/golden/ref_format/: a few small images (`*.zs`) and manifest.json with
+the reference verifier's verdict on each.  The GPU box has no reference; the
+GPU tests (tests/test_gpu_ref_format.py) read those fixtures.
+"""
+from __future__ import annotations
+
+import json
+import os
+import random
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+from oracle import zs_format as zf  # noqa: E402
+
+DEMO = os.path.join(ROOT, "oracle", "_ref", "format_demo")
+OUTDIR = os.path.join(ROOT, "tests", "golden", "ref_format")
+
+
+def build_demo() -> str:
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "ref-format"])
+    return DEMO
+
+
+class Script:
+    """One file's worth of format_demo ops, mirrored into the oracle writer."""
+
+    def __init__(self, uuid: bytes, idx: int = 0):
+        self.blob = bytearray()
+        self.ops = [f"H {uuid.hex()} {idx} {idx}"]
+        self.fw = zf.FileWriter(uuid, idx)
+
+    def _put(self, b: bytes) -> int:
+        off = len(self.blob)
+        self.blob += b
+        return off
+
+    def add(self, key: bytes, val: bytes):
+        self.ops.append(f"A {self._put(key)} {len(key)} {self._put(val)} {len(val)}")
+        self.fw.add(key, val)
+
+    def remove(self, key: bytes):
+        self.ops.append(f"D {self._put(key)} {len(key)}")
+        self.fw.remove(key)
+
+    def commit(self):
+        """zsdb_commit's file half; with no span running it is the finalise
+        commit over the stale register (FileWriter.finalise)."""
+        self.ops.append("C")
+        if self.fw.begin is None:
+            self.fw.finalise()
+        else:
+            self.fw.commit()
+
+    def run(self, path: str) -> bytes:
+        return run_ops(self.ops, bytes(self.blob), path)
+
+
+def packed_ops(uuid: bytes, startidx: int, endidx: int, records):
+    """format_demo ops for zs_packed_file_new_from_memtree's writes
+    (zeroskip-packed.c:384-473) over records [(key, value-or-None)] in key
+    order; returns (ops, blob)."""
+    blob = bytearray()
+    ops = [f"H {uuid.hex()} {startidx} {endidx}", "B"]
+    ptrs, off = [], zf.HDR_SIZE
+    for k, v in records:
+        ptrs.append(off)
+        ko = len(blob)
+        blob += k
+        if v is None:
+            ops.append(f"d {ko} {len(k)}")
+            off += len(zf.delete_record(k))
+        else:
+            vo = len(blob)
+            blob += v
+            ops.append(f"a {ko} {len(k)} {vo} {len(v)}")
+            off += len(zf.key_record(k)) + len(zf.value_record(v))
+    ops += ["C", "B", "P " + " ".join(str(x) for x in [len(ptrs)] + ptrs), "F"]
+    return ops, bytes(blob)
+
+
+def run_ops(ops, blob: bytes, path: str) -> bytes:
+    with tempfile.NamedTemporaryFile(suffix=".blob") as b:
+        b.write(blob)
+        b.flush()
+        if os.path.exists(path):
+            os.unlink(path)
+        out = subprocess.run([DEMO, "write", path, b.name], input="\n".join(ops) + "\n",
+                             capture_output=True, text=True, timeout=300)
+    if out.returncode != 0:
+        raise RuntimeError(f"format_demo write: rc {out.returncode}: {out.stderr}")
+    with open(path, "rb") as f:
+        return f.read()
+
+
+def ref_verify(path: str) -> dict:
+    out = subprocess.run([DEMO, "verify", path], capture_output=True, text=True, timeout=300)
+    if out.returncode != 0:
+        raise RuntimeError(f"format_demo verify: rc {out.returncode}: {out.stderr}")
+    return json.loads(out.stdout)
+
+
+def mixed_script(seed: int, ntxn: int = 40, long_key: bool = False, stale: bool = True) -> Script:
+    """Transactions of 1-8 adds / removes; keys 1-40 bytes (plus the 65535 /
+    65536 short/long boundary when long_key), values 0-300 bytes; after some
+    commits a second commit with no span running (the finalise case)."""
+    rng = random.Random(seed)
+    s = Script(bytes(rng.randrange(256) for _ in range(16)), rng.randrange(8))
+    for t in range(ntxn):
+        for _ in range(rng.randint(1, 8)):
+            klen = rng.randint(1, 40)
+            if long_key and rng.random() < 0.05:
+                klen = rng.choice([65535, 65536, 70001])
+            key = bytes(rng.randrange(256) for _ in range(klen))
+            if rng.random() < 0.25 and klen <= zf.MAX_SHORT_KEY_LEN:
+                s.remove(key)
+            else:
+                s.add(key, bytes(rng.randrange(256) for _ in range(rng.randint(0, 300))))
+        s.commit()
+        if stale and rng.random() < 0.1:
+            s.commit()
+    return s
+
+
+def fixtures() -> dict:
+    """name -> (image bytes, kind) for the committed fixture set."""
+    out = {}
+    with tempfile.TemporaryDirectory() as d:
+        img = mixed_script(11, ntxn=60, stale=False).run(os.path.join(d, "a"))
+        out["active_clean"] = (img, 0)
+        bad = bytearray(img)
+        commits, _, _ = zf.walk(img)
+        for i in (3, 17, 40):                 # one payload byte in three spans
+            c = commits[i]
+            bad[c["span_off"] + c["span_len"] // 2] ^= 0x20
+        out["active_corrupt"] = (bytes(bad), 0)
+        out["active_stale"] = (mixed_script(12, ntxn=50, stale=True).run(os.path.join(d, "b")), 0)
+        out["active_longkey"] = (mixed_script(13, ntxn=12, long_key=True).run(os.path.join(d, "c")), 0)
+        rng = random.Random(14)
+        recs = sorted({b"%016d" % rng.randrange(10 ** 9): (None if rng.random() < 0.2 else
+                                                          bytes(rng.randrange(256) for _ in range(rng.randint(0, 90))))
+                       for _ in range(400)}.items())
+        ops, blob = packed_ops(bytes(range(16)), 2, 5, recs)
+        out["packed"] = (run_ops(ops, blob, os.path.join(d, "p")), 2)
+    return out
+
+
+def main():
+    build_demo()
+    os.makedirs(OUTDIR, exist_ok=True)
+    manifest = {}
+    for name, (img, kind) in fixtures().items():
+        path = os.path.join(OUTDIR, name + ".zs")
+        with open(path, "wb") as f:
+            f.write(img)
+        manifest[name] = dict(kind=kind, size=len(img), reference=ref_verify(path))
+    with open(os.path.join(OUTDIR, "manifest.json"), "w") as f:
+        json.dump(manifest, f, indent=1, sort_keys=True)
+        f.write("\n")
+    print(json.dumps({k: (v["size"], len(v["reference"]["commits"])) for k, v in manifest.items()}))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,84 @@
+"""The GPU verifiers on images the reference's OWN writer produced, held to
+the reference's OWN verifier (tests/golden/ref_format/: written and judged by
+src/zeroskip-file.c / -record.c / -header.c compiled unmodified, see
+tests/golden/make_ref_format.py and tests/test_reference_format.py).
+
+* zscrc_zs_verify_image: the bad commits are exactly the ones the reference
+  rejects (ZS_INVALID_DB from zs_read_and_verify_commit_record, record.c:227-231),
+  finalise commits over the stale register included;
+* zscrc_zs_verify_files over the whole set: the same commits, with the
+  finalise commits that chain from the previous span's CRC reported as
+  stale (src/mfile.c:534-546) rather than bad.
+"""
+import json
+import os
+
+import pytest
+
+from oracle import oracle
+from oracle import zs_format as zf
+from zeroskip_amd import zsfile
+
+pytestmark = pytest.mark.gpu
+
+DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ref_format")
+MANIFEST = json.load(open(os.path.join(DIR, "manifest.json")))
+
+
+def fixture(name):
+    with open(os.path.join(DIR, name + ".zs"), "rb") as f:
+        return f.read()
+
+
+def ref_rejected(name):
+    return [c[0] for c in MANIFEST[name]["reference"]["commits"] if c[1] != 0]
+
+
+def stale_chained(img):
+    """Rejected zero-length commits the oracle reads as finalise commits
+    chained from the previous span's CRC (FileWriter.finalise)."""
+    out, prev = 0, None
+    for c in zf.walk(img)[0]:
+        if not c["ok"] and c["span_len"] == 0 and prev is not None:
+            out += zf._commit_check(img, c["commit_off"], seed=prev)[3:5] == (c["stored"],) * 2
+        if c["span_len"]:
+            prev = oracle.crc32c_hw(0, bytes(img[c["span_off"]:c["commit_off"]]))
+    return out
+
+
+@pytest.mark.parametrize("name", sorted(n for n in MANIFEST if MANIFEST[n]["kind"] == zsfile.ACTIVE))
+def test_verify_image_matches_reference_verifier(gpu, name):
+    img = fixture(name)
+    rep = zsfile.verify_image(img)
+    ref = MANIFEST[name]["reference"]
+    commits = [c["commit_off"] for c in zf.walk(img)[0]]
+    bad = ref_rejected(name)
+    assert rep["header_rc"] == 0 and rep["walk_rc"] == zsfile.END and rep["end_off"] == ref["stop"]
+    assert rep["n_commits"] == len(ref["commits"]) + len(ref["long_commits"]) == len(commits)
+    assert rep["n_bad"] == len(bad)
+    if bad:
+        assert commits[rep["first_bad"]] == bad[0]
+
+
+def test_verify_image_packed_reference_written(gpu):
+    img = fixture("packed")
+    rep = zsfile.verify_image(img, zsfile.PACKED)
+    assert rep["header_rc"] == 0 and rep["n_commits"] == 2 and rep["n_bad"] == 0
+    bad = bytearray(img)
+    bad[MANIFEST["packed"]["reference"]["stop"] + 11] ^= 0x10   # a pointer word
+    rep = zsfile.verify_image(bytes(bad), zsfile.PACKED)
+    assert rep["n_bad"] == 1
+
+
+def test_verify_files_matches_reference_verifier(gpu):
+    names = sorted(MANIFEST)
+    imgs = [fixture(n) for n in names]
+    kinds = [MANIFEST[n]["kind"] for n in names]
+    rep = zsfile.verify_files(imgs, kinds)
+    active = [n for n in names if MANIFEST[n]["kind"] == zsfile.ACTIVE]
+    rejected = sum(len(ref_rejected(n)) for n in active)
+    stale = sum(stale_chained(fixture(n)) for n in active)
+    assert stale > 0
+    assert rep["files"] == len(names) and rep["header_errors"] == 0 and rep["walk_errors"] == 0
+    assert rep["bad_commits"] + rep["stale_empty_commits"] == rejected
+    assert rep["stale_empty_commits"] == stale

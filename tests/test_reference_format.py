@@ -1,0 +1,200 @@
+"""Format-layer parity pinned on the reference's OWN code.
+
+oracle/_ref/format_demo runs the reference's writer and verifier --
+src/zeroskip-file.c (records, commits :188-393), zeroskip-record.c (walk and
+commit verify :188-331), zeroskip-header.c (:30-170) and mfile.c (the CRC
+span, :526-546) -- compiled unmodified from /root/reference
+(oracle/Makefile `ref-format`), linked against libzscrc.so.
+
+* live (where /root/reference exists): images the reference writes from
+  zsdb_add / zsdb_remove / commit steps equal oracle/zs_format.FileWriter's
+  byte for byte (short and long keys, deletes restarting the span, finalise
+  commits over the stale register, long values and long commits, packed
+  files); the reference verifier's verdict on every short commit equals the
+  oracle walk's, on clean and corrupted images; the committed fixtures
+  regenerate bit for bit.
+* fixtures (everywhere, no reference needed): tests/golden/ref_format/ --
+  images the reference wrote and its verifier's verdicts -- against the
+  oracle walk and the product's host walk / header CRC in libzscrc.  The GPU
+  verifier's turn is tests/test_gpu_ref_format.py.
+"""
+import json
+import os
+import random
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle import zs_format as zf
+from tests.golden import make_ref_format as mrf
+from zeroskip_amd import zsfile
+
+REF = "/root/reference"
+HAVE_REF = os.path.isdir(os.path.join(REF, "src")) and os.path.exists("/opt/conda/include/uuid/uuid.h")
+live = pytest.mark.skipif(not HAVE_REF, reason="no /root/reference (or its libuuid header) here")
+MANIFEST = json.load(open(os.path.join(mrf.OUTDIR, "manifest.json")))
+
+
+def fixture(name):
+    with open(os.path.join(mrf.OUTDIR, name + ".zs"), "rb") as f:
+        return f.read()
+
+
+def ref_commit_offsets(rep):
+    return sorted([c[0] for c in rep["commits"]] + rep["long_commits"])
+
+
+# ---------------------------------------------------------------- fixtures
+@pytest.mark.parametrize("name", sorted(MANIFEST))
+def test_fixture_oracle_agrees_with_reference_verdict(name):
+    img, m = fixture(name), MANIFEST[name]
+    rep = m["reference"]
+    assert len(img) == m["size"] and rep["header"] == 0
+    assert zf.header_check(img)[0]
+    rc, stored, computed = zsfile.header_crc(img)
+    assert rc == 0 and stored == computed
+    if m["kind"] == zsfile.PACKED:
+        pc = {c["kind"]: c for c in zf.packed_check(img)}
+        assert pc["records"]["ok"] and pc["pointers"]["ok"]
+        # the reference walk verifies the records commit, then stops at the
+        # pointer count (type byte 0): zeroskip-record.c:324-325
+        assert rep["commits"] == [[pc["records"]["commit_off"], 0]]
+        assert rep["why"] == "stopped" and rep["stop"] == pc["pointers"]["span_off"]
+        off, ln, prc = zsfile.packed_spans(img)
+        assert prc == 0
+        assert sorted(zip(off.tolist(), ln.tolist())) == sorted(
+            (c["span_off"], c["span_len"]) for c in pc.values())
+        return
+    commits, end, why = zf.walk(img)
+    assert why == "end" and end == rep["stop"] == len(img)
+    assert [c["commit_off"] for c in commits] == ref_commit_offsets(rep)
+    verdict = {c[0]: c[1] == 0 for c in rep["commits"]}
+    for c in commits:
+        if c["commit_off"] in verdict:
+            assert c["ok"] == verdict[c["commit_off"]], c
+    off, ln, wrc, wend = zsfile.walk(img)
+    assert wrc == zsfile.END and wend == len(img)
+    assert (off + ln).tolist() == [c["commit_off"] for c in commits]
+    assert ln.tolist() == [c["span_len"] for c in commits]
+
+
+def test_fixture_set_covers_bad_and_stale():
+    bad = {k: sum(c[1] != 0 for c in v["reference"]["commits"]) for k, v in MANIFEST.items()}
+    assert bad["active_clean"] == 0 and bad["active_corrupt"] == 3 and bad["active_stale"] > 0
+
+
+# ---------------------------------------------------------------- live reference
+@pytest.fixture(scope="module")
+def demo():
+    return mrf.build_demo()
+
+
+@live
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_reference_writer_equals_oracle(demo, tmp_path, seed):
+    s = mrf.mixed_script(seed, ntxn=40, long_key=seed % 2 == 0)
+    img = s.run(str(tmp_path / "f"))
+    assert img == s.fw.image()
+    rep = mrf.ref_verify(str(tmp_path / "f"))
+    commits, end, _ = zf.walk(img)
+    assert rep["header"] == 0 and rep["stop"] == end == len(img)
+    assert [c["commit_off"] for c in commits] == ref_commit_offsets(rep)
+    assert {c[0]: c[1] == 0 for c in rep["commits"]} == {c["commit_off"]: c["ok"] for c in commits}
+
+
+@live
+def test_reference_verifier_on_corruption(demo, tmp_path):
+    s = mrf.mixed_script(21, ntxn=60, stale=False)
+    img = s.run(str(tmp_path / "f"))
+    commits, _, _ = zf.walk(img)
+    rng = random.Random(21)
+    for trial in range(6):
+        bad = bytearray(img)
+        hit = sorted(rng.sample(range(len(commits)), 3))
+        for i in hit:
+            c = commits[i]
+            if trial % 2:                      # the stored CRC in the trailer
+                bad[c["commit_off"] + 7] ^= 1 << rng.randrange(8)
+            else:                              # a payload byte inside the span
+                k = c["span_off"] + 24 + rng.randrange(max(1, c["span_len"] - 48))
+                bad[k] ^= 1 << rng.randrange(8)
+        p = tmp_path / f"bad{trial}"
+        p.write_bytes(bytes(bad))
+        rep = mrf.ref_verify(str(p))
+        got = {c[0]: c[1] for c in rep["commits"]}
+        want = {c["commit_off"]: c["ok"] for c in zf.walk(bytes(bad))[0]}
+        assert {o for o, r in got.items() if r != 0} == {commits[i]["commit_off"] for i in hit}
+        assert {o: r == 0 for o, r in got.items()} == want
+
+
+@live
+def test_reference_header_verdict(demo, tmp_path):
+    img = bytearray(mrf.mixed_script(5, ntxn=3).run(str(tmp_path / "f")))
+    for byte in (8, 15, 30, 34, 39):           # version, uuid, start / end index, stored CRC
+        bad = bytearray(img)
+        bad[byte] ^= 0x04
+        p = tmp_path / f"h{byte}"
+        p.write_bytes(bytes(bad))
+        assert mrf.ref_verify(str(p))["header"] == -9      # ZS_INVALID_DB
+        assert not zf.header_check(bytes(bad))[0]
+        rc, stored, computed = zsfile.header_crc(bytes(bad))
+        assert stored != computed
+
+
+@live
+def test_reference_long_value_long_commit(demo, tmp_path):
+    """A span over MAX_SHORT_VAL_LEN: long value record and long commit
+    (zeroskip-file.c:266-302); the reference's verifier cannot check a long
+    commit (zeroskip-record.c:258), so the oracle's long verify is held to the
+    reference WRITER's bytes."""
+    rng = np.random.default_rng(7)
+    s = mrf.Script(bytes(range(16, 32)), 3)
+    s.add(b"small", b"v" * 9)
+    s.commit()
+    s.add(b"big-value", rng.integers(0, 256, zf.MAX_SHORT_VAL_LEN + 9, dtype=np.uint8).tobytes())
+    s.add(b"k" * 70000, b"after")
+    s.commit()
+    s.remove(b"small")
+    s.commit()
+    img = s.run(str(tmp_path / "f"))
+    assert img == s.fw.image()
+    rep = mrf.ref_verify(str(tmp_path / "f"))
+    commits, end, _ = zf.walk(img)
+    assert len(rep["long_commits"]) == 1 and all(c[1] == 0 for c in rep["commits"])
+    assert [c["commit_off"] for c in commits] == ref_commit_offsets(rep)
+    assert all(c["ok"] for c in commits)
+    off, ln, wrc, wend = zsfile.walk(img)
+    assert wrc == zsfile.END and (off + ln).tolist() == ref_commit_offsets(rep)
+
+
+@live
+def test_reference_packed_writer_equals_oracle(demo, tmp_path):
+    rng = random.Random(9)
+    recs = sorted({b"%016d" % rng.randrange(10 ** 9): (None if rng.random() < 0.3 else
+                                                      bytes(rng.randrange(256) for _ in range(rng.randint(0, 200))))
+                   for _ in range(700)}.items())
+    ops, blob = mrf.packed_ops(bytes(range(3, 19)), 4, 9, recs)
+    img = mrf.run_ops(ops, blob, str(tmp_path / "p"))
+    assert img == zf.packed_file(recs, bytes(range(3, 19)), 4, 9)
+    assert zf.packed_records(img) == recs
+
+
+@live
+def test_committed_fixtures_regenerate(demo, tmp_path):
+    for name, (img, kind) in mrf.fixtures().items():
+        assert img == fixture(name), name
+        p = tmp_path / name
+        p.write_bytes(img)
+        assert mrf.ref_verify(str(p)) == MANIFEST[name]["reference"]
+        assert MANIFEST[name]["kind"] == kind
+
+
+@live
+def test_demo_links_reference_objects_unmodified(demo):
+    """format_demo's CRCs resolve in libzscrc.so, and the reference objects it
+    links are the ones `ref-lib` compiled from /root/reference."""
+    out = subprocess.run(["ldd", demo], capture_output=True, text=True, check=True).stdout
+    assert "libzscrc.so" in out and "libuuid" not in out
+    und = subprocess.run(["nm", "-u", demo], capture_output=True, text=True, check=True).stdout.split()
+    assert {"crc32c", "crc32c_hw"} <= set(und)

@@ -6,13 +6,19 @@ where /root/reference is absent (the GPU box).
   header: it is compiled UNMODIFIED (oracle/Makefile `ref`), linked against
   libzscrc.so, and run -- crc32_begin / mfile_write / crc32_end
   (src/mfile.c:526-546) over the drop-in crc32c_hw, checked by the oracle.
-* src/zeroskip-{file,record,header,packed,dotzsdb}.c include
-  zeroskip-priv.h -> <uuid/uuid.h>, which this image lacks (no libuuid
-  headers); a stand-in header would be a reference build with a stand-in, so
-  they are not compiled.  For them: every crc32c* identifier they call is an
-  exported symbol of libzscrc.so, and the reference's crc32c.h and
-  include/zscrc.h compile in one translation unit (a prototype that differs
-  in any parameter or return type is a hard "conflicting types" error).
+* every other reference source (src/*.c except crc32c.c, which needs the
+  autoconf-generated config.h) is compiled UNMODIFIED to objects
+  (oracle/Makefile `ref-lib`); the format callers' <uuid/uuid.h>
+  (src/zeroskip-priv.h:28) is the image's real libuuid header under
+  /opt/conda/include.  The objects are linked, as the reference's library,
+  against libzscrc.so with --no-undefined and NOT against libuuid: the only
+  unresolved symbols must be libuuid's three, so every crc32c* reference in
+  the reference's compiled code -- the five format callers
+  zeroskip-{file,record,header,packed,dotzsdb}.c included -- binds to
+  libzscrc.so.  Nothing from this link is run.
+* the reference's crc32c.h and include/zscrc.h compile in one translation
+  unit (a prototype that differs in any parameter or return type is a hard
+  "conflicting types" error).
 """
 import json
 import os
@@ -51,6 +57,33 @@ def test_mfile_links_unmodified_and_runs(tmp_path):
     data = open(f, "rb").read()
     assert rep["span"] == len(data) - 40 and rep["gpu_calls"] == 0
     assert rep["crc"] == oracle.crc32c_hw(0, data[40:])
+
+
+UUID_INC = "/opt/conda/include"
+UUID_SYMS = {"uuid_generate", "uuid_parse", "uuid_unparse_lower"}   # src/zeroskip-dotzsdb.c
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(UUID_INC, "uuid", "uuid.h")), reason="no libuuid header")
+def test_reference_library_links_against_libzscrc(tmp_path):
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "ref-lib"])
+    libdir = os.path.join(ROOT, "oracle", "_ref", "lib")
+    objs = sorted(os.path.join(libdir, f) for f in os.listdir(libdir) if f.endswith(".o"))
+    names = {os.path.basename(o)[:-2] for o in objs}
+    assert set(n[:-2] for n in CALLERS) <= names and "crc32c" not in names
+    needed = set()
+    for o in objs:
+        und = subprocess.run(["nm", "-u", o], capture_output=True, text=True, check=True).stdout.split()
+        needed |= {s for s in und if s.startswith("crc32c")}
+    assert {"crc32c", "crc32c_hw"} <= needed
+    trace = [f"-Wl,--trace-symbol={s}" for s in sorted(needed)]
+    out = subprocess.run(["gcc", "-shared", "-o", str(tmp_path / "libzeroskip.so"), *objs,
+                          "-L", os.path.dirname(LIB_PATH), "-lzscrc", "-Wl,--no-undefined", *trace],
+                         capture_output=True, text=True)
+    unresolved = set(re.findall(r"undefined reference to `([^']+)'", out.stderr))
+    assert unresolved == UUID_SYMS, out.stderr[-2000:]
+    for s in needed:                     # each one defined by libzscrc.so, nowhere else
+        defs = re.findall(rf"(\S+): definition of {s}$", out.stdout + out.stderr, re.M)
+        assert defs and all(d.endswith("libzscrc.so") for d in defs), (s, defs)
 
 
 def test_every_reference_caller_resolves():
