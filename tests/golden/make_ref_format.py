@@ -136,6 +136,41 @@ def mixed_script(seed: int, ntxn: int = 40, long_key: bool = False, stale: bool 
     return s
 
 
+def long_script() -> Script:
+    """A span over MAX_SHORT_VAL_LEN: a 16 MiB + 9 value (long value record)
+    and a 70,000-byte key (long key record) in one transaction, so a long
+    commit (zeroskip-file.c:266-302), between two short ones."""
+    import numpy as np
+    rng = np.random.default_rng(7)
+    s = Script(bytes(range(16, 32)), 3)
+    s.add(b"small", b"v" * 9)
+    s.commit()
+    s.add(b"big-value", rng.integers(0, 256, zf.MAX_SHORT_VAL_LEN + 9, dtype=np.uint8).tobytes())
+    s.add(b"k" * 70000, b"after")
+    s.commit()
+    s.remove(b"small")
+    s.commit()
+    return s
+
+
+def long_fixture() -> dict:
+    """The long-commit image is 16 MiB: committed as its generator
+    (long_script, whose oracle mirror regenerates it) and the reference-written
+    image's sha256 and commit records, not as bytes."""
+    import hashlib
+    import struct
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "long")
+        img = long_script().run(path)
+        rep = ref_verify(path)
+    commits = sorted([c[0] for c in rep["commits"]] + rep["long_commits"])
+    words = {str(o): img[o:o + (24 if o in rep["long_commits"] else 8)].hex() for o in commits}
+    return dict(kind=0, size=len(img), generator="long_script", sha256=hashlib.sha256(img).hexdigest(),
+                commit_records=words, reference=rep, header=img[:40].hex(),
+                note="bytes not committed (16 MiB): regenerate with long_script().fw (the oracle writer, "
+                     "equal to the reference writer byte for byte) and check sha256")
+
+
 def fixtures() -> dict:
     """name -> (image bytes, kind) for the committed fixture set."""
     out = {}
@@ -168,6 +203,7 @@ def main():
         with open(path, "wb") as f:
             f.write(img)
         manifest[name] = dict(kind=kind, size=len(img), reference=ref_verify(path))
+    manifest["long_value"] = long_fixture()
     with open(os.path.join(OUTDIR, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)
         f.write("\n")

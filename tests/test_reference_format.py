@@ -23,7 +23,6 @@ import os
 import random
 import subprocess
 
-import numpy as np
 import pytest
 
 from oracle import zs_format as zf
@@ -34,6 +33,7 @@ REF = "/root/reference"
 HAVE_REF = os.path.isdir(os.path.join(REF, "src")) and os.path.exists("/opt/conda/include/uuid/uuid.h")
 live = pytest.mark.skipif(not HAVE_REF, reason="no /root/reference (or its libuuid header) here")
 MANIFEST = json.load(open(os.path.join(mrf.OUTDIR, "manifest.json")))
+IMAGES = sorted(n for n in MANIFEST if "generator" not in MANIFEST[n])   # committed as bytes
 
 
 def fixture(name):
@@ -46,7 +46,7 @@ def ref_commit_offsets(rep):
 
 
 # ---------------------------------------------------------------- fixtures
-@pytest.mark.parametrize("name", sorted(MANIFEST))
+@pytest.mark.parametrize("name", IMAGES)
 def test_fixture_oracle_agrees_with_reference_verdict(name):
     img, m = fixture(name), MANIFEST[name]
     rep = m["reference"]
@@ -79,8 +79,27 @@ def test_fixture_oracle_agrees_with_reference_verdict(name):
     assert ln.tolist() == [c["span_len"] for c in commits]
 
 
+def test_long_fixture_regenerates_reference_image():
+    """The 16 MiB long-commit image is committed as its generator: the oracle
+    writer's mirror of the script reproduces the reference-written bytes
+    (sha256), and its long commit checks under the writer's semantics."""
+    import hashlib
+    m = MANIFEST["long_value"]
+    img = mrf.long_script().fw.image()
+    assert len(img) == m["size"] and hashlib.sha256(img).hexdigest() == m["sha256"]
+    assert img[:40].hex() == m["header"]
+    for off, words in m["commit_records"].items():
+        assert img[int(off):int(off) + len(words) // 2].hex() == words
+    commits, end, why = zf.walk(img)
+    assert why == "end" and all(c["ok"] for c in commits)
+    assert [c["commit_off"] for c in commits] == ref_commit_offsets(m["reference"])
+    assert len(m["reference"]["long_commits"]) == 1
+    off, ln, wrc, wend = zsfile.walk(img)
+    assert wrc == zsfile.END and (off + ln).tolist() == ref_commit_offsets(m["reference"])
+
+
 def test_fixture_set_covers_bad_and_stale():
-    bad = {k: sum(c[1] != 0 for c in v["reference"]["commits"]) for k, v in MANIFEST.items()}
+    bad = {k: sum(c[1] != 0 for c in MANIFEST[k]["reference"]["commits"]) for k in IMAGES}
     assert bad["active_clean"] == 0 and bad["active_corrupt"] == 3 and bad["active_stale"] > 0
 
 
@@ -148,15 +167,7 @@ def test_reference_long_value_long_commit(demo, tmp_path):
     (zeroskip-file.c:266-302); the reference's verifier cannot check a long
     commit (zeroskip-record.c:258), so the oracle's long verify is held to the
     reference WRITER's bytes."""
-    rng = np.random.default_rng(7)
-    s = mrf.Script(bytes(range(16, 32)), 3)
-    s.add(b"small", b"v" * 9)
-    s.commit()
-    s.add(b"big-value", rng.integers(0, 256, zf.MAX_SHORT_VAL_LEN + 9, dtype=np.uint8).tobytes())
-    s.add(b"k" * 70000, b"after")
-    s.commit()
-    s.remove(b"small")
-    s.commit()
+    s = mrf.long_script()
     img = s.run(str(tmp_path / "f"))
     assert img == s.fw.image()
     rep = mrf.ref_verify(str(tmp_path / "f"))
@@ -188,6 +199,7 @@ def test_committed_fixtures_regenerate(demo, tmp_path):
         p.write_bytes(img)
         assert mrf.ref_verify(str(p)) == MANIFEST[name]["reference"]
         assert MANIFEST[name]["kind"] == kind
+    assert mrf.long_fixture() == MANIFEST["long_value"]
 
 
 @live
