@@ -81,6 +81,11 @@ constexpr int NSLOT = 2;
 
 void cpass_free(zscrc_cpass *p)
 {
+    /* a submitted pass not yet collected may still be writing its host slot
+     * and the device blocks; its completion may be the caller's event, which
+     * the caller may have recorded again or destroyed: wait for the device */
+    if (p->pending[0] || p->pending[1])
+        (void)hipDeviceSynchronize();
     for (hipEvent_t &e : p->done)
         if (e) {
             (void)hipEventSynchronize(e);
