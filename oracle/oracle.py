@@ -164,9 +164,10 @@ def pick_cpus(n: int) -> list:
 def batch_rate(base: np.ndarray, offs=None, lens=None, seeds=None, *, n=None, stride=0, fixed_len=0,
                impl: str = "hw", threads: int = 1, cpus=None, budget: float = 5.0):
     """The bench's CPU timing leg (oracle_batch_rate): the batch's records laid
-    end to end and cut into equal byte ranges, one per persistent thread
-    (pinned to `cpus` if given), records cut by a range joined by the zero
-    shift; passes repeated for `budget` seconds.  impl "read" times a plain
+    end to end and dealt in byte chunks (~16 per thread, >= 256 KiB) from a
+    counter to persistent threads (pinned to `cpus` if given), records cut by
+    a chunk boundary joined by the zero shift; passes repeated for `budget`
+    seconds.  impl "read" times a plain
     read of the same bytes (the host memory bound).  Returns (crcs of the
     last pass, seconds, passes)."""
     base = np.ascontiguousarray(base).view(np.uint8)

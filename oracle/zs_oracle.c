@@ -355,6 +355,8 @@ struct rate_piece {
     uint32_t crc;
 };
 
+#define RATE_MAX_CHUNKS 4096
+
 struct rate_pool {
     const uint8_t *base;
     const uint64_t *off, *len, *pos; /* pos: prefix sums of the lengths (n + 1) */
@@ -370,8 +372,13 @@ struct rate_pool {
     volatile int stop;
     double t0, budget;
     uint64_t passes;
-    struct rate_piece piece[256][2];
-    int npiece[256];
+    /* the bytes are dealt in chunks from a counter (a thread slowed by
+     * another tenant on its core takes fewer: a static share per thread made
+     * every pass wait for the slowest one, profiles/r05/cpu_threads64.jsonl) */
+    uint64_t chunk, nchunks;
+    uint64_t next_chunk;
+    struct rate_piece piece[RATE_MAX_CHUNKS][2];
+    int npiece[RATE_MAX_CHUNKS];
     volatile uint64_t sink[256 * 8];
 };
 
@@ -431,11 +438,12 @@ static uint64_t read_sum(const uint8_t *p, uint64_t n)
 #endif
 }
 
-static void rate_share(struct rate_pool *P, int t, int mode)
+/* chunk c: bytes [c chunk, (c + 1) chunk) of the records laid end to end */
+static void rate_chunk(struct rate_pool *P, uint64_t c, int t, int mode)
 {
-    const uint64_t b0 = P->total * (uint64_t)t / (uint64_t)P->nthreads;
-    const uint64_t b1 = P->total * (uint64_t)(t + 1) / (uint64_t)P->nthreads;
-    const int last = t == P->nthreads - 1;
+    const uint64_t b0 = c * P->chunk;
+    const uint64_t b1 = b0 + P->chunk < P->total ? b0 + P->chunk : P->total;
+    const int last = c == P->nchunks - 1;
     uint64_t sum = 0;
     int np = 0;
     for (uint64_t i = rp_first(P, b0); i < P->n; ++i) {
@@ -450,16 +458,26 @@ static void rate_share(struct rate_pool *P, int t, int mode)
             continue;
         }
         const uint32_t sd = s == 0 && P->seed ? P->seed[i] : 0;
-        const uint32_t c = P->impl == 1 ? oracle_crc32c_hw(sd, p, e - s)
+        const uint32_t v = P->impl == 1 ? oracle_crc32c_hw(sd, p, e - s)
                          : P->impl == 2 ? oracle_crc32c_bitwise(sd, p, e - s)
                                         : oracle_crc32c_sw(sd, p, e - s);
         if (s == 0 && e == li)
-            P->out[i] = c;
+            P->out[i] = v;
         else if (np < 2)
-            P->piece[t][np++] = (struct rate_piece){i, s, e - s, c};
+            P->piece[c][np++] = (struct rate_piece){i, s, e - s, v};
     }
-    P->npiece[t] = np;
-    P->sink[8 * t] = sum;
+    P->npiece[c] = np;
+    P->sink[8 * t] += sum;
+}
+
+static void rate_share(struct rate_pool *P, int t, int mode)
+{
+    for (;;) {
+        const uint64_t c = __atomic_fetch_add(&P->next_chunk, 1, __ATOMIC_RELAXED);
+        if (c >= P->nchunks)
+            break;
+        rate_chunk(P, c, t, mode);
+    }
 }
 
 static void *rate_worker(void *arg)
@@ -486,6 +504,7 @@ static void *rate_worker(void *arg)
         rate_share(P, t, mode);
         pthread_barrier_wait(&P->bar);
         if (t == 0) {
+            P->next_chunk = 0; /* the others wait at the next pass's barrier */
             ++P->passes;
             if (oracle_now() - P->t0 >= P->budget)
                 P->stop = 1;
@@ -526,6 +545,18 @@ double oracle_batch_rate(const uint8_t *base, const uint64_t *off, const uint64_
     P.stride = stride;
     P.fixed_len = fixed_len;
     P.total = len ? pos[n] : n * fixed_len;
+    /* ~16 chunks per thread, at least 256 KiB each (a record cut by a chunk
+     * boundary is joined by the zero shift, as a range's were) */
+    {
+        const uint64_t want = (uint64_t)(nthreads < 1 ? 1 : nthreads) * 16;
+        uint64_t ch = (P.total + want - 1) / want;
+        if (ch < (256u << 10))
+            ch = 256u << 10;
+        if ((P.total + ch - 1) / ch > RATE_MAX_CHUNKS)
+            ch = (P.total + RATE_MAX_CHUNKS - 1) / RATE_MAX_CHUNKS;
+        P.chunk = ch ? ch : 1;
+        P.nchunks = P.total ? (P.total + P.chunk - 1) / P.chunk : 1;
+    }
     P.impl = impl;
     P.nthreads = nthreads;
     P.cpus = cpus;
@@ -571,9 +602,9 @@ double oracle_batch_rate(const uint8_t *base, const uint64_t *off, const uint64_
     if (impl != 3) {
         uint64_t cur = UINT64_MAX;
         uint32_t crc = 0;
-        for (int t = 0; t < nthreads; ++t)
-            for (int k = 0; k < P.npiece[t]; ++k) {
-                const struct rate_piece *q = &P.piece[t][k];
+        for (uint64_t c = 0; c < P.nchunks; ++c)
+            for (int k = 0; k < P.npiece[c]; ++k) {
+                const struct rate_piece *q = &P.piece[c][k];
                 if (q->rec != cur) {
                     cur = q->rec;
                     crc = q->crc;
