@@ -315,6 +315,27 @@ def test_pipelined_passes(gpu):
     assert job.run().ok
 
 
+def test_destroy_with_uncollected_passes(gpu):
+    """A pass destroyed with two submits never collected (their completion
+    the caller's own end events, recorded on the stream): zscrc_cpass_destroy
+    waits for the device before freeing the host slots the post kernels
+    write, and a new pass over the same DB runs clean after."""
+    db = small_db(long_region=True)
+    job = cs.Consistent(cs.open_db(db), 0, 1).prepare()
+    assert job._cpass is not None
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(2)]
+    assert job.submit(evs[0]) and job.submit(evs[1])
+    assert job.pending() == 2
+    from zeroskip_amd._lib import lib
+    h, job._cpass = job._cpass, None
+    lib().zscrc_cpass_destroy(h)
+    del evs
+    torch.cuda.synchronize()
+    job2 = cs.Consistent(cs.open_db(db), 0, 1).prepare()
+    rep = job2.run()
+    assert rep.ok and len(rep.stale_empty_commits) == 3
+
+
 @pytest.mark.parametrize("case", ["clean", "corrupt", "bad_2000", "bad_5000"])
 def test_device_row_matches_host_digest(gpu, case):
     """zscrc_cpass_submit_row's digest row (cpass_row_kernel: the listed
