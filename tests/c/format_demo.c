@@ -1,9 +1,10 @@
 /*
  * Format-layer demonstrator (TEST INFRASTRUCTURE ONLY): the reference's OWN
- * writer and verifier -- src/zeroskip-file.c, zeroskip-record.c,
- * zeroskip-header.c and mfile.c (with util.c, log.c, cstring.c), compiled
- * unmodified from /root/reference by oracle/Makefile's `ref-format` target --
- * linked against libzscrc.so instead of src/crc32c.c.  Every CRC these
+ * writer and verifiers -- src/zeroskip-file.c, zeroskip-record.c,
+ * zeroskip-header.c, zeroskip-packed.c and mfile.c (with what they pull from
+ * the rest of the library), compiled unmodified from /root/reference by
+ * oracle/Makefile's `ref-format` target -- linked against libzscrc.so
+ * instead of src/crc32c.c.  Every CRC these
  * sources compute goes through the drop-in crc32c / crc32c_hw symbols.
  * tests/test_reference_format.py drives it and holds oracle/zs_format.py and
  * the product's walk / GPU verifier to what it writes and what it accepts.
@@ -25,6 +26,12 @@
  *     P <count> <off>...                  the packed pointer section's words, big-endian
  *   prints {"size": N}
  *
+ * usage: format_demo packed FILE
+ *   zs_packed_file_open (zeroskip-packed.c:215-365): the header, then the
+ *   pointer section's commit -- short or long FINAL, the reference's one
+ *   correct long-trailer verifier -- and the pointers.
+ *   Prints {"rc": rc, "count": pointers read}.
+ *
  * usage: format_demo verify FILE
  *   zs_header_validate (zeroskip-header.c:105), then zs_record_read_from_file
  *   (zeroskip-record.c:283) from offset 40 until the offset stops moving.
@@ -39,6 +46,7 @@
 #include <string.h>
 
 #include <libzeroskip/mfile.h>
+#include <libzeroskip/vecu64.h>
 #include <libzeroskip/zeroskip.h>
 
 #include "zeroskip-priv.h"
@@ -199,12 +207,25 @@ static int do_verify(const char *path)
     return 0;
 }
 
+static int do_packed(const char *path)
+{
+    struct zsdb_file *f = NULL;
+    const int rc = zs_packed_file_open(path, &f);
+    unsigned long long count = rc == ZS_OK && f && f->index ? (unsigned long long)f->index->count : 0;
+    printf("{\"rc\": %d, \"count\": %llu}\n", rc, count);
+    if (rc == ZS_OK && f)
+        zs_packed_file_close(&f);
+    return 0;
+}
+
 int main(int argc, char **argv)
 {
     if (argc == 4 && strcmp(argv[1], "write") == 0)
         return do_write(argv[2], argv[3]);
     if (argc == 3 && strcmp(argv[1], "verify") == 0)
         return do_verify(argv[2]);
-    fprintf(stderr, "usage: %s write OUT BLOB < OPS | verify FILE\n", argv[0]);
+    if (argc == 3 && strcmp(argv[1], "packed") == 0)
+        return do_packed(argv[2]);
+    fprintf(stderr, "usage: %s write OUT BLOB < OPS | verify FILE | packed FILE\n", argv[0]);
     return 2;
 }

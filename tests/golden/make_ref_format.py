@@ -89,7 +89,9 @@ def packed_ops(uuid: bytes, startidx: int, endidx: int, records):
             blob += v
             ops.append(f"a {ko} {len(k)} {vo} {len(v)}")
             off += len(zf.key_record(k)) + len(zf.value_record(v))
-    ops += ["C", "B", "P " + " ".join(str(x) for x in [len(ptrs)] + ptrs), "F"]
+    words = [len(ptrs)] + ptrs
+    ops += ["C", "B"] + ["P " + " ".join(str(x) for x in words[k:k + 2048]) for k in range(0, len(words), 2048)]
+    ops.append("F")
     return ops, bytes(blob)
 
 
@@ -171,6 +173,53 @@ def long_fixture() -> dict:
                      "equal to the reference writer byte for byte) and check sha256")
 
 
+PACKED_LONG_N = 2_200_000   # pointer section 17.6 MB > MAX_SHORT_VAL_LEN: a long FINAL commit
+
+
+def packed_long_records():
+    """2.2 M records (8-byte keys, empty values) for a packed file whose
+    pointer section ends in a long FINAL commit."""
+    return [(b"%08d" % i, b"") for i in range(PACKED_LONG_N)]
+
+
+PACKED_LONG_HDR = (bytes(range(16)), 1, 4)   # uuid, startidx, endidx
+
+
+def ref_packed(path: str) -> dict:
+    """zs_packed_file_open's verdict (the reference's packed verifier)."""
+    out = subprocess.run([DEMO, "packed", path], capture_output=True, text=True, timeout=300)
+    if out.returncode != 0:
+        raise RuntimeError(f"format_demo packed: rc {out.returncode}: {out.stderr}")
+    return json.loads(out.stdout)
+
+
+def packed_long_fixture() -> dict:
+    """The long-FINAL packed image (123 MB): written by the reference's own
+    writer (~1 min of mmap remaps), committed as its generator, sha256 and the
+    reference verifier's verdicts on it and on two corruptions."""
+    import hashlib
+    recs = packed_long_records()
+    ops, blob = packed_ops(*PACKED_LONG_HDR, recs)
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "pl")
+        img = run_ops(ops, blob, path)
+        clean = ref_packed(path)
+        pc = {c["kind"]: c for c in zf.packed_check(img)}
+        flips = {"pointer_word": pc["pointers"]["span_off"] + 8 * 5 + 3, "final_crc": len(img) - 1}
+        verdicts = {}
+        for k, at in flips.items():
+            bad = bytearray(img)
+            bad[at] ^= 0x01
+            with open(path, "wb") as f:
+                f.write(bad)
+            verdicts[k] = dict(offset=at, reference=ref_packed(path))
+    return dict(kind=2, size=len(img), generator="packed_long_records", sha256=hashlib.sha256(img).hexdigest(),
+                header=img[:40].hex(), trailer=img[-24:].hex(), reference_packed=clean, corruptions=verdicts,
+                note="bytes not committed (123 MB): regenerate with zs_format.packed_file(packed_long_records(), "
+                     "*PACKED_LONG_HDR) (the oracle writer; equal to the reference writer byte for byte) and "
+                     "check sha256")
+
+
 def fixtures() -> dict:
     """name -> (image bytes, kind) for the committed fixture set."""
     out = {}
@@ -204,10 +253,11 @@ def main():
             f.write(img)
         manifest[name] = dict(kind=kind, size=len(img), reference=ref_verify(path))
     manifest["long_value"] = long_fixture()
+    manifest["packed_long"] = packed_long_fixture()
     with open(os.path.join(OUTDIR, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)
         f.write("\n")
-    print(json.dumps({k: (v["size"], len(v["reference"]["commits"])) for k, v in manifest.items()}))
+    print(json.dumps({k: v["size"] for k, v in manifest.items()}))
 
 
 if __name__ == "__main__":

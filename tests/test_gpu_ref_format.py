@@ -89,6 +89,25 @@ def test_verify_image_long_commit_reference_written(gpu):
     assert rep["n_bad"] == 1 and rep["first_bad"] == 1
 
 
+def test_verify_image_packed_long_final(gpu):
+    """The long-FINAL packed image (regenerated; sha256 of the
+    reference-written bytes): both commits verify on the GPU, and each
+    corruption the reference's packed verifier rejects is one bad commit."""
+    import hashlib
+    from tests.golden import make_ref_format as mrf
+    m = MANIFEST["packed_long"]
+    img = zf.packed_file(mrf.packed_long_records(), *mrf.PACKED_LONG_HDR)
+    assert hashlib.sha256(img).hexdigest() == m["sha256"]
+    rep = zsfile.verify_image(img, zsfile.PACKED)
+    assert rep["header_rc"] == 0 and rep["n_commits"] == 2 and rep["n_bad"] == 0
+    for k, c in m["corruptions"].items():
+        bad = bytearray(img)
+        bad[c["offset"]] ^= 0x01
+        assert c["reference"]["rc"] == -9
+        rep = zsfile.verify_image(bytes(bad), zsfile.PACKED)
+        assert rep["n_bad"] == 1, (k, rep)
+
+
 def test_verify_files_matches_reference_verifier(gpu):
     names = IMAGES
     imgs = [fixture(n) for n in names]

@@ -98,6 +98,38 @@ def test_long_fixture_regenerates_reference_image():
     assert wrc == zsfile.END and (off + ln).tolist() == ref_commit_offsets(m["reference"])
 
 
+@pytest.fixture(scope="module")
+def packed_long():
+    """The long-FINAL packed image, from the oracle writer (its sha256 is
+    the reference-written image's)."""
+    return zf.packed_file(mrf.packed_long_records(), *mrf.PACKED_LONG_HDR)
+
+
+def test_packed_long_fixture_regenerates_reference_image(packed_long):
+    """A packed file whose pointer section (17.6 MB) ends in a long FINAL
+    commit -- the long-trailer layout the reference's packed verifier checks
+    correctly (zeroskip-packed.c:289-312): the oracle writer reproduces the
+    reference writer's bytes, the oracle and libzscrc's span walk read it as
+    the reference's verifier does, and both corruptions are caught."""
+    import hashlib
+    m = MANIFEST["packed_long"]
+    img = packed_long
+    assert len(img) == m["size"] and hashlib.sha256(img).hexdigest() == m["sha256"]
+    assert img[:40].hex() == m["header"] and img[-24:].hex() == m["trailer"]
+    assert img[-24] == zf.REC_LONG_FINAL
+    pc = {c["kind"]: c for c in zf.packed_check(img)}
+    assert pc["pointers"]["ok"] and pc["records"]["ok"] and pc["pointers"]["span_len"] > zf.MAX_SHORT_VAL_LEN
+    assert m["reference_packed"] == {"rc": 0, "count": mrf.PACKED_LONG_N}
+    off, ln, prc = zsfile.packed_spans(img)
+    assert prc == 0 and sorted(zip(off.tolist(), ln.tolist())) == sorted(
+        (c["span_off"], c["span_len"]) for c in pc.values())
+    for k, c in m["corruptions"].items():
+        bad = bytearray(img)
+        bad[c["offset"]] ^= 0x01
+        assert c["reference"]["rc"] == -9                 # ZS_INVALID_DB
+        assert not zf.packed_check(bytes(bad))[0]["ok"], k
+
+
 def test_fixture_set_covers_bad_and_stale():
     bad = {k: sum(c[1] != 0 for c in MANIFEST[k]["reference"]["commits"]) for k in IMAGES}
     assert bad["active_clean"] == 0 and bad["active_corrupt"] == 3 and bad["active_stale"] > 0
@@ -189,6 +221,23 @@ def test_reference_packed_writer_equals_oracle(demo, tmp_path):
     img = mrf.run_ops(ops, blob, str(tmp_path / "p"))
     assert img == zf.packed_file(recs, bytes(range(3, 19)), 4, 9)
     assert zf.packed_records(img) == recs
+
+
+@live
+def test_reference_packed_verifier_on_oracle_image(demo, tmp_path, packed_long):
+    """The reference's own zs_packed_file_open over the oracle-written
+    long-FINAL image and its corruptions (the manifest's verdicts were taken
+    on the reference-written bytes, which the oracle's equal)."""
+    p = tmp_path / "pl"
+    p.write_bytes(packed_long)
+    assert mrf.ref_packed(str(p)) == {"rc": 0, "count": mrf.PACKED_LONG_N}
+    for k, c in MANIFEST["packed_long"]["corruptions"].items():
+        bad = bytearray(packed_long)
+        bad[c["offset"]] ^= 0x01
+        p.write_bytes(bytes(bad))
+        assert mrf.ref_packed(str(p)) == c["reference"], k
+    # the small reference-written packed fixture too
+    assert mrf.ref_packed(os.path.join(mrf.OUTDIR, "packed.zs")) == {"rc": 0, "count": 400}
 
 
 @live
