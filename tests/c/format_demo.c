@@ -32,6 +32,20 @@
  *   correct long-trailer verifier -- and the pointers.
  *   Prints {"rc": rc, "count": pointers read}.
  *
+ * usage: format_demo repack1 OUT UUIDHEX STARTIDX ENDIDX FINALISED...
+ *   zsdb_repack's branch 1 (src/zeroskip.c:1460-1505) on the reference's own
+ *   code: the finalised files opened (zs_finalised_file_open), ordered and
+ *   loaded into the memtree as zsdb_open does (zeroskip.c:749-767: a pqueue by
+ *   natural_strcasecmp of the names, list_add_head, loaded in reverse, a later
+ *   record of a key replacing an earlier one -- the two 10-line static
+ *   callbacks of zeroskip.c:72-96 restated here), then
+ *   zs_packed_file_new_from_memtree writes OUT.  Prints {"rc": rc}.
+ * usage: format_demo repack2 OUT UUIDHEX STARTIDX ENDIDX PACKED...
+ *   Branch 2 (zeroskip.c:1510-1565): the packed files opened
+ *   (zs_packed_file_open), ordered and given priorities as zsdb_open does
+ *   (zeroskip.c:512-526), the first two of that list merged by
+ *   zs_iterator_new + zs_packed_file_new_from_packed_files into OUT.
+ *
  * usage: format_demo verify FILE
  *   zs_header_validate (zeroskip-header.c:105), then zs_record_read_from_file
  *   (zeroskip-record.c:283) from offset 40 until the offset stops moving.
@@ -45,10 +59,13 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <libzeroskip/memtree.h>
 #include <libzeroskip/mfile.h>
+#include <libzeroskip/util.h>
 #include <libzeroskip/vecu64.h>
 #include <libzeroskip/zeroskip.h>
 
+#include "pqueue.h"
 #include "zeroskip-priv.h"
 
 static int hexbyte(const char *s)
@@ -207,6 +224,101 @@ static int do_verify(const char *path)
     return 0;
 }
 
+/* zeroskip.c:64-70 */
+static int dbfname_cmp(const void *d1, const void *d2, void *cbdata)
+{
+    (void)cbdata;
+    return natural_strcasecmp(((const struct zsdb_file *)d1)->fname.buf, ((const struct zsdb_file *)d2)->fname.buf);
+}
+
+/* zeroskip.c:72-96 */
+static int load_cb(void *data, const unsigned char *key, size_t keylen, const unsigned char *value, size_t vallen)
+{
+    memtree_replace((struct memtree *)data, record_new(key, keylen, value, vallen, 0));
+    return 0;
+}
+
+static int load_deleted_cb(void *data, const unsigned char *key, size_t keylen, const unsigned char *value,
+                           size_t vallen)
+{
+    memtree_replace((struct memtree *)data, record_new(key, keylen, value, vallen, 1));
+    return 0;
+}
+
+static int do_repack(int branch, const char *out, const char *uuidhex, uint32_t sidx, uint32_t eidx, int nf,
+                     char **files)
+{
+    struct zsdb db;
+    struct zsdb_priv priv;
+    memset(&db, 0, sizeof db);
+    memset(&priv, 0, sizeof priv);
+    if (strlen(uuidhex) != 32)
+        return 2;
+    for (int i = 0; i < 16; ++i)
+        priv.uuid[i] = (unsigned char)hexbyte(uuidhex + 2 * i);
+    priv.open = 1;
+    cstring_init(&priv.dbdir, 0);
+    db.priv = &priv;
+    struct pqueue pq;
+    memset(&pq, 0, sizeof pq);
+    pq.cmp = dbfname_cmp;
+    for (int i = 0; i < nf; ++i) {
+        struct zsdb_file *f = NULL;
+        const int rc = branch == 1 ? zs_finalised_file_open(files[i], &f) : zs_packed_file_open(files[i], &f);
+        if (rc != ZS_OK || !f) {
+            printf("{\"rc\": %d, \"open\": \"%s\"}\n", rc, files[i]);
+            return 0;
+        }
+        pqueue_put(&pq, f);
+    }
+    /* the lists zsdb_open builds: priv->dbfiles.fflist / pflist */
+    list_head_init(&priv.dbfiles.fflist);
+    list_head_init(&priv.dbfiles.pflist);
+    struct list_head *lst = branch == 1 ? &priv.dbfiles.fflist : &priv.dbfiles.pflist;
+    while (pq.count) {
+        struct zsdb_file *f = pqueue_get(&pq);
+        list_add_head(&f->list, lst);
+    }
+    pqueue_free(&pq);
+    struct list_head *pos, *p;
+    int rc = ZS_OK, priority = 0;
+    struct zsdb_file *nf_out = NULL;
+    if (branch == 1) {
+        priv.fmemtree = memtree_new(NULL, NULL);
+        list_for_each_reverse(pos, lst) {
+            struct zsdb_file *f = list_entry(pos, struct zsdb_file, list);
+            zs_finalised_file_record_foreach(f, load_cb, load_deleted_cb, priv.fmemtree);
+            f->priority = ++priority;
+        }
+        rc = zs_packed_file_new_from_memtree(out, sidx, eidx, &priv, &nf_out);
+    } else {
+        list_for_each_forward(pos, lst) {
+            struct zsdb_file *f = list_entry(pos, struct zsdb_file, list);
+            f->priority = ++priority;
+        }
+        struct list_head two;
+        list_head_init(&two);
+        int i = 0;
+        list_for_each_forward_safe(pos, p, lst) {
+            struct zsdb_file *f = list_entry(pos, struct zsdb_file, list);
+            if (i == 2)
+                break;
+            list_del(pos);
+            list_add_head(&f->list, &two);
+            ++i;
+        }
+        struct zsdb_iter *iter = NULL;
+        rc = zs_iterator_new(&db, &iter);
+        if (rc == ZS_OK)
+            rc = zs_packed_file_new_from_packed_files(out, sidx, eidx, &priv, &two, &iter, &nf_out);
+        zs_iterator_end(&iter);
+    }
+    if (nf_out)
+        zs_packed_file_close(&nf_out);
+    printf("{\"rc\": %d}\n", rc);
+    return 0;
+}
+
 static int do_packed(const char *path)
 {
     struct zsdb_file *f = NULL;
@@ -226,6 +338,9 @@ int main(int argc, char **argv)
         return do_verify(argv[2]);
     if (argc == 3 && strcmp(argv[1], "packed") == 0)
         return do_packed(argv[2]);
+    if (argc >= 7 && (strcmp(argv[1], "repack1") == 0 || strcmp(argv[1], "repack2") == 0))
+        return do_repack(argv[1][6] - '0', argv[2], argv[3], (uint32_t)strtoul(argv[4], NULL, 0),
+                         (uint32_t)strtoul(argv[5], NULL, 0), argc - 6, argv + 6);
     fprintf(stderr, "usage: %s write OUT BLOB < OPS | verify FILE | packed FILE\n", argv[0]);
     return 2;
 }

@@ -220,6 +220,129 @@ def packed_long_fixture() -> dict:
                      "check sha256")
 
 
+def ref_repack(branch: int, out: str, uuid: bytes, sidx: int, eidx: int, files) -> dict:
+    """zsdb_repack's branch 1 or 2 on the reference's own code (format_demo
+    repack1 / repack2)."""
+    r = subprocess.run([DEMO, f"repack{branch}", out, uuid.hex(), str(sidx), str(eidx), *files],
+                       capture_output=True, text=True, timeout=300)
+    if r.returncode != 0:
+        raise RuntimeError(f"format_demo repack{branch}: rc {r.returncode}: {r.stderr}")
+    return json.loads(r.stdout)
+
+
+def ref_merge_packed(sources):
+    """The records zs_packed_file_new_from_packed_files writes
+    (zeroskip-packed.c:617-742 over zeroskip-iterator.c), restated with its
+    quirks: sources = [(priority, [(key, value-or-None)])] in the order of the
+    file list.  A key in several sources goes to the higher priority; the
+    iterator's `deleted` flag is set when it steps onto a delete
+    (zeroskip-iterator.c:250-251) and never cleared, so from a source's first
+    delete after its first record on, none of that source's records is
+    written; a delete as a source's FIRST record is never flagged
+    (zs_iterator_begin_for_packed_files reads its key without the type) and
+    is written as a delete record."""
+    import heapq
+    its = [dict(prio=p, recs=r, pos=0, deleted=False, done=False) for p, r in sources]
+    ht, pq = {}, []
+
+    def process(key, it):
+        old = ht.get(key)
+        if old is not None:
+            if it["prio"] > old["prio"]:
+                ht[key] = it
+                step(old)
+            else:
+                step(it)
+        else:
+            ht[key] = it
+            heapq.heappush(pq, key)
+
+    def step(it):
+        if it["done"]:
+            return
+        it["pos"] += 1
+        if it["pos"] < len(it["recs"]):
+            k, v = it["recs"][it["pos"]]
+            if v is None:
+                it["deleted"] = True
+            process(k, it)
+        else:
+            it["done"] = True
+
+    for it in its:
+        if it["recs"]:
+            process(it["recs"][0][0], it)
+    out = []
+    while pq:
+        key = heapq.heappop(pq)
+        it = ht.pop(key)
+        if not it["deleted"]:
+            out.append(it["recs"][it["pos"]])
+        step(it)
+    return out
+
+
+UUIDSTR = "00010203-0405-0607-0809-0a0b0c0d0e0f"   # the repack fixtures' DB uuid (bytes 0..15)
+
+
+def repack1_inputs():
+    """Five finalised files (idx 3..7; adds, removes, a key often rewritten)
+    and an empty active file (idx 8): zsdb_repack branch 1's input."""
+    import numpy as np
+    rng = np.random.default_rng(31)
+    files = {}
+    for idx in range(3, 8):
+        w = zf.FileWriter(bytes(range(16)), idx=idx)
+        for t in range(100):
+            k = b"%016d" % int(rng.integers(0, 300))
+            if t % 11 == 3:
+                w.remove(k)
+            else:
+                w.add(k, rng.integers(0, 256, int(rng.integers(0, 200)), dtype=np.uint8).tobytes())
+            w.commit()
+        files[f"zeroskip-{UUIDSTR}-{idx}-{idx}"] = w.image()
+    files[f"zeroskip-{UUIDSTR}-8"] = zf.FileWriter(bytes(range(16)), idx=8).image()
+    return files
+
+
+def repack2_inputs():
+    """Three packed files without deletes (0-3, 4-7, 8-9): branch 2's input,
+    on which the reference's merge has no quirk (ref_merge_packed)."""
+    import numpy as np
+    rng = np.random.default_rng(32)
+
+    def recs(n, lo, hi, vmax):
+        return sorted({b"%016d" % int(rng.integers(lo, hi)):
+                       rng.integers(0, 256, int(rng.integers(0, vmax)), dtype=np.uint8).tobytes()
+                       for _ in range(n)}.items())
+    spec = {(0, 3): recs(100, 0, 500, 200), (4, 7): recs(400, 200, 4000, 200), (8, 9): recs(150, 0, 1000, 200)}
+    return {f"zeroskip-{UUIDSTR}-{a}-{b}": zf.packed_file(r, bytes(range(16)), a, b) for (a, b), r in spec.items()}
+
+
+def repack_fixture(branch: int) -> dict:
+    """The inputs, and the output the reference's own repack writes from them
+    (format_demo repack1 / repack2), under tests/golden/ref_format/repackN/."""
+    import hashlib
+    files = repack1_inputs() if branch == 1 else repack2_inputs()
+    d = os.path.join(OUTDIR, f"repack{branch}")
+    os.makedirs(d, exist_ok=True)
+    for f in os.listdir(d):
+        os.unlink(os.path.join(d, f))
+    for name, img in files.items():
+        with open(os.path.join(d, name), "wb") as fh:
+            fh.write(img)
+    if branch == 1:
+        srcs, (sidx, eidx) = [n for n in files if n.count("-") == 7], (3, 7)
+    else:
+        srcs, (sidx, eidx) = sorted(files), (4, 9)
+    out = os.path.join(d, "reference_out.zs")
+    rep = ref_repack(branch, out, bytes(range(16)), sidx, eidx, [os.path.join(d, n) for n in srcs])
+    img = open(out, "rb").read()
+    return dict(repack=branch, inputs=sorted(files), startidx=sidx, endidx=eidx, reference=rep, size=len(img),
+                sha256=hashlib.sha256(img).hexdigest(),
+                out_name=f"zeroskip-{UUIDSTR}-{sidx}-{eidx}")
+
+
 def fixtures() -> dict:
     """name -> (image bytes, kind) for the committed fixture set."""
     out = {}
@@ -254,6 +377,8 @@ def main():
         manifest[name] = dict(kind=kind, size=len(img), reference=ref_verify(path))
     manifest["long_value"] = long_fixture()
     manifest["packed_long"] = packed_long_fixture()
+    manifest["repack1"] = repack_fixture(1)
+    manifest["repack2"] = repack_fixture(2)
     with open(os.path.join(OUTDIR, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)
         f.write("\n")

@@ -23,7 +23,7 @@ pytestmark = pytest.mark.gpu
 
 DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ref_format")
 MANIFEST = json.load(open(os.path.join(DIR, "manifest.json")))
-IMAGES = sorted(n for n in MANIFEST if "generator" not in MANIFEST[n])   # committed as bytes
+IMAGES = sorted(n for n in MANIFEST if "generator" not in MANIFEST[n] and "repack" not in MANIFEST[n])
 
 
 def fixture(name):
@@ -120,3 +120,27 @@ def test_verify_files_matches_reference_verifier(gpu):
     assert rep["files"] == len(names) and rep["header_errors"] == 0 and rep["walk_errors"] == 0
     assert rep["bad_commits"] + rep["stale_empty_commits"] == rejected
     assert rep["stale_empty_commits"] == stale
+
+
+@pytest.mark.parametrize("branch", [1, 2])
+def test_product_repack_equals_reference_repack(gpu, tmp_path, branch):
+    """zscrc_zs_repack (the product's zsdb_repack, GPU checksums) over the
+    inputs the reference's own repack read (tests/golden/ref_format/repackN,
+    with a .zsdb): the packed file it writes is the reference's output byte
+    for byte -- branch 1 from five finalised files, branch 2 from three
+    packed files (delete-free: the reference's merge quirk does not apply)."""
+    import shutil
+    from zeroskip_amd import repack
+    m = MANIFEST[f"repack{branch}"]
+    src = os.path.join(DIR, f"repack{branch}")
+    for n in m["inputs"]:
+        shutil.copy(os.path.join(src, n), tmp_path / n)
+    curidx = 8 if branch == 1 else 10
+    uuidstr = m["out_name"].split("-", 1)[1].rsplit("-", 2)[0]
+    (tmp_path / ".zsdb").write_bytes(zf.dotzsdb_bytes(4096, uuidstr.encode() + b"\0", curidx))
+    rep = repack.repack_dir(str(tmp_path))
+    assert rep["branch"] == branch and os.path.basename(rep["path"]) == m["out_name"]
+    with open(os.path.join(src, "reference_out.zs"), "rb") as f:
+        want = f.read()
+    with open(tmp_path / m["out_name"], "rb") as f:
+        assert f.read() == want

@@ -33,7 +33,7 @@ REF = "/root/reference"
 HAVE_REF = os.path.isdir(os.path.join(REF, "src")) and os.path.exists("/opt/conda/include/uuid/uuid.h")
 live = pytest.mark.skipif(not HAVE_REF, reason="no /root/reference (or its libuuid header) here")
 MANIFEST = json.load(open(os.path.join(mrf.OUTDIR, "manifest.json")))
-IMAGES = sorted(n for n in MANIFEST if "generator" not in MANIFEST[n])   # committed as bytes
+IMAGES = sorted(n for n in MANIFEST if "generator" not in MANIFEST[n] and "repack" not in MANIFEST[n])
 
 
 def fixture(name):
@@ -128,6 +128,30 @@ def test_packed_long_fixture_regenerates_reference_image(packed_long):
         bad[c["offset"]] ^= 0x01
         assert c["reference"]["rc"] == -9                 # ZS_INVALID_DB
         assert not zf.packed_check(bytes(bad))[0]["ok"], k
+
+
+def _repack_dir(branch):
+    d = os.path.join(mrf.OUTDIR, f"repack{branch}")
+    m = MANIFEST[f"repack{branch}"]
+    inputs = {n: open(os.path.join(d, n), "rb").read() for n in m["inputs"]}
+    return m, inputs, open(os.path.join(d, "reference_out.zs"), "rb").read()
+
+
+def test_repack_fixtures_match_oracle():
+    """The reference's own repack (zeroskip-packed.c:384-473 from the memtree
+    of finalised files; :617-742 over two packed files) wrote
+    tests/golden/ref_format/repackN/reference_out.zs from the inputs beside
+    it: the oracle's repack_finalised / repack_packed give the same bytes."""
+    import hashlib
+    m, inputs, out = _repack_dir(1)
+    assert hashlib.sha256(out).hexdigest() == m["sha256"] and m["reference"]["rc"] == 0
+    fin = [inputs[n] for n in sorted(inputs, key=lambda n: int(n.rsplit("-", 1)[1])) if n.count("-") == 7]
+    assert len(fin) == 5
+    assert zf.packed_file(zf.repack_finalised(fin), bytes(range(16)), m["startidx"], m["endidx"]) == out
+    m, inputs, out = _repack_dir(2)
+    assert hashlib.sha256(out).hexdigest() == m["sha256"] and m["reference"]["rc"] == 0
+    older, newer = (inputs[f"zeroskip-{mrf.UUIDSTR}-{r}"] for r in ("4-7", "8-9"))
+    assert zf.packed_file(zf.repack_packed(older, newer), bytes(range(16)), 4, 9) == out
 
 
 def test_fixture_set_covers_bad_and_stale():
@@ -241,6 +265,74 @@ def test_reference_packed_verifier_on_oracle_image(demo, tmp_path, packed_long):
 
 
 @live
+@pytest.mark.parametrize("seed", [41, 42, 43])
+def test_reference_repack_finalised_equals_oracle(demo, tmp_path, seed):
+    """Branch 1 on the reference's own code (finalised files -> memtree ->
+    zs_packed_file_new_from_memtree): the oracle's merge (a later record of a
+    key replaces an earlier one, deletes kept) byte for byte."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    images, paths = [], []
+    for idx in range(2, 2 + int(rng.integers(2, 6))):
+        w = zf.FileWriter(bytes(range(16)), idx=idx)
+        for t in range(int(rng.integers(20, 120))):
+            k = b"%016d" % int(rng.integers(0, 150))
+            if rng.integers(0, 6) == 0:
+                w.remove(k)
+            else:
+                w.add(k, rng.integers(0, 256, int(rng.integers(0, 300)), dtype=np.uint8).tobytes())
+            if rng.integers(0, 3) == 0:
+                w.commit()
+        w.commit()
+        images.append(w.image())
+        paths.append(tmp_path / f"zeroskip-{mrf.UUIDSTR}-{idx}-{idx}")
+        paths[-1].write_bytes(images[-1])
+    out = tmp_path / "out"
+    assert mrf.ref_repack(1, str(out), bytes(range(16)), 2, 1 + len(images), [str(p) for p in paths]) == {"rc": 0}
+    want = zf.packed_file(zf.repack_finalised(images), bytes(range(16)), 2, 1 + len(images))
+    assert out.read_bytes() == want
+
+
+@live
+def test_reference_repack_packed_and_its_delete_quirk(demo, tmp_path):
+    """Branch 2 on the reference's own code (zs_iterator_* +
+    zs_packed_file_new_from_packed_files).  Without deletes its output is
+    the oracle's merge (the older of the two newest files wins a key)
+    byte for byte -- so the product's, which the GPU tests hold to the
+    oracle.  With deletes the reference loses data: its packed iterator sets
+    `deleted` on the first delete it steps onto and never clears it
+    (zeroskip-iterator.c:250-251), so every later record of that source is
+    dropped.  ref_merge_packed restates that exactly (bytes equal); the
+    product keeps the records, as the oracle does."""
+    import numpy as np
+    rng = np.random.default_rng(44)
+
+    def recs(n, lo, hi, pdel):
+        return sorted({b"%016d" % int(rng.integers(lo, hi)):
+                       (None if pdel and rng.integers(0, pdel) == 0 else
+                        rng.integers(0, 256, int(rng.integers(0, 300)), dtype=np.uint8).tobytes())
+                       for _ in range(n)}.items())
+    for pdel in (0, 12, 4):
+        spec = {(0, 3): recs(100, 0, 900, pdel), (4, 7): recs(700, 300, 9000, pdel), (8, 9): recs(300, 0, 3000, pdel)}
+        imgs = {k: zf.packed_file(r, bytes(range(16)), *k) for k, r in spec.items()}
+        paths = []
+        for (a, b), img in imgs.items():
+            paths.append(tmp_path / f"zeroskip-{mrf.UUIDSTR}-{a}-{b}")
+            paths[-1].write_bytes(img)
+        out = tmp_path / f"out{pdel}"
+        assert mrf.ref_repack(2, str(out), bytes(range(16)), 4, 9, [str(p) for p in paths]) == {"rc": 0}
+        got = out.read_bytes()
+        quirk = zf.packed_file(mrf.ref_merge_packed([(2, spec[(4, 7)]), (1, spec[(8, 9)])]), bytes(range(16)), 4, 9)
+        fixed = zf.packed_file(zf.repack_packed(imgs[(4, 7)], imgs[(8, 9)]), bytes(range(16)), 4, 9)
+        assert got == quirk
+        assert (got == fixed) == (pdel == 0)
+        if pdel:
+            assert len(zf.packed_records(got)) < len(zf.packed_records(fixed))
+        for p in paths:
+            p.unlink()
+
+
+@live
 def test_committed_fixtures_regenerate(demo, tmp_path):
     for name, (img, kind) in mrf.fixtures().items():
         assert img == fixture(name), name
@@ -249,6 +341,18 @@ def test_committed_fixtures_regenerate(demo, tmp_path):
         assert mrf.ref_verify(str(p)) == MANIFEST[name]["reference"]
         assert MANIFEST[name]["kind"] == kind
     assert mrf.long_fixture() == MANIFEST["long_value"]
+    import hashlib
+    for branch, inputs in ((1, mrf.repack1_inputs()), (2, mrf.repack2_inputs())):
+        m, committed, out = _repack_dir(branch)
+        assert inputs == committed
+        srcs = [n for n in sorted(inputs) if branch == 2 or n.count("-") == 7]
+        d = tmp_path / f"r{branch}"
+        d.mkdir()
+        for n, img in inputs.items():
+            (d / n).write_bytes(img)
+        assert mrf.ref_repack(branch, str(d / "o"), bytes(range(16)), m["startidx"], m["endidx"],
+                              [str(d / n) for n in srcs]) == m["reference"]
+        assert hashlib.sha256((d / "o").read_bytes()).hexdigest() == m["sha256"]
 
 
 @live
