@@ -236,7 +236,7 @@ def ref_merge_packed(sources):
     quirks: sources = [(priority, [(key, value-or-None)])] in the order of the
     file list.  A key in several sources goes to the higher priority; the
     iterator's `deleted` flag is set when it steps onto a delete
-    (zeroskip-iterator.c:250-251) and never cleared, so from a source's first
+    (zeroskip-iterator.c:258-259) and never cleared, so from a source's first
     delete after its first record on, none of that source's records is
     written; a delete as a source's FIRST record is never flagged
     (zs_iterator_begin_for_packed_files reads its key without the type) and

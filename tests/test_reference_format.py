@@ -301,7 +301,7 @@ def test_reference_repack_packed_and_its_delete_quirk(demo, tmp_path):
     byte for byte -- so the product's, which the GPU tests hold to the
     oracle.  With deletes the reference loses data: its packed iterator sets
     `deleted` on the first delete it steps onto and never clears it
-    (zeroskip-iterator.c:250-251), so every later record of that source is
+    (zeroskip-iterator.c:258-259), so every later record of that source is
     dropped.  ref_merge_packed restates that exactly (bytes equal); the
     product keeps the records, as the oracle does."""
     import numpy as np
