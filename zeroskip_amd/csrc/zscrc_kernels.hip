@@ -2120,6 +2120,22 @@ __device__ __forceinline__ void m64_issue(const MultiBatch &m, uint64_t n, const
  * bound_probe.jsonl), the same-GPU streaming read 0.618.  GUARD = 1
  * (tuning bit 128): round 4's guarded stores; 2 (bit 64): unconditional
  * non-temporal stores. */
+/* The result stores' cache policy (zs_launch_multi's m64_store_policy):
+ * vector stores with explicit scope / streaming bits -- 3: sc1 (device
+ * scope: written through the XCD's L2; the default), 4: sc0 sc1 (system
+ * scope), 5: sc1 nt.  Inline asm is invisible to the compiler's vmcnt
+ * bookkeeping, which can then only over-wait (a younger store in the count). */
+template <int POL>
+__device__ __forceinline__ void store_policy(uint32_t *p, uint32_t v)
+{
+    if (POL == 3)
+        asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+    else if (POL == 4)
+        asm volatile("global_store_dword %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+    else
+        asm volatile("global_store_dword %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
+}
+
 template <int K, int GUARD>
 __global__ __launch_bounds__(WG) void multi64_kernel(BatchDesc d, MultiBatch m, const uint32_t *__restrict__ gtab)
 {
@@ -2222,6 +2238,8 @@ __global__ __launch_bounds__(WG) void multi64_kernel(BatchDesc d, MultiBatch m, 
                 uint32_t *at = r0 + 64 * q < n ? out + r0 + 64 * q : m.sink + lane;
                 if (GUARD == 2)
                     __builtin_nontemporal_store(r[q] ^ d.xor_io, at);
+                else if (GUARD >= 3)
+                    store_policy<GUARD>(at, r[q] ^ d.xor_io);
                 else
                     *at = r[q] ^ d.xor_io;
             }
@@ -4877,6 +4895,26 @@ extern "C" int zs_launch_commit(const zs::BatchDesc *d, const uint32_t *gtab, in
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
+/* The result stores' cache policy (multi64_kernel's store_policy; env
+ * ZSCRC_M64_POL for A/B): 3 = sc1, the default -- device-scope stores,
+ * written through the XCD's L2 as they are issued: config 2 0.0125-0.0126
+ * -> 0.0121 ms per batch on one card, 0.0111 -> 0.0107 on another, with sc0
+ * sc1 level and sc1 nt slower (0.0129-0.0130), interleaved runs of the bench
+ * (profiles/r05/m64_store_policy/) -- presumably the 256 MiB of results
+ * leave the L2 as they are issued instead of in write-back bursts amid the
+ * 4 GiB read stream.  The same policy on commit_kernel's
+ * per-commit arrays and the writer's CRC fields measured level (config 4:
+ * arrays 0.677 / 0.675 ms, CRC array 0.578 / 0.574, writer 0.983 / 0.976);
+ * 0 = plain stores (round 5's first form). */
+static int m64_store_policy()
+{
+    static const int pol = [] {
+        const char *e = getenv("ZSCRC_M64_POL");
+        return e ? atoi(e) : 3;
+    }();
+    return pol;
+}
+
 extern "C" int zs_launch_multi(const zs::BatchDesc *d, const zs::MultiBatch *m, const uint32_t *gtab, int grid,
                                hipStream_t stream)
 {
@@ -4891,8 +4929,14 @@ extern "C" int zs_launch_multi(const zs::BatchDesc *d, const zs::MultiBatch *m, 
         hipLaunchKernelGGL((zs::multi64_kernel<2, 1>), dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
     else if (packed64 && (d->opt & 64u)) /* A/B: non-temporal result stores */
         hipLaunchKernelGGL((zs::multi64_kernel<2, 2>), dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
-    else if (packed64) /* two chains per lane (three measured slower: VGPR spills) */
+    else if (packed64 && m64_store_policy() == 5) /* A/B: result stores sc1 nt */
+        hipLaunchKernelGGL((zs::multi64_kernel<2, 5>), dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
+    else if (packed64 && m64_store_policy() == 4) /* A/B: result stores sc0 sc1 */
+        hipLaunchKernelGGL((zs::multi64_kernel<2, 4>), dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
+    else if (packed64 && m64_store_policy() == 0) /* A/B: plain result stores */
         hipLaunchKernelGGL((zs::multi64_kernel<2, 0>), dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
+    else if (packed64) /* two chains per lane (three measured slower: VGPR spills) */
+        hipLaunchKernelGGL((zs::multi64_kernel<2, 3>), dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
     else
         hipLaunchKernelGGL(zs::multi_kernel, dim3(grid), dim3(zs::WG), 0, stream, *d, *m, gtab);
     return hipGetLastError() == hipSuccess ? 0 : -3;
