@@ -1,0 +1,40 @@
+"""The host-side zeroskip parsers of libzscrc (zscrc_zs_walk / _packed_spans
+/ _records / _header_crc / _dotzsdb_crc) on mutated copies of the
+reference-written fixtures: every span and record they return lies inside
+the image, and crc32c_hw == crc32c_sw on random slices (tests/c/parse_fuzz.c,
+built here against the in-tree libzscrc.so; no GPU call).  The same driver
+under AddressSanitizer + UBSan is tools/asan_fuzz.sh."""
+import json
+import os
+import subprocess
+
+import pytest
+
+from oracle import zs_format as zf
+from zeroskip_amd import LIB_PATH
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FIX = os.path.join(ROOT, "tests", "golden", "ref_format")
+FILES = ["active_clean.zs", "active_corrupt.zs", "active_stale.zs", "active_longkey.zs", "packed.zs",
+         "repack1/reference_out.zs", "repack2/reference_out.zs"]
+
+
+@pytest.fixture(scope="module")
+def fuzzer(tmp_path_factory):
+    d = tmp_path_factory.mktemp("fuzz")
+    exe = d / "parse_fuzz"
+    subprocess.check_call(["gcc", "-O2", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "c", "parse_fuzz.c"), "-L", os.path.dirname(LIB_PATH),
+                           "-lzscrc", f"-Wl,-rpath,{os.path.dirname(LIB_PATH)}", "-o", str(exe)])
+    (d / "dotzsdb").write_bytes(zf.dotzsdb_bytes(4096, b"00010203-0405-0607-0809-0a0b0c0d0e0f\0", 8))
+    return str(exe), [os.path.join(FIX, f) for f in FILES] + [str(d / "dotzsdb")]
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_parsers_stay_inside_mutated_images(fuzzer, seed):
+    exe, files = fuzzer
+    out = subprocess.run([exe, "3000", str(seed), *files], capture_output=True, text=True, timeout=300,
+                         env={**os.environ, "ZSCRC_GPU_MIN": "0"})
+    assert out.returncode == 0, out.stderr[-2000:]
+    rep = json.loads(out.stdout)
+    assert rep["violations"] == 0 and rep["walks"] == 3000 and rep["record_lists"] == 9000
