@@ -19,7 +19,7 @@ OBJS="build/zscrc_kernels.o build/zscrc_api.o build/zscrc_zs.o build/zscrc_consi
 ( cd $W/zeroskip_amd && make -s -j8 \
     HIPFLAGS="-O1 -g -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer" \
     CC="$CL" CFLAGS="-O1 -fPIC -std=gnu11 $SAN" CXX="${CL}++ $SAN" $OBJS && \
-  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -fsanitize=address -shared-libasan -o libzscrc.so $OBJS -lpthread )
+  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -Xarch_host -fsanitize=address -Xarch_host -shared-libasan -o libzscrc.so $OBJS -lpthread )
 $CL -O1 $SAN -I"$R/include" "$R/tests/c/parse_fuzz.c" -L$W/zeroskip_amd -lzscrc -Wl,-rpath,$W/zeroskip_amd \
     -shared-libasan -o $W/parse_fuzz
 python3 -c "import sys; sys.path.insert(0, '$R'); from oracle import zs_format as zf; \
