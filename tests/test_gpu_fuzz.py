@@ -1,0 +1,53 @@
+"""The GPU verifier on mutated reference-written images (tests/fuzzlib.py):
+zscrc_zs_verify_image walks on the host and recomputes every commit it
+found on the GPU; its verdict equals the format oracle's on those commits
+(the reference verifier's semantics: stored CRC against the span + trailer
+from 0) -- however the image was cut, flipped or given extreme lengths --
+and a batch of them through zscrc_zs_verify_files agrees too."""
+import os
+import random
+
+import pytest
+
+from tests import fuzzlib
+from zeroskip_amd import zsfile
+
+pytestmark = pytest.mark.gpu
+
+FIX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ref_format")
+FILES = ["active_clean.zs", "active_corrupt.zs", "active_stale.zs", "active_longkey.zs"]
+
+
+def _cases(seed, n):
+    rng = random.Random(seed)
+    imgs = [open(os.path.join(FIX, f), "rb").read() for f in FILES]
+    out = []
+    while len(out) < n:
+        m = fuzzlib.mutate(rng, rng.choice(imgs))
+        if len(m) < 40:
+            continue
+        o = fuzzlib.oracle_walk(m)
+        if o is None:
+            continue
+        off, ln, rc, wend = zsfile.walk(m)
+        bad = [not c["ok"] for c in o[0][:len(off)]]
+        out.append((m, len(off), bad))
+    return out
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_verify_image_on_mutated_images(gpu, seed):
+    for m, ncommits, bad in _cases(seed, 150):
+        rep = zsfile.verify_image(m)
+        assert rep["n_commits"] == ncommits
+        assert rep["n_bad"] == sum(bad), (rep, sum(bad))
+        if any(bad):
+            assert rep["first_bad"] == bad.index(True)
+
+
+def test_verify_files_on_mutated_images(gpu):
+    cases = _cases(3, 60)
+    rep = zsfile.verify_files([m for m, _, _ in cases])
+    assert rep["files"] == len(cases)
+    assert rep["commits"] == sum(n for _, n, _ in cases)
+    assert rep["bad_commits"] + rep["stale_empty_commits"] == sum(sum(b) for _, _, b in cases)

@@ -3,9 +3,16 @@
 reference-written fixtures: every span and record they return lies inside
 the image, and crc32c_hw == crc32c_sw on random slices (tests/c/parse_fuzz.c,
 built here against the in-tree libzscrc.so; no GPU call).  The same driver
-under AddressSanitizer + UBSan is tools/asan_fuzz.sh."""
+under AddressSanitizer + UBSan is tools/asan_fuzz.sh.
+
+Against the format oracle: on every mutated active / finalised image the
+oracle can read, libzscrc's walk either ends like the oracle's (END) with
+the same spans, or stops early (TRUNCATED / STOPPED on a length that leaves
+the image, where the reference would read past the mmap) with a prefix of
+the oracle's spans."""
 import json
 import os
+import random
 import subprocess
 
 import pytest
@@ -38,3 +45,30 @@ def test_parsers_stay_inside_mutated_images(fuzzer, seed):
     assert out.returncode == 0, out.stderr[-2000:]
     rep = json.loads(out.stdout)
     assert rep["violations"] == 0 and rep["walks"] == 3000 and rep["record_lists"] == 9000
+
+
+@pytest.mark.parametrize("seed", [5, 6])
+def test_walk_matches_oracle_or_stops_early(seed):
+    from tests import fuzzlib
+    from zeroskip_amd import zsfile
+    rng = random.Random(seed)
+    imgs = [open(os.path.join(FIX, f), "rb").read() for f in FILES[:4]]
+    full = prefix = 0
+    for _ in range(1500):
+        m = fuzzlib.mutate(rng, rng.choice(imgs))
+        if len(m) < 40:
+            continue
+        o = fuzzlib.oracle_walk(m)
+        if o is None:
+            continue
+        commits, end, why = o
+        off, ln, rc, wend = zsfile.walk(m)
+        got = list(zip(off.tolist(), ln.tolist()))
+        want = [(c["span_off"], c["span_len"]) for c in commits]
+        if rc == zsfile.END:
+            assert why == "end" and end == len(m) == wend and got == want
+            full += 1
+        else:
+            assert rc in (zsfile.TRUNCATED, zsfile.STOPPED) and want[:len(got)] == got
+            prefix += 1
+    assert full > 300 and prefix > 300
