@@ -45,6 +45,31 @@ def test_verify_image_on_mutated_images(gpu, seed):
             assert rep["first_bad"] == bad.index(True)
 
 
+def test_verify_image_on_mutated_packed_images(gpu):
+    """Finalised images (packed.zs, both repack outputs) mutated: accepted
+    ones verify two commits with the oracle's packed_check verdicts;
+    rejected ones report the rejection and launch nothing."""
+    from oracle import zs_format as zf
+    rng = random.Random(4)
+    imgs = [open(os.path.join(FIX, f), "rb").read()
+            for f in ("packed.zs", "repack1/reference_out.zs", "repack2/reference_out.zs")]
+    checked = 0
+    for _ in range(200):
+        m = fuzzlib.mutate(rng, rng.choice(imgs))
+        if len(m) < 48:
+            continue
+        rc = zsfile.packed_spans(m)[2]
+        rep = zsfile.verify_image(m, zsfile.PACKED)
+        assert rep["walk_rc"] == rc
+        if rc != 0:
+            assert rep["n_commits"] == 0
+            continue
+        bad = sum(not c["ok"] for c in zf.packed_check(m))
+        assert rep["n_commits"] == 2 and rep["n_bad"] == bad, (rep, bad)
+        checked += 1
+    assert checked > 60
+
+
 def test_verify_files_on_mutated_images(gpu):
     cases = _cases(3, 60)
     rep = zsfile.verify_files([m for m, _, _ in cases])

@@ -72,3 +72,30 @@ def test_walk_matches_oracle_or_stops_early(seed):
             assert rc in (zsfile.TRUNCATED, zsfile.STOPPED) and want[:len(got)] == got
             prefix += 1
     assert full > 300 and prefix > 300
+
+
+@pytest.mark.parametrize("seed", [7, 8])
+def test_packed_spans_match_oracle(seed):
+    """Mutated finalised images (the reference's packed file and both
+    repack outputs): whenever zscrc_zs_packed_spans accepts one, its two
+    spans are the format oracle's packed_check spans (which then never
+    raises); otherwise it rejects with a parse code (STOPPED / TRUNCATED)
+    or an error."""
+    from tests import fuzzlib
+    from zeroskip_amd import zsfile
+    rng = random.Random(seed)
+    imgs = [open(os.path.join(FIX, f), "rb").read() for f in FILES[4:]]
+    agree = rejected = 0
+    for _ in range(1500):
+        m = fuzzlib.mutate(rng, rng.choice(imgs))
+        if len(m) < 48:
+            continue
+        off, ln, rc = zsfile.packed_spans(m)
+        if rc != 0:
+            assert rc < 0 or rc in (zsfile.STOPPED, zsfile.TRUNCATED), rc
+            rejected += 1
+            continue
+        want = sorted((c["span_off"], c["span_len"]) for c in zf.packed_check(m))
+        assert sorted(zip(off.tolist(), ln.tolist())) == want
+        agree += 1
+    assert agree > 500 and rejected > 200
