@@ -1,0 +1,145 @@
+"""Randomised parity soak of the device batch entry points against the CPU
+oracle (oracle/zs_oracle.c), on shapes the structured tests do not build:
+records in random order, overlapping and duplicated, lengths straddling
+every dispatch boundary (the one-lane / 2-lane / 16-lane / wavefront /
+split-record classes and the 8-byte serial path), the last record ending
+at the buffer's last byte, random seeds, raw registers, correct / loose /
+wrong length bounds, and the fixed-stride and multi-batch forms at random
+strides and base offsets, and single / multi-span calls at random
+lengths, offsets and seeds.  Every CRC is compared, bit for bit."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle
+from zeroskip_amd import device as zd
+from zeroskip_amd._lib import DEFAULT_TEAMS
+
+pytestmark = pytest.mark.gpu
+
+M32 = np.uint32(0xFFFFFFFF)
+EDGES = [0, 1, 7, 8, 9, 15, 16, 63, 64, 65, 127, 128, 129, 639, 640, 641, 1023, 1024, 1025, 4095, 4096,
+         16383, 16384, 65535, 65536, 65537, (1 << 20) - 1, 1 << 20, (1 << 20) + 1]
+
+
+def _lengths(rng, n, kind):
+    if kind == "edges":
+        return rng.choice(np.array(EDGES, np.int64), n)
+    if kind == "short":
+        return rng.integers(0, 700, n).astype(np.int64)
+    if kind == "loguniform":
+        return np.exp(rng.uniform(0, np.log(3 << 20), n)).astype(np.int64)
+    # mixed: mostly short, a few long
+    lens = rng.integers(0, 400, n).astype(np.int64)
+    k = max(1, n // 200)
+    lens[rng.integers(0, n, k)] = rng.integers(1 << 16, 5 << 20, k)
+    return lens
+
+
+def _case(seed):
+    rng = np.random.default_rng(seed)
+    kind = ["edges", "short", "loguniform", "mixed"][seed % 4]
+    n = int(rng.integers(1, [6000, 60000, 600, 20000][seed % 4]))
+    lens = _lengths(rng, n, kind)
+    size = int(max(int(lens.max()) + 1, lens.sum() // 2 + 4096))
+    offs = (rng.integers(0, 1 << 62, n) % (size - lens + 1)).astype(np.int64)  # overlapping, any order
+    if n > 4:
+        dup = rng.integers(0, n, n // 5)
+        offs[dup[1:]], lens[dup[1:]] = offs[dup[0]], lens[dup[0]]             # duplicates
+    j = int(rng.integers(0, n))
+    offs[j] = size - lens[j]                                                  # ends at the last byte
+    seeds = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    data = rng.integers(0, 256, size, dtype=np.uint8)
+    return rng, data, offs, lens, seeds
+
+
+def _dev(a, gpu):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(gpu)
+
+
+def _u32(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy().view(np.uint32)
+
+
+@pytest.mark.parametrize("block", range(4))
+def test_random_batches(gpu, block):
+    for seed in range(25 * block, 25 * block + 25):
+        rng, data, offs, lens, seeds = _case(seed)
+        ref = oracle.batch(data, offs.astype(np.uint64), lens.astype(np.uint64), seeds, impl="hw", threads=8)
+        d, o, l = _dev(data, gpu), _dev(offs, gpu), _dev(lens, gpu)
+        s = _dev(seeds.view(np.int32), gpu)
+        bound = [None, int(lens.max()), int(lens.max()) * 2 + 1, max(1, int(lens.max()) // 2)][seed % 4]
+        out = _u32(zd.crc_batch(d, o, l, s, max_len=bound))
+        bad = np.nonzero(out != ref)[0]
+        assert bad.size == 0, (seed, [(int(i), int(offs[i]), int(lens[i])) for i in bad[:5]])
+        # raw registers: raw(s) = ~crc32c(~s)
+        raw = _u32(zd.crc_batch(d, o, l, s, raw=True))
+        rref = oracle.batch(data, offs.astype(np.uint64), lens.astype(np.uint64), seeds ^ M32, impl="hw",
+                            threads=8) ^ M32
+        assert np.array_equal(raw, rref), seed
+
+
+@pytest.mark.parametrize("teams", [(0, 0), (1 << 40, 1 << 40), (0, 1 << 40)], ids=["g64", "g1", "g16"])
+def test_random_batches_forced_teams(gpu, teams):
+    from zeroskip_amd._lib import lib
+    lib().zscrc_set_teams(*teams)
+    try:
+        for seed in (101, 102, 103, 104):
+            _, data, offs, lens, seeds = _case(seed)
+            lens = np.minimum(lens, 1 << 18)
+            offs = np.minimum(offs, data.size - lens)
+            ref = oracle.batch(data, offs.astype(np.uint64), lens.astype(np.uint64), seeds, impl="hw", threads=8)
+            out = _u32(zd.crc_batch(_dev(data, gpu), _dev(offs, gpu), _dev(lens, gpu),
+                                    _dev(seeds.view(np.int32), gpu)))
+            assert np.array_equal(out, ref), (teams, seed)
+    finally:
+        lib().zscrc_set_teams(*DEFAULT_TEAMS)
+
+
+def test_random_fixed_and_multi(gpu):
+    rng = np.random.default_rng(7)
+    for it in range(24):
+        length = int(rng.choice([1, 5, 8, 31, 63, 64, 65, 129, 312, 640, 641, 4000, 65536]))
+        stride = length + int(rng.choice([0, 0, 1, 8, 13, 64]))
+        n = int(rng.integers(1, max(2, min(200000, (48 << 20) // stride))))
+        shift = int(rng.integers(0, 64))
+        seed = int(rng.integers(0, 1 << 32))
+        data = rng.integers(0, 256, shift + stride * (n - 1) + length, dtype=np.uint8)
+        offs = (np.arange(n, dtype=np.uint64) * stride + shift)
+        lens = np.full(n, length, np.uint64)
+        ref = oracle.batch(data, offs, lens, np.full(n, seed, np.uint32), impl="hw", threads=8)
+        d = _dev(data, gpu)
+        out = _u32(zd.crc_fixed(d[shift:], stride, length, n, seed=seed))
+        assert np.array_equal(out, ref), (it, stride, length, n, shift)
+        if length <= 64 and it % 2 == 0:
+            k = int(rng.integers(1, 5))
+            bufs = [d[shift:]] + [_dev(rng.integers(0, 256, data.size - shift, dtype=np.uint8), gpu)
+                                  for _ in range(k - 1)]
+            outs = zd.crc_fixed_multi(bufs, stride, length, n, seed=seed)
+            for b, (buf, o) in enumerate(zip(bufs, outs)):
+                h = buf.cpu().numpy()
+                r = oracle.batch(h, offs - np.uint64(shift), lens, np.full(n, seed, np.uint32), impl="hw",
+                                 threads=8)
+                assert np.array_equal(_u32(o), r), (it, b, stride, length, n, shift)
+
+
+def test_random_spans(gpu):
+    rng = np.random.default_rng(9)
+    data = rng.integers(0, 256, 96 << 20, dtype=np.uint8)
+    d = _dev(data, gpu)
+    for it in range(16):
+        length = int(np.exp(rng.uniform(np.log(1), np.log(90 << 20))))
+        off = int(rng.integers(0, data.size - length + 1))
+        seed = int(rng.integers(0, 1 << 32))
+        ref = oracle.batch(data, np.array([off], np.uint64), np.array([length], np.uint64),
+                           np.array([seed], np.uint32), impl="hw", threads=8)
+        got = _u32(zd.crc_span(d, seed=seed, length=length, offset=off))
+        assert got[0] == ref[0], (it, off, length)
+        k = int(rng.integers(1, 9))
+        lens = np.exp(rng.uniform(np.log(16 << 10), np.log(24 << 20), k)).astype(np.int64)
+        offs = (rng.integers(0, 1 << 62, k) % (data.size - lens + 1)).astype(np.int64)
+        seeds = rng.integers(0, 1 << 32, k, dtype=np.uint64).astype(np.uint32)
+        ref = oracle.batch(data, offs.astype(np.uint64), lens.astype(np.uint64), seeds, impl="hw", threads=8)
+        got = _u32(zd.crc_spans(d, offs.tolist(), lens.tolist(), seeds.tolist()))
+        assert np.array_equal(got, ref), (it, k)
