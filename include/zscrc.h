@@ -310,7 +310,7 @@ int zscrc_device_verify_commits_bounded(const void *d_image, uint64_t image_size
 /* Device verdict of n commits (the verifier's question: is every commit
  * good, and which are not?): as zscrc_device_verify_commits_bounded (d_seed
  * may be NULL; max_len a bound on the span lengths, ZSCRC_LEN_UNBOUNDED if
- * none is known), but no per-commit output -- *d_nbad (device) = the number
+ * none is known -- results never depend on it), but no per-commit output -- *d_nbad (device) = the number
  * of commits whose status would not be 1 (mismatch, or no commit record in
  * the image), and d_bad (device, cap entries) receives the indices of the
  * first cap of them found, in no particular order.  A clean batch writes

@@ -7,6 +7,8 @@ at the buffer's last byte, random seeds, raw registers, correct / loose /
 wrong length bounds, and the fixed-stride and multi-batch forms at random
 strides and base offsets, and single / multi-span calls at random
 lengths, offsets and seeds.  Every CRC is compared, bit for bit."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -62,9 +64,13 @@ def _u32(t):
     return t.cpu().numpy().view(np.uint32)
 
 
+# env ZSCRC_SOAK_SEEDS: batches per block (default 25; longer soaks on request)
+SEEDS = int(os.environ.get("ZSCRC_SOAK_SEEDS", "25"))
+
+
 @pytest.mark.parametrize("block", range(4))
 def test_random_batches(gpu, block):
-    for seed in range(25 * block, 25 * block + 25):
+    for seed in range(SEEDS * block, SEEDS * block + SEEDS):
         rng, data, offs, lens, seeds = _case(seed)
         ref = oracle.batch(data, offs.astype(np.uint64), lens.astype(np.uint64), seeds, impl="hw", threads=8)
         d, o, l = _dev(data, gpu), _dev(offs, gpu), _dev(lens, gpu)
@@ -143,3 +149,71 @@ def test_random_spans(gpu):
         ref = oracle.batch(data, offs.astype(np.uint64), lens.astype(np.uint64), seeds, impl="hw", threads=8)
         got = _u32(zd.crc_spans(d, offs.tolist(), lens.tolist(), seeds.tolist()))
         assert np.array_equal(got, ref), (it, k)
+
+
+# ---------------------------------------------------------------- wrong bounds
+G1, G16 = 640, 1 << 20
+
+
+def test_wrong_bounds_batches(gpu):
+    """zscrc_device_batch_bounded: a bound below some lengths never changes a
+    result (the header's contract) -- at or below the one-lane bound (one
+    kernel over the caller's arrays) and between the classes (every class
+    still launched).  Includes the soak case that found the class pruning:
+    one 2 MiB record beside 466 short ones, bound 1 MiB."""
+    cases = [_case(339)]
+    rng = np.random.default_rng(17)
+    n = 3000
+    lens = rng.choice(np.array([0, 5, 64, 300, 640, 641, 5000, 8191, 8192, 70000, G16, G16 + 1, 3 << 20], np.int64), n)
+    size = int(lens.sum() // 3 + (4 << 20))
+    offs = (rng.integers(0, 1 << 62, n) % (size - lens + 1)).astype(np.int64)
+    seeds = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    cases.append((rng, rng.integers(0, 256, size, dtype=np.uint8), offs, lens, seeds))
+    for _, data, offs, lens, seeds in cases:
+        ref = oracle.batch(data, offs.astype(np.uint64), lens.astype(np.uint64), seeds, impl="hw", threads=8)
+        d, o, l = _dev(data, gpu), _dev(offs, gpu), _dev(lens, gpu)
+        s = _dev(seeds.view(np.int32), gpu)
+        for bound in (1, 300, G1, G1 + 1, 5000, 8192, 9000, G16 // 2, G16, G16 + 1):
+            out = _u32(zd.crc_batch(d, o, l, s, max_len=bound))
+            bad = np.nonzero(out != ref)[0]
+            assert bad.size == 0, (bound, [(int(i), int(lens[i])) for i in bad[:5]])
+
+
+def test_wrong_bounds_commits(gpu):
+    """The commit entry points with a bound below some span lengths (the
+    _bounded / verdict contract: results never depend on it): per-commit
+    arrays, the verdict (a corruption in a long span still found), the
+    writer's CRC array and the in-place writer, each equal to the unbounded
+    call's; spans of 0-640 bytes with some of 5,000 / 100,000 / 2.1 M."""
+    from zeroskip_amd import zsfile
+    rng = np.random.default_rng(23)
+    n = 20000
+    lens = rng.integers(0, G1 + 1, n)
+    lens[rng.integers(0, n, 40)] = rng.choice([5000, 100000, 2_100_000], 40)
+    offs = np.zeros(n, np.int64)
+    offs[0] = 43
+    offs[1:] = 43 + np.cumsum(lens + 8 + rng.integers(0, 8, n))[:-1]
+    size = int(offs[-1] + lens[-1] + 8 + 64)
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    host[offs + lens] = 4                                   # COMMIT records
+    oracle.write_commits(host, offs.astype(np.uint64), lens.astype(np.uint64), threads=8)
+    img = _dev(host, gpu)
+    o, ln = _dev(offs, gpu), _dev(lens.astype(np.int64), gpu)
+    crc0, st0 = zsfile.verify_commits(img, o, ln)
+    assert bool((st0 == 1).all())
+    long_i = int(np.nonzero(lens == lens.max())[0][0])
+    bad_img = img.clone()
+    bad_img[int(offs[long_i]) + 12345] ^= 1
+    fields = (o + ln + 4).view(-1, 1) + torch.arange(4, device=o.device).view(1, -1)
+    for bound in (300, G1, 1000, 50000, G16):
+        crc, st = zsfile.verify_commits(img, o, ln, max_len=bound)
+        assert torch.equal(crc, crc0) and torch.equal(st, st0), bound
+        nbad, _ = zsfile.verify_commits_verdict(img, o, ln, max_len=bound)
+        assert int(nbad.item()) == 0, bound
+        nbad, badi = zsfile.verify_commits_verdict(bad_img, o, ln, max_len=bound)
+        assert int(nbad.item()) == 1 and int(badi[0].item()) == long_i, bound
+        assert torch.equal(zsfile.commit_crcs(img, o, ln, max_len=bound), crc0), bound
+        z = img.clone()
+        z[fields.view(-1)] = 0
+        zsfile.write_commits(z, o, ln, max_len=bound, crc=False)
+        assert torch.equal(z, img), bound

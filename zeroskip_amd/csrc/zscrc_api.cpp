@@ -538,7 +538,7 @@ int launch(DevCtx *c, int g, const zs::BatchDesc &d, hipStream_t s, int depth_hi
  * (unit ~ class bytes / items wanted, plan_kernel) and a fold kernel combines
  * each record's part registers. */
 int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1, uint64_t g16, uint64_t min_len,
-                          uint64_t max_len);
+                          uint64_t max_len, bool range_holds);
 
 /* A bounded commit batch (every span within the one-lane bound): commit_kernel
  * -- run rounds, verdicts, rounds dealt per workgroup.  Batches of at least
@@ -627,14 +627,16 @@ int launch_commit_two_pass(DevCtx *c, zs::BatchDesc d, hipStream_t s)
     return rc ? rc : rc2;
 }
 
-/* [min_len, max_len]: a range the caller knows every length lies in (the
- * host walk that found the spans does); classes outside it get no launch.
- * Results never depend on the range: a record outside it is still
- * classified and handled by its class's kernel, only the launches the
- * range rules out are skipped -- so a wrong range may leave such records
- * unprocessed, which is why the range must hold. */
+/* max_len: a bound on the lengths -- at most g1_max, one kernel straight
+ * over the caller's arrays (correct for any length: a wrong bound costs only
+ * time).  range_holds: [min_len, max_len] is a range the caller guarantees
+ * (the host walk that found the spans knows it; the _range entry point's
+ * contract), and the length classes outside it get no launch -- a record
+ * outside a wrong range would go unprocessed, so without that guarantee
+ * (the _bounded entry points, whose results never depend on the bound) every
+ * class is launched. */
 int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t max_len = ZSCRC_LEN_UNBOUNDED,
-                   uint64_t min_len = 0)
+                   uint64_t min_len = 0, bool range_holds = false)
 {
     const uint64_t g1 = g_g1_max, g16 = g_g16_max;
     {
@@ -660,7 +662,8 @@ int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t max_len =
     std::lock_guard<std::recursive_mutex> lk(c->mu);
     int rc = scratch_acquire(c, s);
     if (!rc)
-        rc = launch_classes_locked(c, d, s, g1, g16, min_len, max_len);
+        rc = launch_classes_locked(c, d, s, g1, g16, range_holds ? min_len : 0,
+                                   range_holds ? max_len : ZSCRC_LEN_UNBOUNDED, range_holds);
     const int rc2 = scratch_release(c, s);
     return rc ? rc : rc2;
 }
@@ -669,8 +672,9 @@ int launch_classes(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t max_len =
 constexpr uint64_t SMALL_CLASSIFY = 16384;
 
 int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1, uint64_t g16, uint64_t min_len,
-                          uint64_t max_len)
+                          uint64_t max_len, bool range_holds)
 {
+    (void)range_holds; /* (min_len, max_len) are 0 / unbounded unless it holds */
     const uint64_t n = d.n;
     uint64_t b1 = g16 < 8191 ? g16 : 8191;
     if (b1 < g1)
@@ -1509,22 +1513,39 @@ extern "C" int zscrc_internal_verdict_prezeroed(const void *d_image, uint64_t im
     d.bad_idx = d_bad;
     d.bad_cap = cap;
     d.bad_prezeroed = 1;
-    return launch_classes(c, d, static_cast<hipStream_t>(stream), max_len, 0);
+    /* max_len is the pass's own host walk's: the range holds */
+    return launch_classes(c, d, static_cast<hipStream_t>(stream), max_len, 0, true);
 }
+
+static int verdict_impl(const void *d_image, uint64_t image_size, const uint64_t *d_span_off,
+                        const uint64_t *d_span_len, const uint32_t *d_seed, size_t n, uint64_t min_len,
+                        uint64_t max_len, uint64_t *d_nbad, uint64_t *d_bad, size_t cap, void *stream,
+                        bool range_holds);
 
 int zscrc_device_verify_commits_verdict(const void *d_image, uint64_t image_size, const uint64_t *d_span_off,
                                         const uint64_t *d_span_len, const uint32_t *d_seed, size_t n,
                                         uint64_t max_len, uint64_t *d_nbad, uint64_t *d_bad, size_t cap,
                                         void *stream)
 {
-    return zscrc_device_verify_commits_verdict_range(d_image, image_size, d_span_off, d_span_len, d_seed, n, 0,
-                                                     max_len, d_nbad, d_bad, cap, stream);
+    /* max_len a bound the results never depend on (as _bounded) */
+    return verdict_impl(d_image, image_size, d_span_off, d_span_len, d_seed, n, 0, max_len, d_nbad, d_bad, cap,
+                        stream, false);
 }
 
 int zscrc_device_verify_commits_verdict_range(const void *d_image, uint64_t image_size, const uint64_t *d_span_off,
                                               const uint64_t *d_span_len, const uint32_t *d_seed, size_t n,
                                               uint64_t min_len, uint64_t max_len, uint64_t *d_nbad, uint64_t *d_bad,
                                               size_t cap, void *stream)
+{
+    /* the caller guarantees the range */
+    return verdict_impl(d_image, image_size, d_span_off, d_span_len, d_seed, n, min_len, max_len, d_nbad, d_bad,
+                        cap, stream, true);
+}
+
+static int verdict_impl(const void *d_image, uint64_t image_size, const uint64_t *d_span_off,
+                        const uint64_t *d_span_len, const uint32_t *d_seed, size_t n, uint64_t min_len,
+                        uint64_t max_len, uint64_t *d_nbad, uint64_t *d_bad, size_t cap, void *stream,
+                        bool range_holds)
 {
     if (min_len > max_len)
         return ZSCRC_EINVAL;
@@ -1557,7 +1578,7 @@ int zscrc_device_verify_commits_verdict_range(const void *d_image, uint64_t imag
     d.bad_count = reinterpret_cast<unsigned long long *>(d_nbad);
     d.bad_idx = d_bad;
     d.bad_cap = cap;
-    return launch_classes(c, d, s, max_len, min_len);
+    return launch_classes(c, d, s, max_len, min_len, range_holds);
 }
 
 const char *zscrc_last_error(void) { return t_err; }

@@ -118,9 +118,11 @@ def verify_commits_verdict(d_image: torch.Tensor, span_off: torch.Tensor, span_l
     """Device verdict (zscrc_device_verify_commits_verdict): (nbad, bad)
     int64 device tensors -- nbad[0] = commits that do not verify, bad[:min(
     nbad, cap)] their indices in no particular order.  No per-commit output.
-    `out`: preallocated (nbad, bad) tensors to reuse.  min_len / max_len: a
-    range every span length lies in (zscrc_device_verify_commits_verdict_range:
-    classes outside it get no launch)."""
+    `out`: preallocated (nbad, bad) tensors to reuse.  max_len alone: a bound
+    the results never depend on (zscrc_device_verify_commits_verdict); with
+    min_len > 0, [min_len, max_len] is a range every span length must lie in
+    (zscrc_device_verify_commits_verdict_range: classes outside it get no
+    launch)."""
     n = span_off.numel()
     size = d_image.numel() * d_image.element_size()
     dev = d_image.device
@@ -128,12 +130,20 @@ def verify_commits_verdict(d_image: torch.Tensor, span_off: torch.Tensor, span_l
         out = (torch.empty(1, dtype=torch.int64, device=dev), torch.empty(max(cap, 1), dtype=torch.int64, device=dev))
     nbad, bad = out
     assert seed is None or (seed.numel() == n and seed.dtype == torch.int32)
+    mx = LEN_UNBOUNDED if max_len is None else max_len
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    sp = None if seed is None else seed.data_ptr()
     with torch.cuda.device(dev):
-        check(lib().zscrc_device_verify_commits_verdict_range(
-            d_image.data_ptr(), size, span_off.data_ptr(), span_len.data_ptr(),
-            None if seed is None else seed.data_ptr(), n, min_len, LEN_UNBOUNDED if max_len is None else max_len,
-            nbad.data_ptr(), bad.data_ptr(), min(cap, bad.numel()),
-            torch.cuda.current_stream(dev).cuda_stream), "zscrc_device_verify_commits_verdict_range")
+        if min_len > 0:
+            check(lib().zscrc_device_verify_commits_verdict_range(
+                d_image.data_ptr(), size, span_off.data_ptr(), span_len.data_ptr(), sp, n, min_len, mx,
+                nbad.data_ptr(), bad.data_ptr(), min(cap, bad.numel()), stream),
+                "zscrc_device_verify_commits_verdict_range")
+        else:
+            check(lib().zscrc_device_verify_commits_verdict(
+                d_image.data_ptr(), size, span_off.data_ptr(), span_len.data_ptr(), sp, n, mx,
+                nbad.data_ptr(), bad.data_ptr(), min(cap, bad.numel()), stream),
+                "zscrc_device_verify_commits_verdict")
     return nbad, bad
 
 
