@@ -217,3 +217,86 @@ def test_wrong_bounds_commits(gpu):
         z[fields.view(-1)] = 0
         zsfile.write_commits(z, o, ln, max_len=bound, crc=False)
         assert torch.equal(z, img), bound
+
+
+# ------------------------------------------------------------ random commits
+T_KEY, T_COMMIT, T_FINAL = 1, 4, 16
+
+
+def _commit_case(seed):
+    rng = np.random.default_rng(1000 + seed)
+    n = int(rng.choice([37, 2000, 30000, 250_000]))
+    kind = seed % 3
+    if kind == 0:                                   # 0-640 uniform, edges weighted
+        lens = rng.integers(0, G1 + 1, n)
+        lens[rng.random(n) < 0.05] = rng.integers(0, 9)
+    elif kind == 1:                                 # zsbench-like: mostly 312, some others
+        lens = np.full(n, 312)
+        odd = rng.random(n) < 0.03
+        lens[odd] = rng.integers(0, 2000, int(odd.sum()))
+    else:                                           # short with long ones among them
+        lens = rng.integers(0, 400, n)
+        k = max(1, n // 500)
+        lens[rng.integers(0, n, k)] = rng.choice([641, 5000, 70000, 1_100_000, 2_500_000], k)
+    lens = lens.astype(np.int64)
+    gaps = rng.integers(0, 8, n) * int(rng.integers(0, 2))       # back to back, or gaps
+    offs = np.zeros(n, np.int64)
+    offs[0] = 40 + int(rng.integers(0, 8))
+    offs[1:] = offs[0] + np.cumsum(lens + 8 + gaps)[:-1]
+    size = int(offs[-1] + lens[-1] + 8 + 64)
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    u = rng.random(n)
+    has_rec = u >= 0.03
+    final = has_rec & (u < 0.08)
+    at = offs + lens
+    host[at[~has_rec]] = T_KEY
+    host[at[has_rec & ~final]] = T_COMMIT
+    host[at[final]] = T_FINAL
+    oracle.write_commits(host, offs[has_rec].astype(np.uint64), lens[has_rec].astype(np.uint64), threads=8)
+    clean = host.copy()
+    rec = np.nonzero(has_rec)[0]
+    hit = rng.choice(rec, min(rec.size, 1 + n // 2000), replace=False)
+    for j, i in enumerate(hit):
+        o, ln = int(offs[i]), int(lens[i])
+        if ln and j % 2 == 0:
+            host[o + int(rng.integers(0, ln))] ^= 0x40
+        else:
+            host[o + ln + 4 + j % 4] ^= 0x02
+    bound = [None, int(lens.max()), max(1, int(lens.max()) // 3), 300][seed % 4]
+    return host, clean, offs, lens, has_rec, hit, bound
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("ZSCRC_SOAK_COMMITS", "12"))))
+def test_random_commit_batches(gpu, seed):
+    """Random commit images -- lengths short / zsbench-like / with long spans,
+    back to back or with gaps, 3 % without a commit record, FINAL records,
+    a few corruptions in spans and stored CRCs, batches below and above the
+    run-only split, bounds none / exact / wrong -- through the per-commit
+    arrays, the verdict, the writer's CRC array and the in-place writer,
+    each against the oracle's writer (src/zeroskip-file.c:253-350)."""
+    from zeroskip_amd import zsfile
+    host, clean, offs, lens, has_rec, hit, bound = _commit_case(seed)
+    n = offs.size
+    img, o, ln = _dev(host, gpu), _dev(offs, gpu), _dev(lens, gpu)
+    want = oracle.commit_crcs(host, offs[has_rec].astype(np.uint64), lens[has_rec].astype(np.uint64), threads=8)
+    crc, st = zsfile.verify_commits(img, o, ln, max_len=bound)
+    crc, st = crc.cpu().numpy().view(np.uint32), st.cpu().numpy()
+    assert np.array_equal(crc[has_rec], want), seed
+    want_st = np.where(has_rec, 1, 2)
+    want_st[hit] = 0
+    assert np.array_equal(st, want_st), (seed, np.nonzero(st != want_st)[0][:5])
+    bad = set(np.nonzero(want_st != 1)[0].tolist())
+    nbad, badi = zsfile.verify_commits_verdict(img, o, ln, max_len=bound, cap=max(4096, len(bad)))
+    k = int(nbad.item())
+    assert k == len(bad) and set(badi[:k].cpu().tolist()) == bad, seed
+    # the writer on the clean image: its CRC array, then in place over zeroed fields
+    sel = np.nonzero(has_rec)[0]
+    os_, ls_ = _dev(offs[sel], gpu), _dev(lens[sel], gpu)
+    cimg = _dev(clean, gpu)
+    wc = oracle.commit_crcs(clean, offs[sel].astype(np.uint64), lens[sel].astype(np.uint64), threads=8)
+    assert np.array_equal(_u32(zsfile.commit_crcs(cimg, os_, ls_, max_len=bound)), wc), seed
+    fields = (os_ + ls_ + 4).view(-1, 1) + torch.arange(4, device=os_.device).view(1, -1)
+    z = cimg.clone()
+    z[fields.view(-1)] = 0
+    zsfile.write_commits(z, os_, ls_, max_len=bound, crc=False)
+    assert torch.equal(z, cimg), seed
