@@ -300,3 +300,77 @@ def test_random_commit_batches(gpu, seed):
     z[fields.view(-1)] = 0
     zsfile.write_commits(z, os_, ls_, max_len=bound, crc=False)
     assert torch.equal(z, cimg), seed
+
+
+# ------------------------------------------------- host-memory entry points
+def test_random_streams(gpu):
+    """zscrc_stream_*: random totals cut into random updates (empty, 1 byte,
+    unaligned, larger than a chunk), random chunk sizes and seeds, copied or
+    NOCOPY -- the final CRC equals the oracle's over the concatenation."""
+    from zeroskip_amd.stream import CrcStream
+    rng = np.random.default_rng(31)
+    pool = rng.integers(0, 256, 96 << 20, dtype=np.uint8)
+    for it in range(24):
+        total = int(np.exp(rng.uniform(0, np.log(90 << 20))))
+        start = int(rng.integers(0, pool.size - total + 1))
+        buf = pool[start:start + total]
+        cuts = np.sort(rng.integers(0, total + 1, int(rng.integers(0, 40))))
+        cuts = np.concatenate([[0], cuts, [total]])
+        seed = int(rng.integers(0, 1 << 32))
+        chunk = int(rng.choice([0, 4096, 1 << 20, 3 << 20, 64 << 20]))
+        nocopy = bool(it % 3 == 0)
+        s = CrcStream(seed=seed, chunk_bytes=chunk, nocopy=nocopy)
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            s.update(buf[a:b])
+        want = oracle.batch(buf, np.array([0], np.uint64), np.array([total], np.uint64),
+                            np.array([seed], np.uint32), impl="hw")[0]
+        assert s.final() == want, (it, total, chunk, nocopy, len(cuts))
+
+
+def test_random_dropin_offload(gpu):
+    """The drop-in symbols with the offload threshold lowered to 4 KiB, so
+    random lengths around it and far above it go to the GPU: crc32c_hw /
+    crc32c / crc32c_iovec chained from random seeds at random alignments
+    equal the oracle's; the counters show the GPU ran."""
+    from zeroskip_amd import crc32c as zc
+    from zeroskip_amd._lib import lib, stats
+    rng = np.random.default_rng(37)
+    pool = rng.integers(0, 256, 40 << 20, dtype=np.uint8)
+    warm, cold = lib().zscrc_gpu_min(0), lib().zscrc_gpu_min(1)
+    lib().zscrc_set_gpu_min(4096)
+    try:
+        before = stats()[1]
+        for it in range(40):
+            n = int(rng.choice([4095, 4096, 4097, 65537, int(rng.integers(0, 40 << 20))]))
+            a = int(rng.integers(0, pool.size - n + 1))
+            seed = int(rng.integers(0, 1 << 32))
+            want = oracle.batch(pool[a:a + n], np.array([0], np.uint64), np.array([n], np.uint64),
+                                np.array([seed], np.uint32), impl="hw")[0]
+            assert zc.crc32c_hw(seed, pool[a:a + n]) == want, (it, n, a)
+            assert zc.crc32c(seed, pool[a:a + n]) == want, (it, n, a)
+            k = int(rng.integers(1, 6))
+            cuts = np.sort(rng.integers(0, n + 1, k - 1))
+            parts = [pool[a + x:a + y] for x, y in zip(np.concatenate([[0], cuts]), np.concatenate([cuts, [n]]))]
+            want0 = oracle.batch(pool[a:a + n], np.array([0], np.uint64), np.array([n], np.uint64),
+                                 np.array([0], np.uint32), impl="hw")[0]
+            assert zc.crc32c_iovec(parts) == want0, (it, n, k)
+        assert stats()[1] > before
+    finally:
+        lib().zscrc_set_gpu_min_pair(warm, cold)
+
+
+def test_random_host_batches(gpu):
+    """zscrc_host_batch (host arrays in, results back): random records in
+    any order over a host buffer equal the oracle's."""
+    from zeroskip_amd._lib import lib
+    import ctypes
+    for seed in (3, 7, 11, 19):
+        _, data, offs, lens, seeds = _case(seed)
+        o = np.ascontiguousarray(offs.astype(np.uint64))
+        l = np.ascontiguousarray(lens.astype(np.uint64))
+        out = np.zeros(o.size, np.uint32)
+        rc = lib().zscrc_host_batch(data.ctypes.data, o.ctypes.data, l.ctypes.data, seeds.ctypes.data,
+                                    out.ctypes.data, o.size)
+        assert rc == 0
+        ref = oracle.batch(data, o, l, seeds, impl="hw", threads=8)
+        assert np.array_equal(out, ref), seed
