@@ -263,7 +263,12 @@ def _commit_case(seed):
         else:
             host[o + ln + 4 + j % 4] ^= 0x02
     bound = [None, int(lens.max()), max(1, int(lens.max()) // 3), 300][seed % 4]
-    return host, clean, offs, lens, has_rec, hit, bound
+    # verification seeds (the chained finalise commit): a few record spans
+    # verified from a nonzero seed, expected CRC recomputed from it
+    sd = np.zeros(n, np.uint32)
+    pick = has_rec & (rng.random(n) < 0.05)
+    sd[pick] = rng.integers(1, 1 << 32, int(pick.sum()), dtype=np.uint64).astype(np.uint32)
+    return host, clean, offs, lens, has_rec, hit, bound, sd
 
 
 @pytest.mark.parametrize("seed", range(int(os.environ.get("ZSCRC_SOAK_COMMITS", "12"))))
@@ -275,7 +280,7 @@ def test_random_commit_batches(gpu, seed):
     arrays, the verdict, the writer's CRC array and the in-place writer,
     each against the oracle's writer (src/zeroskip-file.c:253-350)."""
     from zeroskip_amd import zsfile
-    host, clean, offs, lens, has_rec, hit, bound = _commit_case(seed)
+    host, clean, offs, lens, has_rec, hit, bound, sd = _commit_case(seed)
     n = offs.size
     img, o, ln = _dev(host, gpu), _dev(offs, gpu), _dev(lens, gpu)
     want = oracle.commit_crcs(host, offs[has_rec].astype(np.uint64), lens[has_rec].astype(np.uint64), threads=8)
@@ -289,6 +294,18 @@ def test_random_commit_batches(gpu, seed):
     nbad, badi = zsfile.verify_commits_verdict(img, o, ln, max_len=bound, cap=max(4096, len(bad)))
     k = int(nbad.item())
     assert k == len(bad) and set(badi[:k].cpu().tolist()) == bad, seed
+    # seeded: span i's CRC continues from sd[i] (0 = from scratch)
+    seeded = np.nonzero(sd)[0]
+    if seeded.size:
+        crc_s, st_s = zsfile.verify_commits(img, o, ln, seed=_dev(sd.view(np.int32), gpu), max_len=bound)
+        crc_s = crc_s.cpu().numpy().view(np.uint32)
+        for i in seeded[:200]:
+            oi, li = int(offs[i]), int(lens[i])
+            fin = host[oi + li] == T_FINAL
+            w = oracle.commit_crc(oracle.crc32c_hw(int(sd[i]), host[oi:oi + li]), li, bool(fin))
+            assert crc_s[i] == w, (seed, int(i))
+        rest = np.nonzero(has_rec & (sd == 0))[0]
+        assert np.array_equal(crc_s[rest], crc[rest]), seed
     # the writer on the clean image: its CRC array, then in place over zeroed fields
     sel = np.nonzero(has_rec)[0]
     os_, ls_ = _dev(offs[sel], gpu), _dev(lens[sel], gpu)
@@ -374,3 +391,29 @@ def test_random_host_batches(gpu):
         assert rc == 0
         ref = oracle.batch(data, o, l, seeds, impl="hw", threads=8)
         assert np.array_equal(out, ref), seed
+
+
+def test_random_spans_any_shape(gpu):
+    """zscrc_device_spans past its one-launch shape (more than 8 spans, spans
+    under 16 KiB, empty ones: one span call each) and zscrc_device_span at 0
+    and tiny lengths, seeds and raw registers -- every result the oracle's."""
+    rng = np.random.default_rng(41)
+    data = rng.integers(0, 256, 24 << 20, dtype=np.uint8)
+    d = _dev(data, gpu)
+    for it in range(20):
+        k = int(rng.integers(1, 13))
+        lens = np.where(rng.random(k) < 0.5, rng.integers(0, 16 << 10, k), rng.integers(16 << 10, 6 << 20, k))
+        offs = (rng.integers(0, 1 << 62, k) % (data.size - lens + 1)).astype(np.int64)
+        seeds = rng.integers(0, 1 << 32, k, dtype=np.uint64).astype(np.uint32)
+        raw = bool(it % 2)
+        got = _u32(zd.crc_spans(d, offs.tolist(), lens.tolist(), seeds.tolist(), raw=raw))
+        s = seeds ^ M32 if raw else seeds
+        ref = oracle.batch(data, offs.astype(np.uint64), lens.astype(np.uint64), s, impl="hw", threads=8)
+        assert np.array_equal(got, ref ^ M32 if raw else ref), (it, k, lens.tolist())
+    for n in (0, 1, 3, 7, 8, 9, 63, 64, 65, 1023):
+        off = int(rng.integers(0, 4096))
+        seed = int(rng.integers(0, 1 << 32))
+        got = _u32(zd.crc_span(d, seed=seed, length=n, offset=off))[0]
+        ref = oracle.batch(data, np.array([off], np.uint64), np.array([n], np.uint64), np.array([seed], np.uint32),
+                           impl="hw")[0]
+        assert got == ref, (n, off)
