@@ -417,3 +417,32 @@ def test_random_spans_any_shape(gpu):
         ref = oracle.batch(data, np.array([off], np.uint64), np.array([n], np.uint64), np.array([seed], np.uint32),
                            impl="hw")[0]
         assert got == ref, (n, off)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_fill(gpu, seed):
+    """zscrc_zs_fill_commits (the writer for host images) on the random
+    commit images with their CRC fields blanked, at random chunk sizes (spans
+    straddling chunk ends, spans longer than a chunk streamed apart), staging
+    threads and bounds: the image comes back byte for byte as the oracle's
+    writer left it; spans without a commit record untouched and counted."""
+    from zeroskip_amd import zsfile
+    _, clean, offs, lens, has_rec, _, bound, _ = _commit_case(seed)
+    rng = np.random.default_rng(77 + seed)
+    blank = clean.copy()
+    rec = np.nonzero(has_rec)[0]
+    blank[(offs[rec] + lens[rec] + 4)[:, None] + np.arange(4)] = 0
+    chunk = [64 << 10, 1 << 20, 3 << 20, 0][seed % 4]
+    old = os.environ.get("ZSCRC_FILL_CHUNK")
+    if chunk:
+        os.environ["ZSCRC_FILL_CHUNK"] = str(chunk)
+    try:
+        rep = zsfile.fill_commits(blank, offs.astype(np.uint64), lens.astype(np.uint64), max_len=bound,
+                                  threads=int(rng.integers(0, 5)))
+    finally:
+        if old is None:
+            os.environ.pop("ZSCRC_FILL_CHUNK", None)
+        else:
+            os.environ["ZSCRC_FILL_CHUNK"] = old
+    assert rep["commits"] == rec.size and rep["no_record"] == offs.size - rec.size, rep
+    assert np.array_equal(blank, clean), (seed, np.nonzero(blank != clean)[0][:5])
