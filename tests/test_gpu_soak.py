@@ -446,3 +446,55 @@ def test_random_fill(gpu, seed):
             os.environ["ZSCRC_FILL_CHUNK"] = old
     assert rep["commits"] == rec.size and rep["no_record"] == offs.size - rec.size, rep
     assert np.array_equal(blank, clean), (seed, np.nonzero(blank != clean)[0][:5])
+
+
+def _random_file(rng, idx):
+    from oracle import zs_format as zf
+    w = zf.FileWriter(bytes(rng.integers(0, 256, 16, dtype=np.uint8)), idx)
+    for _ in range(int(rng.integers(0, 300))):
+        u = rng.random()
+        if u < 0.75:
+            key = bytes(rng.integers(0, 256, int(rng.integers(1, 64)), dtype=np.uint8))
+            val = bytes(rng.integers(0, 256, int(rng.choice([0, 5, 100, 4000, 70000])), dtype=np.uint8))
+            w.add(key, val)
+        elif u < 0.85:
+            w.remove(bytes(rng.integers(0, 256, int(rng.integers(1, 40)), dtype=np.uint8)))
+        else:
+            w.commit(final=bool(rng.random() < 0.1))
+    if rng.random() < 0.5:
+        w.finalise()
+    else:
+        w.commit()
+    img = bytearray(w.image())
+    for _ in range(int(rng.integers(0, 3))):       # corruptions past the header
+        if len(img) > 48:
+            img[int(rng.integers(40, len(img)))] ^= 1 << int(rng.integers(0, 8))
+    return bytes(img)
+
+
+def test_random_files(gpu):
+    """zscrc_zs_verify_image / zscrc_zs_verify_files on random active files
+    written the way zsdb_add / zsdb_remove / zsdb_commit write them (the
+    format oracle's FileWriter: short and 70 KB values, deletes, FINAL
+    commits, the finalise quirk), some bytes flipped: the verdicts equal the
+    format oracle's walk of each image (the fuzz test's semantics)."""
+    from tests import fuzzlib
+    from zeroskip_amd import zsfile
+    rng = np.random.default_rng(53)
+    imgs, bads, ncommits = [], [], []
+    for i in range(40):
+        img = _random_file(rng, i)
+        o = fuzzlib.oracle_walk(img)
+        if o is None:
+            continue
+        off, ln, rc, wend = zsfile.walk(img)
+        bad = [not c["ok"] for c in o[0][:len(off)]]
+        rep = zsfile.verify_image(img)
+        assert rep["n_commits"] == len(off) and rep["n_bad"] == sum(bad), (i, rep, sum(bad))
+        imgs.append(img)
+        bads.append(sum(bad))
+        ncommits.append(len(off))
+    assert len(imgs) > 25
+    rep = zsfile.verify_files(imgs)
+    assert rep["files"] == len(imgs) and rep["commits"] == sum(ncommits)
+    assert rep["bad_commits"] + rep["stale_empty_commits"] == sum(bads), rep
