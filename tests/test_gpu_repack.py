@@ -261,3 +261,38 @@ def test_repack_dir_rename_failure_releases_lock(gpu, tmp_path, monkeypatch):
     rep = repack.repack_dir(str(tmp_path))
     assert rep["branch"] == 0 and not (tmp_path / ".zsdb.lock").exists()
     assert (tmp_path / f"zeroskip-{UUIDSTR}-1-2").exists()
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_repack_finalised(gpu, tmp_path, seed):
+    """zsdb_repack branch 1 on random DBs: 1-7 finalised files of random
+    transactions (binary keys of 1-40 bytes from a small key space so keys
+    repeat across files, values of 0-5,000 bytes, deletes, several records
+    per commit): the packed file byte for byte the format oracle's merge."""
+    rng = np.random.default_rng(100 + seed)
+    keys = [bytes(rng.integers(0, 256, int(rng.integers(1, 41)), dtype=np.uint8)) for _ in range(300)]
+    nfiles = int(rng.integers(1, 8))
+    images = []
+    for idx in range(3, 3 + nfiles):
+        w = zf.FileWriter(UUID, idx=idx)
+        for t in range(int(rng.integers(0, 120))):
+            k = keys[int(rng.integers(0, len(keys)))]
+            if rng.random() < 0.1:
+                w.remove(k)
+            else:
+                w.add(k, rng.integers(0, 256, int(rng.choice([0, 10, 300, 5000])), dtype=np.uint8).tobytes())
+            if rng.random() < 0.4:
+                w.commit()
+        w.commit()
+        images.append(w.image())
+        with open(tmp_path / f"zeroskip-{UUIDSTR}-{idx}-{idx}", "wb") as fh:
+            fh.write(images[-1])
+    last = 3 + nfiles
+    (tmp_path / f"zeroskip-{UUIDSTR}-{last}").write_bytes(zf.FileWriter(UUID, idx=last).image())
+    _dotzsdb(tmp_path, last)
+    rep = repack.repack_dir(str(tmp_path))
+    want_recs = zf.repack_finalised(images)
+    out = tmp_path / f"zeroskip-{UUIDSTR}-3-{last - 1}"
+    assert rep["branch"] == 1 and rep["path"] == str(out), rep
+    assert open(out, "rb").read() == zf.packed_file(want_recs, UUID, 3, last - 1), seed
+    assert rep["records_out"] == len(want_recs)
