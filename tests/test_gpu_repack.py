@@ -296,3 +296,31 @@ def test_random_repack_finalised(gpu, tmp_path, seed):
     assert rep["branch"] == 1 and rep["path"] == str(out), rep
     assert open(out, "rb").read() == zf.packed_file(want_recs, UUID, 3, last - 1), seed
     assert rep["records_out"] == len(want_recs)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_repack_packed(gpu, tmp_path, seed):
+    """zsdb_repack branch 2 on random pairs of packed files: binary keys of
+    1-40 bytes from one key space (overlapping between the files), values of
+    0-5,000 bytes, deletes on both sides -- the merged file byte for byte the
+    format oracle's packed-files merge (the older wins a key in both, a
+    winning delete drops it)."""
+    rng = np.random.default_rng(200 + seed)
+    keys = [bytes(rng.integers(0, 256, int(rng.integers(1, 41)), dtype=np.uint8)) for _ in range(500)]
+
+    def recs(n):
+        out = {}
+        for _ in range(n):
+            k = keys[int(rng.integers(0, len(keys)))]
+            out[k] = None if rng.random() < 0.1 else rng.integers(
+                0, 256, int(rng.choice([0, 10, 300, 5000])), dtype=np.uint8).tobytes()
+        return sorted(out.items())
+    a, b = zf.packed_file(recs(int(rng.integers(0, 400))), UUID, 2, 4), zf.packed_file(
+        recs(int(rng.integers(0, 400))), UUID, 5, 8)
+    (tmp_path / f"zeroskip-{UUIDSTR}-2-4").write_bytes(a)
+    (tmp_path / f"zeroskip-{UUIDSTR}-5-8").write_bytes(b)
+    _dotzsdb(tmp_path, 9)
+    rep = repack.repack_dir(str(tmp_path))
+    out = tmp_path / f"zeroskip-{UUIDSTR}-2-8"
+    assert rep["branch"] == 2 and rep["files_merged"] == 2 and rep["path"] == str(out), rep
+    assert open(out, "rb").read() == zf.packed_file(zf.repack_packed(a, b), UUID, 2, 8), seed
