@@ -391,3 +391,24 @@ def test_device_row_matches_host_digest(gpu, case):
     assert np.array_equal(row, want), np.nonzero(row != want)[0][:10]
     if case == "corrupt":
         assert row[1] >= 1 and row[2] == 3
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("ZSCRC_SOAK_CONSISTENT", "8"))))
+def test_random_corruptions_match_oracle(gpu, seed):
+    """zsdb_consistent on the GPU backend and on the oracle backend over the
+    same DB with 1-4 random bytes flipped anywhere in its files (headers,
+    spans, commit records, pointer sections, the long records region): the
+    same report, field for field."""
+    rng = np.random.default_rng(300 + seed)
+    db = small_db(long_region=seed % 2 == 0, seed=100 + seed)
+    files = sorted(k for k in db if k != ".zsdb")
+    for _ in range(int(rng.integers(1, 5))):
+        f = files[int(rng.integers(0, len(files)))]
+        img = bytearray(db[f])
+        img[int(rng.integers(0, len(img)))] ^= 1 << int(rng.integers(0, 8))
+        db[f] = bytes(img)
+    g = gpu_report(db)
+    o = cs.Consistent(cs.open_db(db), 0, 1, OracleBackend()).prepare().run()
+    assert same(g, o), (seed, g.as_dict(), o.as_dict())
+    print(f"seed {seed}: ok={g.ok} bad={len(g.bad_commits)} header_errors={len(g.header_errors)} "
+          f"issues={len(g.issues)}")
