@@ -498,3 +498,32 @@ def test_random_files(gpu):
     rep = zsfile.verify_files(imgs)
     assert rep["files"] == len(imgs) and rep["commits"] == sum(ncommits)
     assert rep["bad_commits"] + rep["stale_empty_commits"] == sum(bads), rep
+
+
+def test_random_fixed_large(gpu):
+    """Big fixed-stride batches on the 16-lane coalesced teams (qteam: records
+    of 2 KiB and up; parts dealt per workgroup and folded in LDS or by the
+    fold launch on big batches): random lengths 2 KiB-1 MiB (not multiples of
+    the 1 KiB step), strides, misaligned bases and totals up to ~1.2 GB, every
+    CRC against the oracle."""
+    g = torch.Generator(device=gpu)
+    g.manual_seed(61)
+    total = 1_300_000_000
+    d = torch.randint(0, 256, (total,), dtype=torch.uint8, device=gpu, generator=g)
+    host = d.cpu().numpy()
+    rng = np.random.default_rng(61)
+    for it in range(12):
+        length = int(np.exp(rng.uniform(np.log(2048), np.log(1 << 20))))
+        if it % 3 == 0:
+            length = int(rng.choice([2048, 4096, 16384, 65536, 65536 + 8, 1 << 20]))
+        stride = length + int(rng.choice([0, 0, 8, 13, 1024]))
+        shift = int(rng.choice([0, 0, 4, 16, 37]))
+        budget = int(rng.choice([64 << 20, 300 << 20, total - 64]))
+        n = max(1, (budget - shift - length) // stride + 1)
+        seed = int(rng.integers(0, 1 << 32))
+        out = _u32(zd.crc_fixed(d[shift:], stride, length, n, seed=seed))
+        offs = np.arange(n, dtype=np.uint64) * stride + shift
+        ref = oracle.batch(host, offs, np.full(n, length, np.uint64), np.full(n, seed, np.uint32), impl="hw",
+                           threads=16)
+        bad = np.nonzero(out != ref)[0]
+        assert bad.size == 0, (it, length, stride, shift, n, bad[:5].tolist())
