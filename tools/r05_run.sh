@@ -10,6 +10,8 @@ T="python -u -m pytest --maxfail=10 -q --timeout 300 --timeout-method thread"
 for step in "$@"; do
   case "$step" in
     gputests) timeout -k 10 900 $T -m gpu tests > gpurun_out/gputests.log 2>&1 ;;
+    soaklong) ZSCRC_SOAK_SEEDS=250 ZSCRC_SOAK_COMMITS=240 ZSCRC_SOAK_CONSISTENT=60 timeout -k 10 900 \
+                $T tests/test_gpu_soak.py tests/test_gpu_consistent.py -k "random" > gpurun_out/soaklong.log 2>&1 ;;
     newtests) timeout -k 10 600 $T tests/test_gpu_c_link.py tests/test_gpu_fill.py tests/test_gpu_repack.py \
                 tests/test_gpu_mixed.py > gpurun_out/newtests.log 2>&1 ;;
     smoke)    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
