@@ -79,3 +79,22 @@ def test_fold_matches_oracle_any_split():
     bounds = [0] + cuts + [20000]
     digs = [(cpu_partial(torch.from_numpy(d[a:b].copy())), b - a) for a, b in zip(bounds, bounds[1:])]
     assert shard.fold(digs, 0xABCDEF) == oracle.crc32c_hw(0xABCDEF, d)
+
+
+def test_fold_random_splits():
+    """The GF(2) fold of per-piece raw registers over random cuts -- empty
+    pieces, one-byte pieces, a single piece -- and random seeds equals the
+    oracle CRC of the whole stream (200 trials)."""
+    rng = np.random.default_rng(19)
+    for _ in range(200):
+        n = int(rng.integers(0, 5000))
+        d = rng.integers(0, 256, n, dtype=np.uint8)
+        k = int(rng.integers(0, 9))
+        bounds = [0] + sorted(rng.integers(0, n + 1, k).tolist()) + [n]
+        digs = [(cpu_partial(torch.from_numpy(d[a:b].copy())), b - a) for a, b in zip(bounds, bounds[1:])]
+        seed = int(rng.integers(0, 1 << 32))
+        assert shard.fold(digs, seed) == oracle.crc32c_hw(seed, d), (n, bounds, seed)
+
+
+def test_sharded_crc_gloo_four_ranks():
+    test_sharded_crc_gloo(4, 3 * 4096 + 65 * 17)
