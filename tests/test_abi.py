@@ -78,3 +78,22 @@ def test_scalar_wrappers_reference_semantics():
     assert zc.crc32c_iovec([b"lo", b"", b"rem ", b"ipsum"]) == 0xDFB4E6C9
     assert zc.crc32c_iovec([]) == 0
     assert zc.crc32c(0, b"") == 0
+
+
+def test_scalar_cpu_path_random():
+    """The host path (SSE4.2 3-stream / slice-by-8) on random lengths,
+    alignments and seeds, chained in random pieces; crc32c_combine over
+    random splits -- each equal to the oracle."""
+    rng = np.random.default_rng(23)
+    d = rng.integers(0, 256, 300_000, dtype=np.uint8)
+    for _ in range(300):
+        n = int(rng.integers(0, 120_000))
+        a = int(rng.integers(0, d.size - n + 1))
+        seed = int(rng.integers(0, 2**32))
+        x = d[a:a + n]
+        want = oracle.crc32c_hw(seed, x)
+        fn = (zc.crc32c_hw, zc.crc32c_sw, zc.crc32c)[int(rng.integers(0, 3))]
+        assert fn(seed, x) == want, (fn.__name__, n, a)
+        cut = int(rng.integers(0, n + 1))
+        assert zc.crc32c_hw(zc.crc32c_hw(seed, x[:cut]), x[cut:]) == want
+        assert zc.crc32c_combine(oracle.crc32c_hw(seed, x[:cut]), oracle.crc32c_hw(0, x[cut:]), n - cut) == want
