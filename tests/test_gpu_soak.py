@@ -498,6 +498,15 @@ def test_random_files(gpu):
     rep = zsfile.verify_files(imgs)
     assert rep["files"] == len(imgs) and rep["commits"] == sum(ncommits)
     assert rep["bad_commits"] + rep["stale_empty_commits"] == sum(bads), rep
+    # the same files over three device slots (one GPU repeated): the same verdicts
+    zsfile.set_devices([0, 0, 0])
+    try:
+        rep3 = zsfile.verify_files(imgs)
+    finally:
+        zsfile.set_devices([])
+    keys = ("files", "commits", "bytes", "bad_commits", "stale_empty_commits", "header_errors", "walk_errors",
+            "first_bad_file", "first_bad_off", "first_bad_what")
+    assert {k: rep3[k] for k in keys} == {k: rep[k] for k in keys} and rep3["devices"] == 3, (rep, rep3)
 
 
 def test_random_fixed_large(gpu):
