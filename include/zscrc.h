@@ -445,19 +445,34 @@ typedef struct zscrc_cpass_spec {
     const uint64_t *d_off;        /* commit spans: image offsets / lengths       */
     const uint64_t *d_len;
     const uint32_t *d_file;       /* file id of each commit                      */
-    uint64_t max_len;             /* bound on the span lengths (the host walk's) */
+    uint64_t max_len;             /* bound on the span lengths (the host walk's);
+                                   * create reads d_len back once and uses the
+                                   * true maximum, so a wrong value is harmless.
+                                   * d_off / d_len must not change after create
+                                   * (the image's bytes may)                      */
     size_t nspans;                /* raw spans                                   */
     const uint64_t *span_off;     /* host arrays: image offset, length, and the  */
     const uint64_t *span_len;     /* image offset of the span's commit record   */
     const int64_t *span_commit;   /* (-1: not in this image -- a split piece)    */
 } zscrc_cpass_spec;
 typedef struct zscrc_cpass_result {
-    uint64_t n_bad;               /* commits that do not verify (undecided incl.) */
-    uint64_t n_stale;             /* finalise-quirk commits (among the listed ones
-                                   * when the pass is not complete)                */
+    uint64_t n_bad;               /* commits that do not verify (undecided incl.),
+                                   * minus n_stale                                 */
+    uint64_t n_stale;             /* finalise-quirk commits among the first
+                                   * min(mismatches, max(4096, min(n, 2^20)))
+                                   * the verdict kept -- all of them unless more
+                                   * than that many commits mismatch.  The same
+                                   * count the digest row carries, independent of
+                                   * the order the device listed mismatches in.    */
     uint64_t n_undecided;         /* zero-length commits after a long span or with a
                                    * long trailer: the caller decides (indices below) */
-    int32_t complete;             /* 0: more mismatches than one pass lists       */
+    int32_t complete;             /* 0: more mismatches than one pass lists (4096):
+                                   * n_bad + n_stale is still the exact mismatch
+                                   * count and n_stale as above, but WHICH ones
+                                   * bad[] / stale[] / undecided[] hold depends on
+                                   * the order the device found them -- decide such
+                                   * a pass another way (consistent.py: the torch
+                                   * path)                                          */
     int32_t pad_;
     uint64_t n_listed_bad, n_listed_stale;
     uint64_t bad[ZSCRC_CPASS_LIST];        /* commit indices, ascending, undecided excl. */
@@ -482,7 +497,9 @@ int zscrc_cpass_run_timed(zscrc_cpass *p, void *stream, void *start_event, void 
  * zscrc_cpass_run_timed) with the copy back into host slot `slot` (0 or 1)
  * and returns at once; collect waits for that slot's copy and fills `res`.
  * A slot holds one submitted pass until it is collected (ZSCRC_EINVAL
- * otherwise).  Passes on one stream run in order.  A submit's end_event
+ * otherwise).  Passes run in submission order: a pass enqueued on a stream
+ * other than the previous pass's first waits (on the device) for what was
+ * already on that stream, which must still exist.  A submit's end_event
  * (may be NULL) is also what its collect waits on: record it again only
  * after that collect. */
 int zscrc_cpass_submit(zscrc_cpass *p, void *stream, void *start_event, void *end_event, int slot);
@@ -508,7 +525,8 @@ typedef struct zscrc_cpass_row_spec {
 } zscrc_cpass_row_spec;
 int zscrc_cpass_set_row(zscrc_cpass *p, const zscrc_cpass_row_spec *spec);
 /* Enqueue one pass and its row into d_row (device, row length int64);
- * nothing is copied to the host and nothing waits. */
+ * nothing is copied to the host and nothing waits.  The row is built by the
+ * pass's post kernel (its last workgroup): no launch of its own. */
 int zscrc_cpass_submit_row(zscrc_cpass *p, void *stream, void *start_event, void *end_event, int64_t *d_row);
 void zscrc_cpass_destroy(zscrc_cpass *p);
 
@@ -642,6 +660,15 @@ typedef struct zscrc_repack_report {
     double list_s, merge_s, write_s, total_s;
     char path[4096];            /* the new packed file                           */
 } zscrc_repack_report;
+/* ZSCRC_REPACK_REFERENCE_COMPAT (flags): branch 2 writes the reference's
+ * bytes exactly, including its loss of records: the reference's packed-file
+ * iterator sets its `deleted` flag on the first delete it steps onto and never
+ * clears it (src/zeroskip-iterator.c:258-259), so every later record of that
+ * source is dropped, and a delete that is a source's first record is written
+ * as a delete record.  Without the flag (the default) every record is kept:
+ * the older file wins a key in both, a winning delete drops the key -- the
+ * same bytes as the reference whenever the two files hold no delete. */
+#define ZSCRC_REPACK_REFERENCE_COMPAT 2u
 int zscrc_zs_repack(const char *dbdir, unsigned flags, int threads, zscrc_repack_report *rep);
 
 #ifdef __cplusplus

@@ -319,12 +319,37 @@ def repack2_inputs():
     return {f"zeroskip-{UUIDSTR}-{a}-{b}": zf.packed_file(r, bytes(range(16)), a, b) for (a, b), r in spec.items()}
 
 
-def repack_fixture(branch: int) -> dict:
+def repack2d_inputs():
+    """Three packed files WITH deletes (0-3, 4-7, 8-9) -- among them a delete
+    as the first record of one merged source, and keys present in both merged
+    files on either side of each source's first delete: branch 2's input on
+    which the reference's merge loses records (ref_merge_packed), the
+    fixture of its compat mode (ZSCRC_REPACK_REFERENCE_COMPAT)."""
+    import numpy as np
+    rng = np.random.default_rng(33)
+
+    def recs(n, lo, hi, vmax, pdel):
+        return {b"%016d" % int(rng.integers(lo, hi)):
+                (None if rng.integers(0, pdel) == 0 else
+                 rng.integers(0, 256, int(rng.integers(0, vmax)), dtype=np.uint8).tobytes())
+                for _ in range(n)}
+    spec = {(0, 3): recs(100, 0, 500, 200, 6), (4, 7): recs(400, 100, 2000, 200, 25),
+            (8, 9): recs(200, 0, 2000, 200, 15)}
+    spec[(8, 9)][b"%016d" % 0] = None          # a delete as the newest file's first record
+    out = {}
+    for (a, b), r in spec.items():
+        out[f"zeroskip-{UUIDSTR}-{a}-{b}"] = zf.packed_file(sorted(r.items()), bytes(range(16)), a, b)
+    return out
+
+
+def repack_fixture(branch: int, name: str | None = None) -> dict:
     """The inputs, and the output the reference's own repack writes from them
-    (format_demo repack1 / repack2), under tests/golden/ref_format/repackN/."""
+    (format_demo repack1 / repack2), under tests/golden/ref_format/<name>/
+    (repackN; "repack2d": branch 2 on sources holding deletes)."""
     import hashlib
-    files = repack1_inputs() if branch == 1 else repack2_inputs()
-    d = os.path.join(OUTDIR, f"repack{branch}")
+    name = name or f"repack{branch}"
+    files = repack1_inputs() if branch == 1 else repack2d_inputs() if name == "repack2d" else repack2_inputs()
+    d = os.path.join(OUTDIR, name)
     os.makedirs(d, exist_ok=True)
     for f in os.listdir(d):
         os.unlink(os.path.join(d, f))
@@ -379,11 +404,26 @@ def main():
     manifest["packed_long"] = packed_long_fixture()
     manifest["repack1"] = repack_fixture(1)
     manifest["repack2"] = repack_fixture(2)
+    manifest["repack2d"] = repack_fixture(2, "repack2d")
     with open(os.path.join(OUTDIR, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)
         f.write("\n")
     print(json.dumps({k: v["size"] for k, v in manifest.items()}))
 
 
+def main_repack2d():
+    """Only the repack2d fixture, merged into the existing manifest."""
+    build_demo()
+    path = os.path.join(OUTDIR, "manifest.json")
+    with open(path) as f:
+        manifest = json.load(f)
+    manifest["repack2d"] = repack_fixture(2, "repack2d")
+    with open(path, "w") as f:
+        json.dump(manifest, f, indent=1, sort_keys=True)
+        f.write("\n")
+    print(json.dumps(manifest["repack2d"]))
+
+
 if __name__ == "__main__":
-    main()
+    import sys
+    main_repack2d() if sys.argv[1:] == ["repack2d"] else main()

@@ -336,15 +336,18 @@ def test_destroy_with_uncollected_passes(gpu):
     assert rep.ok and len(rep.stale_empty_commits) == 3
 
 
-@pytest.mark.parametrize("case", ["clean", "corrupt", "bad_2000", "bad_5000"])
+@pytest.mark.parametrize("case", ["clean", "corrupt", "bad_2000", "bad_5000", "bad_12000"])
 def test_device_row_matches_host_digest(gpu, case):
-    """zscrc_cpass_submit_row's digest row (cpass_row_kernel: the listed
-    verdict sorted on the device) equals the row the host builds from the same
-    pass's copied-back block (Consistent._pack of the native digest), int64
-    for int64 -- clean, with a bad commit, a bad records region and stale
-    commits, with more bad commits than a row lists (2,000 > 1,000) and more
-    than the pass keeps (5,000 > 4,096: flag 1, the caller takes the torch
-    path)."""
+    """zscrc_cpass_submit_row's digest row (built by cpass_post_kernel's last
+    workgroup: the listed verdict sorted on the device) equals the row the
+    host builds from the same pass's copied-back block (Consistent._pack of
+    the native digest), int64 for int64 -- clean, with a bad commit, a bad
+    records region and stale commits, with more bad commits than a row lists
+    (2,000 > 1,000) and more than the pass lists (5,000 and 12,000 > 4,096:
+    flag 1, the caller takes the torch path).  The counts are the device's
+    over every mismatch on both sides, so they agree whatever order the
+    waves listed the mismatches in -- and equal the torch path's exact
+    counts."""
     import ctypes
     from zeroskip_amd._lib import check, lib
     if case.startswith("bad_"):
@@ -371,19 +374,29 @@ def test_device_row_matches_host_digest(gpu, case):
         live = torch.nonzero(job.d_len > 0).flatten()[:k]
         assert live.numel() == k
         job.buf[job.d_off[live]] ^= 0x5A
+        if k > 4096:
+            # by construction: stale finalise commits (zero-length, at the end
+            # of each finalised file) lie after the 4,097th bad commit in
+            # index order, so a count over only the first 4,096 listed
+            # entries would miss them
+            zero = torch.nonzero(job.d_len == 0).flatten()
+            assert int((zero > live[4096]).sum()) >= 1
     row = job.device_row().cpu().numpy()
     res = cs.CPassResult()
     with torch.cuda.device(job.buf.device):
         check(lib().zscrc_cpass_run(job._cpass, None, ctypes.byref(res)), "zscrc_cpass_run")
     want = job._pack(job._native_digest(res))
     assert row.shape == want.shape
-    if case == "bad_5000":
-        # more mismatches than the pass keeps: WHICH 4,096 a pass lists depends
-        # on the order its waves found them, so two passes list different
-        # subsets -- the counts agree and the row says incomplete (the caller
-        # then decides on the torch path)
-        assert not res.complete and row[6] == 1 and row[1] >= 5000
-        assert np.array_equal(row[:3], want[:3]) and row[3] == job.MAX_LISTED
+    if case in ("bad_5000", "bad_12000"):
+        # more mismatches than the pass lists: WHICH 4,096 a pass lists depends
+        # on the order its waves found them, so the lists may differ; the
+        # counts may not, and the row says incomplete (the caller then
+        # decides on the torch path)
+        assert not res.complete and row[6] == 1 and row[1] + row[2] >= k
+        assert np.array_equal(row[:3], want[:3]), (row[:3], want[:3])
+        assert row[3] == job.MAX_LISTED
+        exact = job._run_torch()
+        assert (int(row[1]), int(row[2])) == (exact.n_bad, exact.n_stale), (row[:3], exact.as_dict())
         return
     assert row[6] == 0
     if case.startswith("bad_"):
@@ -412,3 +425,116 @@ def test_random_corruptions_match_oracle(gpu, seed):
     assert same(g, o), (seed, g.as_dict(), o.as_dict())
     print(f"seed {seed}: ok={g.ok} bad={len(g.bad_commits)} header_errors={len(g.header_errors)} "
           f"issues={len(g.issues)}")
+
+
+def test_cpass_understated_max_len(gpu):
+    """A C caller's zscrc_cpass_spec.max_len below the longest span (ADVICE
+    r05): the verdict launches only the length classes up to the bound, so
+    zscrc_cpass_create takes the lengths' true maximum -- the corrupted
+    longest commit is still found."""
+    import ctypes
+    from zeroskip_amd._lib import check, lib
+    db = small_db(long_region=True)
+    job = cs.Consistent(cs.open_db(db), 0, 1).prepare()
+    i = int(torch.argmax(job.d_len))
+    L = int(job.d_len[i])
+    assert L > 640                         # above the one-lane length class
+    job.buf[int(job.d_off[i]) + L // 2] ^= 0x21
+    h = ctypes.c_void_p()
+    res = cs.CPassResult()
+    with torch.cuda.device(job.buf.device):
+        for max_len in (1, 64, L - 1):
+            spec = cs.CPassSpec(job.buf.data_ptr(), job.buf.numel(), len(job.c_off), job.d_off.data_ptr(),
+                                job.d_len.data_ptr(), job.d_file.data_ptr(), max_len, 0, None, None, None)
+            check(lib().zscrc_cpass_create(ctypes.byref(h), ctypes.byref(spec)), "zscrc_cpass_create")
+            try:
+                check(lib().zscrc_cpass_run(h, None, ctypes.byref(res)), "zscrc_cpass_run")
+            finally:
+                lib().zscrc_cpass_destroy(h)
+            bad = list(res.bad[:res.n_listed_bad])
+            assert res.complete and i in bad, (max_len, i, bad, res.n_bad)
+
+
+def test_passes_alternate_streams(gpu):
+    """Consecutive passes of one handle enqueued on different streams (ADVICE
+    r05): each pass zeroes the counters the next one increments, so a pass on
+    another stream first waits for the previous stream's work -- every
+    report equals the synchronous one, with a corrupted commit counted once
+    per pass."""
+    db = small_db(long_region=True)
+    f = name(7, 7)
+    img = bytearray(db[f])
+    c = zf.walk(img)[0][5]
+    img[c["span_off"] + 3] ^= 0x10
+    db[f] = bytes(img)
+    job = cs.Consistent(cs.open_db(db), 0, 1).prepare()
+    want = job.run()
+    assert not want.ok and len(want.bad_commits) == 1
+    streams = [torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.current_stream()]
+    reps = []
+    for k in range(9):
+        with torch.cuda.stream(streams[k % 3]):
+            assert job.submit()
+            if job.pending() > 1:
+                reps.append(job.collect())
+    while job.pending():
+        reps.append(job.collect())
+    assert len(reps) == 9 and all(same(r, want) for r in reps)
+    for k in range(4):
+        with torch.cuda.stream(streams[k % 2]):
+            assert same(job.run(), want)
+
+
+def _nccl_one_rank(port, q):
+    import torch.distributed as dist
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        torch.cuda.set_device(0)
+        db = small_db(long_region=True)
+        f = name(4, 5)
+        img = bytearray(db[f])
+        c = {c["kind"]: c for c in zf.packed_check(img)}["records"]
+        img[c["span_off"] + 11] ^= 4
+        db[f] = bytes(img)
+        job = cs.Consistent(cs.open_db(db), 0, 1).prepare()
+        want = job.run()
+        # the world > 1 code paths under RCCL, on a one-rank group: the
+        # synchronous row exchange and the pipelined one (the all-gather on
+        # RCCL's stream, the copy to pinned memory on a side stream)
+        sync = job._run_native_rows(None)
+        job._inflight, job._next_slot = [], 0
+        piped = []
+        for _ in range(5):
+            job._submit_rows(None, job._next_slot)
+            if len(job._inflight) > 1:
+                piped.append(job._collect_rows())
+        while job._inflight:
+            piped.append(job._collect_rows())
+        q.put((same(sync, want), [same(r, want) for r in piped], want.ok, want.bad_commits,
+               sync.timing.get("host_round_trips"), c["commit_off"]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_row_exchange_over_rccl_one_rank(gpu):
+    """the nccl branch of the digest-row exchange
+    (Consistent._run_native_rows, _submit_rows / _collect_rows: the async
+    all_gather_into_tensor on RCCL's stream, the side stream waiting on the
+    work, the non-blocking copy into pinned rows) run for real on a one-rank
+    RCCL group (RCCL refuses two ranks on one device): the same report as the
+    one-rank native pass, pass after pass."""
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_one_rank, args=(port, q))
+    p.start()
+    res = q.get(timeout=300)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    sync_ok, piped_ok, ok, bad, trips, at = res
+    assert sync_ok and len(piped_ok) == 5 and all(piped_ok)
+    assert not ok and bad == [(name(4, 5), at)] and trips == 1

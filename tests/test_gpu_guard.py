@@ -1,0 +1,263 @@
+"""Every commit_kernel output mode with its arrays fenced by canaries (VERDICT
+r05 weak #3: round 5's compile-time emit-mode build -- every store
+unconditional -- faulted with an illegal address on the seeded per-commit
+arrays of test_gpu_mixed.py, and its patch was not kept).
+
+Lanes past the last commit (n not a multiple of 64) hold no descriptor
+(burst_meta leaves their span, record index and commit words unset), so a
+store or a trailer load issued for them would go to an undefined address.
+A fault is only the visible form of that bug; a stray store that lands
+inside the allocation corrupts memory silently.  These tests catch the
+silent form too: the image, the per-commit crc / status arrays, the seed
+array and the verdict list are each a slice of a larger device buffer whose
+bytes around the slice hold a canary pattern -- after every call the
+canaries are intact and every result equals the CPU oracle's.  Shapes: n =
+64 k + 37 both below and past the run-only split (ncu x 12 rounds), the last
+commit record ending at the image's last byte, spans of 0-640 bytes at
+unaligned offsets, missing commit records, FINAL records, seeds, long
+(24-byte) commit records, under the default schedule and the tuning bits
+that pick the other commit_kernel forms.  src/zeroskip-file.c:253-350 (the
+commit CRC), src/zeroskip-record.c:188-273 (its verification)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle
+from zeroskip_amd._lib import check, lib
+
+pytestmark = pytest.mark.gpu
+
+NO_RUNSPLIT, RO12, RO_LIST, TWO_PASS = 1 << 29, 1 << 31, 1 << 14, 512
+OPTS = [0, NO_RUNSPLIT, RO12, RO_LIST]
+OPT_IDS = ["default", "no_runsplit", "ro12", "ro_list"]
+T_KEY, T_COMMIT, T_FINAL, T_LONG_COMMIT, T_2ND = 1, 4, 16, 36, 8
+MAXLEN = 640
+PAD = 4096                # canary bytes on each side of every array
+CANARY = 0xA5
+
+
+def _fenced(nbytes: int, dev):
+    """(whole buffer, the nbytes slice in its middle) -- the rest canary."""
+    whole = torch.full((nbytes + 2 * PAD,), CANARY, dtype=torch.uint8, device=dev)
+    return whole, whole[PAD:PAD + nbytes]
+
+
+def _intact(whole: torch.Tensor, nbytes: int) -> bool:
+    h = whole.cpu().numpy()
+    return bool((h[:PAD] == CANARY).all() and (h[PAD + nbytes:] == CANARY).all())
+
+
+def _build(n: int, seed: int):
+    """A host image of n commits ending at its last byte, and what the oracle
+    says about it."""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, MAXLEN + 1, n)
+    edge = rng.random(n)
+    lens[edge < 0.05] = rng.integers(0, 9, int((edge < 0.05).sum()))
+    kind = rng.random(n)
+    has_rec = kind >= 0.04
+    final = has_rec & (kind < 0.10)
+    long_rec = has_rec & ~final & (rng.random(n) < 0.03)
+    has_rec[-1], final[-1], long_rec[-1] = True, False, False   # the last record ends the image
+    rl = np.where(long_rec, 24, 8)
+    gaps = rng.integers(0, 8, n)
+    gaps[-1] = 0
+    offs = np.zeros(n, np.int64)
+    offs[0] = 43
+    offs[1:] = 43 + np.cumsum(lens + rl + gaps)[:-1]
+    size = int(offs[-1] + lens[-1] + 8)
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    at = offs + lens
+    host[at[~has_rec]] = T_KEY
+    seeded = has_rec & ~long_rec & (rng.random(n) < 0.05)
+    seeds = np.where(seeded, rng.integers(1, 1 << 32, n, dtype=np.uint64), 0).astype(np.uint32)
+    want = np.zeros(n, np.uint32)
+    for i in np.nonzero(has_rec)[0]:
+        o, ln, a = int(offs[i]), int(lens[i]), int(at[i])
+        c = oracle.crc32c_hw(int(seeds[i]), host[o:o + ln])
+        if long_rec[i]:
+            w0, w2 = T_LONG_COMMIT << 56, T_2ND << 56
+            words = w0.to_bytes(8, "little") + ln.to_bytes(8, "little") + w2.to_bytes(8, "little")
+            crc = oracle.crc32c_hw(c, words)
+            host[a:a + 8] = np.frombuffer(w0.to_bytes(8, "big"), np.uint8)
+            host[a + 8:a + 16] = np.frombuffer(ln.to_bytes(8, "big"), np.uint8)
+            host[a + 16:a + 24] = np.frombuffer((w2 | crc).to_bytes(8, "big"), np.uint8)
+        else:
+            t = T_FINAL if final[i] else T_COMMIT
+            crc = oracle.commit_crc(c, ln, bool(final[i]))
+            host[a:a + 8] = np.frombuffer(((t << 56) | (ln << 32) | crc).to_bytes(8, "big"), np.uint8)
+        want[i] = crc
+    # corruptions: span bytes and stored CRC fields
+    hit = rng.choice(np.nonzero(has_rec)[0], 40, replace=False)
+    for j, i in enumerate(hit):
+        o, ln, a = int(offs[i]), int(lens[i]), int(at[i])
+        if ln and j % 2 == 0:
+            host[o + int(rng.integers(0, ln))] ^= 0x5A
+        else:
+            host[a + (20 if long_rec[i] else 4) + j % 4] ^= 0x01
+    crc_now = want.copy()
+    for i in hit:
+        o, ln = int(offs[i]), int(lens[i])
+        c = oracle.crc32c_hw(int(seeds[i]), host[o:o + ln])
+        if long_rec[i]:
+            words = (T_LONG_COMMIT << 56).to_bytes(8, "little") + ln.to_bytes(8, "little") + \
+                (T_2ND << 56).to_bytes(8, "little")
+            crc_now[i] = oracle.crc32c_hw(c, words)
+        else:
+            crc_now[i] = oracle.commit_crc(c, ln, bool(final[i]))
+    st = np.where(has_rec, 1, 2).astype(np.int32)
+    st[hit] = 0
+    # the writer's view (no seeds): every CRC field rewritten from register 0
+    field = np.where(long_rec, at + 20, at + 4)
+    w_image = host.copy()
+    w_crc = np.zeros(n, np.uint32)
+    for i in np.nonzero(has_rec)[0]:
+        o, ln = int(offs[i]), int(lens[i])
+        c = oracle.crc32c_hw(0, host[o:o + ln])
+        if long_rec[i]:
+            words = (T_LONG_COMMIT << 56).to_bytes(8, "little") + ln.to_bytes(8, "little") + \
+                (T_2ND << 56).to_bytes(8, "little")
+            w_crc[i] = oracle.crc32c_hw(c, words)
+        else:
+            w_crc[i] = oracle.commit_crc(c, ln, int(host[at[i]]) == T_FINAL)
+        w_image[field[i]:field[i] + 4] = np.frombuffer(int(w_crc[i]).to_bytes(4, "big"), np.uint8)
+    w_blank = w_image.copy()
+    fi = field[has_rec]
+    w_blank[(fi[:, None] + np.arange(4)).reshape(-1)] = 0
+    # a corrupted stored CRC leaves the computed one as written; a corrupted
+    # span changes it (crc_now)
+    return dict(host=host, offs=offs, lens=lens, seeds=seeds, has_rec=has_rec, long_rec=long_rec,
+                st=st, crc=crc_now, n=n, w_image=w_image, w_blank=w_blank, w_crc=w_crc)
+
+
+@pytest.fixture(scope="module", params=[6_437, 200_037], ids=["small", "past_split"])
+def case(request, gpu):
+    n = request.param
+    assert n % 64 == 37
+    m = _build(n, 0xF00D + n)
+    dev = gpu
+    size = m["host"].nbytes
+    img_whole, img = _fenced(size, dev)
+    img.copy_(torch.from_numpy(m["host"]))
+    seed_whole, seed = _fenced(4 * n, dev)
+    seed.copy_(torch.from_numpy(m["seeds"].view(np.uint8)))
+    m.update(dev=dev, size=size, img_whole=img_whole, img=img, seed_whole=seed_whole, seed=seed,
+             d_off=torch.from_numpy(m["offs"]).to(dev), d_len=torch.from_numpy(m["lens"].astype(np.int64)).to(dev))
+    return m
+
+
+def _stream(dev):
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+@pytest.mark.parametrize("opt", OPTS, ids=OPT_IDS)
+def test_seeded_arrays_fenced(case, opt):
+    """Per-commit crc + status arrays with seeds (the form whose emit-mode
+    build faulted): results equal the oracle's, no byte around the image,
+    the seeds or the arrays changes."""
+    m = case
+    n = m["n"]
+    cw, crc = _fenced(4 * n, m["dev"])
+    sw, st = _fenced(4 * n, m["dev"])
+    lib().zscrc_set_opt(opt)
+    try:
+        with torch.cuda.device(m["dev"]):
+            check(lib().zscrc_device_verify_commits_bounded(
+                m["img"].data_ptr(), m["size"], m["d_off"].data_ptr(), m["d_len"].data_ptr(), m["seed"].data_ptr(),
+                n, MAXLEN, crc.data_ptr(), st.data_ptr(), _stream(m["dev"])), "verify_commits_bounded")
+        torch.cuda.synchronize()
+    finally:
+        lib().zscrc_set_opt(0)
+    for whole, nb in ((cw, 4 * n), (sw, 4 * n), (m["img_whole"], m["size"]), (m["seed_whole"], 4 * n)):
+        assert _intact(whole, nb)
+    got_st = st.cpu().numpy().view(np.int32)
+    got_crc = crc.cpu().numpy().view(np.uint32)
+    assert np.array_equal(got_st, m["st"])
+    rec = m["has_rec"]
+    assert np.array_equal(got_crc[rec], m["crc"][rec])
+    assert np.array_equal(m["img"].cpu().numpy(), m["host"])
+
+
+@pytest.mark.parametrize("opt", OPTS, ids=OPT_IDS)
+def test_seeded_verdict_fenced(case, opt):
+    """The verdict list (cap > mismatches, and cap = 7 < mismatches) inside
+    canaries: exactly the oracle's mismatches, nothing written past cap."""
+    m = case
+    n = m["n"]
+    want = set(np.nonzero(m["st"] != 1)[0].tolist())
+    for cap in (4096, 7):
+        nw, nbad = _fenced(8, m["dev"])
+        bw, bad = _fenced(8 * cap, m["dev"])
+        lib().zscrc_set_opt(opt)
+        try:
+            with torch.cuda.device(m["dev"]):
+                check(lib().zscrc_device_verify_commits_verdict(
+                    m["img"].data_ptr(), m["size"], m["d_off"].data_ptr(), m["d_len"].data_ptr(),
+                    m["seed"].data_ptr(), n, MAXLEN, nbad.data_ptr(), bad.data_ptr(), cap, _stream(m["dev"])),
+                    "verify_commits_verdict")
+            torch.cuda.synchronize()
+        finally:
+            lib().zscrc_set_opt(0)
+        assert _intact(nw, 8) and _intact(bw, 8 * cap) and _intact(m["img_whole"], m["size"])
+        k = int(nbad.cpu().view(torch.int64).item())
+        listed = set(bad.cpu().view(torch.int64)[:min(k, cap)].tolist())
+        assert k == len(want) and listed <= want and len(listed) == min(k, cap)
+
+
+@pytest.mark.parametrize("opt", OPTS + [TWO_PASS], ids=OPT_IDS + ["two_pass"])
+def test_writer_fenced(case, opt):
+    """The in-place writer (and its CRC + status arrays) over the image with
+    every CRC field zeroed: the image comes back as the oracle writes it --
+    short fields at +4, long ones at +20, spans without a record untouched --
+    and no byte outside the image or the arrays changes.  The writer has no
+    seeds: the expected image is written from register 0."""
+    m = case
+    n = m["n"]
+    rec, want, blank, crcs = m["has_rec"], m["w_image"], m["w_blank"], m["w_crc"]
+    iw, img = _fenced(blank.nbytes, m["dev"])
+    img.copy_(torch.from_numpy(blank))
+    cw, crc = _fenced(4 * n, m["dev"])
+    sw, st = _fenced(4 * n, m["dev"])
+    lib().zscrc_set_opt(opt)
+    try:
+        with torch.cuda.device(m["dev"]):
+            check(lib().zscrc_device_write_commits_bounded(
+                img.data_ptr(), blank.nbytes, m["d_off"].data_ptr(), m["d_len"].data_ptr(), n, MAXLEN,
+                crc.data_ptr(), st.data_ptr(), _stream(m["dev"])), "write_commits_bounded")
+        torch.cuda.synchronize()
+    finally:
+        lib().zscrc_set_opt(0)
+    assert _intact(iw, blank.nbytes) and _intact(cw, 4 * n) and _intact(sw, 4 * n)
+    assert np.array_equal(img.cpu().numpy(), want)
+    got_st = st.cpu().numpy().view(np.int32)
+    assert np.array_equal(got_st, np.where(rec, 1, 2))
+    assert np.array_equal(crc.cpu().numpy().view(np.uint32)[rec], crcs[rec])
+
+
+@pytest.mark.parametrize("opt", OPTS, ids=OPT_IDS)
+def test_crc_array_fenced(case, opt):
+    """The writer's CRCs out of place (commit mode 3) with and without the
+    status array: the image only read, nothing around the arrays written."""
+    m = case
+    n = m["n"]
+    for with_status in (True, False):
+        cw, crc = _fenced(4 * n, m["dev"])
+        sw, st = _fenced(4 * n, m["dev"])
+        lib().zscrc_set_opt(opt)
+        try:
+            with torch.cuda.device(m["dev"]):
+                check(lib().zscrc_device_commit_crcs_bounded(
+                    m["img"].data_ptr(), m["size"], m["d_off"].data_ptr(), m["d_len"].data_ptr(), n, MAXLEN,
+                    crc.data_ptr(), st.data_ptr() if with_status else None, _stream(m["dev"])), "commit_crcs_bounded")
+            torch.cuda.synchronize()
+        finally:
+            lib().zscrc_set_opt(0)
+        assert _intact(cw, 4 * n) and _intact(m["img_whole"], m["size"])
+        if with_status:
+            assert _intact(sw, 4 * n)
+            assert np.array_equal(st.cpu().numpy().view(np.int32), np.where(m["has_rec"], 1, 2))
+        else:
+            assert (sw.cpu().numpy() == CANARY).all()
+        assert np.array_equal(m["img"].cpu().numpy(), m["host"])

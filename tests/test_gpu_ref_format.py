@@ -10,6 +10,7 @@ tests/golden/make_ref_format.py and tests/test_reference_format.py).
   finalise commits that chain from the previous span's CRC reported as
   stale (src/mfile.c:534-546) rather than bad.
 """
+import hashlib
 import json
 import os
 
@@ -144,3 +145,51 @@ def test_product_repack_equals_reference_repack(gpu, tmp_path, branch):
         want = f.read()
     with open(tmp_path / m["out_name"], "rb") as f:
         assert f.read() == want
+
+
+def test_repack_reference_compat_on_deletes(gpu, tmp_path):
+    """Branch 2 on packed files that hold deletes (tests/golden/ref_format/
+    repack2d: the reference's own repack output on them).  With
+    ZSCRC_REPACK_REFERENCE_COMPAT the product writes the reference's bytes,
+    records lost to its iterator's sticky `deleted` flag included
+    (src/zeroskip-iterator.c:258-259).  The default keeps them: its output is
+    the format oracle's merge, and the two differ by exactly the set the
+    restatement of the reference's merge (make_ref_format.ref_merge_packed)
+    predicts -- the records the reference drops, and the delete record it
+    writes for a source whose first record is a delete."""
+    import shutil
+    from tests.golden.make_ref_format import ref_merge_packed
+    from zeroskip_amd import repack
+    m = MANIFEST["repack2d"]
+    src = os.path.join(DIR, "repack2d")
+    with open(os.path.join(src, "reference_out.zs"), "rb") as f:
+        ref_out = f.read()
+    assert hashlib.sha256(ref_out).hexdigest() == m["sha256"]
+    uuidstr = m["out_name"].split("-", 1)[1].rsplit("-", 2)[0]
+    outs = {}
+    for compat in (True, False):
+        d = tmp_path / ("compat" if compat else "default")
+        d.mkdir()
+        for n in m["inputs"]:
+            shutil.copy(os.path.join(src, n), d / n)
+        (d / ".zsdb").write_bytes(zf.dotzsdb_bytes(4096, uuidstr.encode() + b"\0", 10))
+        rep = repack.repack_dir(str(d), reference_compat=compat)
+        assert rep["branch"] == 2 and os.path.basename(rep["path"]) == m["out_name"]
+        with open(d / m["out_name"], "rb") as f:
+            outs[compat] = f.read()
+        r = zsfile.verify_image(outs[compat], zsfile.PACKED)
+        assert r["n_bad"] == 0 and r["n_commits"] == 2
+    assert outs[True] == ref_out
+    older, newer = (open(os.path.join(src, n), "rb").read() for n in sorted(m["inputs"])[1:])
+    uuid = bytes(range(16))
+    assert outs[False] == zf.packed_file(zf.repack_packed(older, newer), uuid, 4, 9)
+    quirk = ref_merge_packed([(2, zf.packed_records(older)), (1, zf.packed_records(newer))])
+    assert zf.packed_file(quirk, uuid, 4, 9) == ref_out
+    ref_recs, def_recs = zf.packed_records(ref_out), zf.packed_records(outs[False])
+    kept_beyond = [r for r in def_recs if r not in ref_recs]
+    ref_only = [r for r in ref_recs if r not in def_recs]
+    # what the default keeps beyond the reference: every record the quirk drops
+    assert len(kept_beyond) > 50 and all(v is not None for _, v in kept_beyond)
+    assert set(kept_beyond) == set(zf.repack_packed(older, newer)) - set(quirk)
+    # and the reference writes the newest file's leading delete as a delete record
+    assert ref_only == [(b"%016d" % 0, None)]

@@ -26,7 +26,6 @@
 extern "C" {
 const uint32_t *zscrc_internal_gtab(void);
 int zs_launch_cpass_post(const zs::CPassArgs *a, const uint32_t *gtab, hipStream_t stream);
-int zs_launch_cpass_row(const zs::CPassRowArgs *a, hipStream_t stream);
 int zscrc_internal_verdict_prezeroed(const void *d_image, uint64_t image_size, const uint64_t *d_span_off,
                                      const uint64_t *d_span_len, size_t n, uint64_t max_len, uint64_t *d_nbad,
                                      uint64_t *d_bad, size_t cap, void *stream);
@@ -45,10 +44,10 @@ struct zscrc_cpass {
     int dev = 0; /* the device current at create: every buffer lives there */
     std::vector<uint64_t> span_off, span_len;
     std::vector<int64_t> span_commit;
-    /* device block: [0] nbad, [1] nstale, then span_raw[64] (u32),
-     * span_status[64] (i32), flags[LIST_CAP] (u32), bad[LIST_CAP] (u64)
-     * (written by the post kernel) -- the block goes back to the host every
-     * pass */
+    /* device block: [0] nbad, [1] nstale, [2] the post kernel's workgroup
+     * ticket, then span_raw[64] (u32), span_status[64] (i32),
+     * flags[LIST_CAP] (u32), bad[LIST_CAP] (u64) (written by the post
+     * kernel); a host slot has the same layout ([2] unused) */
     /* two device blocks, used by consecutive passes in turn: a pass's post
      * kernel zeroes the other block's counters for the next pass, so no
      * memset launch precedes a pass (two fill kernels of ~4.5 us and their
@@ -57,6 +56,13 @@ struct zscrc_cpass {
     int blk_next = 0;
     uint8_t *hblk = nullptr;   /* NSLOT host blocks (zscrc_cpass_submit / _collect) */
     hipEvent_t done[2] = {};   /* each slot's completion */
+    /* passes in stream order (the blocks' counters are zeroed by the
+     * previous pass): a pass enqueued on another stream than the previous
+     * one first waits for everything already on that stream (`order`,
+     * recorded there only then -- nothing extra per pass on one stream) */
+    hipStream_t last_stream = nullptr;
+    bool have_last = false;
+    hipEvent_t order = nullptr;
     hipEvent_t wait[2] = {};   /* what collect waits on: done[], or the caller's end event */
     bool pending[2] = {};
     /* the digest row (zscrc_cpass_set_row / _submit_row) */
@@ -74,7 +80,7 @@ struct zscrc_cpass {
 
 namespace {
 
-constexpr size_t OFF_RAW = 16, OFF_ST = OFF_RAW + 4 * zs::CPASS_SPANS, OFF_FLAGS = OFF_ST + 4 * zs::CPASS_SPANS,
+constexpr size_t NCOUNT = 3, OFF_RAW = 32, OFF_ST = OFF_RAW + 4 * zs::CPASS_SPANS, OFF_FLAGS = OFF_ST + 4 * zs::CPASS_SPANS,
                  OFF_BAD = OFF_FLAGS + 4 * LIST_CAP, BLK = OFF_BAD + 8 * LIST_CAP;
 
 constexpr int NSLOT = 2;
@@ -91,6 +97,8 @@ void cpass_free(zscrc_cpass *p)
             (void)hipEventSynchronize(e);
             (void)hipEventDestroy(e);
         }
+    if (p->order)
+        (void)hipEventDestroy(p->order);
     if (p->dblk)
         (void)hipFree(p->dblk);
     if (p->hblk)
@@ -144,6 +152,8 @@ extern "C" int zscrc_cpass_create(zscrc_cpass **out, const zscrc_cpass_spec *spe
     for (int k = 0; k < NSLOT && e == hipSuccess; ++k)
         e = hipEventCreateWithFlags(&p->done[k], hipEventDisableTiming);
     if (e == hipSuccess)
+        e = hipEventCreateWithFlags(&p->order, hipEventDisableTiming);
+    if (e == hipSuccess)
         e = hipMalloc(&p->dbad_full, 8 * p->cap);
     if (e == hipSuccess)
         e = hipMalloc(&p->dspan_commit, (8 + 4) * zs::CPASS_SPANS);
@@ -157,6 +167,19 @@ extern "C" int zscrc_cpass_create(zscrc_cpass **out, const zscrc_cpass_spec *spe
          hipMemcpy(p->dspan_init, init.data(), 4 * spec->nspans, hipMemcpyHostToDevice) != hipSuccess)) {
         cpass_free(p);
         return ZSCRC_EHIP;
+    }
+    /* max_len selects which length classes the verdict launches (a range
+     * that holds: the classes above it get no launch), so it must bound every
+     * span: the lengths are read back once here and the bound used is their
+     * true maximum -- a caller's under-stated max_len cannot leave long
+     * commits unchecked (an over-stated one would only cost time) */
+    if (spec->n) {
+        std::vector<uint64_t> lens(spec->n);
+        if (hipMemcpy(lens.data(), spec->d_len, 8 * spec->n, hipMemcpyDeviceToHost) != hipSuccess) {
+            cpass_free(p);
+            return ZSCRC_EHIP;
+        }
+        p->spec.max_len = *std::max_element(lens.begin(), lens.end());
     }
     *out = p;
     return ZSCRC_OK;
@@ -272,7 +295,8 @@ extern "C" int zscrc_cpass_set_row(zscrc_cpass *p, const zscrc_cpass_row_spec *r
 }
 
 namespace {
-int cpass_enqueue(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, uint8_t **blk, uint8_t *host);
+int cpass_enqueue(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, uint8_t **blk, uint8_t *host,
+                  int64_t *d_row = nullptr);
 }
 
 extern "C" int zscrc_cpass_submit_row(zscrc_cpass *p, void *stream, void *start_event, void *end_event,
@@ -285,14 +309,8 @@ extern "C" int zscrc_cpass_submit_row(zscrc_cpass *p, void *stream, void *start_
         return ZSCRC_EHIP;
     hipStream_t s = static_cast<hipStream_t>(stream);
     uint8_t *blk = nullptr;
-    int rc = cpass_enqueue(p, s, static_cast<hipEvent_t>(start_event), &blk, nullptr);
-    if (!rc) {
-        zs::CPassRowArgs a = p->row;
-        a.blk = blk;
-        a.row = d_row;
-        if (zs_launch_cpass_row(&a, s))
-            rc = ZSCRC_EHIP;
-    }
+    /* the post kernel's last workgroup builds the row: no launch of its own */
+    int rc = cpass_enqueue(p, s, static_cast<hipEvent_t>(start_event), &blk, nullptr, d_row);
     if (!rc && end_event && hipEventRecord(static_cast<hipEvent_t>(end_event), s) != hipSuccess)
         rc = ZSCRC_EHIP;
     return rc;
@@ -327,8 +345,13 @@ int cpass_submit(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1, 
  * of the two device blocks (*blk).  Passes must follow one another in
  * stream order (one stream, or the caller's own ordering): the blocks'
  * counters are zeroed by the previous pass. */
-int cpass_enqueue(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, uint8_t **blk, uint8_t *host)
+int cpass_enqueue(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, uint8_t **blk, uint8_t *host, int64_t *d_row)
 {
+    if (p->have_last && s != p->last_stream &&
+        (hipEventRecord(p->order, p->last_stream) != hipSuccess || hipStreamWaitEvent(s, p->order, 0) != hipSuccess))
+        return ZSCRC_EHIP;
+    p->last_stream = s;
+    p->have_last = true;
     if (ev0 && hipEventRecord(ev0, s) != hipSuccess)
         return ZSCRC_EHIP;
     const zscrc_cpass_spec &sp = p->spec;
@@ -378,18 +401,24 @@ int cpass_enqueue(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, uint8_t **blk, 
         }
         a.out_cap = LIST_CAP;
         a.nstale = reinterpret_cast<unsigned long long *>(b + 8);
+        a.ticket = reinterpret_cast<unsigned long long *>(b + 16);
         a.next_counters = reinterpret_cast<unsigned long long *>(other);
         a.nspans = (uint32_t)sp.nspans;
         a.span_raw = d_raw;
         a.span_commit = p->dspan_commit;
         a.span_init = p->dspan_init;
         a.span_status = reinterpret_cast<int32_t *>(o + OFF_ST);
+        if (d_row) {
+            a.row = p->row;
+            a.row.blk = b;
+            a.row.row = d_row;
+        }
         if (zs_launch_cpass_post(&a, zscrc_internal_gtab(), s))
             rc = ZSCRC_EHIP;
     }
     if (rc) { /* a pass cut short did not zero the next block: start both over */
-        (void)hipMemsetAsync(b, 0, 16, s);
-        (void)hipMemsetAsync(other, 0, 16, s);
+        (void)hipMemsetAsync(b, 0, 8 * NCOUNT, s);
+        (void)hipMemsetAsync(other, 0, 8 * NCOUNT, s);
     }
     return rc;
 }
@@ -403,16 +432,15 @@ int cpass_collect(zscrc_cpass *p, int slot, zscrc_cpass_result *res)
     const zscrc_cpass_spec &sp = p->spec;
     const uint8_t *blk = p->hblk + slot * BLK;
     const uint64_t nbad = reinterpret_cast<const uint64_t *>(blk)[0];
+    /* the device's stale count over every classified entry (the post
+     * kernel's last workgroup), not a recount of the listed flags: the same
+     * number the device row carries, whatever order the entries were listed
+     * in */
+    const uint64_t nstale = reinterpret_cast<const uint64_t *>(blk)[1];
     const uint32_t *flags = reinterpret_cast<const uint32_t *>(blk + OFF_FLAGS);
     const uint64_t *bad = reinterpret_cast<const uint64_t *>(blk + OFF_BAD);
     memset(res, 0, sizeof *res);
     const uint64_t nl = std::min<uint64_t>(nbad, LIST_CAP);
-    /* the stale count from the listed flags (the device's counter stays in
-     * its own block): exact when every mismatch is listed, and a pass that
-     * lists only part of them is incomplete anyway */
-    uint64_t nstale = 0;
-    for (uint64_t k = 0; k < nl; ++k)
-        nstale += flags[k] == 1;
     res->complete = nbad <= LIST_CAP;
     std::vector<uint64_t> b, st, und;
     for (uint64_t k = 0; k < nl; ++k)

@@ -201,32 +201,8 @@ struct XParts {
  * verdict's bad list classified (stale finalise commit / bad / undecided),
  * the whole raw spans' commit trailers checked. */
 constexpr uint32_t CPASS_SPANS = 64;
-struct CPassArgs {
-    const uint8_t *base;
-    uint64_t img_size;
-    const uint64_t *off, *len;   /* commits */
-    const uint32_t *file;        /* file id per commit */
-    const unsigned long long *nbad;
-    const uint64_t *bad;         /* the verdict's list (first `cap` of *nbad) */
-    uint64_t cap;
-    uint32_t *flags;             /* per listed entry: 0 bad, 1 stale, 2 undecided (host) */
-    uint64_t *bad_out;           /* the first `out_cap` entries of bad[], beside flags, for */
-    uint64_t out_cap;            /* the one copy back (flags holds out_cap entries)         */
-    unsigned long long *nstale;
-    uint32_t nspans;
-    const uint32_t *span_raw;    /* raw registers from 0 */
-    const int64_t *span_commit;  /* image offset of the span's commit record, -1 = none here */
-    const uint32_t *span_init;   /* shift(~0, span length): the register of ~0 after the span */
-    int32_t *span_status;        /* 1 ok, 0 mismatch, 2 no commit record, -1 not checked */
-    unsigned long long *next_counters; /* the next pass's [nbad, nstale]: zeroed here */
-    /* host_nbad != NULL: flags / bad_out / span_status point into a pinned
-     * host block, and the kernel also writes *nbad and the span registers
-     * there (host_raw) -- no copy back after it */
-    uint64_t *host_nbad;
-    uint32_t *host_raw;
-};
-
-/* cpass_row_kernel: one rank's digest of a consistent pass as the fixed-shape
+/* cpass_post_kernel<true>'s last workgroup: one rank's digest of a consistent
+ * pass as the fixed-shape
  * int64 row the ranks all-gather (zeroskip_amd/consistent.py Consistent._pack):
  * [commits, n_bad, n_stale, listed bad, listed stale, pieces, flags]
  * + listed x (file, record offset) of bad commits, ascending commit index
@@ -246,6 +222,34 @@ struct CPassRowArgs {
     uint32_t listed, pmax;
     int64_t checked[4];          /* piece codes of checked spans: ok, bad, tail ok, tail bad */
     int64_t *row;
+};
+
+struct CPassArgs {
+    const uint8_t *base;
+    uint64_t img_size;
+    const uint64_t *off, *len;   /* commits */
+    const uint32_t *file;        /* file id per commit */
+    const unsigned long long *nbad;
+    const uint64_t *bad;         /* the verdict's list (first `cap` of *nbad) */
+    uint64_t cap;
+    uint32_t *flags;             /* per listed entry: 0 bad, 1 stale, 2 undecided (host) */
+    uint64_t *bad_out;           /* the first `out_cap` entries of bad[], beside flags, for */
+    uint64_t out_cap;            /* the one copy back (flags holds out_cap entries)         */
+    unsigned long long *nstale;  /* stale count over all min(*nbad, cap) entries */
+    unsigned long long *ticket;  /* workgroups done (the last one publishes) */
+    uint32_t nspans;
+    const uint32_t *span_raw;    /* raw registers from 0 */
+    const int64_t *span_commit;  /* image offset of the span's commit record, -1 = none here */
+    const uint32_t *span_init;   /* shift(~0, span length): the register of ~0 after the span */
+    int32_t *span_status;        /* 1 ok, 0 mismatch, 2 no commit record, -1 not checked */
+    unsigned long long *next_counters; /* the next pass's [nbad, nstale, ticket]: zeroed here */
+    /* host_nbad != NULL: flags / bad_out / span_status point into a pinned
+     * host block, and the kernel also writes *nbad, the stale count
+     * (host_nbad[1], by the last workgroup) and the span registers there
+     * (host_raw) -- no copy back after it */
+    uint64_t *host_nbad;
+    uint32_t *host_raw;
+    CPassRowArgs row;            /* row.row != NULL: build the digest row too */
 };
 
 struct RecDesc {

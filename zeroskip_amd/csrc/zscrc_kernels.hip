@@ -2124,7 +2124,13 @@ __device__ __forceinline__ void m64_issue(const MultiBatch &m, uint64_t n, const
  * vector stores with explicit scope / streaming bits -- 3: sc1 (device
  * scope: written through the XCD's L2; the default), 4: sc0 sc1 (system
  * scope), 5: sc1 nt.  Inline asm is invisible to the compiler's vmcnt
- * bookkeeping, which can then only over-wait (a younger store in the count). */
+ * bookkeeping, which can then only over-wait (a younger store in the count):
+ * correct because gfx9's vector memory operations of a wave complete in issue
+ * order, which `vmcnt` counting relies on.  The `sc0` / `sc1` / `nt` bits
+ * are gfx940-family (gfx950) syntax; the build below pins the target. */
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "zscrc_kernels.hip is CDNA4 (gfx950) code: its inline stores use gfx950 cache bits and in-order vmcnt"
+#endif
 template <int POL>
 __device__ __forceinline__ void store_policy(uint32_t *p, uint32_t v)
 {
@@ -3496,6 +3502,134 @@ __global__ __launch_bounds__(RO ? RT : BWG) void commit_kernel(BatchDesc d, cons
     }
 }
 
+/* ------------------------------------------------ consistent: the digest row */
+/* The last workgroup of cpass_post_kernel<true> (1,024 threads): the pass's
+ * listed verdict entries (flag 0 bad, 1 stale, 2 undecided) ordered by
+ * (flag, commit index) in LDS, then written as the rank's digest row in the
+ * layout of consistent.py's Consistent._pack, so the ranks all-gather it
+ * straight from the device (one RCCL all-gather, one copy to the host)
+ * instead of copying the block back, building the row in numpy and copying
+ * it up again.  Until round 6 this was a kernel of its own (cpass_row_kernel,
+ * 16 us and a launch gap on the N > 1 critical path).  (A fixed 4,096-key
+ * bitonic sort with four guarded pairs per thread took 60 us; a rank by
+ * counting 28 -- 16 waves x nl broadcast LDS reads.) */
+constexpr uint32_t ROW_SORT = 4096;
+
+__device__ __forceinline__ void cpass_build_row(const CPassRowArgs &a, uint64_t nbad, uint64_t nstale, uint64_t *key,
+                                                uint32_t *cnt)
+{
+    const uint32_t tid = threadIdx.x;
+    const uint32_t nl = (uint32_t)(nbad < a.list_cap ? nbad : a.list_cap);
+    const uint32_t *flags = reinterpret_cast<const uint32_t *>(a.blk + a.off_flags);
+    const uint64_t *bad = reinterpret_cast<const uint64_t *>(a.blk + a.off_bad);
+    if (tid < 3)
+        cnt[tid] = 0;
+    __syncthreads();
+    for (uint32_t k = tid; k < nl; k += blockDim.x) {
+        const uint32_t f = flags[k] > 2 ? 2u : flags[k];
+        key[k] = ((uint64_t)f << 56) | bad[k];
+        atomicAdd(&cnt[f], 1u);
+    }
+    __syncthreads();
+    /* bitonic over the next power of two >= nl (padded with ~0).  Up to
+     * 1,024 entries (config 5 lists 1,024 stale commits): one key per
+     * thread in a register, strides below 64 exchanged inside the wave
+     * (__shfl_xor, no barrier), only strides of 64 and up through LDS --
+     * 10 of config 5's 55 stages.  More: the same network on LDS, one
+     * compare-exchange pair per thread per stage. */
+    uint32_t n2 = 2;
+    while (n2 < nl)
+        n2 <<= 1;
+    if (n2 <= blockDim.x) {
+        uint64_t x = tid < nl ? key[tid] : ~0ull;
+        for (uint32_t size = 2; size <= n2; size <<= 1)
+            for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+                uint64_t y;
+                if (stride >= 64) {
+                    __syncthreads();
+                    key[tid] = x;
+                    __syncthreads();
+                    y = key[tid ^ stride];
+                } else {
+                    const uint32_t lo = __shfl_xor((uint32_t)x, (int)stride);
+                    const uint32_t hi = __shfl_xor((uint32_t)(x >> 32), (int)stride);
+                    y = ((uint64_t)hi << 32) | lo;
+                }
+                const bool up = (tid & size) == 0, lower = (tid & stride) == 0;
+                x = (lower == up) ? (x < y ? x : y) : (x < y ? y : x);
+            }
+        __syncthreads();
+        key[tid] = x;
+        __syncthreads();
+    } else {
+        for (uint32_t k = nl + tid; k < n2; k += blockDim.x)
+            key[k] = ~0ull;
+        __syncthreads();
+        for (uint32_t size = 2; size <= n2; size <<= 1)
+            for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+                for (uint32_t q = tid; q < n2 / 2; q += blockDim.x) {
+                    const uint32_t k = 2 * q - (q & (stride - 1)), j = k + stride;
+                    const uint64_t x = key[k], y = key[j];
+                    if ((x > y) == ((k & size) == 0)) {
+                        key[k] = y;
+                        key[j] = x;
+                    }
+                }
+                __syncthreads();
+            }
+    }
+    const uint32_t nb = cnt[0], ns = cnt[1], nu = cnt[2];
+    const uint32_t lb = nb < a.listed ? nb : a.listed, ls = ns < a.listed ? ns : a.listed;
+    int64_t *row = a.row;
+    if (tid == 0) {
+        row[0] = (int64_t)a.commits;
+        row[1] = (int64_t)(nbad - nstale); /* undecided ones included, as the host report */
+        row[2] = (int64_t)nstale;
+        row[3] = lb;
+        row[4] = ls;
+        row[5] = a.nspans;
+        row[6] = (nbad > a.list_cap ? (int64_t)ROW_FLAG_INCOMPLETE : 0) | (nu ? (int64_t)ROW_FLAG_UNDECIDED : 0);
+    }
+    int64_t *rb = row + ROW_HEAD, *rs = rb + 2 * a.listed, *rp = rs + 2 * a.listed;
+    const uint64_t IDX = (1ull << 56) - 1;
+    for (uint32_t k = tid; k < a.listed; k += blockDim.x) {
+        int64_t f = 0, r = 0;
+        if (k < lb) {
+            const uint64_t i = key[k] & IDX;
+            f = a.file[i];
+            r = a.rec[i];
+        }
+        rb[2 * k] = f;
+        rb[2 * k + 1] = r;
+        f = r = 0;
+        if (k < ls) {
+            const uint64_t i = key[nb + k] & IDX;
+            f = a.file[i];
+            r = a.rec[i];
+        }
+        rs[2 * k] = f;
+        rs[2 * k + 1] = r;
+    }
+    const uint32_t *raw = reinterpret_cast<const uint32_t *>(a.blk + a.off_raw);
+    const int32_t *st = reinterpret_cast<const int32_t *>(a.blk + a.off_st);
+    for (uint32_t k = tid; k < a.pmax; k += blockDim.x) {
+        int64_t q[4] = {0, 0, 0, 0};
+        if (k < a.nspans) {
+            const int64_t fid = a.piece[3 * k], pc = a.piece[3 * k + 1], len = a.piece[3 * k + 2];
+            q[0] = fid;
+            q[2] = len;
+            if (st[k] < 0) {
+                q[1] = pc;
+                q[3] = raw[k];
+            } else {
+                q[1] = pc < 0 ? (st[k] == 1 ? a.checked[2] : a.checked[3]) : (st[k] == 1 ? a.checked[0] : a.checked[1]);
+            }
+        }
+        for (int j = 0; j < 4; ++j)
+            rp[4 * k + j] = q[j];
+    }
+}
+
 /* ------------------------------------------------- consistent post pass */
 /* crc32c register r through the bytes [p, p + n) (any alignment): one
  * thread, the compact slice-by-4 table T (GT_S4 in LDS). */
@@ -3550,13 +3684,18 @@ __device__ __forceinline__ uint32_t crc_word(const char *T, uint32_t r, uint64_t
  * (src/zeroskip-file.c:266-302).  Everything stays on the device: the host
  * copies one small block back.
  */
-__global__ __launch_bounds__(256) void cpass_post_kernel(CPassArgs a, const uint32_t *__restrict__ gtab)
+template <bool ROW>
+__global__ __launch_bounds__(ROW ? 1024 : 256) void cpass_post_kernel(CPassArgs a, const uint32_t *__restrict__ gtab)
 {
     __shared__ __attribute__((aligned(16))) char T[4096];
+    __shared__ uint64_t key[ROW ? ROW_SORT : 1];
+    __shared__ uint32_t cnt[3];
+    __shared__ uint32_t last;
     /* the next pass's block: nothing reads it during this pass (its last
-     * copy back ran before this pass's kernels), so its counters are zeroed
-     * here instead of by a memset launch ahead of the next pass */
-    if (a.next_counters && blockIdx.x == 0 && threadIdx.x < 2)
+     * copy back ran before this pass's kernels), so its counters (nbad,
+     * nstale, the ticket) are zeroed here instead of by a memset launch ahead
+     * of the next pass */
+    if (a.next_counters && blockIdx.x == 0 && threadIdx.x < 3)
         a.next_counters[threadIdx.x] = 0ull;
     if (a.host_nbad && blockIdx.x == 0) { /* the pass's count and span registers, straight to the host */
         if (threadIdx.x == 0)
@@ -3568,6 +3707,7 @@ __global__ __launch_bounds__(256) void cpass_post_kernel(CPassArgs a, const uint
     __syncthreads();
     const uint64_t nbad = *a.nbad, nl = nbad < a.cap ? nbad : a.cap;
     const uint64_t nt = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t mine = 0; /* stale commits this thread found */
     for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nl; k += nt) {
         const uint64_t i = a.bad[k];
         uint32_t flag = 0;
@@ -3592,9 +3732,10 @@ __global__ __launch_bounds__(256) void cpass_post_kernel(CPassArgs a, const uint
             a.flags[k] = flag;
             a.bad_out[k] = i;
         }
-        if (flag == 1)
-            atomicAdd(a.nstale, 1ull);
+        mine += flag == 1;
     }
+    if (mine)
+        atomicAdd(a.nstale, (unsigned long long)mine);
     if (blockIdx.x == 0 && threadIdx.x < a.nspans) {
         const uint32_t s = threadIdx.x;
         int32_t st = -1;
@@ -3626,6 +3767,29 @@ __global__ __launch_bounds__(256) void cpass_post_kernel(CPassArgs a, const uint
         }
         a.span_status[s] = st;
     }
+    /* The last workgroup to finish (a ticket) publishes the stale count over
+     * ALL classified entries -- the same set the device row counts, whatever
+     * order the verdict's waves listed them in (round 5's host recount over
+     * the 4,096 listed flags was order-dependent on an incomplete pass) --
+     * and, for a row pass, builds the digest row.  Each workgroup's stores
+     * and its count are released (agent scope: the writeback reaches the
+     * other XCDs' view) before it takes its ticket; the last one acquires. */
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long t =
+            __hip_atomic_fetch_add(a.ticket, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        last = t == gridDim.x - 1 ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!last)
+        return;
+    __threadfence();
+    const uint64_t nstale = __hip_atomic_load(a.nstale, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    if (a.host_nbad && threadIdx.x == 0)
+        a.host_nbad[1] = nstale;
+    if constexpr (ROW)
+        cpass_build_row(a.row, nbad, nstale, key, cnt);
 }
 
 /* ------------------------------------------------------------ span fold */
@@ -4410,135 +4574,6 @@ __global__ __launch_bounds__(256) void part_fold_kernel(FoldPair fp, const uint3
     }
 }
 
-/* ------------------------------------------------ consistent: the digest row */
-/* One workgroup: the pass's listed verdict entries (flag 0 bad, 1 stale, 2
- * undecided) ordered by (flag, commit index) in LDS, then written as the
- * rank's digest row in the layout of consistent.py's Consistent._pack, so the
- * ranks all-gather it straight from the device (one RCCL all-gather, one copy
- * to the host) instead of copying the block back, building the row in numpy
- * and copying it up again.  (A fixed 4,096-key bitonic sort with four
- * guarded pairs per thread took 60 us; a rank by counting 28 -- 16 waves x
- * nl broadcast LDS reads.) */
-constexpr uint32_t ROW_SORT = 4096;
-
-__global__ __launch_bounds__(1024) void cpass_row_kernel(CPassRowArgs a)
-{
-    __shared__ uint64_t key[ROW_SORT];
-    __shared__ uint32_t cnt[3];
-    const uint32_t tid = threadIdx.x;
-    const uint64_t nbad = reinterpret_cast<const uint64_t *>(a.blk)[0];
-    const uint64_t nstale = reinterpret_cast<const uint64_t *>(a.blk)[1];
-    const uint32_t nl = (uint32_t)(nbad < a.list_cap ? nbad : a.list_cap);
-    const uint32_t *flags = reinterpret_cast<const uint32_t *>(a.blk + a.off_flags);
-    const uint64_t *bad = reinterpret_cast<const uint64_t *>(a.blk + a.off_bad);
-    if (tid < 3)
-        cnt[tid] = 0;
-    __syncthreads();
-    for (uint32_t k = tid; k < nl; k += blockDim.x) {
-        const uint32_t f = flags[k] > 2 ? 2u : flags[k];
-        key[k] = ((uint64_t)f << 56) | bad[k];
-        atomicAdd(&cnt[f], 1u);
-    }
-    __syncthreads();
-    /* bitonic over the next power of two >= nl (padded with ~0).  Up to
-     * 1,024 entries (config 5 lists 1,024 stale commits): one key per
-     * thread in a register, strides below 64 exchanged inside the wave
-     * (__shfl_xor, no barrier), only strides of 64 and up through LDS --
-     * 10 of config 5's 55 stages.  More: the same network on LDS, one
-     * compare-exchange pair per thread per stage. */
-    uint32_t n2 = 2;
-    while (n2 < nl)
-        n2 <<= 1;
-    if (n2 <= blockDim.x) {
-        uint64_t x = tid < nl ? key[tid] : ~0ull;
-        for (uint32_t size = 2; size <= n2; size <<= 1)
-            for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-                uint64_t y;
-                if (stride >= 64) {
-                    __syncthreads();
-                    key[tid] = x;
-                    __syncthreads();
-                    y = key[tid ^ stride];
-                } else {
-                    const uint32_t lo = __shfl_xor((uint32_t)x, (int)stride);
-                    const uint32_t hi = __shfl_xor((uint32_t)(x >> 32), (int)stride);
-                    y = ((uint64_t)hi << 32) | lo;
-                }
-                const bool up = (tid & size) == 0, lower = (tid & stride) == 0;
-                x = (lower == up) ? (x < y ? x : y) : (x < y ? y : x);
-            }
-        __syncthreads();
-        key[tid] = x;
-        __syncthreads();
-    } else {
-        for (uint32_t k = nl + tid; k < n2; k += blockDim.x)
-            key[k] = ~0ull;
-        __syncthreads();
-        for (uint32_t size = 2; size <= n2; size <<= 1)
-            for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-                for (uint32_t q = tid; q < n2 / 2; q += blockDim.x) {
-                    const uint32_t k = 2 * q - (q & (stride - 1)), j = k + stride;
-                    const uint64_t x = key[k], y = key[j];
-                    if ((x > y) == ((k & size) == 0)) {
-                        key[k] = y;
-                        key[j] = x;
-                    }
-                }
-                __syncthreads();
-            }
-    }
-    const uint32_t nb = cnt[0], ns = cnt[1], nu = cnt[2];
-    const uint32_t lb = nb < a.listed ? nb : a.listed, ls = ns < a.listed ? ns : a.listed;
-    int64_t *row = a.row;
-    if (tid == 0) {
-        row[0] = (int64_t)a.commits;
-        row[1] = (int64_t)(nbad - nstale); /* undecided ones included, as the host report */
-        row[2] = (int64_t)nstale;
-        row[3] = lb;
-        row[4] = ls;
-        row[5] = a.nspans;
-        row[6] = (nbad > a.list_cap ? (int64_t)ROW_FLAG_INCOMPLETE : 0) | (nu ? (int64_t)ROW_FLAG_UNDECIDED : 0);
-    }
-    int64_t *rb = row + ROW_HEAD, *rs = rb + 2 * a.listed, *rp = rs + 2 * a.listed;
-    const uint64_t IDX = (1ull << 56) - 1;
-    for (uint32_t k = tid; k < a.listed; k += blockDim.x) {
-        int64_t f = 0, r = 0;
-        if (k < lb) {
-            const uint64_t i = key[k] & IDX;
-            f = a.file[i];
-            r = a.rec[i];
-        }
-        rb[2 * k] = f;
-        rb[2 * k + 1] = r;
-        f = r = 0;
-        if (k < ls) {
-            const uint64_t i = key[nb + k] & IDX;
-            f = a.file[i];
-            r = a.rec[i];
-        }
-        rs[2 * k] = f;
-        rs[2 * k + 1] = r;
-    }
-    const uint32_t *raw = reinterpret_cast<const uint32_t *>(a.blk + a.off_raw);
-    const int32_t *st = reinterpret_cast<const int32_t *>(a.blk + a.off_st);
-    for (uint32_t k = tid; k < a.pmax; k += blockDim.x) {
-        int64_t q[4] = {0, 0, 0, 0};
-        if (k < a.nspans) {
-            const int64_t fid = a.piece[3 * k], pc = a.piece[3 * k + 1], len = a.piece[3 * k + 2];
-            q[0] = fid;
-            q[2] = len;
-            if (st[k] < 0) {
-                q[1] = pc;
-                q[3] = raw[k];
-            } else {
-                q[1] = pc < 0 ? (st[k] == 1 ? a.checked[2] : a.checked[3]) : (st[k] == 1 ? a.checked[0] : a.checked[1]);
-            }
-        }
-        for (int j = 0; j < 4; ++j)
-            rp[4 * k + j] = q[j];
-    }
-}
-
 /* ------------------------------------------------ the writer's second pass */
 /* The in-place commit writer as two passes (round 5, tuning bit 512):
  * commit_kernel computes every CRC into crc[] without touching the image
@@ -4861,17 +4896,19 @@ extern "C" int zs_launch_commit_scatter(uint8_t *base, const uint64_t *off, cons
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
-extern "C" int zs_launch_cpass_row(const zs::CPassRowArgs *a, hipStream_t stream)
-{
-    if (a->list_cap > zs::ROW_SORT)
-        return -1;
-    hipLaunchKernelGGL(zs::cpass_row_kernel, dim3(1), dim3(1024), 0, stream, *a);
-    return hipGetLastError() == hipSuccess ? 0 : -3;
-}
-
+/* a->row.row != NULL: the pass's digest row too, built by the last
+ * workgroup (1,024 threads); otherwise 256-thread workgroups */
 extern "C" int zs_launch_cpass_post(const zs::CPassArgs *a, const uint32_t *gtab, hipStream_t stream)
 {
-    hipLaunchKernelGGL(zs::cpass_post_kernel, dim3(64), dim3(256), 0, stream, *a, gtab);
+    if (!a->ticket || !a->nstale)
+        return -1;
+    if (a->row.row) {
+        if (a->row.list_cap > zs::ROW_SORT || a->row.list_cap > a->out_cap)
+            return -1;
+        hipLaunchKernelGGL(zs::cpass_post_kernel<true>, dim3(64), dim3(1024), 0, stream, *a, gtab);
+    } else {
+        hipLaunchKernelGGL(zs::cpass_post_kernel<false>, dim3(64), dim3(256), 0, stream, *a, gtab);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

@@ -61,6 +61,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
 #include <thread>
 #include <vector>
@@ -197,6 +198,96 @@ void parallel_sort(std::vector<MRec> &a, int threads)
     }
     if (src != &a)
         a.swap(*src);
+}
+
+/* ZSCRC_REPACK_REFERENCE_COMPAT: branch 2 exactly as the reference's
+ * packed-files iterator merges (zs_iterator_begin_for_packed_files /
+ * zsdb_iter_data_next / zsdb_iter_data_process, src/zeroskip-iterator.c
+ * :220-300, driven by zs_packed_file_new_from_packed_files,
+ * src/zeroskip-packed.c:617-742).  Each source is a cursor over its records
+ * (key order) with a priority (pflist order: 1 = the newest, 2 = the older
+ * file) and a `deleted` flag.  The current key of every cursor sits in one
+ * ordered table (the iterator's hash table + priority queue); a cursor whose
+ * key is already there either takes the entry (higher priority: the other
+ * cursor steps on) or steps on itself.  The smallest key is written unless
+ * its cursor's flag is set.  The flag is set when a cursor STEPS onto a
+ * delete (:258-259) and never cleared, so from a source's first delete after
+ * its first record on, none of that source's records is written; a delete as
+ * a source's first record is never flagged (begin reads the key without its
+ * type) and is written as a delete record.  That loses data; the default
+ * merge does not (it keeps every record, the older file winning a key and a
+ * winning delete dropping it). */
+struct Cursor {
+    const uint8_t *img = nullptr;
+    const std::vector<zscrc_zs_record> *recs = nullptr;
+    int prio = 0;
+    size_t pos = 0;
+    bool deleted = false, done = false;
+};
+
+struct KeyRef {
+    const uint8_t *k;
+    uint64_t kl;
+    bool operator<(const KeyRef &o) const { return memcmp_raw(k, kl, o.k, o.kl) < 0; }
+};
+
+void compat_merge(std::vector<Cursor> &cur, std::vector<MRec> &out)
+{
+    std::map<KeyRef, size_t> table; /* current key -> cursor */
+    /* offer cursor c's current key; a cursor that loses steps on (iterative:
+     * each live cursor holds at most one entry) */
+    auto offer = [&](size_t c) {
+        for (;;) {
+            Cursor &u = cur[c];
+            if (u.done)
+                return;
+            const zscrc_zs_record &r = (*u.recs)[u.pos];
+            const KeyRef key{u.img + r.key_off, r.key_len};
+            auto it = table.find(key);
+            if (it == table.end()) {
+                table.emplace(key, c);
+                return;
+            }
+            size_t loser = c;
+            if (u.prio > cur[it->second].prio) {
+                loser = it->second;
+                table.erase(it);
+                table.emplace(key, c);
+            }
+            /* the loser steps on (zsdb_iter_data_next) */
+            Cursor &l = cur[loser];
+            if (++l.pos >= l.recs->size()) {
+                l.done = true;
+                return;
+            }
+            if ((*l.recs)[l.pos].val_off == ZSCRC_ZS_DELETED)
+                l.deleted = true;
+            c = loser;
+        }
+    };
+    for (size_t c = 0; c < cur.size(); ++c) {
+        cur[c].done = cur[c].recs->empty();
+        offer(c);
+    }
+    uint64_t seq = 0;
+    while (!table.empty()) {
+        const auto first = table.begin();
+        const size_t c = first->second;
+        table.erase(first);
+        Cursor &u = cur[c];
+        if (!u.deleted) {
+            const zscrc_zs_record &r = (*u.recs)[u.pos];
+            out.push_back({u.img + r.key_off, r.val_off == ZSCRC_ZS_DELETED ? nullptr : u.img + r.val_off,
+                           r.key_len, r.val_len, seq++});
+        }
+        if (++u.pos >= u.recs->size()) {
+            u.done = true;
+            continue;
+        }
+        if ((*u.recs)[u.pos].val_off == ZSCRC_ZS_DELETED)
+            u.deleted = true;
+        offer(c);
+    }
 }
 
 struct DbFile {
@@ -488,7 +579,23 @@ extern "C" int zscrc_zs_repack(const char *dbdir, unsigned flags, int threads, z
 
     /* merge: one sorted sequence, the winner of every key */
     std::vector<MRec> all;
-    if (!rc) {
+    const bool compat = rep->branch == 2 && (flags & ZSCRC_REPACK_REFERENCE_COMPAT);
+    if (!rc && compat) {
+        size_t total = 0;
+        for (auto &l : lists)
+            total += l.size();
+        rep->records_in = total;
+        /* pflist order: the newest file first, priority 1; the older, 2 */
+        std::vector<Cursor> cur(src.size());
+        for (size_t i = 0; i < src.size(); ++i) {
+            const size_t fi = src.size() - 1 - i;
+            cur[i].img = src[fi].img;
+            cur[i].recs = &lists[fi];
+            cur[i].prio = (int)i + 1;
+        }
+        compat_merge(cur, all);
+        std::vector<std::vector<zscrc_zs_record>>().swap(lists);
+    } else if (!rc) {
         size_t total = 0;
         for (auto &l : lists)
             total += l.size();

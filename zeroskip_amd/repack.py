@@ -130,13 +130,18 @@ class RepackReport(ctypes.Structure):
         return d
 
 
-def repack_dir(dbdir: str, threads: int = 0, fsync: bool = False) -> dict:
+REFERENCE_COMPAT = 2  # ZSCRC_REPACK_REFERENCE_COMPAT
+
+
+def repack_dir(dbdir: str, threads: int = 0, fsync: bool = False, reference_compat: bool = False) -> dict:
     """zsdb_repack over a DB directory (zscrc_zs_repack): branch 1 merges the
     finalised files, branch 2 the reference's two packed files; returns the
-    report (branch 0: nothing to pack)."""
+    report (branch 0: nothing to pack).  reference_compat: branch 2 writes the
+    reference's bytes including its loss of records after a delete
+    (src/zeroskip-iterator.c:258-259; include/zscrc.h)."""
     rep = RepackReport()
-    check(lib().zscrc_zs_repack(os.fsencode(dbdir), FSYNC if fsync else 0, threads, ctypes.byref(rep)),
-          "zscrc_zs_repack")
+    flags = (FSYNC if fsync else 0) | (REFERENCE_COMPAT if reference_compat else 0)
+    check(lib().zscrc_zs_repack(os.fsencode(dbdir), flags, threads, ctypes.byref(rep)), "zscrc_zs_repack")
     return rep.as_dict()
 
 
