@@ -63,6 +63,9 @@ __device__ __forceinline__ void gstore32(const void *p, uint32_t v)
 {
     *(gw32p)reinterpret_cast<uintptr_t>(p) = v;
 }
+#ifndef ZS_DIAG_BLOCK_STORE
+#define ZS_DIAG_BLOCK_STORE 0 /* 1, 2: A/B diagnostic builds of the writer (emit; 2: + nt run loads) */
+#endif
 
 /* The only readfirstlane / readlane in this file.  The builtins return int:
  * widened straight into a 64-bit value they sign-extend from 2^31 (s_bfe_i64;
@@ -450,8 +453,31 @@ __device__ __forceinline__ void emit(const BatchDesc &d, const Item &it, uint32_
         st = 0;
     }
     const uint32_t crc = r ^ 0xffffffffu;
+#if ZS_DIAG_BLOCK_STORE
+    /* A/B diagnostic build only (tools/probes/block_store_ab.sh; wrong
+     * image bytes): the writer stores the whole 64-byte aligned block around
+     * each CRC field instead of the 4-byte field -- the cost of whole-block
+     * stores in this loop, without the cross-lane assembly of their bytes */
+    if (d.commit == 2 && st == 0) {
+        const uintptr_t a = crc_at & ~uintptr_t(63), b0 = reinterpret_cast<uintptr_t>(d.base);
+        if (a >= b0 && a + 64 <= b0 + d.img_size && (crc_at & 3) == 0) {
+            /* the commit word's first 4 bytes (type, length) kept, so the
+             * next call still finds a commit record there and stores again */
+            typedef __attribute__((address_space(1))) u32x4 *g4w;
+            const int32_t tw = (int32_t)((crc_at - a) >> 2) - 1; /* -1: in the block before */
+            const uint32_t cw = it.c0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                *(g4w)(a + 16 * k) = u32x4{tw == 4 * k ? cw : crc, tw == 4 * k + 1 ? cw : crc,
+                                           tw == 4 * k + 2 ? cw : crc, tw == 4 * k + 3 ? cw : crc};
+        } else {
+            gstore32(reinterpret_cast<const void *>(crc_at), __builtin_bswap32(crc));
+        }
+    }
+#else
     if (d.commit == 2 && st == 0)
         gstore32(reinterpret_cast<const void *>(crc_at), __builtin_bswap32(crc));
+#endif
     /* commit 3 (the writer's CRCs out of place): out[] only, image untouched;
      * commit 4 (the two-pass writer's first pass): as 3, status 3 for a long
      * commit record (its CRC field at +20, not +4) */
@@ -3456,7 +3482,7 @@ __global__ __launch_bounds__(RO ? RT : BWG) void commit_kernel(BatchDesc d, cons
         ++rounds;
         runs += run ? 1u : 0u;
         if (run)
-            run_issue<5, !WR>(b, w, lane);
+            run_issue<5, !WR || ZS_DIAG_BLOCK_STORE == 2>(b, w, lane);
         else
             burst_issue_x(b, dummy, w, lane);
         const uint64_t i_nxt = 64 * r_nxt + (uint64_t)lane;
