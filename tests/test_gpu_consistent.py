@@ -538,3 +538,66 @@ def test_row_exchange_over_rccl_one_rank(gpu):
     sync_ok, piped_ok, ok, bad, trips, at = res
     assert sync_ok and len(piped_ok) == 5 and all(piped_ok)
     assert not ok and bad == [(name(4, 5), at)] and trips == 1
+
+
+def test_cpass_stale_rehash_ragged_spans(gpu):
+    """The post kernel's finalise-quirk check rehashes the span before each
+    zero-length commit (crc_run: its ragged head and tail from the aligned
+    dword around them, the body in 64-byte steps, the last words loaded
+    together).  Zeroskip's own spans are 8-byte aligned, so here a synthetic
+    image places them at every byte alignment with lengths 1..1,500 and on
+    the step edges; each span's commit record is followed by nothing but a
+    zero-length commit that reuses it -- stale (the quirk) when both commits
+    are of one file, bad when the file ids differ.  Counts and listed
+    indices equal what the construction says.  src/zeroskip-active.c:122,
+    src/mfile.c:534-546 (the quirk); src/zeroskip-file.c:266-302 (the
+    commit CRC)."""
+    import ctypes
+    from oracle import oracle
+    from zeroskip_amd._lib import check, lib
+    rng = np.random.default_rng(606)
+    # (length 0 is no case: the zero-length commit would then verify like its
+    # predecessor, which is not the quirk)
+    edges = [1, 2, 3, 4, 5, 7, 8, 60, 63, 64, 65, 67, 127, 128, 129, 131, 192, 312, 319, 320, 1023]
+    lens = edges + rng.integers(1, 1501, 200).tolist()
+    m = len(lens)
+    size = sum(lens) + m * (8 + 7 + 64) + 4096
+    img = rng.integers(0, 256, size, dtype=np.uint8)
+    off, ln, fid, stale, bad = [], [], [], [], []
+    pos = 1
+    for k, pl in enumerate(lens):
+        pos += int(rng.integers(0, 64))          # any byte alignment
+        at = pos + pl
+        img[at:at + 4] = (4, 0, 0, 0)            # COMMIT, length 0 in the record's header word
+        S = oracle.crc32c_hw(0, img[pos:pos + pl].tobytes())
+        hi = int.from_bytes(img[at:at + 4].tobytes() + b"\0\0\0\0", "big")
+        c = oracle.crc32c_hw(S, hi.to_bytes(8, "little"))
+        img[at + 4:at + 8] = np.frombuffer(c.to_bytes(4, "big"), np.uint8)
+        same_file = k % 7 != 3
+        i = len(off)
+        off += [pos, at]
+        ln += [pl, 0]
+        fid += [2 * k, 2 * k if same_file else 2 * k + 1]
+        (stale if same_file else bad).append(i + 1)
+        pos = at + 8
+    assert pos <= size
+    dev = torch.device("cuda", 0)
+    buf = torch.from_numpy(img).to(dev)
+    d_off = torch.tensor(off, dtype=torch.int64, device=dev)
+    d_len = torch.tensor(ln, dtype=torch.int64, device=dev)
+    d_file = torch.tensor(fid, dtype=torch.int32, device=dev)
+    h = ctypes.c_void_p()
+    res = cs.CPassResult()
+    with torch.cuda.device(dev):
+        spec = cs.CPassSpec(buf.data_ptr(), buf.numel(), len(off), d_off.data_ptr(), d_len.data_ptr(),
+                            d_file.data_ptr(), max(ln), 0, None, None, None)
+        check(lib().zscrc_cpass_create(ctypes.byref(h), ctypes.byref(spec)), "zscrc_cpass_create")
+        try:
+            for _ in range(3):                    # both device blocks, and back
+                check(lib().zscrc_cpass_run(h, None, ctypes.byref(res)), "zscrc_cpass_run")
+                assert res.complete and res.n_undecided == 0
+                assert (res.n_stale, res.n_bad) == (len(stale), len(bad)), (res.n_stale, res.n_bad)
+                assert list(res.stale[:res.n_listed_stale]) == stale
+                assert list(res.bad[:res.n_listed_bad]) == bad
+        finally:
+            lib().zscrc_cpass_destroy(h)

@@ -3658,36 +3658,77 @@ __device__ __forceinline__ void cpass_build_row(const CPassRowArgs &a, uint64_t 
 
 /* ------------------------------------------------- consistent post pass */
 /* crc32c register r through the bytes [p, p + n) (any alignment): one
- * thread, the compact slice-by-4 table T (GT_S4 in LDS). */
+ * thread, the compact slice-by-4 table T (GT_S4 in LDS).  Every load of a
+ * stage is issued before its first use, so a span costs about two memory
+ * latencies instead of one per word: the ragged ends come from the aligned
+ * dword around them (a 4-byte aligned dword never crosses a page), the body
+ * in 64-byte steps with the next step's four 16-byte loads (4-byte aligned
+ * dwordx4: tools/probes/unaligned_probe) in flight, the last < 64 bytes as
+ * up to 15 dword loads issued together.  (Measured level with one load per
+ * tail word: config 5's post kernel 16.7 against 17.0 us for 1,024 rehashed
+ * 312-byte spans, profiles/r06/config5/ -- the kernel's time is not in
+ * these loads; kept for spans whose ends are ragged.) */
+__device__ __forceinline__ uint32_t crc_byte(const char *T, uint32_t r, uint32_t byte)
+{
+    return lds32(T, 3072 + (((r ^ byte) & 0xffu) << 2)) ^ (r >> 8);
+}
+
 __device__ __forceinline__ uint32_t crc_run(const char *T, uint32_t r, const uint8_t *p, uint64_t n)
 {
-    while (n && ((uintptr_t)p & 3)) {
-        r = lds32(T, 3072 + (((r ^ *(g8p)p) & 0xffu) << 2)) ^ (r >> 8);
-        ++p;
-        --n;
+    const uint32_t mis = (uint32_t)((uintptr_t)p & 3);
+    if (n && mis) { /* the head: bytes up to the next dword boundary */
+        const uint32_t wd = *(g32p)((uintptr_t)p - mis);
+        const uint32_t h = 4 - mis < n ? 4 - mis : (uint32_t)n;
+        for (uint32_t k = 0; k < h; ++k)
+            r = crc_byte(T, r, wd >> (8 * (mis + k)));
+        p += h;
+        n -= h;
     }
-    for (; n >= 4 && ((uintptr_t)p & 15); n -= 4, p += 4)
-        r = op4(T, 0, r ^ *(g32p)p);
-    /* 64 bytes per step, their four 16-byte loads issued together (a load
-     * per word made every word wait one memory latency: cpass_post_kernel
-     * 21 us for 1,024 rehashed 312-byte spans) */
-    for (; n >= 64; n -= 64, p += 64) {
+    if (n >= 64) {
         u32x4 v[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
             v[i] = *(g4p)(p + 16 * i);
+        for (;;) {
+            const bool more = n >= 128;
+            u32x4 nx[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            r = op4(T, 0, r ^ v[i].x);
-            r = op4(T, 0, r ^ v[i].y);
-            r = op4(T, 0, r ^ v[i].z);
-            r = op4(T, 0, r ^ v[i].w);
+            for (int i = 0; i < 4; ++i)
+                nx[i] = *(g4p)(p + (more ? 64 : 0) + 16 * i);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                r = op4(T, 0, r ^ v[i].x);
+                r = op4(T, 0, r ^ v[i].y);
+                r = op4(T, 0, r ^ v[i].z);
+                r = op4(T, 0, r ^ v[i].w);
+            }
+            n -= 64;
+            p += 64;
+            if (!more)
+                break;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                v[i] = nx[i];
         }
     }
-    for (; n >= 4; n -= 4, p += 4)
-        r = op4(T, 0, r ^ *(g32p)p);
-    for (; n; --n, ++p)
-        r = lds32(T, 3072 + (((r ^ *(g8p)p) & 0xffu) << 2)) ^ (r >> 8);
+    const uint32_t nw = (uint32_t)(n >> 2); /* < 16 */
+    if (nw) {
+        uint32_t t[15];
+#pragma unroll
+        for (uint32_t j = 0; j < 15; ++j)
+            t[j] = *(g32p)(p + 4 * (j < nw ? j : 0));
+#pragma unroll
+        for (uint32_t j = 0; j < 15; ++j)
+            if (j < nw)
+                r = op4(T, 0, r ^ t[j]);
+    }
+    p += 4 * nw;
+    n -= 4 * nw;
+    if (n) { /* the last 1-3 bytes, from their aligned dword */
+        const uint32_t wd = *(g32p)p;
+        for (uint32_t k = 0; k < n; ++k)
+            r = crc_byte(T, r, wd >> (8 * k));
+    }
     return r;
 }
 
@@ -3716,7 +3757,7 @@ __global__ __launch_bounds__(ROW ? 1024 : 256) void cpass_post_kernel(CPassArgs 
     __shared__ __attribute__((aligned(16))) char T[4096];
     __shared__ uint64_t key[ROW ? ROW_SORT : 1];
     __shared__ uint32_t cnt[3];
-    __shared__ uint32_t last;
+    __shared__ uint32_t last, wg_stale, tot_stale;
     /* the next pass's block: nothing reads it during this pass (its last
      * copy back ran before this pass's kernels), so its counters (nbad,
      * nstale, the ticket) are zeroed here instead of by a memset launch ahead
@@ -3729,6 +3770,8 @@ __global__ __launch_bounds__(ROW ? 1024 : 256) void cpass_post_kernel(CPassArgs 
         for (uint32_t k = threadIdx.x; k < a.nspans; k += blockDim.x)
             a.host_raw[k] = a.span_raw[k];
     }
+    if (threadIdx.x == 0)
+        wg_stale = 0;
     load_gmul_table(T, gtab); /* GT_S4, compact: table j at 1024 j */
     __syncthreads();
     const uint64_t nbad = *a.nbad, nl = nbad < a.cap ? nbad : a.cap;
@@ -3736,15 +3779,19 @@ __global__ __launch_bounds__(ROW ? 1024 : 256) void cpass_post_kernel(CPassArgs 
     uint32_t mine = 0; /* stale commits this thread found */
     for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nl; k += nt) {
         const uint64_t i = a.bad[k];
+        /* every descriptor this entry may need, loaded together (one latency
+         * instead of a chain of them) */
+        const uint64_t ip = i ? i - 1 : 0;
+        const uint64_t li = a.len[i], at = a.off[i], pl = a.len[ip], po = a.off[ip];
+        const uint32_t fi = a.file[i], fp = a.file[ip];
         uint32_t flag = 0;
-        if (a.len[i] == 0 && i > 0 && a.file[i - 1] == a.file[i]) {
-            const uint64_t at = a.off[i]; /* the zero-length span's commit record */
-            const uint64_t pl = a.len[i - 1];
-            if (at + 8 <= a.img_size && pl <= 65536) {
+        if (li == 0 && i > 0 && fp == fi) {
+            /* the zero-length span's commit record at `at` */
+            if (at + 8 <= a.img_size && pl <= 65536 && po <= a.img_size && pl <= a.img_size - po) {
                 const uint64_t w0 = load_be64(reinterpret_cast<uintptr_t>(a.base) + at);
+                const uint32_t S = crc_run(T, 0xffffffffu, a.base + po, pl) ^ 0xffffffffu;
                 const uint32_t t = (uint32_t)(w0 >> 56);
                 if (t == REC_COMMIT || t == REC_FINAL) {
-                    const uint32_t S = crc_run(T, 0xffffffffu, a.base + a.off[i - 1], pl) ^ 0xffffffffu;
                     const uint32_t c = crc_word(T, S ^ 0xffffffffu, w0 & 0xFFFFFFFF00000000ull) ^ 0xffffffffu;
                     flag = c == (uint32_t)w0 ? 1u : 0u;
                 } else {
@@ -3761,7 +3808,7 @@ __global__ __launch_bounds__(ROW ? 1024 : 256) void cpass_post_kernel(CPassArgs 
         mine += flag == 1;
     }
     if (mine)
-        atomicAdd(a.nstale, (unsigned long long)mine);
+        atomicAdd(&wg_stale, mine);
     if (blockIdx.x == 0 && threadIdx.x < a.nspans) {
         const uint32_t s = threadIdx.x;
         int32_t st = -1;
@@ -3793,27 +3840,42 @@ __global__ __launch_bounds__(ROW ? 1024 : 256) void cpass_post_kernel(CPassArgs 
         }
         a.span_status[s] = st;
     }
-    /* The last workgroup to finish (a ticket) publishes the stale count over
-     * ALL classified entries -- the same set the device row counts, whatever
+    /* The last workgroup to finish publishes the stale count over ALL
+     * classified entries -- the same set the device row counts, whatever
      * order the verdict's waves listed them in (round 5's host recount over
      * the 4,096 listed flags was order-dependent on an incomplete pass) --
-     * and, for a row pass, builds the digest row.  Each workgroup's stores
-     * and its count are released (agent scope: the writeback reaches the
-     * other XCDs' view) before it takes its ticket; the last one acquires. */
-    __threadfence();
+     * and, for a row pass, builds the digest row.  Count and ticket are ONE
+     * 64-bit word (workgroups done << 32 | stale commits): each workgroup adds
+     * (1 << 32) + its stale count in one atomic, so the one that sees the
+     * last ticket also sees the whole sum -- no fence is needed for the count
+     * (a release fence per workgroup and the acquire are an L2 write-back and
+     * invalidate each, buffer_wbl2 / buffer_inv: config 5's post kernel took
+     * 23.2 us with them against 17.0 without, profiles/r06/config5/).  The row
+     * builder reads the other workgroups' listed entries, so a row pass
+     * still releases them (agent scope: the other XCDs' view) and the last
+     * workgroup acquires. */
+    if constexpr (ROW)
+        __threadfence();
     __syncthreads();
     if (threadIdx.x == 0) {
+        const unsigned long long add = (1ull << 32) | wg_stale;
         const unsigned long long t =
-            __hip_atomic_fetch_add(a.ticket, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        last = t == gridDim.x - 1 ? 1u : 0u;
+            ROW ? __hip_atomic_fetch_add(a.ticket, add, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT)
+                : __hip_atomic_fetch_add(a.ticket, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = (t >> 32) == gridDim.x - 1 ? 1u : 0u;
+        tot_stale = (uint32_t)(t + add);
     }
     __syncthreads();
     if (!last)
         return;
-    __threadfence();
-    const uint64_t nstale = __hip_atomic_load(a.nstale, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-    if (a.host_nbad && threadIdx.x == 0)
-        a.host_nbad[1] = nstale;
+    if constexpr (ROW)
+        __threadfence();
+    const uint64_t nstale = tot_stale;
+    if (threadIdx.x == 0) {
+        *a.nstale = nstale;
+        if (a.host_nbad)
+            a.host_nbad[1] = nstale;
+    }
     if constexpr (ROW)
         cpass_build_row(a.row, nbad, nstale, key, cnt);
 }
