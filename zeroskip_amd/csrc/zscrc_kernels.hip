@@ -3529,34 +3529,28 @@ __global__ __launch_bounds__(RO ? RT : BWG) void commit_kernel(BatchDesc d, cons
 }
 
 /* ------------------------------------------------ consistent: the digest row */
-/* The last workgroup of cpass_post_kernel<true> (1,024 threads): the pass's
- * listed verdict entries (flag 0 bad, 1 stale, 2 undecided) ordered by
- * (flag, commit index) in LDS, then written as the rank's digest row in the
- * layout of consistent.py's Consistent._pack, so the ranks all-gather it
- * straight from the device (one RCCL all-gather, one copy to the host)
- * instead of copying the block back, building the row in numpy and copying
- * it up again.  Until round 6 this was a kernel of its own (cpass_row_kernel,
- * 16 us and a launch gap on the N > 1 critical path).  (A fixed 4,096-key
- * bitonic sort with four guarded pairs per thread took 60 us; a rank by
- * counting 28 -- 16 waves x nl broadcast LDS reads.) */
+/* The last workgroup of cpass_post_kernel<true> (1,024 threads) writes the
+ * rank's digest row in the layout of consistent.py's Consistent._pack, so
+ * the ranks all-gather it straight from the device (one RCCL all-gather, one
+ * copy to the host) instead of copying the block back, building the row in
+ * numpy and copying it up again: the pass's listed verdict entries (flag 0
+ * bad, 1 stale, 2 undecided) as LDS keys (flag << 56 | commit index),
+ * ordered by (flag, commit index).  Until round 6 this was a kernel of its
+ * own (cpass_row_kernel, 16 us and a launch gap on the N > 1 critical path).
+ * Folded into the post kernel with a __threadfence in every wave before the
+ * ticket it took 71 us; the entries classified by workgroup 0 alone (no
+ * cross-workgroup data) 53 us -- and so did one release per workgroup: the
+ * 1,024-thread workgroups put all 1,024 listed entries on one CU; dealt in
+ * 64-entry chunks over the workgroups, 31.5 us, against 13.8 for the same
+ * kernel without the row (profiles/r06/config5/).  (A fixed 4,096-key bitonic sort with four
+ * guarded pairs per thread took 60 us; a rank by counting 28 -- 16 waves x
+ * nl broadcast LDS reads.) */
 constexpr uint32_t ROW_SORT = 4096;
 
-__device__ __forceinline__ void cpass_build_row(const CPassRowArgs &a, uint64_t nbad, uint64_t nstale, uint64_t *key,
-                                                uint32_t *cnt)
+__device__ __forceinline__ void cpass_write_row(const CPassRowArgs &a, uint64_t nbad, uint32_t nl, uint64_t *key,
+                                                const uint32_t *cnt, const int32_t *sst)
 {
     const uint32_t tid = threadIdx.x;
-    const uint32_t nl = (uint32_t)(nbad < a.list_cap ? nbad : a.list_cap);
-    const uint32_t *flags = reinterpret_cast<const uint32_t *>(a.blk + a.off_flags);
-    const uint64_t *bad = reinterpret_cast<const uint64_t *>(a.blk + a.off_bad);
-    if (tid < 3)
-        cnt[tid] = 0;
-    __syncthreads();
-    for (uint32_t k = tid; k < nl; k += blockDim.x) {
-        const uint32_t f = flags[k] > 2 ? 2u : flags[k];
-        key[k] = ((uint64_t)f << 56) | bad[k];
-        atomicAdd(&cnt[f], 1u);
-    }
-    __syncthreads();
     /* bitonic over the next power of two >= nl (padded with ~0).  Up to
      * 1,024 entries (config 5 lists 1,024 stale commits): one key per
      * thread in a register, strides below 64 exchanged inside the wave
@@ -3609,8 +3603,6 @@ __device__ __forceinline__ void cpass_build_row(const CPassRowArgs &a, uint64_t 
     int64_t *row = a.row;
     if (tid == 0) {
         row[0] = (int64_t)a.commits;
-        row[1] = (int64_t)(nbad - nstale); /* undecided ones included, as the host report */
-        row[2] = (int64_t)nstale;
         row[3] = lb;
         row[4] = ls;
         row[5] = a.nspans;
@@ -3637,18 +3629,17 @@ __device__ __forceinline__ void cpass_build_row(const CPassRowArgs &a, uint64_t 
         rs[2 * k + 1] = r;
     }
     const uint32_t *raw = reinterpret_cast<const uint32_t *>(a.blk + a.off_raw);
-    const int32_t *st = reinterpret_cast<const int32_t *>(a.blk + a.off_st);
     for (uint32_t k = tid; k < a.pmax; k += blockDim.x) {
         int64_t q[4] = {0, 0, 0, 0};
         if (k < a.nspans) {
             const int64_t fid = a.piece[3 * k], pc = a.piece[3 * k + 1], len = a.piece[3 * k + 2];
             q[0] = fid;
             q[2] = len;
-            if (st[k] < 0) {
+            if (sst[k] < 0) {
                 q[1] = pc;
                 q[3] = raw[k];
             } else {
-                q[1] = pc < 0 ? (st[k] == 1 ? a.checked[2] : a.checked[3]) : (st[k] == 1 ? a.checked[0] : a.checked[1]);
+                q[1] = pc < 0 ? (sst[k] == 1 ? a.checked[2] : a.checked[3]) : (sst[k] == 1 ? a.checked[0] : a.checked[1]);
             }
         }
         for (int j = 0; j < 4; ++j)
@@ -3751,12 +3742,36 @@ __device__ __forceinline__ uint32_t crc_word(const char *T, uint32_t r, uint64_t
  * (src/zeroskip-file.c:266-302).  Everything stays on the device: the host
  * copies one small block back.
  */
+/* One listed verdict entry k (commit bad[k]): 0 bad, 1 the finalise quirk
+ * (stale), 2 undecided (the host decides). */
+__device__ __forceinline__ uint32_t cpass_classify(const CPassArgs &a, const char *T, uint64_t i)
+{
+    /* every descriptor this entry may need, loaded together (one latency
+     * instead of a chain of them) */
+    const uint64_t ip = i ? i - 1 : 0;
+    const uint64_t li = a.len[i], at = a.off[i], pl = a.len[ip], po = a.off[ip];
+    const uint32_t fi = a.file[i], fp = a.file[ip];
+    if (!(li == 0 && i > 0 && fp == fi))
+        return 0;
+    /* the zero-length span's commit record at `at` */
+    if (!(at + 8 <= a.img_size && pl <= 65536 && po <= a.img_size && pl <= a.img_size - po))
+        return 2;
+    const uint64_t w0 = load_be64(reinterpret_cast<uintptr_t>(a.base) + at);
+    const uint32_t S = crc_run(T, 0xffffffffu, a.base + po, pl) ^ 0xffffffffu;
+    const uint32_t t = (uint32_t)(w0 >> 56);
+    if (t != REC_COMMIT && t != REC_FINAL)
+        return 2;
+    const uint32_t c = crc_word(T, S ^ 0xffffffffu, w0 & 0xFFFFFFFF00000000ull) ^ 0xffffffffu;
+    return c == (uint32_t)w0 ? 1u : 0u;
+}
+
 template <bool ROW>
 __global__ __launch_bounds__(ROW ? 1024 : 256) void cpass_post_kernel(CPassArgs a, const uint32_t *__restrict__ gtab)
 {
     __shared__ __attribute__((aligned(16))) char T[4096];
     __shared__ uint64_t key[ROW ? ROW_SORT : 1];
     __shared__ uint32_t cnt[3];
+    __shared__ int32_t sst[ROW ? CPASS_SPANS : 1];
     __shared__ uint32_t last, wg_stale, tot_stale;
     /* the next pass's block: nothing reads it during this pass (its last
      * copy back ran before this pass's kernels), so its counters (nbad,
@@ -3772,40 +3787,35 @@ __global__ __launch_bounds__(ROW ? 1024 : 256) void cpass_post_kernel(CPassArgs 
     }
     if (threadIdx.x == 0)
         wg_stale = 0;
+    if (ROW && threadIdx.x < 3)
+        cnt[threadIdx.x] = 0;
     load_gmul_table(T, gtab); /* GT_S4, compact: table j at 1024 j */
     __syncthreads();
     const uint64_t nbad = *a.nbad, nl = nbad < a.cap ? nbad : a.cap;
-    const uint64_t nt = (uint64_t)gridDim.x * blockDim.x;
     uint32_t mine = 0; /* stale commits this thread found */
-    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nl; k += nt) {
-        const uint64_t i = a.bad[k];
-        /* every descriptor this entry may need, loaded together (one latency
-         * instead of a chain of them) */
-        const uint64_t ip = i ? i - 1 : 0;
-        const uint64_t li = a.len[i], at = a.off[i], pl = a.len[ip], po = a.off[ip];
-        const uint32_t fi = a.file[i], fp = a.file[ip];
-        uint32_t flag = 0;
-        if (li == 0 && i > 0 && fp == fi) {
-            /* the zero-length span's commit record at `at` */
-            if (at + 8 <= a.img_size && pl <= 65536 && po <= a.img_size && pl <= a.img_size - po) {
-                const uint64_t w0 = load_be64(reinterpret_cast<uintptr_t>(a.base) + at);
-                const uint32_t S = crc_run(T, 0xffffffffu, a.base + po, pl) ^ 0xffffffffu;
-                const uint32_t t = (uint32_t)(w0 >> 56);
-                if (t == REC_COMMIT || t == REC_FINAL) {
-                    const uint32_t c = crc_word(T, S ^ 0xffffffffu, w0 & 0xFFFFFFFF00000000ull) ^ 0xffffffffu;
-                    flag = c == (uint32_t)w0 ? 1u : 0u;
-                } else {
-                    flag = 2;
-                }
+    auto list = [&](uint64_t k, uint64_t i, uint32_t flag) {
+        if (k < a.out_cap) { /* the listed part goes back to the host in one copy */
+            if constexpr (ROW) { /* read back by the last workgroup: agent-scope stores */
+                __hip_atomic_store(&a.flags[k], flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&a.bad_out[k], i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else {
-                flag = 2;
+                a.flags[k] = flag;
+                a.bad_out[k] = i;
             }
         }
-        if (k < a.out_cap) { /* the listed part goes back to the host in one copy */
-            a.flags[k] = flag;
-            a.bad_out[k] = i;
-        }
         mine += flag == 1;
+    };
+    /* 64-entry chunks dealt across the workgroups first, then their waves:
+     * config 5's 1,024 listed commits land on 16 CUs, not on the first
+     * workgroup's (each entry rehashes a span: one CU's memory rate bound
+     * the row pass at 53 us, profiles/r06/config5/) */
+    const uint64_t nwv = blockDim.x >> 6, lane = threadIdx.x & 63;
+    for (uint64_t c = blockIdx.x + (uint64_t)gridDim.x * (threadIdx.x >> 6); 64 * c < nl; c += gridDim.x * nwv) {
+        const uint64_t k = 64 * c + lane;
+        if (k < nl) {
+            const uint64_t i = a.bad[k];
+            list(k, i, cpass_classify(a, T, i));
+        }
     }
     if (mine)
         atomicAdd(&wg_stale, mine);
@@ -3838,24 +3848,32 @@ __global__ __launch_bounds__(ROW ? 1024 : 256) void cpass_post_kernel(CPassArgs 
                     st = (r ^ 0xffffffffu) == stored ? 1 : 0;
             }
         }
-        a.span_status[s] = st;
+        if constexpr (ROW)
+            __hip_atomic_store(&a.span_status[s], st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+            a.span_status[s] = st;
     }
     /* The last workgroup to finish publishes the stale count over ALL
      * classified entries -- the same set the device row counts, whatever
      * order the verdict's waves listed them in (round 5's host recount over
-     * the 4,096 listed flags was order-dependent on an incomplete pass) --
-     * and, for a row pass, builds the digest row.  Count and ticket are ONE
-     * 64-bit word (workgroups done << 32 | stale commits): each workgroup adds
-     * (1 << 32) + its stale count in one atomic, so the one that sees the
-     * last ticket also sees the whole sum -- no fence is needed for the count
-     * (a release fence per workgroup and the acquire are an L2 write-back and
-     * invalidate each, buffer_wbl2 / buffer_inv: config 5's post kernel took
-     * 23.2 us with them against 17.0 without, profiles/r06/config5/).  The row
-     * builder reads the other workgroups' listed entries, so a row pass
-     * still releases them (agent scope: the other XCDs' view) and the last
-     * workgroup acquires. */
+     * the 4,096 listed flags was order-dependent on an incomplete pass).
+     * Count and ticket are ONE 64-bit word (workgroups done << 32 | stale
+     * commits): each workgroup adds (1 << 32) + its stale count in one
+     * atomic, so the one that sees the last ticket also sees the whole sum
+     * -- no fence (a release fence per workgroup and the acquire are an L2
+     * write-back and invalidate each, buffer_wbl2 / buffer_inv: config 5's
+     * post kernel took 23.2 us with them against 17.0 without,
+     * profiles/r06/config5/).  A row pass's last workgroup also reads the
+     * listed entries the others classified: those are agent-scope atomic
+     * stores and loads (sc1: past the XCDs' non-coherent L2s, no write-back
+     * of them), ordered by the ticket as a release / acquire taken by one
+     * thread per workgroup after its barrier -- one L2 write-back per
+     * workgroup, not one per wave (every wave's __threadfence: 71 us).
+     * Every wave first waits for its own stores (a workgroup barrier does
+     * not: in the ISA no vmcnt wait precedes s_barrier), so they are in the
+     * L2 before thread 0's write-back is issued. */
     if constexpr (ROW)
-        __threadfence();
+        __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     if (threadIdx.x == 0) {
         const unsigned long long add = (1ull << 32) | wg_stale;
@@ -3868,16 +3886,30 @@ __global__ __launch_bounds__(ROW ? 1024 : 256) void cpass_post_kernel(CPassArgs 
     __syncthreads();
     if (!last)
         return;
-    if constexpr (ROW)
-        __threadfence();
     const uint64_t nstale = tot_stale;
     if (threadIdx.x == 0) {
         *a.nstale = nstale;
         if (a.host_nbad)
             a.host_nbad[1] = nstale;
     }
-    if constexpr (ROW)
-        cpass_build_row(a.row, nbad, nstale, key, cnt);
+    if constexpr (ROW) {
+        /* the listed entries as sort keys (flag << 56 | commit index) */
+        const uint32_t lc = (uint32_t)(nl < a.row.list_cap ? nl : a.row.list_cap);
+        for (uint32_t k = threadIdx.x; k < lc; k += blockDim.x) {
+            const uint32_t f = __hip_atomic_load(&a.flags[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t i = __hip_atomic_load(&a.bad_out[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            key[k] = ((uint64_t)(f > 2 ? 2u : f) << 56) | i;
+            atomicAdd(&cnt[f > 2 ? 2u : f], 1u);
+        }
+        if (threadIdx.x < a.nspans)
+            sst[threadIdx.x] = __hip_atomic_load(&a.span_status[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (threadIdx.x == 0) {
+            a.row.row[1] = (int64_t)(nbad - nstale); /* undecided ones included, as the host report */
+            a.row.row[2] = (int64_t)nstale;
+        }
+        __syncthreads();
+        cpass_write_row(a.row, nbad, lc, key, cnt, sst);
+    }
 }
 
 /* ------------------------------------------------------------ span fold */
