@@ -1221,8 +1221,30 @@ int zscrc_device_span(const void *d_buf, uint64_t len, uint32_t seed, uint32_t *
     return rc ? rc : rc2;
 }
 
-int zscrc_device_spans(const void *const *d_bufs, const uint64_t *lens, const uint32_t *seeds, uint32_t *d_out,
-                       size_t k, unsigned flags, void *stream)
+/* The multi-span launch's segment size and segment count (its partial
+ * registers) for spans of these lengths. */
+static uint64_t spans_seg(const DevCtx *c, uint64_t total)
+{
+    /* one segment size for every span (g_xdeal segments per wave in all,
+     * dealt per workgroup; or two, static), so a short span is as many
+     * segments as its length needs, not one wave's walk */
+    /* at most 4 segments per wave here: on config 5's shape (two 3 GiB
+     * regions + two pointer sections) 4 per wave 1.014 ms, static 1.021, 16
+     * per wave 1.028; a lone 3 GiB span wants 16 (0.502 against 0.523)
+     * (interleaved, profiles/r04/ab_spans_xdeal.jsonl) */
+    const uint32_t deal = std::min<uint32_t>(xdeal_for(g_opt), 4u);
+    const uint64_t target = (uint64_t)(deal > 2 ? deal : 2) * (uint64_t)c->ncu * 16;
+    uint64_t seg = ((total + target - 1) / target + 1023) & ~1023ull;
+    return seg < SEG_MIN ? SEG_MIN : seg;
+}
+
+/* part_own != NULL (zscrc_cpass, which owns it and orders its own passes):
+ * the segments' partial registers go there, not to the device's shared
+ * scratch, so the call needs no scratch ordering -- its event record put a
+ * ~6 us gap before the next launch on the stream (config 5's pass,
+ * profiles/r06/config5/rt5). */
+static int device_spans(const void *const *d_bufs, const uint64_t *lens, const uint32_t *seeds, uint32_t *d_out,
+                        size_t k, unsigned flags, void *stream, uint32_t *part_own, uint64_t part_words)
 {
     if (k == 0)
         return ZSCRC_OK;
@@ -1237,6 +1259,8 @@ int zscrc_device_spans(const void *const *d_bufs, const uint64_t *lens, const ui
             multi = false;
         total += lens[i];
     }
+    if (!multi && part_own)
+        return ZSCRC_EINVAL; /* the private form is the one-launch shape only */
     if (!multi) { /* short spans or many: one call each */
         for (size_t i = 0; i < k; ++i) {
             const int rc = zscrc_device_span(d_bufs[i], lens[i], seeds ? seeds[i] : 0u, d_out + i, nullptr, flags,
@@ -1253,18 +1277,8 @@ int zscrc_device_spans(const void *const *d_bufs, const uint64_t *lens, const ui
     std::lock_guard<std::recursive_mutex> lk(c->mu);
     hipStream_t s = static_cast<hipStream_t>(stream);
     const uint32_t xio = (flags & ZSCRC_RAW) ? 0u : 0xffffffffu;
-    /* one segment size for every span (g_xdeal segments per wave in all,
-     * dealt per workgroup; or two, static), so a short span is as many
-     * segments as its length needs, not one wave's walk */
-    /* at most 4 segments per wave here: on config 5's shape (two 3 GiB
-     * regions + two pointer sections) 4 per wave 1.014 ms, static 1.021, 16
-     * per wave 1.028; a lone 3 GiB span wants 16 (0.502 against 0.523)
-     * (interleaved, profiles/r04/ab_spans_xdeal.jsonl) */
     const uint32_t deal = std::min<uint32_t>(xdeal_for(g_opt), 4u);
-    const uint64_t target = (uint64_t)(deal > 2 ? deal : 2) * (uint64_t)c->ncu * 16;
-    uint64_t seg = ((total + target - 1) / target + 1023) & ~1023ull;
-    if (seg < SEG_MIN)
-        seg = SEG_MIN;
+    const uint64_t seg = spans_seg(c, total);
     zs::XMulti m;
     memset(&m, 0, sizeof m);
     zs::SpanFolds fs;
@@ -1281,11 +1295,14 @@ int zscrc_device_spans(const void *const *d_bufs, const uint64_t *lens, const ui
         w += W;
     }
     m.first[k] = w;
-    if ((rc = scratch_acquire(c, s)))
+    if (part_own && w > part_words)
+        return ZSCRC_EINVAL;
+    if (!part_own && (rc = scratch_acquire(c, s)))
         return rc;
-    rc = grow(&c->scratch, &c->scratch_bytes, w * 4);
+    if (!part_own)
+        rc = grow(&c->scratch, &c->scratch_bytes, w * 4);
     if (!rc) {
-        uint32_t *part = static_cast<uint32_t *>(c->scratch);
+        uint32_t *part = part_own ? part_own : static_cast<uint32_t *>(c->scratch);
         const uint32_t kseg = zs_gf2_xpow8n(seg);
         for (size_t i = 0; i < k; ++i) {
             zs::SpanFold &f = fs.f[i];
@@ -1318,8 +1335,26 @@ int zscrc_device_spans(const void *const *d_bufs, const uint64_t *lens, const ui
             g_stat[3] += total;
         }
     }
+    if (part_own)
+        return rc;
     const int rc2 = scratch_release(c, s);
     return rc ? rc : rc2;
+}
+
+int zscrc_device_spans(const void *const *d_bufs, const uint64_t *lens, const uint32_t *seeds, uint32_t *d_out,
+                       size_t k, unsigned flags, void *stream)
+{
+    return device_spans(d_bufs, lens, seeds, d_out, k, flags, stream, nullptr, 0);
+}
+
+/* For zscrc_cpass: the one-launch multi-span call into the caller's own
+ * buffer of segment registers (part_words of them). */
+extern "C" int zscrc_internal_spans_private(const void *const *d_bufs, const uint64_t *lens, uint32_t *d_out, size_t k,
+                                            unsigned flags, uint32_t *part, uint64_t part_words, void *stream)
+{
+    if (!part)
+        return ZSCRC_EINVAL;
+    return device_spans(d_bufs, lens, nullptr, d_out, k, flags, stream, part, part_words);
 }
 
 int zscrc_device_mismatch_rows(const uint32_t *d_status, const uint32_t *d_crc, const int64_t *d_span_end,

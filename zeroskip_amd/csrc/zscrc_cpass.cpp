@@ -26,6 +26,8 @@
 extern "C" {
 const uint32_t *zscrc_internal_gtab(void);
 int zs_launch_cpass_post(const zs::CPassArgs *a, const uint32_t *gtab, hipStream_t stream);
+int zscrc_internal_spans_private(const void *const *d_bufs, const uint64_t *lens, uint32_t *d_out, size_t k,
+                                 unsigned flags, uint32_t *part, uint64_t part_words, void *stream);
 int zscrc_internal_verdict_prezeroed(const void *d_image, uint64_t image_size, const uint64_t *d_span_off,
                                      const uint64_t *d_span_len, size_t n, uint64_t max_len, uint64_t *d_nbad,
                                      uint64_t *d_bad, size_t cap, void *stream);
@@ -73,6 +75,11 @@ struct zscrc_cpass {
     uint64_t cap = 0;
     int64_t *dspan_commit = nullptr;
     uint32_t *dspan_init = nullptr;
+    /* the multi-span launches' segment registers: the handle's own, so a
+     * pass needs no ordering event on the device's shared scratch (its
+     * record put ~6 us between the folds and the post kernel) */
+    uint32_t *dpart = nullptr;
+    uint64_t part_words = 0;
     /* one stream: the raw spans on a second stream beside the verdict batch
      * measured slower (config 5: 1.659 vs 1.542 ms per pass,
      * profiles/r03/cpass_streams.jsonl) */
@@ -109,6 +116,8 @@ void cpass_free(zscrc_cpass *p)
         (void)hipFree(p->dspan_commit);
     if (p->dpiece)
         (void)hipFree(p->dpiece);
+    if (p->dpart)
+        (void)hipFree(p->dpart);
     delete p;
 }
 
@@ -157,6 +166,13 @@ extern "C" int zscrc_cpass_create(zscrc_cpass **out, const zscrc_cpass_spec *spe
         e = hipMalloc(&p->dbad_full, 8 * p->cap);
     if (e == hipSuccess)
         e = hipMalloc(&p->dspan_commit, (8 + 4) * zs::CPASS_SPANS);
+    /* segment registers of the multi-span launches: any segment size is at
+     * least 1 KiB (SEG_MIN), so this bounds every launch shape the tuning
+     * can pick */
+    for (size_t k = 0; k < spec->nspans; ++k)
+        p->part_words += (p->span_len[k] + 1023) / 1024;
+    if (e == hipSuccess && p->part_words)
+        e = hipMalloc(&p->dpart, 4 * p->part_words);
     if (e != hipSuccess) {
         cpass_free(p);
         return ZSCRC_ENOMEM;
@@ -374,7 +390,9 @@ int cpass_enqueue(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, uint8_t **blk, 
             ++k;
         }
         if (k >= 2) {
-            rc = zscrc_device_spans(bufs, lens, nullptr, d_raw + i, k, ZSCRC_RAW, s);
+            rc = zscrc_internal_spans_private(bufs, lens, d_raw + i, k, ZSCRC_RAW, p->dpart, p->part_words, s);
+            if (rc == ZSCRC_EINVAL) /* a tuning without the one-launch shape: the shared path */
+                rc = zscrc_device_spans(bufs, lens, nullptr, d_raw + i, k, ZSCRC_RAW, s);
             i += k;
         } else {
             rc = zscrc_device_span(img + p->span_off[i], p->span_len[i], 0, d_raw + i, nullptr, ZSCRC_RAW, s);
