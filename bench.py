@@ -386,34 +386,23 @@ def run_config3(args, world, rank, dev, stream):
     g = torch.Generator(device=dev)
     g.manual_seed(0x9E3779B9 + rank)
     data = torch.randint(0, 256, (NCHUNK * CHUNK,), dtype=torch.uint8, device=dev, generator=g)
-    # two digest buffers: step k's all-gather (async, on the collective's own
-    # stream) runs beside step k+1's kernel; a buffer is reused only after
-    # the gather that read it is done, and every gather completes inside the
-    # timed region (drain)
+    # Every rank checksums its own 4 GiB of chunks: independent shards, so no
+    # collective inside the steps (round 5 all-gathered every step's digests
+    # over RCCL beside the next kernel -- an exchange the path does not have,
+    # whose RCCL kernels wait for CUs the persistent kernel holds); the last
+    # step's digests are gathered once, after the timed region, and checked
     outs = [torch.empty(NCHUNK, dtype=torch.int32, device=dev) for _ in range(2)]
-    gathered = [torch.empty(NCHUNK * world, dtype=torch.int32, device=dev) for _ in range(2)] if world > 1 else None
-    pend, nstep = [None, None], [0]
+    nstep = [0]
 
     def step(ev):
         i = nstep[0] % 2
         nstep[0] += 1
-        if pend[i] is not None:
-            pend[i].wait()
-            pend[i] = None
         if ev:
             ev[0].record(stream)
         check(lib().zscrc_device_fixed(data.data_ptr(), CHUNK, CHUNK, 0, outs[i].data_ptr(), NCHUNK,
                                        0, stream.cuda_stream), "zscrc_device_fixed")
         if ev:
             ev[1].record(stream)
-        if world > 1:
-            pend[i] = dist.all_gather_into_tensor(gathered[i], outs[i], async_op=True)
-
-    def drain():
-        for i in range(2):
-            if pend[i] is not None:
-                pend[i].wait()
-                pend[i] = None
 
     # The same-GPU read ceiling is measured first, right before the warmup:
     # config 3 runs at the package's 1400 W cap, and the power controller's
@@ -423,12 +412,15 @@ def run_config3(args, world, rank, dev, stream):
     # its loaded operating point as a sustained checksum job finds it.
     read_peak = read_ceiling(data, NCHUNK * CHUNK, stream)
     tm = Timer(world, dev, stream)
-    elapsed = tm.run(step, args.steps, args.warmup, drain=drain)
+    elapsed = tm.run(step, args.steps, args.warmup)
     kern_ms = float(np.mean(tm.kern_ms))
     out = outs[(nstep[0] - 1) % 2]   # the last timed step's digests
     if world > 1:
-        # every rank's digests of the last step, as gathered
-        assert torch.equal(gathered[(nstep[0] - 1) % 2][rank * NCHUNK:(rank + 1) * NCHUNK], out)
+        # every rank's digests of the last step, gathered once (untimed)
+        gathered = torch.empty(NCHUNK * world, dtype=torch.int32, device=dev)
+        dist.all_gather_into_tensor(gathered, out)
+        torch.cuda.synchronize()
+        assert torch.equal(gathered[rank * NCHUNK:(rank + 1) * NCHUNK], out)
     # after the timed region, reported beside it (never the value): the
     # kernel over 200 back-to-back calls, the sustained power-capped rate
     sus = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(200)]
@@ -456,8 +448,8 @@ def run_config3(args, world, rank, dev, stream):
     out_line = line(args, world, elapsed, NCHUNK * CHUNK * world * args.steps,
                     {"workload": "config3: 65536 x 64 KiB chunks per GPU (4 GiB), batched CRC-32C",
                      "records_per_gpu": NCHUNK, "record_bytes": CHUNK,
-                     "parallelism": f"shard{world}" + (("+rccl_allgather_digests" if os.environ.get("BENCH_DIST", "nccl") == "nccl"
-                                                        else "+gloo_allgather_digests") if world > 1 else "")}, r,
+                     "parallelism": f"shard{world}" + ("; digests gathered once after the timed steps "
+                                                       f"({os.environ.get('BENCH_DIST', 'nccl')})" if world > 1 else "")}, r,
                     parity={"sampled_chunks": int(idx.size), "mismatches": n_bad, "checker": "oracle crc32c_hw"},
                     sustained=sustained)
     if rank == 0 and world == 1 and not args.no_cpu:

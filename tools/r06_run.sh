@@ -30,6 +30,9 @@ for step in "$@"; do
     traffic2|traffic3|traffic4|traffic5)   # FETCH_SIZE and WRITE_SIZE passes, 5 passes each
               c=config${step#traffic}
               bash tools/pmc_traffic.sh $c 5 ;;
+    rehearse3)
+              BENCH_SHARE_GPU=1 BENCH_DIST=gloo timeout -k 10 600 python bench.py --gpus 2 --workload config3 \
+                --no-cpu > $O/rehearse3_n2.json 2> $O/rehearse3_n2.err ;;
     rehearse5)
               BENCH_SHARE_GPU=1 BENCH_DIST=gloo timeout -k 10 900 python bench.py --gpus 2 --workload config5 \
                 --no-cpu > $O/rehearse5_n2.json 2> $O/rehearse5_n2.err ;;
