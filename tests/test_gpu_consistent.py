@@ -406,7 +406,9 @@ def test_device_row_matches_host_digest(gpu, case):
         assert row[1] >= 1 and row[2] == 3
 
 
-@pytest.mark.parametrize("seed", range(int(os.environ.get("ZSCRC_SOAK_CONSISTENT", "8"))))
+@pytest.mark.parametrize("seed", range(int(os.environ.get("ZSCRC_SOAK_BASE", "0")),
+                                      int(os.environ.get("ZSCRC_SOAK_BASE", "0")) +
+                                      int(os.environ.get("ZSCRC_SOAK_CONSISTENT", "8"))))
 def test_random_corruptions_match_oracle(gpu, seed):
     """zsdb_consistent on the GPU backend and on the oracle backend over the
     same DB with 1-4 random bytes flipped anywhere in its files (headers,

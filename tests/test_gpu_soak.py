@@ -64,13 +64,16 @@ def _u32(t):
     return t.cpu().numpy().view(np.uint32)
 
 
-# env ZSCRC_SOAK_SEEDS: batches per block (default 25; longer soaks on request)
+# env ZSCRC_SOAK_SEEDS: batches per block (default 25; longer soaks on request);
+# ZSCRC_SOAK_BASE: first seed of every randomised test here and in
+# test_gpu_consistent.py (default 0; another base explores new cases)
 SEEDS = int(os.environ.get("ZSCRC_SOAK_SEEDS", "25"))
+BASE = int(os.environ.get("ZSCRC_SOAK_BASE", "0"))
 
 
 @pytest.mark.parametrize("block", range(4))
 def test_random_batches(gpu, block):
-    for seed in range(SEEDS * block, SEEDS * block + SEEDS):
+    for seed in range(BASE + SEEDS * block, BASE + SEEDS * block + SEEDS):
         rng, data, offs, lens, seeds = _case(seed)
         ref = oracle.batch(data, offs.astype(np.uint64), lens.astype(np.uint64), seeds, impl="hw", threads=8)
         d, o, l = _dev(data, gpu), _dev(offs, gpu), _dev(lens, gpu)
@@ -271,7 +274,7 @@ def _commit_case(seed):
     return host, clean, offs, lens, has_rec, hit, bound, sd
 
 
-@pytest.mark.parametrize("seed", range(int(os.environ.get("ZSCRC_SOAK_COMMITS", "12"))))
+@pytest.mark.parametrize("seed", range(BASE, BASE + int(os.environ.get("ZSCRC_SOAK_COMMITS", "12"))))
 def test_random_commit_batches(gpu, seed):
     """Random commit images -- lengths short / zsbench-like / with long spans,
     back to back or with gaps, 3 % without a commit record, FINAL records,

@@ -13,6 +13,10 @@ for step in "$@"; do
   case "$step" in
     gputests) timeout -k 10 900 $T -m gpu tests > $O/gputests.log 2>&1 ;;
     smoke)    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 ;;
+    soaknew)  # fresh seeds: ZSCRC_SOAK_BASE=100000
+              ZSCRC_SOAK_BASE=100000 ZSCRC_SOAK_SEEDS=250 ZSCRC_SOAK_COMMITS=240 ZSCRC_SOAK_CONSISTENT=60 \
+                timeout -k 10 900 $T tests/test_gpu_soak.py tests/test_gpu_consistent.py -k "random" \
+                > $O/soaknew.log 2>&1 ;;
     cpass)    timeout -k 10 600 $T tests/test_gpu_consistent.py > $O/cpass_tests.log 2>&1 ;;
     soaklong) ZSCRC_SOAK_SEEDS=250 ZSCRC_SOAK_COMMITS=240 ZSCRC_SOAK_CONSISTENT=60 timeout -k 10 900 \
                 $T tests/test_gpu_soak.py tests/test_gpu_consistent.py -k "random" > $O/soaklong.log 2>&1 ;;
