@@ -25,7 +25,7 @@
 
 extern "C" {
 const uint32_t *zscrc_internal_gtab(void);
-int zs_launch_cpass_post(const zs::CPassArgs *a, const uint32_t *gtab, hipStream_t stream);
+int zs_launch_cpass_post(const zs::CPassArgs *a, const uint32_t *gtab, hipStream_t stream, hipEvent_t done);
 int zscrc_internal_spans_private(const void *const *d_bufs, const uint64_t *lens, uint32_t *d_out, size_t k,
                                  unsigned flags, uint32_t *part, uint64_t part_words, void *stream);
 int zscrc_internal_verdict_prezeroed(const void *d_image, uint64_t image_size, const uint64_t *d_span_off,
@@ -312,7 +312,7 @@ extern "C" int zscrc_cpass_set_row(zscrc_cpass *p, const zscrc_cpass_row_spec *r
 
 namespace {
 int cpass_enqueue(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, uint8_t **blk, uint8_t *host,
-                  int64_t *d_row = nullptr);
+                  int64_t *d_row = nullptr, hipEvent_t done = nullptr);
 }
 
 extern "C" int zscrc_cpass_submit_row(zscrc_cpass *p, void *stream, void *start_event, void *end_event,
@@ -325,11 +325,10 @@ extern "C" int zscrc_cpass_submit_row(zscrc_cpass *p, void *stream, void *start_
         return ZSCRC_EHIP;
     hipStream_t s = static_cast<hipStream_t>(stream);
     uint8_t *blk = nullptr;
-    /* the post kernel's last workgroup builds the row: no launch of its own */
-    int rc = cpass_enqueue(p, s, static_cast<hipEvent_t>(start_event), &blk, nullptr, d_row);
-    if (!rc && end_event && hipEventRecord(static_cast<hipEvent_t>(end_event), s) != hipSuccess)
-        rc = ZSCRC_EHIP;
-    return rc;
+    /* the post kernel's last workgroup builds the row: no launch of its own;
+     * the end event completes with the post kernel's dispatch */
+    return cpass_enqueue(p, s, static_cast<hipEvent_t>(start_event), &blk, nullptr, d_row,
+                         static_cast<hipEvent_t>(end_event));
 }
 
 namespace {
@@ -342,16 +341,12 @@ int cpass_submit(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1, 
     /* the post kernel writes the listed part of the verdict, the count and
      * the span registers straight into the pinned host slot: no copy back
      * (a blit launch and ~12 us of gap per pass) */
-    int rc = cpass_enqueue(p, s, ev0, &blk, p->hblk + slot * BLK);
-    /* the end event right behind the post kernel: the device's part of the
-     * pass, without the host's wait and the list sorting */
-    if (!rc && ev1 && hipEventRecord(ev1, s) != hipSuccess)
-        rc = ZSCRC_EHIP;
-    /* the caller's end event doubles as the slot's completion (one event
-     * record less between passes); otherwise the slot's own */
+    /* the end event completes with the post kernel's own dispatch: the
+     * device's part of the pass, without the host's wait and the list
+     * sorting.  The caller's end event doubles as the slot's completion;
+     * otherwise the slot's own */
     p->wait[slot] = ev1 ? ev1 : p->done[slot];
-    if (!rc && !ev1 && hipEventRecord(p->done[slot], s) != hipSuccess)
-        rc = ZSCRC_EHIP;
+    int rc = cpass_enqueue(p, s, ev0, &blk, p->hblk + slot * BLK, nullptr, p->wait[slot]);
     if (!rc)
         p->pending[slot] = true;
     return rc;
@@ -361,7 +356,8 @@ int cpass_submit(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1, 
  * of the two device blocks (*blk).  Passes must follow one another in
  * stream order (one stream, or the caller's own ordering): the blocks'
  * counters are zeroed by the previous pass. */
-int cpass_enqueue(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, uint8_t **blk, uint8_t *host, int64_t *d_row)
+int cpass_enqueue(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, uint8_t **blk, uint8_t *host, int64_t *d_row,
+                  hipEvent_t done)
 {
     if (p->have_last && s != p->last_stream &&
         (hipEventRecord(p->order, p->last_stream) != hipSuccess || hipStreamWaitEvent(s, p->order, 0) != hipSuccess))
@@ -431,7 +427,7 @@ int cpass_enqueue(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, uint8_t **blk, 
             a.row.blk = b;
             a.row.row = d_row;
         }
-        if (zs_launch_cpass_post(&a, zscrc_internal_gtab(), s))
+        if (zs_launch_cpass_post(&a, zscrc_internal_gtab(), s, done))
             rc = ZSCRC_EHIP;
     }
     if (rc) { /* a pass cut short did not zero the next block: start both over */

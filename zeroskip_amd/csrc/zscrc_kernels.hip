@@ -32,6 +32,7 @@
  *   [132K, 156K) Z_k, k = 0..5: shift by 64<<k bytes (4 x 256 dwords each)
  */
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -5018,16 +5019,20 @@ extern "C" int zs_launch_commit_scatter(uint8_t *base, const uint64_t *off, cons
 
 /* a->row.row != NULL: the pass's digest row too, built by the last
  * workgroup (1,024 threads); otherwise 256-thread workgroups */
-extern "C" int zs_launch_cpass_post(const zs::CPassArgs *a, const uint32_t *gtab, hipStream_t stream)
+/* done != NULL: the event completes with the post kernel's own dispatch
+ * (hipExtLaunchKernel's stop event) -- a separate hipEventRecord after it is
+ * a marker packet that held the next pass's first launch ~6 us
+ * (profiles/r06/config5/) */
+extern "C" int zs_launch_cpass_post(const zs::CPassArgs *a, const uint32_t *gtab, hipStream_t stream, hipEvent_t done)
 {
     if (!a->ticket || !a->nstale)
         return -1;
     if (a->row.row) {
         if (a->row.list_cap > zs::ROW_SORT || a->row.list_cap > a->out_cap)
             return -1;
-        hipLaunchKernelGGL(zs::cpass_post_kernel<true>, dim3(64), dim3(1024), 0, stream, *a, gtab);
+        hipExtLaunchKernelGGL(zs::cpass_post_kernel<true>, dim3(64), dim3(1024), 0, stream, nullptr, done, 0, *a, gtab);
     } else {
-        hipLaunchKernelGGL(zs::cpass_post_kernel<false>, dim3(64), dim3(256), 0, stream, *a, gtab);
+        hipExtLaunchKernelGGL(zs::cpass_post_kernel<false>, dim3(64), dim3(256), 0, stream, nullptr, done, 0, *a, gtab);
     }
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
