@@ -121,6 +121,11 @@ struct BatchDesc {
     int round_mode;
     uint32_t *round_list;
     uint32_t *round_count;
+    /* commit_kernel verdict without a zeroing launch: bad_count points at a
+     * library counter pair that is 0 at rest (count, then workgroups done);
+     * the last workgroup out moves the count to *bad_publish (the caller's)
+     * and leaves both at 0 */
+    unsigned long long *bad_publish;
 };
 
 /* A fixed-stride batch for xteam_kernel (what it reads of a BatchDesc: few

@@ -3507,6 +3507,24 @@ __global__ __launch_bounds__(RO ? RT : BWG) void commit_kernel(BatchDesc d, cons
         r_cur = r_nxt;
         r_nxt = round_at(rs, t + 2, f2);
     }
+    if (d.bad_publish) {
+        /* Verdict without a zeroing launch: every increment of this
+         * workgroup's waves returned (its index was used) before they left
+         * the loop, so the workgroup that takes the last ticket sees the
+         * whole count -- it publishes it and leaves the pair at 0 for the
+         * next call on this stream.  Relaxed returning atomics, no fence (a
+         * fence per wave is an L2 write-back each). */
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long *done = d.bad_count + 1;
+            const uint64_t nb = (count + TPB - 1) / TPB;
+            const unsigned long long active = nb < gridDim.x ? nb : gridDim.x;
+            if (atomicAdd(done, 1ull) == active - 1) {
+                *d.bad_publish = atomicExch(d.bad_count, 0ull);
+                atomicExch(done, 0ull);
+            }
+        }
+    }
     if (RO && d.round_mode == 1) { /* the workgroup's gathered leftover rounds to the list */
         __syncthreads();
         __shared__ uint32_t lbase;
