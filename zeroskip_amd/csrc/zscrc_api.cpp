@@ -639,7 +639,10 @@ int launch_commit_two_pass(DevCtx *c, zs::BatchDesc d, hipStream_t s)
  * up to 64 streams get one.  Config 4's bench batch: the fill launch and its
  * gap (~5 us of a 0.52 ms call) gone.  Round 5's form of this shared one
  * pair between streams and ordered it with the scratch event -- whose
- * marker packet cost more than the fill (profiles/r05/verdict_publish/). */
+ * marker packet cost more than the fill (profiles/r05/verdict_publish/).
+ * A pair is keyed by the stream handle: a stream destroyed while one of its
+ * verdicts still runs, and a new stream given the same handle at once, would
+ * share it -- ROCm's hipStreamDestroy drains the stream first. */
 unsigned long long *verdict_slot(DevCtx *c, hipStream_t s)
 {
     const char *e = getenv("ZSCRC_VERDICT_MEMSET"); /* A/B: the fill launch */
