@@ -261,3 +261,44 @@ def test_crc_array_fenced(case, opt):
         else:
             assert (sw.cpu().numpy() == CANARY).all()
         assert np.array_equal(m["img"].cpu().numpy(), m["host"])
+
+
+def test_verdicts_on_many_streams(case):
+    """The verdict's count comes from a counter pair per stream (four in
+    turn) that commit_kernel's last workgroup publishes and zeroes -- no
+    fill launch before it.  Verdicts enqueued back to back on three streams
+    at once, six per stream, each into its own count and list, none waited
+    for until all are queued: every count and list is the oracle's, and the
+    pairs are at rest for the next calls (the default stream after)."""
+    m = case
+    n = m["n"]
+    want = set(np.nonzero(m["st"] != 1)[0].tolist())
+    cap = max(4096, len(want))
+    streams = [torch.cuda.Stream(m["dev"]) for _ in range(3)]
+    outs = [(torch.full((1,), -1, dtype=torch.int64, device=m["dev"]),
+             torch.empty(cap, dtype=torch.int64, device=m["dev"])) for _ in range(6 * len(streams))]
+    torch.cuda.synchronize()
+    with torch.cuda.device(m["dev"]):
+        for rep in range(6):
+            for j, s in enumerate(streams):
+                nbad, bad = outs[rep * len(streams) + j]
+                check(lib().zscrc_device_verify_commits_verdict(
+                    m["img"].data_ptr(), m["size"], m["d_off"].data_ptr(), m["d_len"].data_ptr(),
+                    m["seed"].data_ptr(), n, MAXLEN, nbad.data_ptr(), bad.data_ptr(), cap, s.cuda_stream),
+                    "verify_commits_verdict")
+        torch.cuda.synchronize()
+        for nbad, bad in outs:
+            k = int(nbad.item())
+            assert k == len(want) and set(bad[:k].cpu().tolist()) == want
+        nbad = torch.full((1,), -1, dtype=torch.int64, device=m["dev"])
+        bad = torch.empty(cap, dtype=torch.int64, device=m["dev"])
+        torch.cuda.synchronize()
+        for s in streams + [torch.cuda.current_stream(m["dev"])]:
+            nbad.fill_(-1)
+            torch.cuda.synchronize()
+            check(lib().zscrc_device_verify_commits_verdict(
+                m["img"].data_ptr(), m["size"], m["d_off"].data_ptr(), m["d_len"].data_ptr(),
+                m["seed"].data_ptr(), n, MAXLEN, nbad.data_ptr(), bad.data_ptr(), cap, s.cuda_stream),
+                "verify_commits_verdict")
+            torch.cuda.synchronize()
+            assert int(nbad.item()) == len(want)

@@ -147,12 +147,13 @@ struct DevCtx {
     hipEvent_t last = nullptr; /* end of the last scratch user's work ... */
     hipStream_t last_stream = nullptr; /* ... enqueued on this stream */
     bool last_valid = false;
-    /* verdict counters published by commit_kernel's last workgroup: one
-     * (count, workgroups done) pair per stream that used one, 0 at rest --
+    /* verdict counters published by commit_kernel's last workgroup: four
+     * (count, workgroups done) pairs per stream that used one, 0 at rest --
      * calls on one stream are ordered, so a stream's own pair needs no
      * event (verdict_slot) */
     unsigned long long *vctr = nullptr;
     hipStream_t vctr_stream[64] = {};
+    uint32_t vctr_turn[64] = {};
     int vctr_n = 0;
 };
 DevCtx g_ctx[MAX_DEV];
@@ -640,9 +641,10 @@ int launch_commit_two_pass(DevCtx *c, zs::BatchDesc d, hipStream_t s)
  * gap (~5 us of a 0.52 ms call) gone.  Round 5's form of this shared one
  * pair between streams and ordered it with the scratch event -- whose
  * marker packet cost more than the fill (profiles/r05/verdict_publish/).
- * A pair is keyed by the stream handle: a stream destroyed while one of its
- * verdicts still runs, and a new stream given the same handle at once, would
- * share it -- ROCm's hipStreamDestroy drains the stream first. */
+ * Pairs are keyed by the stream handle, four per stream used in turn: a
+ * stream destroyed while one of its verdicts still runs (hipStreamDestroy
+ * need not drain it) and a new stream given the same handle would share
+ * a pair only after four of the new stream's calls ran in that time. */
 unsigned long long *verdict_slot(DevCtx *c, hipStream_t s)
 {
     const char *e = getenv("ZSCRC_VERDICT_MEMSET"); /* A/B: the fill launch */
@@ -651,21 +653,24 @@ unsigned long long *verdict_slot(DevCtx *c, hipStream_t s)
     std::lock_guard<std::recursive_mutex> lk(c->mu);
     if (!c->vctr) {
         void *p = nullptr;
-        if (hipMalloc(&p, 64 * 128) != hipSuccess)
+        if (hipMalloc(&p, 64 * 4 * 128) != hipSuccess)
             return nullptr;
-        if (hipMemset(p, 0, 64 * 128) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        if (hipMemset(p, 0, 64 * 4 * 128) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
             (void)hipFree(p);
             return nullptr;
         }
         c->vctr = static_cast<unsigned long long *>(p);
     }
-    for (int k = 0; k < c->vctr_n; ++k)
-        if (c->vctr_stream[k] == s)
-            return c->vctr + 16 * k;
-    if (c->vctr_n == 64)
-        return nullptr;
-    c->vctr_stream[c->vctr_n] = s;
-    return c->vctr + 16 * c->vctr_n++;
+    int k = 0;
+    while (k < c->vctr_n && c->vctr_stream[k] != s)
+        ++k;
+    if (k == c->vctr_n) {
+        if (c->vctr_n == 64)
+            return nullptr;
+        c->vctr_stream[c->vctr_n++] = s;
+    }
+    const uint32_t turn = c->vctr_turn[k]++ & 3;
+    return c->vctr + 16 * (4 * k + turn);
 }
 
 /* max_len: a bound on the lengths -- at most g1_max, one kernel straight
