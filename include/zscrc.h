@@ -314,9 +314,10 @@ int zscrc_device_verify_commits_bounded(const void *d_image, uint64_t image_size
  * of commits whose status would not be 1 (mismatch, or no commit record in
  * the image), and d_bad (device, cap entries) receives the indices of the
  * first cap of them found, in no particular order.  A clean batch writes
- * nothing but the count.  *d_nbad is written once, in stream order, when the
- * batch is done (no zeroing launch before it: the library keeps a small
- * counter per stream that its kernel publishes and zeroes). */
+ * nothing but the count.  *d_nbad holds the count once the batch is done
+ * (in stream order); until then it may hold anything (a bounded batch's
+ * kernel counts into a small library counter of the stream's and writes
+ * *d_nbad at its end: no zeroing launch before it). */
 int zscrc_device_verify_commits_verdict(const void *d_image, uint64_t image_size, const uint64_t *d_span_off,
                                         const uint64_t *d_span_len, const uint32_t *d_seed, size_t n,
                                         uint64_t max_len, uint64_t *d_nbad, uint64_t *d_bad, size_t cap,
