@@ -603,3 +603,64 @@ def test_cpass_stale_rehash_ragged_spans(gpu):
                 assert list(res.bad[:res.n_listed_bad]) == bad
         finally:
             lib().zscrc_cpass_destroy(h)
+
+
+def _corrupt_db(seed):
+    """test_random_corruptions_match_oracle's DB for `seed`."""
+    rng = np.random.default_rng(300 + seed)
+    db = small_db(long_region=seed % 2 == 0, seed=100 + seed)
+    files = sorted(k for k in db if k != ".zsdb")
+    for _ in range(int(rng.integers(1, 5))):
+        f = files[int(rng.integers(0, len(files)))]
+        img = bytearray(db[f])
+        img[int(rng.integers(0, len(img)))] ^= 1 << int(rng.integers(0, 8))
+        db[f] = bytes(img)
+    return db
+
+
+def _random_rank_worker(rank, world, port, seeds, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        out = []
+        for seed in seeds:
+            rep = cs.Consistent(cs.open_db(_corrupt_db(seed)), rank, world).prepare().run()
+            out.append((seed, rep.ok, rep.commits, rep.bad_commits, rep.stale_empty_commits,
+                        sorted(map(tuple, rep.header_errors)), rep.issues))
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ranks_random_corruptions_match_one_rank(gpu, world):
+    """The N-rank path -- shares cut by byte weight, each rank's pass with its
+    digest row built by the post kernel's last workgroup, the rows exchanged
+    (gloo here: RCCL refuses two ranks on one device), split regions folded
+    from the ranks' raw registers -- over the randomly corrupted DBs of
+    test_random_corruptions_match_oracle: every rank's report equals the
+    one-rank report, field for field."""
+    import torch.multiprocessing as mp
+    seeds = list(range(int(os.environ.get("ZSCRC_SOAK_BASE", "0")),
+                       int(os.environ.get("ZSCRC_SOAK_BASE", "0")) + 6))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_random_rank_worker, args=(r, world, port, seeds, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for seed_i, seed in enumerate(seeds):
+        one = gpu_report(_corrupt_db(seed))
+        want = (seed, one.ok, one.commits, one.bad_commits, one.stale_empty_commits,
+                sorted(map(tuple, one.header_errors)), one.issues)
+        for rank, out in res:
+            assert out[seed_i] == want, (world, rank, seed, out[seed_i], want)
