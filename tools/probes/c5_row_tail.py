@@ -2,7 +2,7 @@
 measured on one GPU: the device pass with its digest row vs with the block
 copy back (event-timed, 20 passes each, medians), the copy of N rows to the
 host, and the host's unpack + merge of N rows.  Run under rocprofv3
---kernel-trace for cpass_row_kernel's own duration.
+--kernel-trace for the post kernel's duration with and without the row (round 5: cpass_row_kernel, a kernel of its own).
 usage: python tools/probes/c5_row_tail.py [N=8]"""
 import json
 import os
