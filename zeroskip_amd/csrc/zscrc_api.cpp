@@ -1302,7 +1302,8 @@ static uint64_t spans_seg(const DevCtx *c, uint64_t total)
  * ~6 us gap before the next launch on the stream (config 5's pass,
  * profiles/r06/config5/rt5). */
 static int device_spans(const void *const *d_bufs, const uint64_t *lens, const uint32_t *seeds, uint32_t *d_out,
-                        size_t k, unsigned flags, void *stream, uint32_t *part_own, uint64_t part_words)
+                        size_t k, unsigned flags, void *stream, uint32_t *part_own, uint64_t part_words,
+                        zs::SpanFolds *defer_folds = nullptr)
 {
     if (k == 0)
         return ZSCRC_OK;
@@ -1385,7 +1386,9 @@ static int device_spans(const void *const *d_bufs, const uint64_t *lens, const u
         x.stride = seg;
         x.fixed_len = seg;
         x.last_len = seg;
-        if (zs_launch_spans(&x, &m, &fs, c->gtab, c->ncu, deal != 0, s)) {
+        if (defer_folds) /* the caller's kernel folds them (zscrc_cpass's post kernel) */
+            *defer_folds = fs;
+        if (zs_launch_spans(&x, &m, defer_folds ? nullptr : &fs, c->gtab, c->ncu, deal != 0, s)) {
             set_err("multi-span launch", hipGetLastError());
             rc = ZSCRC_EHIP;
         } else {
@@ -1408,11 +1411,12 @@ int zscrc_device_spans(const void *const *d_bufs, const uint64_t *lens, const ui
 /* For zscrc_cpass: the one-launch multi-span call into the caller's own
  * buffer of segment registers (part_words of them). */
 extern "C" int zscrc_internal_spans_private(const void *const *d_bufs, const uint64_t *lens, uint32_t *d_out, size_t k,
-                                            unsigned flags, uint32_t *part, uint64_t part_words, void *stream)
+                                            unsigned flags, uint32_t *part, uint64_t part_words, void *stream,
+                                            zs::SpanFolds *defer_folds)
 {
     if (!part)
         return ZSCRC_EINVAL;
-    return device_spans(d_bufs, lens, nullptr, d_out, k, flags, stream, part, part_words);
+    return device_spans(d_bufs, lens, nullptr, d_out, k, flags, stream, part, part_words, defer_folds);
 }
 
 int zscrc_device_mismatch_rows(const uint32_t *d_status, const uint32_t *d_crc, const int64_t *d_span_end,

@@ -25,9 +25,11 @@
 
 extern "C" {
 const uint32_t *zscrc_internal_gtab(void);
-int zs_launch_cpass_post(const zs::CPassArgs *a, const uint32_t *gtab, hipStream_t stream, hipEvent_t done);
+int zs_launch_cpass_post(const zs::CPassArgs *a, const zs::SpanFolds *fs, uint32_t nfold, const uint32_t *gtab,
+                         hipStream_t stream, hipEvent_t done);
 int zscrc_internal_spans_private(const void *const *d_bufs, const uint64_t *lens, uint32_t *d_out, size_t k,
-                                 unsigned flags, uint32_t *part, uint64_t part_words, void *stream);
+                                 unsigned flags, uint32_t *part, uint64_t part_words, void *stream,
+                                 zs::SpanFolds *defer_folds);
 int zscrc_internal_verdict_prezeroed(const void *d_image, uint64_t image_size, const uint64_t *d_span_off,
                                      const uint64_t *d_span_len, size_t n, uint64_t max_len, uint64_t *d_nbad,
                                      uint64_t *d_bad, size_t cap, void *stream);
@@ -374,8 +376,16 @@ int cpass_enqueue(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, uint8_t **blk, 
     uint32_t *d_raw = reinterpret_cast<uint32_t *>(b + OFF_RAW);
     int rc = zscrc_internal_verdict_prezeroed(sp.d_image, sp.image_size, sp.d_off, sp.d_len, sp.n, sp.max_len,
                                               d_nbad, p->dbad_full, p->cap, s);
-    /* raw spans: up to 8 of >= 16 KiB per launch pair, else one by one */
+    /* raw spans: up to 8 of >= 16 KiB per launch pair, else one by one.
+     * When they all make one multi-span launch (config 5: two records
+     * regions, two pointer sections) and no row is built, its folds run in
+     * the post kernel (nfold): a launch fewer per pass. */
     const uint8_t *img = static_cast<const uint8_t *>(sp.d_image);
+    zs::SpanFolds folds;
+    uint32_t nfold = 0;
+    bool defer = !d_row && sp.nspans >= 2 && sp.nspans <= (size_t)zs::SPANS_MAX;
+    for (size_t i = 0; defer && i < sp.nspans; ++i)
+        defer = p->span_len[i] >= (16u << 10);
     for (size_t i = 0; !rc && i < sp.nspans;) {
         const void *bufs[8];
         uint64_t lens[8];
@@ -386,9 +396,12 @@ int cpass_enqueue(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, uint8_t **blk, 
             ++k;
         }
         if (k >= 2) {
-            rc = zscrc_internal_spans_private(bufs, lens, d_raw + i, k, ZSCRC_RAW, p->dpart, p->part_words, s);
+            zs::SpanFolds *df = defer && k == sp.nspans ? &folds : nullptr;
+            rc = zscrc_internal_spans_private(bufs, lens, d_raw + i, k, ZSCRC_RAW, p->dpart, p->part_words, s, df);
             if (rc == ZSCRC_EINVAL) /* a tuning without the one-launch shape: the shared path */
                 rc = zscrc_device_spans(bufs, lens, nullptr, d_raw + i, k, ZSCRC_RAW, s);
+            else if (!rc && df)
+                nfold = (uint32_t)k;
             i += k;
         } else {
             rc = zscrc_device_span(img + p->span_off[i], p->span_len[i], 0, d_raw + i, nullptr, ZSCRC_RAW, s);
@@ -427,7 +440,7 @@ int cpass_enqueue(zscrc_cpass *p, hipStream_t s, hipEvent_t ev0, uint8_t **blk, 
             a.row.blk = b;
             a.row.row = d_row;
         }
-        if (zs_launch_cpass_post(&a, zscrc_internal_gtab(), s, done))
+        if (zs_launch_cpass_post(&a, &folds, nfold, zscrc_internal_gtab(), s, done))
             rc = ZSCRC_EHIP;
     }
     if (rc) { /* a pass cut short did not zero the next block: start both over */

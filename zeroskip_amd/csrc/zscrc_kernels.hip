@@ -3547,6 +3547,98 @@ __global__ __launch_bounds__(RO ? RT : BWG) void commit_kernel(BatchDesc d, cons
     }
 }
 
+/* ------------------------------------------------------------ span fold */
+/* K^m from the table K^(2^b). */
+__device__ __forceinline__ uint32_t kpow(const char *T, const uint32_t *kp2, uint32_t m)
+{
+    uint32_t r = 0x80000000u;
+    for (int b = 0; m; ++b, m >>= 1)
+        if (m & 1)
+            r = gmul_t(T, r, kp2[b]);
+    return r;
+}
+
+/*
+ * Fold W raw segment registers P_0..P_{W-1} of a span whose segments are all
+ * SEG bytes long except the last:
+ *   H = Horner_{i<W-1}(P_i, K = x^(8 SEG));  reg = H * x^(8 lastlen) ^ P_{W-1}
+ *   reg ^= R0 * x^(8 L)                       (initial register)
+ * Spread over blocks (one part per thread up to 256 x 256 parts): a thread
+ * Horner-folds its run of parts and shifts it by K^(parts after the run)
+ * (square-and-multiply: ~14 gmul chains, latency-bound, so one wave per
+ * SIMD); each block XOR-reduces, multiplies by
+ * x^(8 lastlen) and XORs into *out, which the host preset to the constant
+ * R0 * x^(8 L) ^ xor_out (hipMemsetD32Async); block 0 adds P_{W-1}.
+ */
+constexpr int FWG = 256; /* span fold: one wave per SIMD, the gmul chains are latency-bound */
+
+/* One span's fold by block bid of nblk (tables already in LDS). */
+__device__ __forceinline__ void fold_blocks(const SpanFold &f, const char *T, const uint32_t *kp2, uint32_t *red,
+                                            uint32_t bid, uint32_t nblk)
+{
+    const uint32_t W = f.w;
+    const uint32_t nh = W - 1; /* Horner terms */
+    const uint32_t nt = nblk * (uint32_t)FWG;
+    const uint32_t per = (nh + nt - 1) / nt;
+    const uint32_t s = (bid * (uint32_t)FWG + threadIdx.x) * per;
+    const uint32_t e = s + per < nh ? s + per : nh;
+    uint32_t h = 0;
+    for (uint32_t i = s; i < e; ++i)
+        h = gmul_t(T, h, f.k) ^ f.part[i];
+    if (s < e)
+        h = gmul_t(T, h, kpow(T, kp2, nh - e));
+    for (int o = 32; o > 0; o >>= 1)
+        h ^= __shfl_xor(h, o);
+    if ((threadIdx.x & 63) == 0)
+        red[threadIdx.x >> 6] = h;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t x = 0;
+        for (int k = 0; k < FWG / 64; ++k)
+            x ^= red[k];
+        x = gmul_t(T, x, f.x_last);
+        if (bid == 0)
+            x ^= f.part[W - 1];
+        atomicXor(f.out, x);
+    }
+}
+
+__global__ __launch_bounds__(FWG) void span_fold_kernel(SpanFold f, const uint32_t *__restrict__ gtab)
+{
+    __shared__ uint32_t red[FWG / 64];
+    __shared__ __attribute__((aligned(16))) char T[4096];
+    __shared__ uint32_t kp2[32];
+    load_gmul_table(T, gtab);
+    if (threadIdx.x < 32)
+        kp2[threadIdx.x] = f.kp2[threadIdx.x];
+    __syncthreads();
+    fold_blocks(f, T, kp2, red, blockIdx.x, gridDim.x);
+}
+
+/* The folds of a multi-span launch: blockIdx.y = span, each span over the
+ * first fold_nblk(W) blocks of its row. */
+__device__ __forceinline__ uint32_t fold_nblk(uint32_t w)
+{
+    const uint32_t b = (w + FWG - 1) / FWG;
+    return b < 1 ? 1 : b > 256 ? 256 : b;
+}
+
+__global__ __launch_bounds__(FWG) void span_folds_kernel(SpanFolds fs, const uint32_t *__restrict__ gtab)
+{
+    const SpanFold &f = fs.f[blockIdx.y];
+    const uint32_t nb = fold_nblk(f.w);
+    if (blockIdx.x >= nb)
+        return;
+    __shared__ uint32_t red[FWG / 64];
+    __shared__ __attribute__((aligned(16))) char T[4096];
+    __shared__ uint32_t kp2[32];
+    load_gmul_table(T, gtab);
+    if (threadIdx.x < 32)
+        kp2[threadIdx.x] = f.kp2[threadIdx.x];
+    __syncthreads();
+    fold_blocks(f, T, kp2, red, blockIdx.x, nb);
+}
+
 /* ------------------------------------------------ consistent: the digest row */
 /* The last workgroup of cpass_post_kernel<true> (1,024 threads) writes the
  * rank's digest row in the layout of consistent.py's Consistent._pack, so
@@ -3784,8 +3876,40 @@ __device__ __forceinline__ uint32_t cpass_classify(const CPassArgs &a, const cha
     return c == (uint32_t)w0 ? 1u : 0u;
 }
 
+/* The commit trailer after raw span s of a pass (its register from 0
+ * `raw`): 1 ok, 0 mismatch, 2 no commit record, -1 not checked here
+ * (src/zeroskip-file.c:266-302). */
+__device__ __forceinline__ int32_t span_check(const CPassArgs &a, const char *T, uint32_t s, uint32_t raw)
+{
+    const int64_t at = a.span_commit[s];
+    if (at < 0)
+        return -1;
+    /* crc32c(0, span) = (shift(~0, len) ^ raw) ^ ~0: continue the register */
+    uint32_t r = a.span_init[s] ^ raw;
+    if ((uint64_t)at + 8 > a.img_size)
+        return 2;
+    const uintptr_t e = reinterpret_cast<uintptr_t>(a.base) + (uint64_t)at;
+    const uint64_t w0 = load_be64(e);
+    const uint32_t t = (uint32_t)(w0 >> 56);
+    uint32_t stored = 0;
+    if (t == REC_COMMIT || t == REC_FINAL) {
+        r = crc_word(T, r, w0 & 0xFFFFFFFF00000000ull);
+        stored = (uint32_t)w0;
+    } else if ((t == REC_LONG_COMMIT || t == REC_LONG_FINAL) && (uint64_t)at + 24 <= a.img_size) {
+        const uint64_t w2 = load_be64(e + 16);
+        r = crc_word(T, r, w0);
+        r = crc_word(T, r, load_be64(e + 8));
+        r = crc_word(T, r, w2 & 0xFF00000000000000ull);
+        stored = (uint32_t)w2;
+    } else {
+        return 2;
+    }
+    return (r ^ 0xffffffffu) == stored ? 1 : 0;
+}
+
 template <bool ROW>
-__global__ __launch_bounds__(ROW ? 1024 : 256) void cpass_post_kernel(CPassArgs a, const uint32_t *__restrict__ gtab)
+__global__ __launch_bounds__(ROW ? 1024 : 256) void cpass_post_kernel(CPassArgs a, SpanFolds fs, uint32_t nfold,
+                                                                 const uint32_t *__restrict__ gtab)
 {
     __shared__ __attribute__((aligned(16))) char T[4096];
     __shared__ uint64_t key[ROW ? ROW_SORT : 1];
@@ -3801,7 +3925,7 @@ __global__ __launch_bounds__(ROW ? 1024 : 256) void cpass_post_kernel(CPassArgs 
     if (a.host_nbad && blockIdx.x == 0) { /* the pass's count and span registers, straight to the host */
         if (threadIdx.x == 0)
             *a.host_nbad = *a.nbad;
-        for (uint32_t k = threadIdx.x; k < a.nspans; k += blockDim.x)
+        for (uint32_t k = threadIdx.x; k < a.nspans && !nfold; k += blockDim.x)
             a.host_raw[k] = a.span_raw[k];
     }
     if (threadIdx.x == 0)
@@ -3810,6 +3934,28 @@ __global__ __launch_bounds__(ROW ? 1024 : 256) void cpass_post_kernel(CPassArgs 
         cnt[threadIdx.x] = 0;
     load_gmul_table(T, gtab); /* GT_S4, compact: table j at 1024 j */
     __syncthreads();
+    uint32_t cls0 = 0; /* the first workgroup that classifies */
+    if (!ROW && nfold) {
+        /* The multi-span launch's folds (span_folds_kernel's blocks) on the
+         * post kernel's first workgroups, one fold block each (the spans'
+         * blocks laid end to end), XOR-ing into the span's register (preset
+         * by xteam_kernel), while the workgroups after them classify -- one
+         * launch and its ramp fewer per pass.  The span checks then wait
+         * for the last workgroup. */
+        __shared__ uint32_t red[FWG / 64], kp2s[32];
+        for (uint32_t k = 0; k < nfold; ++k)
+            cls0 += fold_nblk(fs.f[k].w);
+        if (blockIdx.x < cls0) {
+            uint32_t k = 0, base = 0;
+            while (blockIdx.x >= base + fold_nblk(fs.f[k].w))
+                base += fold_nblk(fs.f[k++].w);
+            const SpanFold &f = fs.f[k];
+            if (threadIdx.x < 32)
+                kp2s[threadIdx.x] = f.kp2[threadIdx.x];
+            __syncthreads();
+            fold_blocks(f, T, kp2s, red, blockIdx.x - base, fold_nblk(f.w));
+        }
+    }
     const uint64_t nbad = *a.nbad, nl = nbad < a.cap ? nbad : a.cap;
     uint32_t mine = 0; /* stale commits this thread found */
     auto list = [&](uint64_t k, uint64_t i, uint32_t flag) {
@@ -3829,7 +3975,8 @@ __global__ __launch_bounds__(ROW ? 1024 : 256) void cpass_post_kernel(CPassArgs 
      * workgroup's (each entry rehashes a span: one CU's memory rate bound
      * the row pass at 53 us, profiles/r06/config5/) */
     const uint64_t nwv = blockDim.x >> 6, lane = threadIdx.x & 63;
-    for (uint64_t c = blockIdx.x + (uint64_t)gridDim.x * (threadIdx.x >> 6); 64 * c < nl; c += gridDim.x * nwv) {
+    const uint64_t cb = blockIdx.x >= cls0 ? blockIdx.x - cls0 : ~0ull, cg = gridDim.x - cls0;
+    for (uint64_t c = cb + cg * (threadIdx.x >> 6); cb != ~0ull && 64 * c < nl; c += cg * nwv) {
         const uint64_t k = 64 * c + lane;
         if (k < nl) {
             const uint64_t i = a.bad[k];
@@ -3838,35 +3985,9 @@ __global__ __launch_bounds__(ROW ? 1024 : 256) void cpass_post_kernel(CPassArgs 
     }
     if (mine)
         atomicAdd(&wg_stale, mine);
-    if (blockIdx.x == 0 && threadIdx.x < a.nspans) {
+    if (blockIdx.x == 0 && threadIdx.x < a.nspans && !nfold) {
         const uint32_t s = threadIdx.x;
-        int32_t st = -1;
-        const int64_t at = a.span_commit[s];
-        if (at >= 0) {
-            st = 2;
-            /* crc32c(0, span) = (shift(~0, len) ^ raw) ^ ~0: continue the register */
-            uint32_t r = a.span_init[s] ^ a.span_raw[s];
-            if ((uint64_t)at + 8 <= a.img_size) {
-                const uintptr_t e = reinterpret_cast<uintptr_t>(a.base) + (uint64_t)at;
-                const uint64_t w0 = load_be64(e);
-                const uint32_t t = (uint32_t)(w0 >> 56);
-                uint32_t stored = 0;
-                if (t == REC_COMMIT || t == REC_FINAL) {
-                    r = crc_word(T, r, w0 & 0xFFFFFFFF00000000ull);
-                    stored = (uint32_t)w0;
-                    st = 0;
-                } else if ((t == REC_LONG_COMMIT || t == REC_LONG_FINAL) && (uint64_t)at + 24 <= a.img_size) {
-                    const uint64_t w2 = load_be64(e + 16);
-                    r = crc_word(T, r, w0);
-                    r = crc_word(T, r, load_be64(e + 8));
-                    r = crc_word(T, r, w2 & 0xFF00000000000000ull);
-                    stored = (uint32_t)w2;
-                    st = 0;
-                }
-                if (st == 0)
-                    st = (r ^ 0xffffffffu) == stored ? 1 : 0;
-            }
-        }
+        const int32_t st = span_check(a, T, s, a.span_raw[s]);
         if constexpr (ROW)
             __hip_atomic_store(&a.span_status[s], st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         else
@@ -3891,7 +4012,7 @@ __global__ __launch_bounds__(ROW ? 1024 : 256) void cpass_post_kernel(CPassArgs 
      * Every wave first waits for its own stores (a workgroup barrier does
      * not: in the ISA no vmcnt wait precedes s_barrier), so they are in the
      * L2 before thread 0's write-back is issued. */
-    if constexpr (ROW)
+    if (ROW || nfold) /* (the folds' XORs, too) */
         __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -3911,6 +4032,15 @@ __global__ __launch_bounds__(ROW ? 1024 : 256) void cpass_post_kernel(CPassArgs 
         if (a.host_nbad)
             a.host_nbad[1] = nstale;
     }
+    if (!ROW && nfold && threadIdx.x < a.nspans) {
+        /* every fold is in: the span registers (read past the XCDs' L2s,
+         * where the other workgroups' XORs went) and their checks */
+        const uint32_t sp = threadIdx.x;
+        const uint32_t raw = __hip_atomic_load(const_cast<uint32_t *>(a.span_raw) + sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        a.span_status[sp] = span_check(a, T, sp, raw);
+        if (a.host_nbad)
+            a.host_raw[sp] = raw;
+    }
     if constexpr (ROW) {
         /* the listed entries as sort keys (flag << 56 | commit index) */
         const uint32_t lc = (uint32_t)(nl < a.row.list_cap ? nl : a.row.list_cap);
@@ -3929,98 +4059,6 @@ __global__ __launch_bounds__(ROW ? 1024 : 256) void cpass_post_kernel(CPassArgs 
         __syncthreads();
         cpass_write_row(a.row, nbad, lc, key, cnt, sst);
     }
-}
-
-/* ------------------------------------------------------------ span fold */
-/* K^m from the table K^(2^b). */
-__device__ __forceinline__ uint32_t kpow(const char *T, const uint32_t *kp2, uint32_t m)
-{
-    uint32_t r = 0x80000000u;
-    for (int b = 0; m; ++b, m >>= 1)
-        if (m & 1)
-            r = gmul_t(T, r, kp2[b]);
-    return r;
-}
-
-/*
- * Fold W raw segment registers P_0..P_{W-1} of a span whose segments are all
- * SEG bytes long except the last:
- *   H = Horner_{i<W-1}(P_i, K = x^(8 SEG));  reg = H * x^(8 lastlen) ^ P_{W-1}
- *   reg ^= R0 * x^(8 L)                       (initial register)
- * Spread over blocks (one part per thread up to 256 x 256 parts): a thread
- * Horner-folds its run of parts and shifts it by K^(parts after the run)
- * (square-and-multiply: ~14 gmul chains, latency-bound, so one wave per
- * SIMD); each block XOR-reduces, multiplies by
- * x^(8 lastlen) and XORs into *out, which the host preset to the constant
- * R0 * x^(8 L) ^ xor_out (hipMemsetD32Async); block 0 adds P_{W-1}.
- */
-constexpr int FWG = 256; /* span fold: one wave per SIMD, the gmul chains are latency-bound */
-
-/* One span's fold by block bid of nblk (tables already in LDS). */
-__device__ __forceinline__ void fold_blocks(const SpanFold &f, const char *T, const uint32_t *kp2, uint32_t *red,
-                                            uint32_t bid, uint32_t nblk)
-{
-    const uint32_t W = f.w;
-    const uint32_t nh = W - 1; /* Horner terms */
-    const uint32_t nt = nblk * (uint32_t)FWG;
-    const uint32_t per = (nh + nt - 1) / nt;
-    const uint32_t s = (bid * (uint32_t)FWG + threadIdx.x) * per;
-    const uint32_t e = s + per < nh ? s + per : nh;
-    uint32_t h = 0;
-    for (uint32_t i = s; i < e; ++i)
-        h = gmul_t(T, h, f.k) ^ f.part[i];
-    if (s < e)
-        h = gmul_t(T, h, kpow(T, kp2, nh - e));
-    for (int o = 32; o > 0; o >>= 1)
-        h ^= __shfl_xor(h, o);
-    if ((threadIdx.x & 63) == 0)
-        red[threadIdx.x >> 6] = h;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t x = 0;
-        for (int k = 0; k < FWG / 64; ++k)
-            x ^= red[k];
-        x = gmul_t(T, x, f.x_last);
-        if (bid == 0)
-            x ^= f.part[W - 1];
-        atomicXor(f.out, x);
-    }
-}
-
-__global__ __launch_bounds__(FWG) void span_fold_kernel(SpanFold f, const uint32_t *__restrict__ gtab)
-{
-    __shared__ uint32_t red[FWG / 64];
-    __shared__ __attribute__((aligned(16))) char T[4096];
-    __shared__ uint32_t kp2[32];
-    load_gmul_table(T, gtab);
-    if (threadIdx.x < 32)
-        kp2[threadIdx.x] = f.kp2[threadIdx.x];
-    __syncthreads();
-    fold_blocks(f, T, kp2, red, blockIdx.x, gridDim.x);
-}
-
-/* The folds of a multi-span launch: blockIdx.y = span, each span over the
- * first fold_nblk(W) blocks of its row. */
-__device__ __forceinline__ uint32_t fold_nblk(uint32_t w)
-{
-    const uint32_t b = (w + FWG - 1) / FWG;
-    return b < 1 ? 1 : b > 256 ? 256 : b;
-}
-
-__global__ __launch_bounds__(FWG) void span_folds_kernel(SpanFolds fs, const uint32_t *__restrict__ gtab)
-{
-    const SpanFold &f = fs.f[blockIdx.y];
-    const uint32_t nb = fold_nblk(f.w);
-    if (blockIdx.x >= nb)
-        return;
-    __shared__ uint32_t red[FWG / 64];
-    __shared__ __attribute__((aligned(16))) char T[4096];
-    __shared__ uint32_t kp2[32];
-    load_gmul_table(T, gtab);
-    if (threadIdx.x < 32)
-        kp2[threadIdx.x] = f.kp2[threadIdx.x];
-    __syncthreads();
-    fold_blocks(f, T, kp2, red, blockIdx.x, nb);
 }
 
 /* ------------------------------------------------- classes and parts */
@@ -5041,16 +5079,30 @@ extern "C" int zs_launch_commit_scatter(uint8_t *base, const uint64_t *off, cons
  * (hipExtLaunchKernel's stop event) -- a separate hipEventRecord after it is
  * a marker packet that held the next pass's first launch ~6 us
  * (profiles/r06/config5/) */
-extern "C" int zs_launch_cpass_post(const zs::CPassArgs *a, const uint32_t *gtab, hipStream_t stream, hipEvent_t done)
+extern "C" int zs_launch_cpass_post(const zs::CPassArgs *a, const zs::SpanFolds *fs, uint32_t nfold,
+                                    const uint32_t *gtab, hipStream_t stream, hipEvent_t done)
 {
-    if (!a->ticket || !a->nstale)
+    if (!a->ticket || !a->nstale || (nfold && (!fs || a->row.row || nfold > (uint32_t)zs::SPANS_MAX)))
         return -1;
+    zs::SpanFolds none;
+    if (!nfold)
+        memset(&none, 0, sizeof none);
+    const zs::SpanFolds &f = nfold ? *fs : none;
     if (a->row.row) {
         if (a->row.list_cap > zs::ROW_SORT || a->row.list_cap > a->out_cap)
             return -1;
-        hipExtLaunchKernelGGL(zs::cpass_post_kernel<true>, dim3(64), dim3(1024), 0, stream, nullptr, done, 0, *a, gtab);
+        hipExtLaunchKernelGGL(zs::cpass_post_kernel<true>, dim3(64), dim3(1024), 0, stream, nullptr, done, 0, *a, f,
+                              0u, gtab);
     } else {
-        hipExtLaunchKernelGGL(zs::cpass_post_kernel<false>, dim3(64), dim3(256), 0, stream, nullptr, done, 0, *a, gtab);
+        /* a workgroup per fold block, then the 64 that classify */
+        uint32_t tot = 0;
+        for (uint32_t k = 0; k < nfold; ++k) {
+            const uint32_t b = (f.f[k].w + zs::FWG - 1) / zs::FWG;
+            tot += b < 1 ? 1u : b > 256 ? 256u : b;
+        }
+        const uint32_t grid = 64 + tot;
+        hipExtLaunchKernelGGL(zs::cpass_post_kernel<false>, dim3(grid), dim3(256), 0, stream, nullptr, done, 0, *a, f,
+                              nfold, gtab);
     }
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
@@ -5133,6 +5185,8 @@ extern "C" int zs_launch_spans(const zs::XDesc *x, const zs::XMulti *m, const zs
         hipLaunchKernelGGL(zs::xteam_kernel<1>, dim3(grid), dim3(zs::WG), 0, stream, *x, *m, np, gtab);
     if (hipGetLastError() != hipSuccess)
         return -3;
+    if (!fs) /* the caller's own kernel folds (zscrc_cpass: the post kernel) */
+        return 0;
     uint32_t bx = 1;
     for (uint32_t k = 0; k < m->k; ++k) {
         const uint32_t b = (fs->f[k].w + zs::FWG - 1) / zs::FWG;
