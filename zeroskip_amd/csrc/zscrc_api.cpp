@@ -655,10 +655,6 @@ unsigned long long *verdict_slot(DevCtx *c, hipStream_t s)
         void *p = nullptr;
         if (hipMalloc(&p, 64 * 4 * 128) != hipSuccess)
             return nullptr;
-        if (hipMemset(p, 0, 64 * 4 * 128) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-            (void)hipFree(p);
-            return nullptr;
-        }
         c->vctr = static_cast<unsigned long long *>(p);
     }
     int k = 0;
@@ -666,6 +662,10 @@ unsigned long long *verdict_slot(DevCtx *c, hipStream_t s)
         ++k;
     if (k == c->vctr_n) {
         if (c->vctr_n == 64)
+            return nullptr;
+        /* the stream's four pairs zeroed on the stream itself, ahead of
+         * their first use (once per stream, no device-wide wait) */
+        if (hipMemsetAsync(c->vctr + 16 * 4 * k, 0, 4 * 128, s) != hipSuccess)
             return nullptr;
         c->vctr_stream[c->vctr_n++] = s;
     }
