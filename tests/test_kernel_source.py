@@ -56,6 +56,10 @@ CAPPED_LISTS = {
     # out-of-image commits listed by the classify passes into the same verdict
     "classify_scatter": "verdict",
     "classify_only3": "verdict",
+    # the one-launch class-3 verdict (xteam_kernel MODE 3): out-of-image
+    # commits listed by workgroup 0's scan, the rest by nbv_check (MODE 3 or its fold)
+    "xteam_kernel": "verdict",
+    "nbv_check": "verdict",
     # cpass post kernel: the first out_cap classified entries go to the host
     # block; counts (nbad, nstale) are over every classified entry, published
     # by the last workgroup; the host and the device row read the same block

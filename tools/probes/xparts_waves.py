@@ -55,6 +55,14 @@ def main():
     o, ln = zg.log_spans(nf, ppf, False, False, dev)
     vout = (torch.empty(1, dtype=torch.int64, device=dev), torch.empty(64, dtype=torch.int64, device=dev))
     waves("notbatched verdict (xteam parts)", lambda: zsfile.verify_commits_verdict(img, o, ln, out=vout), nw)
+    if os.environ.get("WAVES_NB_RANGE"):  # the bench's ranged verdict: one launch (MODE 3) and tuning bit 64
+        lo, hi = int(ln.min().item()), int(ln.max().item())
+        for opt in (0, 64):
+            lib().zscrc_set_opt(opt)
+            waves(f"notbatched ranged verdict opt {opt}",
+                  lambda: zsfile.verify_commits_verdict(img, o, ln, out=vout, min_len=lo, max_len=hi), nw)
+        lib().zscrc_set_opt(0)
+        return
     del img
     c3 = torch.randint(0, 256, (3 << 30,), dtype=torch.uint8, device=dev, generator=g)
     waves("span 3 GiB (xteam segments)", lambda: zd.crc_span(c3), nw)

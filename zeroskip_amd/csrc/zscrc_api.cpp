@@ -48,6 +48,7 @@ int zs_launch_commit_scatter(uint8_t *base, const uint64_t *off, const uint64_t 
 int zs_launch_qdyn(const zs::BatchDesc *bd, const zs::QDyn *q, uint32_t K, uint32_t K_last, const uint32_t *gtab,
                    int grid, hipStream_t stream);
 int zs_launch_xparts(const zs::BatchDesc *d, const uint32_t *gtab, int grid, int deal, hipStream_t stream);
+int zs_launch_nbv(const zs::XParts *p, const uint32_t *gtab, int grid, hipStream_t stream);
 int zs_launch_spans(const zs::XDesc *x, const zs::XMulti *m, const zs::SpanFolds *fs, const uint32_t *gtab,
                     int grid, int deal, hipStream_t stream);
 int zs_launch_mismatch_rows(const uint32_t *st, const uint32_t *crc, const int64_t *end, const uint8_t *img,
@@ -152,6 +153,10 @@ struct DevCtx {
      * calls on one stream are ordered, so a stream's own pair needs no
      * event (verdict_slot) */
     unsigned long long *vctr = nullptr;
+    /* class-3-only verdicts (xteam_kernel MODE 3 + nbv_fold_kernel): part
+     * registers per segment, then the commits' starts; used under the
+     * scratch's cross-stream ordering */
+    uint32_t *nbv = nullptr;
     hipStream_t vctr_stream[64] = {};
     uint32_t vctr_turn[64] = {};
     int vctr_n = 0;
@@ -857,6 +862,67 @@ int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1
                        !(d.opt & zs::OPT_NO_ONLY3)
                    ? 1
                    : 0;
+    /* tuning bit OPT_NBV: a class-3-only verdict of at most NBV_MAX commits
+     * in two launches instead of three -- every workgroup of xteam_kernel
+     * MODE 3 scans the commits' lengths itself (no classify launch), a wave
+     * finishes the commits inside its segment and stores the parts of longer
+     * ones, nbv_fold_kernel folds those.  Not the default: interleaved on
+     * NOTBATCHED it measured level with the three launches (0.5269 against
+     * 0.5285 ms) -- the per-workgroup scan and the hashing
+     * launch's longer tail cost what the classify launch did.  A wave holds
+     * its segment's part registers in one register across the wave: at most
+     * NBV_PARTS_MAX parts per segment, which the range bounds (a segment of
+     * G bytes meets at most G / min_len + 2 commits) */
+    auto nbv_parts_fit = [&]() {
+        if (!min_len || max_len > UINT64_MAX / 2 / n)
+            return false;
+        uint64_t G = (n * max_len + nseg3 - 1) / nseg3;
+        G = (G + 63) & ~63ull;
+        if (G < pa[1].unit_min)
+            G = pa[1].unit_min;
+        return G / min_len + 2 <= zs::NBV_PARTS_MAX;
+    };
+    if (cl.only3 && n <= zs::NBV_MAX && (d.opt & zs::OPT_NBV) && !d.bad_prezeroed && d.off && d.len &&
+        pa[1].nseg == nseg3 && nseg3 == (size_t)c->ncu * 16 && nbv_parts_fit()) {
+        unsigned long long *pair = verdict_slot(c, s);
+        if (pair) {
+            if (!c->nbv) {
+                void *p = nullptr;
+                const size_t bytes = 2 * nseg3 * sizeof(uint32_t) + (zs::NBV_MAX + 1) * sizeof(uint64_t);
+                hipError_t e = hipMalloc(&p, bytes);
+                if (e != hipSuccess) {
+                    if (p)
+                        (void)hipFree(p);
+                    set_err("nbv buffers", e);
+                    return ZSCRC_EHIP;
+                }
+                c->nbv = static_cast<uint32_t *>(p);
+            }
+            zs::XParts x;
+            memset(&x, 0, sizeof x);
+            x.base = d.base;
+            x.xor_io = d.xor_io;
+            x.off3 = d.off;
+            x.len3 = d.len;
+            x.seed3 = d.seed;
+            x.n3 = n;
+            x.img_size = d.img_size;
+            x.nbv = c->nbv;
+            x.rstart = reinterpret_cast<uint64_t *>(c->nbv + 2 * nseg3);
+            x.vpair = pair;
+            x.publish = d.bad_count;
+            x.bad_idx = d.bad_idx;
+            x.bad_cap = d.bad_cap;
+            x.nseg = (uint32_t)nseg3;
+            x.unit_min = pa[1].unit_min;
+            if (zs_launch_nbv(&x, c->gtab, c->ncu, s)) {
+                set_err("nbv launch", hipGetLastError());
+                return ZSCRC_EHIP;
+            }
+            g_stat[2] += 2; /* the hashing launch and its fold */
+            return ZSCRC_OK;
+        }
+    }
     if (cl.single) {
         cl.plan[0] = pa[0];
         cl.plan[1] = pa[1];

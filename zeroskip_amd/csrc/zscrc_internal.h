@@ -65,6 +65,8 @@ struct BatchDesc {
      * raw part registers go to part_out[p], part_fold_kernel folds them */
     uint32_t split;
     uint32_t opt;         /* tuning bits: 1 = no three-chain five-piece bursts, 2 = no multi64_kernel,
+                             64 = class-3-only range verdicts on xteam_kernel MODE 3 +
+                             nbv_fold_kernel (OPT_NBV, two launches, no classify),
                              4 / 8 = qteam_kernel with XOR3 grouping 1 / 2,
                              16 = team_kernel<16>'s two-level walk with XOR3 grouping 2,
                              1024 = direct burst batches without the descriptor prefetch,
@@ -200,7 +202,30 @@ struct XParts {
     uint32_t seg;              /* the plan's seg (read on the device)     */
     uint32_t first_rec;        /* the class's first record in desc (device) */
     uint64_t U;                /* the plan's unit / segment bytes (device)  */
+    /* MODE 3, a class-3-only commit verdict in one launch (no classify, no
+     * plan, no fold launch): every workgroup scans the caller's lengths
+     * itself, wave w hashes segment w of the commits' bytes laid end to end;
+     * a commit in one segment is finished by its wave; a longer one's parts
+     * are stored (head[j]: a commit's first part, cont[j]: the part at
+     * segment j's start) for nbv_fold_kernel, which folds and checks them.
+     * The verdict counts into vpair (count, blocks done; 0 at rest); the
+     * fold launch's last block moves the count to *publish. */
+    const uint64_t *off3, *len3;
+    const uint32_t *seed3; /* NULL: seed 0 */
+    uint64_t n3, img_size;
+    uint32_t *nbv;    /* head[nseg], then cont[nseg] */
+    uint64_t *rstart; /* the commits' starts end to end, [n3] = their total */
+    unsigned long long *vpair, *publish;
+    uint64_t *bad_idx;
+    uint64_t bad_cap;
+    uint32_t nseg;
+    uint64_t unit_min;
+    uint64_t seg_lo, seg_hi, G; /* per wave, set on the device */
 };
+/* MODE 3's record limit: the workgroup's 64-bit scan of the starts in LDS */
+constexpr uint32_t NBV_MAX = 16384;
+constexpr uint32_t NBV_PARTS_MAX = 62; /* parts per segment (one lane each) */
+constexpr uint32_t OPT_NBV = 64u; /* tuning: class-3-only verdicts on MODE 3 + nbv_fold_kernel (round 6 A/B: level) */
 
 /* consistent's device post pass (zscrc_cpass, cpass_post_kernel): the
  * verdict's bad list classified (stale finalise commit / bad / undecided),

@@ -1010,11 +1010,65 @@ struct XLoad {
     XItem cur;     /* the record's whole geometry: the hashing walk, one step
                       behind, takes it when it reaches the record (one
                       geometry per record, not one per walk) */
+    uint64_t S3, L3; /* MODE 3: record w's first byte end to end, its length */
 };
+
+/* MODE 3: record l.w's part inside the wave's segment [seg_lo, seg_hi) --
+ * commits outside the image (length 0 here) skipped, the walk ended
+ * (l.wend = l.w) at the first record starting at or past seg_hi. */
+__device__ __forceinline__ void xrec3(const XParts &xp, XLoad &l)
+{
+    typedef const __attribute__((address_space(1))) uint64_t *g64p;
+    uint64_t off = 0;
+    for (;;) {
+        if (l.w >= l.wend)
+            break;
+        if (l.S3 >= xp.seg_hi) {
+            l.wend = l.w;
+            break;
+        }
+        off = uni64(((g64p)xp.off3)[l.w]);
+        const uint64_t len = uni64(((g64p)xp.len3)[l.w]);
+        if (commit_fits(xp.img_size, off, len) && len) {
+            l.L3 = len;
+            break;
+        }
+        ++l.w; /* empty: the workgroup's scan gave it no bytes */
+    }
+    if (l.w >= l.wend) {
+        l.ok = false;
+        l.left = 0;
+        return;
+    }
+    const uint64_t b0 = l.S3 > xp.seg_lo ? l.S3 : xp.seg_lo;
+    const uint64_t e3 = l.S3 + l.L3;
+    const uint64_t b1 = e3 < xp.seg_hi ? e3 : xp.seg_hi;
+    const uint64_t a = b0 - l.S3, len = b1 - b0;
+    const uintptr_t A = reinterpret_cast<uintptr_t>(xp.base) + off + a;
+    const uint32_t seed = a ? 0u : (xp.seed3 ? rfl_u32(((g32p)xp.seed3)[l.w]) : 0u);
+    l.lo = reinterpret_cast<uintptr_t>(xp.base) & ~uintptr_t(3);
+    const uintptr_t E = len < 8 ? A : ((A + len) & ~uintptr_t(3));
+    const uint64_t S = len < 8 ? 0 : (E - A + XSTEP - 1) / XSTEP;
+    l.V = E - S * XSTEP;
+    l.left = S ? (uint32_t)(S - 1) : 0u;
+    l.ok = S != 0;
+    l.cur.A = A;
+    l.cur.E = E;
+    l.cur.V0 = l.V;
+    l.cur.S = (uint32_t)S;
+    l.cur.len = len;
+    l.cur.w = l.w;
+    l.cur.R0 = a ? 0u : seed ^ xp.xor_io;
+    l.cur.lo = l.lo;
+}
 
 template <int MODE>
 __device__ __forceinline__ void xrec(const XDesc &d, const XMulti &m, const XParts &xp, XLoad &l)
 {
+    if (MODE == 3) {
+        xrec3(xp, l);
+        return;
+    }
     uintptr_t A;
     uint64_t len;
     uint32_t R0;
@@ -1044,9 +1098,104 @@ __device__ __forceinline__ void xnext(const XDesc &d, const XMulti &m, const XPa
     }
     if (l.w >= l.wend)
         return;
+    if (MODE == 3)
+        l.S3 += l.L3;
     l.w += 1;
     xrec<MODE>(d, m, xp, l);
 }
+
+
+
+/* MODE 3 / nbv_fold_kernel: commit rec's register reg (its span hashed)
+ * continued over the commit trailer at end (emit's rules; feed(r, w) = r
+ * through one host-order 64-bit word), compared with the stored CRC; a
+ * mismatch or no commit record counted into vpair[0] and listed. */
+template <class Feed>
+__device__ __forceinline__ void nbv_check(const XParts &xp, uint64_t rec, uint64_t off, uint64_t len, uint32_t reg,
+                                          Feed feed)
+{
+    const uintptr_t end = reinterpret_cast<uintptr_t>(xp.base) + off + len;
+    const uint64_t room = xp.img_size - off - len; /* >= 8: commit_fits */
+    const uint64_t w0 = load_be64(end);
+    const uint32_t t = (uint32_t)(w0 >> 56);
+    uint32_t stored = 0;
+    bool found = false;
+    if (t == REC_COMMIT || t == REC_FINAL) {
+        reg = feed(reg, w0 & 0xFFFFFFFF00000000ull);
+        stored = (uint32_t)w0;
+        found = true;
+    } else if ((t == REC_LONG_COMMIT || t == REC_LONG_FINAL) && room >= 24) {
+        const uint64_t w1 = load_be64(end + 8), w2 = load_be64(end + 16);
+        reg = feed(reg, w0);
+        reg = feed(reg, w1);
+        reg = feed(reg, w2 & 0xFF00000000000000ull);
+        stored = (uint32_t)w2;
+        found = true;
+    }
+    if (!(found && (reg ^ 0xffffffffu) == stored)) {
+        const unsigned long long k = atomicAdd(xp.vpair, 1ull);
+        if (k < xp.bad_cap)
+            xp.bad_idx[k] = rec;
+    }
+}
+
+/* MODE 3 after the hashing loop: the wave's nst parts (registers in stash,
+ * lane k = part k), one lane each -- the segment's commits from r3 (the
+ * first byte s3) loaded 64 at a time, their starts a prefix scan, a commit
+ * outside the image skipped as by the walk.  A lane whose part is a whole
+ * commit finishes it (nbv_finish); a part of a longer commit is stored,
+ * head[j] for its first part, cont[j] for the one at the segment's start,
+ * for nbv_fold_kernel (next on the stream).  No atomics here but a
+ * mismatch's count: device-scope atomics under the read stream of the other
+ * waves took tens of microseconds each. */
+__device__ __forceinline__ void nbv_parts(const XParts &xp, uint64_t n, uint64_t r3, uint64_t s3, uint32_t nst,
+                                          uint32_t stash, const char *L)
+{
+    typedef const __attribute__((address_space(1))) uint64_t *g64p;
+    const int lane = threadIdx.x & 63;
+    const uint32_t c_lo = (uint32_t)(lane & 31) << 2;
+    const uint32_t c_hi = c_lo | 0x10000u;
+    uint64_t first = r3, S0 = s3;
+    uint32_t k0 = 0;
+    while (k0 < nst && first < n && S0 < xp.seg_hi) {
+        const uint64_t rec = first + (uint64_t)lane;
+        uint64_t off = 0, len = 0;
+        if (rec < n) {
+            off = ((g64p)xp.off3)[rec];
+            len = ((g64p)xp.len3)[rec];
+            if (!commit_fits(xp.img_size, off, len))
+                len = 0;
+        }
+        uint64_t inc = len; /* inclusive scan of the lengths across the wave */
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint64_t u = __shfl_up(inc, o);
+            if (lane >= o)
+                inc += u;
+        }
+        const uint64_t S = S0 + inc - len;
+        const bool has = len && S < xp.seg_hi;
+        const uint64_t m = __ballot(has);
+        const uint32_t kp = k0 + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+        const uint32_t v = __shfl(stash, (int)(kp & 63));
+        if (has && kp < nst) {
+            const uint64_t b0 = S > xp.seg_lo ? S : xp.seg_lo;
+            const uint64_t b1 = S + len < xp.seg_hi ? S + len : xp.seg_hi;
+            const uint64_t a = b0 - S, plen = b1 - b0;
+            const bool fin = a == 0 && plen == len;
+            if (!fin) {
+                const uint64_t j = xp.seg_lo / xp.G;
+                gstore32(xp.nbv + (a == 0 ? j : xp.nseg + j), v);
+            } else {
+                nbv_check(xp, rec, off, len, v,
+                          [&](uint32_t r, uint64_t w) { return feed64(L, r, w, c_lo, c_hi); });
+            }
+        }
+        k0 += (uint32_t)__popcll(m);
+        first += 64;
+        S0 += __shfl(inc, 63);
+    }
+}
+
 
 /* Diagnostic (zscrc_diag_wave_times): when set, every wave of xteam_kernel
  * records [entry, after the table fill, end] (s_memrealtime, 100 MHz) and
@@ -1075,6 +1224,8 @@ __device__ __forceinline__ void cstamp(int k)
  * static walk's waves' ends on a 3 GiB span between 424 us (p10) and 503 us,
  * the median workgroup's 16 waves 57 us apart
  * (profiles/r04/wave_spread.jsonl), as with qteam. */
+__device__ __forceinline__ uint64_t block_scan64(uint64_t v, unsigned long long *ws, uint64_t *tot);
+
 template <int MODE, bool DEAL = false>
 __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp, const uint32_t *__restrict__ gtab)
 {
@@ -1095,8 +1246,81 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp,
         xp.first_rec = first;
         xp.U = uni64(((const __attribute__((address_space(1))) uint64_t *)(xp.plan + xp.klass))[0]);
     }
+    /* MODE 3: the workgroup's own plan -- the commits' starts end to end
+     * (an out-of-image commit adds no bytes; workgroup 0 counts it into the
+     * verdict) as a 64-bit scan in LDS before the tables go there, the
+     * segment unit G as seg_unit's, and wave w's first record (the one
+     * holding byte w G) found by a binary search of the starts */
+    uint64_t r3 = 0, s3 = 0;
+    if (MODE == 3) {
+        typedef const __attribute__((address_space(1))) uint64_t *g64p;
+        uint64_t *Sr = reinterpret_cast<uint64_t *>(L);
+        unsigned long long *ws = reinterpret_cast<unsigned long long *>(L + 8 * (NBV_MAX + 1));
+        const uint64_t n = xp.n3;
+        uint64_t run = 0;
+        for (uint64_t c0 = 0; c0 < n; c0 += 4 * WG) {
+            uint64_t eff[4]; /* four chunks' lengths in flight at once, then their scans */
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint64_t r = c0 + (uint64_t)i * WG + threadIdx.x;
+                eff[i] = 0;
+                if (r < n) {
+                    const uint64_t off = ((g64p)xp.off3)[r], len = ((g64p)xp.len3)[r];
+                    if (commit_fits(xp.img_size, off, len))
+                        eff[i] = len;
+                    else if (blockIdx.x == 0) {
+                        const unsigned long long k = atomicAdd(xp.vpair, 1ull);
+                        if (k < xp.bad_cap)
+                            xp.bad_idx[k] = r;
+                    }
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if (c0 + (uint64_t)i * WG >= n)
+                    break;
+                const uint64_t r = c0 + (uint64_t)i * WG + threadIdx.x;
+                uint64_t tot;
+                const uint64_t S = run + block_scan64(eff[i], ws, &tot);
+                if (r < n) {
+                    Sr[r] = S;
+                    if (blockIdx.x == 0) /* for the fold launch */
+                        xp.rstart[r] = S;
+                }
+                run += tot;
+            }
+        }
+        __syncthreads();
+        run = uni64(run);
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+            xp.rstart[n] = run;
+        uint64_t G = (run + xp.nseg - 1) / xp.nseg;
+        G = (G + 63) & ~63ull;
+        xp.G = uni64(G < xp.unit_min ? xp.unit_min : G);
+        const uint64_t j = uni64((uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6));
+        xp.seg_lo = xp.seg_hi = 0;
+        r3 = n;
+        if (j < xp.nseg && j * xp.G < run) {
+            xp.seg_lo = uni64(j * xp.G);
+            xp.seg_hi = uni64(xp.seg_lo + xp.G < run ? xp.seg_lo + xp.G : run);
+            /* the last record starting at or before seg_lo (it has bytes) */
+            uint64_t lo = 0, hi = n - 1;
+            while (lo < hi) {
+                const uint64_t mid = (lo + hi + 1) / 2;
+                if (Sr[mid] <= xp.seg_lo)
+                    lo = mid;
+                else
+                    hi = mid - 1;
+            }
+            r3 = uni64(lo);
+            s3 = uni64(Sr[lo]);
+        }
+        d.n = n;
+        d.xor_io = 0;
+        __syncthreads(); /* the starts are read: the tables may overwrite them */
+    }
     /* segment plans: wave w takes segment w's parts (every block works) */
-    if ((MODE != 2 || !xp.seg) && (uint64_t)blockIdx.x * WAVES >= d.n)
+    if (MODE != 3 && (MODE != 2 || !xp.seg) && (uint64_t)blockIdx.x * WAVES >= d.n)
         return;
     if (MULTI && blockIdx.x == 0 && threadIdx.x < m.k)
         m.out[threadIdx.x][0] = m.preset[threadIdx.x]; /* the fold kernel (next on the stream) XORs into it */
@@ -1120,6 +1344,10 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp,
             wbeg = rfl_u32(((g32p)xp.seg_first)[team]);
             wend = rfl_u32(((g32p)xp.seg_first)[team + 1]);
         }
+    }
+    if (MODE == 3) { /* from the segment's first record until one starts past it */
+        wbeg = r3;
+        wend = d.n;
     }
     const uintptr_t dummy = reinterpret_cast<uintptr_t>(gtab);
     /* DEAL: the workgroup's counter (lane 0 asks; the answer stays in its
@@ -1167,6 +1395,8 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp,
         ld.w = wbeg;
         ld.wend = wend;
     }
+    ld.S3 = s3;
+    ld.L3 = 0;
     xrec<MODE>(d, m, xp, ld);
     /* the load walk's next step: a dealt item after the current one */
     auto advance = [&]() {
@@ -1194,7 +1424,7 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp,
     /* the hashing walk's next record / part: the one the load walk (a step
      * ahead; at the start, level) is on, with the geometry it computed */
     auto take = [&]() -> bool {
-        if (ld.w >= wend)
+        if (ld.w >= (MODE == 3 ? ld.wend : wend)) /* MODE 3: the walk finds its end */
             return false;
         it = ld.cur;
         return true;
@@ -1208,6 +1438,10 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp,
     uint64_t first = wbeg;
     auto stash_put = [&](uint32_t r) {
         stash = lane == (int)nst ? r : stash;
+        if (MODE == 3) { /* the segment's parts wait here to the end (< 64: host check) */
+            nst += nst < 63 ? 1u : 0u;
+            return;
+        }
         if (++nst == 64) {
             d.out[first + (uint64_t)lane] = stash;
             first += 64;
@@ -1272,8 +1506,13 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp,
         xissue(ld.V, ld.ok, voff, dummy, ld.lo, b0);
         hash(b1);
     }
-    if ((uint32_t)lane < nst)
+    if (MODE != 3 && (uint32_t)lane < nst)
         d.out[first + (uint64_t)lane] = stash;
+    if (MODE == 3) {
+        /* the segment's parts finished after the loop (its load buffers
+         * dead: no registers taken from the hashing), one lane each */
+        nbv_parts(xp, d.n, r3, s3, nst, stash, L);
+    }
     uint64_t *wt = zs_wave_times;
     if (wt && lane == 0) {
         const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
@@ -4751,6 +4990,92 @@ __global__ __launch_bounds__(256) void part_fold_kernel(FoldPair fp, const uint3
     }
 }
 
+/* The fold launch after xteam_kernel MODE 3 (one class-3-only verdict):
+ * 16 lanes per commit that spans segments j0 < j1 (the commit's starts and
+ * the bytes' total from workgroup 0 of that launch), Horner over head[j0]
+ * and cont[j0 < j <= j1] by K = x^(8 G), the last part shifted by its own
+ * length (16-lane product tree, part_fold_kernel's), then the trailer
+ * check; the last block out publishes the verdict count (commit_kernel's
+ * ticket: every increment returned before its block's ticket). */
+__global__ __launch_bounds__(256) void nbv_fold_kernel(XParts xp, const uint32_t *__restrict__ gtab)
+{
+    __shared__ __attribute__((aligned(16))) char T[4096];
+    __shared__ uint32_t TK[1024];
+    __shared__ uint32_t basis[32];
+    __shared__ uint32_t Ks;
+    typedef const __attribute__((address_space(1))) uint64_t *g64p;
+    load_gmul_table(T, gtab);
+    const uint64_t n = xp.n3;
+    const uint64_t total = ((const volatile uint64_t *)xp.rstart)[n];
+    uint64_t G = (total + xp.nseg - 1) / xp.nseg;
+    G = (G + 63) & ~63ull;
+    G = G < xp.unit_min ? xp.unit_min : G;
+    const int lane = threadIdx.x & 63;
+    __syncthreads();
+    if (threadIdx.x < 64) { /* K = x^(8 G): a product tree across wave 0 */
+        uint32_t v = ((G >> lane) & 1) ? gtab[GT_POW2 + lane] : 0x80000000u;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1)
+            v = gmul_t(T, v, __shfl_xor(v, o));
+        if (lane == 0)
+            Ks = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 32) /* a * K is linear in a's bits */
+        basis[threadIdx.x] = gmul_t(T, 1u << threadIdx.x, Ks);
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < 1024; e += blockDim.x) {
+        const uint32_t jb = e >> 8, b = e & 255;
+        uint32_t v = 0;
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+            if ((b >> t) & 1)
+                v ^= basis[8 * jb + t];
+        TK[e] = v;
+    }
+    __syncthreads();
+    const uint32_t sub = threadIdx.x & 15;
+    const uint64_t ngrp = (uint64_t)gridDim.x * blockDim.x / 16;
+    for (uint64_t idx = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / 16; __any(idx < n); idx += ngrp) {
+        uint64_t off = 0, len = 0, S = 0, j0 = 0, j1 = 0;
+        bool split = false;
+        if (idx < n) {
+            off = ((g64p)xp.off3)[idx];
+            len = ((g64p)xp.len3)[idx];
+            if (commit_fits(xp.img_size, off, len) && len) {
+                S = ((g64p)xp.rstart)[idx];
+                j0 = S / G;
+                j1 = (S + len - 1) / G;
+                split = j0 != j1; /* one segment: MODE 3's wave finished it */
+            }
+        }
+        const uint64_t blast = split ? S + len - j1 * G : 0;
+        uint32_t pw = 0x80000000u;
+        for (uint32_t t = sub; t < 48; t += 16)
+            if ((blast >> t) & 1)
+                pw = gmul_t(T, pw, gtab[GT_POW2 + t]);
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1)
+            pw = gmul_t(T, pw, __shfl_xor(pw, o));
+        if (!split || sub)
+            continue;
+        uint32_t reg = xp.nbv[j0];
+        for (uint64_t q = j0 + 1; q < j1; ++q)
+            reg = TK[reg & 255] ^ TK[256 + ((reg >> 8) & 255)] ^ TK[512 + ((reg >> 16) & 255)] ^ TK[768 + (reg >> 24)] ^
+                  xp.nbv[xp.nseg + q];
+        reg = gmul_t(T, reg, pw) ^ xp.nbv[xp.nseg + j1];
+        nbv_check(xp, idx, off, len, reg, [&](uint32_t r, uint64_t w) {
+            r = op4(T, 0, r ^ (uint32_t)w);
+            return op4(T, 0, r ^ (uint32_t)(w >> 32));
+        });
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && atomicAdd(xp.vpair + 1, 1ull) == gridDim.x - 1) {
+        *xp.publish = atomicExch(xp.vpair, 0ull);
+        atomicExch(xp.vpair + 1, 0ull);
+    }
+}
+
 /* ------------------------------------------------ the writer's second pass */
 /* The in-place commit writer as two passes (round 5, tuning bit 512):
  * commit_kernel computes every CRC into crc[] without touching the image
@@ -4973,6 +5298,7 @@ extern "C" int zs_launch_xparts(const zs::BatchDesc *bd, const uint32_t *gtab, i
     zs::XMulti none;
     none.k = 0;
     zs::XParts p;
+    memset(&p, 0, sizeof p);
     p.base = bd->base;
     p.desc = bd->desc;
     p.class_count = bd->class_count;
@@ -4989,6 +5315,27 @@ extern "C" int zs_launch_xparts(const zs::BatchDesc *bd, const uint32_t *gtab, i
         hipLaunchKernelGGL((zs::xteam_kernel<2, true>), dim3(grid), dim3(zs::WG), 0, stream, x, none, p, gtab);
     else
         hipLaunchKernelGGL(zs::xteam_kernel<2>, dim3(grid), dim3(zs::WG), 0, stream, x, none, p, gtab);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+/* a class-3-only commit verdict in two launches (XParts MODE 3, then
+ * nbv_fold_kernel); the host checks n3 <= NBV_MAX and that grid x 16 waves
+ * cover nseg segments */
+extern "C" int zs_launch_nbv(const zs::XParts *p, const uint32_t *gtab, int grid, hipStream_t stream)
+{
+    if (p->n3 > zs::NBV_MAX || (uint64_t)grid * zs::WAVES < p->nseg || !p->nseg)
+        return -3;
+    zs::XDesc x;
+    memset(&x, 0, sizeof x);
+    x.base = p->base;
+    zs::XMulti none;
+    none.k = 0;
+    hipLaunchKernelGGL(zs::xteam_kernel<3>, dim3(grid), dim3(zs::WG), 0, stream, x, none, *p, gtab);
+    if (hipGetLastError() != hipSuccess)
+        return -3;
+    uint64_t blocks = (p->n3 * 16 + 255) / 256;
+    blocks = blocks < 1 ? 1 : blocks > 256 ? 256 : blocks;
+    hipLaunchKernelGGL(zs::nbv_fold_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, *p, gtab);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
