@@ -209,8 +209,9 @@ unsigned zscrc_set_xdeal(unsigned per_wave);
 /* tuning bits (env ZSCRC_OPT), for A/B runs: 1 = hash five-piece record
  * bursts as one chain instead of three; 2 = 64-byte record batches of
  * zscrc_device_fixed_multi by the per-lane piece walk instead of coalesced
- * chunks; 64 = a _verdict_range batch of long commits only (at most 16,384)
- * in two launches without the classify launch; the rest are listed in
+ * chunks; 64 = a _verdict_range batch of long commits only (at most 4,096)
+ * through the classify, parts and fold launches (default: two launches
+ * without the classify); the rest are listed in
  * zscrc_internal.h (BatchDesc::opt).  Results never depend on them. */
 void zscrc_set_opt(unsigned bits);
 /* the xteam mode the fixed-stride path uses for n packed records of len

@@ -1,13 +1,13 @@
-"""Class-3-only commit verdicts in two launches (tuning bit 64, OPT_NBV:
-xteam_kernel MODE 3 + nbv_fold_kernel, "nbv";
+"""Class-3-only commit verdicts in two launches (xteam_kernel MODE 3 +
+nbv_fold_kernel, "nbv", the default since round 6;
 zscrc_device_verify_commits_verdict_range with a range above class 2, the
 bench's NOTBATCHED verdict).  Every workgroup scans the commit lengths
 itself, wave w hashes segment w of the commits laid end to end, finishes the
 commits inside it and stores the parts of longer ones, which the fold
 launch folds and checks -- so the verdict is checked here against the
 format oracle (src/zeroskip-file.c:253-350's trailer semantics,
-zf._commit_check) and against the default three-launch route (classify +
-parts + fold) on:
+zf._commit_check) and against the three-launch route (classify + parts +
+fold, tuning bit 64) on:
   * commits shorter than a segment (whole commits finished by their wave),
     several per segment, and commits over many segments (class 3 lowered to
     8 KiB with zscrc_set_teams);
@@ -30,7 +30,7 @@ from zeroskip_amd._lib import DEFAULT_TEAMS, lib, stats
 
 pytestmark = pytest.mark.gpu
 
-NBV = 64           # zs::OPT_NBV: MODE 3 + nbv_fold_kernel (default: classify + parts + fold)
+NO_NBV = 64        # zs::OPT_NO_NBV: the classify + parts + fold launches
 UNIT_MIN = 1 << 16  # class 3's segment floor (64-lane teams x 16 steps of 1 KiB)
 
 
@@ -140,10 +140,10 @@ def test_nbv_short_and_long_commits(small_class3, seed):
     d = torch.from_numpy(img).cuda()
     o, ln = torch.from_numpy(offs).cuda(), torch.from_numpy(lens).cuda()
     lo, hi = int(lens.min()), int(lens.max())
-    n1, b1, k1 = _verdict(NBV, d, o, ln, lo, hi)
+    n1, b1, k1 = _verdict(0, d, o, ln, lo, hi)
     assert k1 == 2, "the two-launch route did not run"
     assert n1 == len(want) and b1 == want
-    n3, b3, k3 = _verdict(0, d, o, ln, lo, hi)
+    n3, b3, k3 = _verdict(NO_NBV, d, o, ln, lo, hi)
     assert k3 > 1 and n3 == n1 and b3 == b1
 
 
@@ -164,9 +164,9 @@ def test_nbv_out_of_image_entries(small_class3):
     d = torch.from_numpy(img).cuda()
     o, ln = torch.from_numpy(o_np).cuda(), torch.from_numpy(l_np).cuda()
     lo, hi = int(l_np.min()), int(l_np.max())
-    n1, b1, k1 = _verdict(NBV, d, o, ln, lo, hi)
+    n1, b1, k1 = _verdict(0, d, o, ln, lo, hi)
     assert k1 == 2 and n1 == len(want) and b1 == want
-    n3, b3, _ = _verdict(0, d, o, ln, lo, hi)
+    n3, b3, _ = _verdict(NO_NBV, d, o, ln, lo, hi)
     assert n3 == n1 and b3 == b1
 
 
@@ -186,12 +186,12 @@ def test_nbv_seeded_and_long_trailer(small_class3):
     o, ln = torch.from_numpy(offs).cuda(), torch.from_numpy(lens).cuda()
     sd = torch.from_numpy(seeds.view(np.int32)).cuda()
     lo, hi = int(lens.min()), int(lens.max())
-    n1, b1, k1 = _verdict(NBV, d, o, ln, lo, hi, seed=sd)
+    n1, b1, k1 = _verdict(0, d, o, ln, lo, hi, seed=sd)
     assert k1 == 2 and n1 == len(want) and b1 == want
-    n3, b3, _ = _verdict(0, d, o, ln, lo, hi, seed=sd)
+    n3, b3, _ = _verdict(NO_NBV, d, o, ln, lo, hi, seed=sd)
     assert n3 == n1 and b3 == b1
     # unseeded: the stored CRCs all match
-    n0, b0, _ = _verdict(NBV, d, o, ln, lo, hi)
+    n0, b0, _ = _verdict(0, d, o, ln, lo, hi)
     assert n0 == 0 and not b0
 
 
@@ -212,7 +212,7 @@ def test_nbv_repeated_calls_two_streams(small_class3):
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
     for k in range(6):
         with torch.cuda.stream(s1 if k % 2 else s2):
-            n, b, launches = _verdict(NBV, db if k % 3 else dg, o, ln, lo, hi)
+            n, b, launches = _verdict(0, db if k % 3 else dg, o, ln, lo, hi)
         assert launches == 2
         if k % 3:
             assert n == len(want_bad) and b == want_bad, k
@@ -233,5 +233,5 @@ def test_nbv_notbatched_shape(gpu):
     d = torch.from_numpy(img).cuda()
     o, ln = torch.from_numpy(offs).cuda(), torch.from_numpy(lens).cuda()
     lo, hi = int(lens.min()), int(lens.max())
-    n1, b1, k1 = _verdict(NBV, d, o, ln, lo, hi)
+    n1, b1, k1 = _verdict(0, d, o, ln, lo, hi)
     assert k1 == 2 and n1 == len(want) and b1 == want

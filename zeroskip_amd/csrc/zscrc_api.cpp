@@ -862,17 +862,16 @@ int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1
                        !(d.opt & zs::OPT_NO_ONLY3)
                    ? 1
                    : 0;
-    /* tuning bit OPT_NBV: a class-3-only verdict of at most NBV_MAX commits
-     * in two launches instead of three -- every workgroup of xteam_kernel
-     * MODE 3 scans the commits' lengths itself (no classify launch), a wave
-     * finishes the commits inside its segment and stores the parts of longer
-     * ones, nbv_fold_kernel folds those.  Not the default: interleaved on
-     * NOTBATCHED it measured level with the three launches (0.5269 against
-     * 0.5285 ms) -- the per-workgroup scan and the hashing
-     * launch's longer tail cost what the classify launch did.  A wave holds
-     * its segment's part registers in one register across the wave: at most
-     * NBV_PARTS_MAX parts per segment, which the range bounds (a segment of
-     * G bytes meets at most G / min_len + 2 commits) */
+    /* a class-3-only verdict of at most NBV_MAX commits in two launches
+     * instead of three: every workgroup of xteam_kernel MODE 3 scans the
+     * commits' lengths itself while its tables fill (no classify launch), a
+     * wave finishes the commits inside its segment and stores the parts of
+     * longer ones, nbv_fold_kernel folds those.  NOTBATCHED interleaved:
+     * 0.5122 against 0.5266 ms (tuning bit
+     * OPT_NO_NBV: the three launches).  A wave holds its segment's part
+     * registers in one register across the wave: at most NBV_PARTS_MAX
+     * parts per segment, which the range bounds (a segment of G bytes meets
+     * at most G / min_len + 2 commits) */
     auto nbv_parts_fit = [&]() {
         if (!min_len || max_len > UINT64_MAX / 2 / n)
             return false;
@@ -882,7 +881,7 @@ int launch_classes_locked(DevCtx *c, zs::BatchDesc d, hipStream_t s, uint64_t g1
             G = pa[1].unit_min;
         return G / min_len + 2 <= zs::NBV_PARTS_MAX;
     };
-    if (cl.only3 && n <= zs::NBV_MAX && (d.opt & zs::OPT_NBV) && !d.bad_prezeroed && d.off && d.len &&
+    if (cl.only3 && n <= zs::NBV_MAX && !(d.opt & zs::OPT_NO_NBV) && !d.bad_prezeroed && d.off && d.len &&
         pa[1].nseg == nseg3 && nseg3 == (size_t)c->ncu * 16 && nbv_parts_fit()) {
         unsigned long long *pair = verdict_slot(c, s);
         if (pair) {

@@ -65,8 +65,9 @@ struct BatchDesc {
      * raw part registers go to part_out[p], part_fold_kernel folds them */
     uint32_t split;
     uint32_t opt;         /* tuning bits: 1 = no three-chain five-piece bursts, 2 = no multi64_kernel,
-                             64 = class-3-only range verdicts on xteam_kernel MODE 3 +
-                             nbv_fold_kernel (OPT_NBV, two launches, no classify),
+                             64 = class-3-only range verdicts through the classify, parts and
+                             fold launches instead of xteam_kernel MODE 3 + nbv_fold_kernel
+                             (OPT_NO_NBV),
                              4 / 8 = qteam_kernel with XOR3 grouping 1 / 2,
                              16 = team_kernel<16>'s two-level walk with XOR3 grouping 2,
                              1024 = direct burst batches without the descriptor prefetch,
@@ -222,10 +223,10 @@ struct XParts {
     uint64_t unit_min;
     uint64_t seg_lo, seg_hi, G; /* per wave, set on the device */
 };
-/* MODE 3's record limit: the workgroup's 64-bit scan of the starts in LDS */
-constexpr uint32_t NBV_MAX = 16384;
+/* MODE 3's commit limit: four lengths per thread of the workgroup's scan */
+constexpr uint32_t NBV_MAX = 4096;
 constexpr uint32_t NBV_PARTS_MAX = 62; /* parts per segment (one lane each) */
-constexpr uint32_t OPT_NBV = 64u; /* tuning: class-3-only verdicts on MODE 3 + nbv_fold_kernel (round 6 A/B: level) */
+constexpr uint32_t OPT_NO_NBV = 64u; /* tuning: class-3-only range verdicts through classify + parts + fold */
 
 /* consistent's device post pass (zscrc_cpass, cpass_post_kernel): the
  * verdict's bad list classified (stale finalise commit / bad / undecided),

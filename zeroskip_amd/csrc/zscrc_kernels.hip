@@ -1246,78 +1246,36 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp,
         xp.first_rec = first;
         xp.U = uni64(((const __attribute__((address_space(1))) uint64_t *)(xp.plan + xp.klass))[0]);
     }
-    /* MODE 3: the workgroup's own plan -- the commits' starts end to end
-     * (an out-of-image commit adds no bytes; workgroup 0 counts it into the
-     * verdict) as a 64-bit scan in LDS before the tables go there, the
-     * segment unit G as seg_unit's, and wave w's first record (the one
-     * holding byte w G) found by a binary search of the starts */
-    uint64_t r3 = 0, s3 = 0;
+    /* MODE 3: the workgroup's own plan.  The commits' lengths (<= NBV_MAX,
+     * four per thread; an out-of-image commit counts as 0 bytes and
+     * workgroup 0 counts it into the verdict) are loaded while the tables
+     * fill LDS; then a 64-bit scan gives every commit its start end to end,
+     * G is seg_unit's, and the thread holding a commit that contains the
+     * first byte j G of one of this workgroup's 16 segments hands (commit,
+     * start) to that segment's wave through LDS -- after the tables, in the
+     * bytes past the DEAL counter. */
+    typedef const __attribute__((address_space(1))) uint64_t *g64p;
+    static_assert(NBV_MAX <= 4 * WG, "MODE 3 holds four lengths per thread");
+    static_assert(OFF_Z + 6 * 4096 + 16 + 16 * 8 + 16 * 16 <= LDS_BYTES, "no room for MODE 3's scan");
+    uint64_t r3 = 0, s3 = 0, run3 = 0, e3[4] = {0, 0, 0, 0};
     if (MODE == 3) {
-        typedef const __attribute__((address_space(1))) uint64_t *g64p;
-        uint64_t *Sr = reinterpret_cast<uint64_t *>(L);
-        unsigned long long *ws = reinterpret_cast<unsigned long long *>(L + 8 * (NBV_MAX + 1));
         const uint64_t n = xp.n3;
-        uint64_t run = 0;
-        for (uint64_t c0 = 0; c0 < n; c0 += 4 * WG) {
-            uint64_t eff[4]; /* four chunks' lengths in flight at once, then their scans */
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const uint64_t r = c0 + (uint64_t)i * WG + threadIdx.x;
-                eff[i] = 0;
-                if (r < n) {
-                    const uint64_t off = ((g64p)xp.off3)[r], len = ((g64p)xp.len3)[r];
-                    if (commit_fits(xp.img_size, off, len))
-                        eff[i] = len;
-                    else if (blockIdx.x == 0) {
-                        const unsigned long long k = atomicAdd(xp.vpair, 1ull);
-                        if (k < xp.bad_cap)
-                            xp.bad_idx[k] = r;
-                    }
+        for (int i = 0; i < 4; ++i) {
+            const uint64_t r = (uint64_t)i * WG + threadIdx.x;
+            if (r < n) {
+                const uint64_t off = ((g64p)xp.off3)[r], len = ((g64p)xp.len3)[r];
+                if (commit_fits(xp.img_size, off, len))
+                    e3[i] = len;
+                else if (blockIdx.x == 0) {
+                    const unsigned long long k = atomicAdd(xp.vpair, 1ull);
+                    if (k < xp.bad_cap)
+                        xp.bad_idx[k] = r;
                 }
             }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                if (c0 + (uint64_t)i * WG >= n)
-                    break;
-                const uint64_t r = c0 + (uint64_t)i * WG + threadIdx.x;
-                uint64_t tot;
-                const uint64_t S = run + block_scan64(eff[i], ws, &tot);
-                if (r < n) {
-                    Sr[r] = S;
-                    if (blockIdx.x == 0) /* for the fold launch */
-                        xp.rstart[r] = S;
-                }
-                run += tot;
-            }
-        }
-        __syncthreads();
-        run = uni64(run);
-        if (blockIdx.x == 0 && threadIdx.x == 0)
-            xp.rstart[n] = run;
-        uint64_t G = (run + xp.nseg - 1) / xp.nseg;
-        G = (G + 63) & ~63ull;
-        xp.G = uni64(G < xp.unit_min ? xp.unit_min : G);
-        const uint64_t j = uni64((uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6));
-        xp.seg_lo = xp.seg_hi = 0;
-        r3 = n;
-        if (j < xp.nseg && j * xp.G < run) {
-            xp.seg_lo = uni64(j * xp.G);
-            xp.seg_hi = uni64(xp.seg_lo + xp.G < run ? xp.seg_lo + xp.G : run);
-            /* the last record starting at or before seg_lo (it has bytes) */
-            uint64_t lo = 0, hi = n - 1;
-            while (lo < hi) {
-                const uint64_t mid = (lo + hi + 1) / 2;
-                if (Sr[mid] <= xp.seg_lo)
-                    lo = mid;
-                else
-                    hi = mid - 1;
-            }
-            r3 = uni64(lo);
-            s3 = uni64(Sr[lo]);
         }
         d.n = n;
         d.xor_io = 0;
-        __syncthreads(); /* the starts are read: the tables may overwrite them */
     }
     /* segment plans: wave w takes segment w's parts (every block works) */
     if (MODE != 3 && (MODE != 2 || !xp.seg) && (uint64_t)blockIdx.x * WAVES >= d.n)
@@ -1327,7 +1285,59 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp,
     if (DEAL && threadIdx.x == 0)
         lctr = 0;
     fill_lds<64>(L, gtab);
+    if (MODE == 3) {
+        unsigned long long *ws = reinterpret_cast<unsigned long long *>(L + OFF_Z + 6 * 4096 + 16);
+        uint64_t *slot = reinterpret_cast<uint64_t *>(L + OFF_Z + 6 * 4096 + 16 + 16 * 8);
+        const uint64_t n = d.n;
+        if (threadIdx.x < 16)
+            slot[2 * threadIdx.x] = n; /* no commit: the segment is past the bytes */
+        uint64_t run = 0, S[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { /* (block_scan64's barriers order the slot reset too) */
+            if ((uint64_t)i * WG >= n)
+                break;
+            uint64_t tot;
+            S[i] = run + block_scan64(e3[i], ws, &tot);
+            run += tot;
+        }
+        run3 = run = uni64(run);
+        uint64_t G = (run + xp.nseg - 1) / xp.nseg;
+        G = (G + 63) & ~63ull;
+        xp.G = uni64(G < xp.unit_min ? xp.unit_min : G);
+        const uint64_t j0 = (uint64_t)blockIdx.x * WAVES;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint64_t r = (uint64_t)i * WG + threadIdx.x;
+            if (r >= n)
+                continue;
+            if (blockIdx.x == 0) /* for the fold launch */
+                xp.rstart[r] = S[i];
+            if (!e3[i])
+                continue;
+            uint64_t ja = (S[i] + xp.G - 1) / xp.G, jb = (S[i] + e3[i] - 1) / xp.G;
+            ja = ja > j0 ? ja : j0;
+            jb = jb < j0 + WAVES - 1 ? jb : j0 + WAVES - 1;
+            for (uint64_t q = ja; q <= jb; ++q) {
+                slot[2 * (q - j0)] = r;
+                slot[2 * (q - j0) + 1] = S[i];
+            }
+        }
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+            xp.rstart[n] = run;
+    }
     __syncthreads();
+    if (MODE == 3) {
+        const uint64_t *slot = reinterpret_cast<const uint64_t *>(L + OFF_Z + 6 * 4096 + 16 + 16 * 8);
+        const uint64_t w = threadIdx.x >> 6, j = (uint64_t)blockIdx.x * WAVES + w;
+        xp.seg_lo = xp.seg_hi = 0;
+        r3 = d.n;
+        if (j < xp.nseg && j * xp.G < run3) {
+            xp.seg_lo = uni64(j * xp.G);
+            xp.seg_hi = uni64(xp.seg_lo + xp.G < run3 ? xp.seg_lo + xp.G : run3);
+            r3 = uni64(slot[2 * w]);
+            s3 = uni64(slot[2 * w + 1]);
+        }
+    }
     const uint64_t t_fill = __builtin_amdgcn_s_memrealtime();
     const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
     const uint32_t c_lo = (uint32_t)(lane & 31) << 2;
@@ -1519,7 +1529,7 @@ __global__ __launch_bounds__(WG) void xteam_kernel(XDesc d, XMulti m, XParts xp,
         wt[4 * team + 0] = t_entry;
         wt[4 * team + 1] = t_fill;
         wt[4 * team + 2] = t_end;
-        wt[4 * team + 3] = DEAL ? items : wend - wbeg;
+        wt[4 * team + 3] = DEAL ? items : MODE == 3 ? nst : wend - wbeg;
     }
 }
 
