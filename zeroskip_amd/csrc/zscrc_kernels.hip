@@ -5003,36 +5003,60 @@ __global__ __launch_bounds__(256) void part_fold_kernel(FoldPair fp, const uint3
 /* The fold launch after xteam_kernel MODE 3 (one class-3-only verdict):
  * 16 lanes per commit that spans segments j0 < j1 (the commit's starts and
  * the bytes' total from workgroup 0 of that launch), Horner over head[j0]
- * and cont[j0 < j <= j1] by K = x^(8 G), the last part shifted by its own
- * length (16-lane product tree, part_fold_kernel's), then the trailer
- * check; the last block out publishes the verdict count (commit_kernel's
- * ticket: every increment returned before its block's ticket). */
+ * and cont[j0 < j <= j1] by K = x^(8 G) (a per-block table of K's byte
+ * products), the last part shifted by its own length; K's product tree and
+ * the last part's run side by side (ab10 in profiles/r06/notbatched/); then
+ * the trailer check; the last block out publishes the verdict count
+ * (commit_kernel's ticket: every increment returned before its block's). */
 __global__ __launch_bounds__(256) void nbv_fold_kernel(XParts xp, const uint32_t *__restrict__ gtab)
 {
     __shared__ __attribute__((aligned(16))) char T[4096];
     __shared__ uint32_t TK[1024];
     __shared__ uint32_t basis[32];
-    __shared__ uint32_t Ks;
     typedef const __attribute__((address_space(1))) uint64_t *g64p;
-    load_gmul_table(T, gtab);
     const uint64_t n = xp.n3;
-    const uint64_t total = ((const volatile uint64_t *)xp.rstart)[n];
+    /* one commit per 16-lane group (the grid covers them: n <= NBV_MAX), its
+     * descriptors and start loaded beside the table */
+    const uint64_t idx = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / 16;
+    const uint32_t sub = threadIdx.x & 15;
+    const int lane = threadIdx.x & 63;
+    uint64_t off = 0, len = 0, S = 0;
+    if (idx < n) {
+        off = ((g64p)xp.off3)[idx];
+        len = ((g64p)xp.len3)[idx];
+        S = ((g64p)xp.rstart)[idx];
+    }
+    const uint64_t total = ((g64p)xp.rstart)[n];
+    load_gmul_table(T, gtab);
     uint64_t G = (total + xp.nseg - 1) / xp.nseg;
     G = (G + 63) & ~63ull;
     G = G < xp.unit_min ? xp.unit_min : G;
-    const int lane = threadIdx.x & 63;
-    __syncthreads();
-    if (threadIdx.x < 64) { /* K = x^(8 G): a product tree across wave 0 */
-        uint32_t v = ((G >> lane) & 1) ? gtab[GT_POW2 + lane] : 0x80000000u;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1)
-            v = gmul_t(T, v, __shfl_xor(v, o));
-        if (lane == 0)
-            Ks = v;
-    }
-    __syncthreads();
+    const bool fits = idx < n && len && commit_fits(xp.img_size, off, len);
+    const uint64_t j0 = fits ? S / G : 0, j1 = fits ? (S + len - 1) / G : 0;
+    const bool split = fits && j0 != j1; /* one segment: MODE 3's wave finished it */
+    const uint64_t blast = split ? S + len - j1 * G : 0;
+    /* K = x^(8 G) (a 64-lane product tree, every wave) and the last part's
+     * shift x^(8 blast) (a 16-lane tree per commit), interleaved: two
+     * independent chains of six products */
+    constexpr uint32_t ONE = 0x80000000u;
+    const uint32_t k0 = ((G >> lane) & 1) ? gtab[GT_POW2 + lane] : ONE;
+    const uint32_t g0 = ((blast >> sub) & 1) ? gtab[GT_POW2 + sub] : ONE;
+    const uint32_t g1 = ((blast >> (sub + 16)) & 1) ? gtab[GT_POW2 + sub + 16] : ONE;
+    const uint32_t g2 = ((blast >> (sub + 32)) & 1) ? gtab[GT_POW2 + sub + 32] : ONE;
+    __syncthreads(); /* the table */
+    uint32_t K = gmul_t(T, k0, __shfl_xor(k0, 1)), pw = gmul_t(T, g0, g1);
+    K = gmul_t(T, K, __shfl_xor(K, 2));
+    pw = gmul_t(T, pw, g2);
+    K = gmul_t(T, K, __shfl_xor(K, 4));
+    pw = gmul_t(T, pw, __shfl_xor(pw, 1));
+    K = gmul_t(T, K, __shfl_xor(K, 8));
+    pw = gmul_t(T, pw, __shfl_xor(pw, 2));
+    K = gmul_t(T, K, __shfl_xor(K, 16));
+    pw = gmul_t(T, pw, __shfl_xor(pw, 4));
+    K = gmul_t(T, K, __shfl_xor(K, 32));
+    pw = gmul_t(T, pw, __shfl_xor(pw, 8));
     if (threadIdx.x < 32) /* a * K is linear in a's bits */
-        basis[threadIdx.x] = gmul_t(T, 1u << threadIdx.x, Ks);
+        basis[threadIdx.x] = gmul_t(T, 1u << threadIdx.x, K);
     __syncthreads();
     for (uint32_t e = threadIdx.x; e < 1024; e += blockDim.x) {
         const uint32_t jb = e >> 8, b = e & 255;
@@ -5044,31 +5068,7 @@ __global__ __launch_bounds__(256) void nbv_fold_kernel(XParts xp, const uint32_t
         TK[e] = v;
     }
     __syncthreads();
-    const uint32_t sub = threadIdx.x & 15;
-    const uint64_t ngrp = (uint64_t)gridDim.x * blockDim.x / 16;
-    for (uint64_t idx = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / 16; __any(idx < n); idx += ngrp) {
-        uint64_t off = 0, len = 0, S = 0, j0 = 0, j1 = 0;
-        bool split = false;
-        if (idx < n) {
-            off = ((g64p)xp.off3)[idx];
-            len = ((g64p)xp.len3)[idx];
-            if (commit_fits(xp.img_size, off, len) && len) {
-                S = ((g64p)xp.rstart)[idx];
-                j0 = S / G;
-                j1 = (S + len - 1) / G;
-                split = j0 != j1; /* one segment: MODE 3's wave finished it */
-            }
-        }
-        const uint64_t blast = split ? S + len - j1 * G : 0;
-        uint32_t pw = 0x80000000u;
-        for (uint32_t t = sub; t < 48; t += 16)
-            if ((blast >> t) & 1)
-                pw = gmul_t(T, pw, gtab[GT_POW2 + t]);
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1)
-            pw = gmul_t(T, pw, __shfl_xor(pw, o));
-        if (!split || sub)
-            continue;
+    if (split && sub == 0) {
         uint32_t reg = xp.nbv[j0];
         for (uint64_t q = j0 + 1; q < j1; ++q)
             reg = TK[reg & 255] ^ TK[256 + ((reg >> 8) & 255)] ^ TK[512 + ((reg >> 16) & 255)] ^ TK[768 + (reg >> 24)] ^
@@ -5343,8 +5343,9 @@ extern "C" int zs_launch_nbv(const zs::XParts *p, const uint32_t *gtab, int grid
     hipLaunchKernelGGL(zs::xteam_kernel<3>, dim3(grid), dim3(zs::WG), 0, stream, x, none, *p, gtab);
     if (hipGetLastError() != hipSuccess)
         return -3;
+    static_assert(zs::NBV_MAX * 16 / 256 <= 65535, "nbv_fold_kernel: one commit per 16-lane group");
     uint64_t blocks = (p->n3 * 16 + 255) / 256;
-    blocks = blocks < 1 ? 1 : blocks > 256 ? 256 : blocks;
+    blocks = blocks < 1 ? 1 : blocks;
     hipLaunchKernelGGL(zs::nbv_fold_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, *p, gtab);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
